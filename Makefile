@@ -1,0 +1,49 @@
+# Build of the MI355X UHSDR RX hot path (gfx950) and its CPU oracle.
+#
+#   make            -> uhsdr_amd/lib/libuhsdr_amd.so   (product: C-ABI, HIP kernels + host setup)
+#                      oracle/build/libuhsdr_oracle.so (test infrastructure: CPU restatement)
+#   make ref        -> oracle/_ref/uhsdr_ref           (reference firmware chain, needs /root/reference)
+#
+# Host C is compiled without FP contraction and without -march, like the reference build,
+# so every binary32 rounding of the setup math and of the oracle matches the reference.
+
+HIPCC   ?= /opt/rocm/bin/hipcc
+CC      ?= gcc
+ARCH    ?= gfx950
+HOSTCFLAGS := -O2 -fPIC -ffp-contract=off -std=gnu11 -Wall -Wno-unused-function
+HIPFLAGS   := --offload-arch=$(ARCH) -O3 -fPIC -ffp-contract=off -std=c++17 -Wno-unused-result
+
+LIB     := uhsdr_amd/lib/libuhsdr_amd.so
+ORACLE  := oracle/build/libuhsdr_oracle.so
+OBJDIR  := uhsdr_amd/build
+
+HOST_SRCS := uhsdr_amd/csrc/uhsdr_setup.c uhsdr_amd/csrc/uhsdr_filter_tables.c
+HIP_SRCS  := uhsdr_amd/csrc/uhsdr_rx.hip
+HOST_OBJS := $(patsubst uhsdr_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRCS))
+HIP_OBJS  := $(patsubst uhsdr_amd/csrc/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
+HDRS := include/uhsdr.h uhsdr_amd/csrc/uhsdr_internal.h
+
+all: $(LIB) $(ORACLE)
+
+$(OBJDIR) uhsdr_amd/lib oracle/build:
+	mkdir -p $@
+
+$(OBJDIR)/%.o: uhsdr_amd/csrc/%.c $(HDRS) | $(OBJDIR)
+	$(CC) $(HOSTCFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.o: uhsdr_amd/csrc/%.hip $(HDRS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(HOST_OBJS) $(HIP_OBJS) | uhsdr_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -lm
+
+$(ORACLE): oracle/uhsdr_oracle.c oracle/uhsdr_oracle.h include/uhsdr.h | oracle/build
+	$(CC) $(HOSTCFLAGS) -shared -o $@ $< -lm -lpthread
+
+ref:
+	$(MAKE) -C oracle/ref
+
+clean:
+	rm -rf $(OBJDIR) uhsdr_amd/lib oracle/build
+
+.PHONY: all ref clean

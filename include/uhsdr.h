@@ -1,0 +1,199 @@
+/*
+ * uhsdr.h -- C ABI of the MI355X-native UHSDR RX DSP hot path (libuhsdr_amd.so).
+ *
+ * Drop-in boundary for the reference firmware's per-block receive chain
+ * (SURVEY.md §8(b)):
+ *
+ *   reference                                             this ABI
+ *   ---------------------------------------------------   --------------------------------
+ *   AudioDriver_SetProcessingChain(dmod_mode, reset)      uhsdr_rx_plan_build()  (host setup,
+ *     drivers/audio/audio_driver.c:1093-1251                restates the chain selection,
+ *   AudioFilter_SetRxHilbertAndDecimationFIR()              filter tables, biquad designers
+ *     drivers/audio/audio_filter.c:1134-1223                and AGC parameter math)
+ *   AudioAgc_SetupAgcWdsp(rate, remove_dc)
+ *     drivers/audio/audio_agc.c:126-339
+ *   AudioDriver_Init() + SetProcessingChain()             uhsdr_rx_create() / uhsdr_rx_reset()
+ *     audio_driver.c:677-704                                (zeroes all per-channel state)
+ *   AudioDriver_I2SCallback(audio, iq, dst, 32)           uhsdr_rx_process()  -- C channels x
+ *     audio_driver.c:2962-3049 ->                           N frames per call, N % 32 == 0,
+ *   AudioDriver_RxProcessor(iq, audio, 32, mute)            one call == N/32 consecutive ISR
+ *     audio_driver.c:2603-2942                              invocations on every channel
+ *
+ * Buffers follow the firmware's DMA formats, channel-major:
+ *   iq    : IqSample_t    {int32 l (I), int32 r (Q)}  [C][N]  (audio_driver.h:44-52)
+ *   audio : float         adb.a_buffer[1]             [C][N]  (audio_driver.h:147-157)
+ *   dst   : AudioSample_t {int32 l, int32 r}           [C][N]  codec frames (audio_driver.c:2911-2923)
+ * Device pointers are HIP device allocations.  Status codes follow CMSIS arm_status
+ * (CMSIS/Include/arm_math.h:375-382): 0 success, -1 argument error, -2 length error.
+ *
+ * Threading: a handle is not re-entrant (like the ISR, audio_driver.c:1804-1806); calls on
+ * one handle are ordered on the handle's HIP stream.  Different handles are independent.
+ */
+#ifndef UHSDR_H
+#define UHSDR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UHSDR_ABI_VERSION 1
+
+typedef enum
+{
+    UHSDR_OK = 0,                 /* ARM_MATH_SUCCESS */
+    UHSDR_ARGUMENT_ERROR = -1,    /* ARM_MATH_ARGUMENT_ERROR */
+    UHSDR_LENGTH_ERROR = -2,      /* ARM_MATH_LENGTH_ERROR: N % 32 != 0, bad sizes */
+    UHSDR_UNSUPPORTED = -10,      /* mode / filter path not implemented on the device yet */
+    UHSDR_DEVICE_ERROR = -11      /* HIP runtime error */
+} uhsdr_status;
+
+/* DemodModes_t, hardware/uhsdr_board.h:72-85 */
+enum { UHSDR_DEMOD_USB = 0, UHSDR_DEMOD_LSB = 1, UHSDR_DEMOD_CW = 2, UHSDR_DEMOD_AM = 3,
+       UHSDR_DEMOD_SAM = 4, UHSDR_DEMOD_FM = 5, UHSDR_DEMOD_DIGI = 6 };
+
+/* FREQ_IQ_CONV_*, drivers/audio/audio_driver.h:520-526 */
+enum { UHSDR_IQ_CONV_OFF = 0, UHSDR_IQ_CONV_P6KHZ = 1, UHSDR_IQ_CONV_M6KHZ = 2,
+       UHSDR_IQ_CONV_P12KHZ = 3, UHSDR_IQ_CONV_M12KHZ = 4 };
+
+/* ts.dsp.active bits honoured by the chain (drivers/ui/ui_driver.c:425-433) */
+#define UHSDR_DSP_MNOTCH_ENABLE 0x10
+#define UHSDR_DSP_MPEAK_ENABLE  0x20
+
+#define UHSDR_IQ_BLOCK_SIZE 32        /* IQ_BLOCK_SIZE, hardware/uhsdr_board_config.h:217 */
+#define UHSDR_FILTER_PATH_NUM 87      /* AUDIO_FILTER_PATH_NUM, audio_filter.h:139 */
+#define UHSDR_MAX_FIR_TAPS 200        /* IQ_RX_NUM_TAPS_MAX (199 rounded) */
+#define UHSDR_MAX_DEC_TAPS 96         /* 89-tap AM tables reused as decimator */
+#define UHSDR_MAX_LATTICE 10          /* IIR_RXAUDIO_NUM_STAGES_MAX */
+#define UHSDR_MAX_INTERP 16
+#define UHSDR_AGC_RING 192            /* AGC_WDSP_RB_SIZE, audio_agc.c:19 */
+
+/*
+ * User-facing receiver configuration: the subset of TransceiverState `ts` /
+ * AudioDriverState `ads` / agc_wdsp_conf that the RX chain reads.  Defaults
+ * (uhsdr_rx_config_default) are the firmware's, drivers/ui/ui_configuration.c:70-230.
+ */
+typedef struct uhsdr_rx_config
+{
+    int32_t dmod_mode;            /* ts.dmod_mode */
+    int32_t filter_path;          /* ts.filter_path_mem[mode][0]: index into FilterPathInfo */
+    int32_t iq_freq_mode;         /* ts.iq_freq_mode */
+    int32_t iq_auto_correction;   /* ts.iq_auto_correction */
+    float   iq_gain_i;            /* ts.rx_adj_gain_var.i */
+    float   iq_gain_q;            /* ts.rx_adj_gain_var.q */
+    float   iq_phase_balance;     /* ads.iq_phase_balance_rx */
+    int32_t dsp_active;           /* ts.dsp.active (MNOTCH / MPEAK bits) */
+    int32_t notch_frequency;      /* ts.dsp.notch_frequency */
+    int32_t peak_frequency;       /* ts.dsp.peak_frequency */
+    int32_t bass_gain;            /* ts.dsp.bass_gain */
+    int32_t treble_gain;          /* ts.dsp.treble_gain */
+    int32_t cw_lsb;               /* ts.cw_lsb */
+    int32_t digi_lsb;             /* ts.digi_lsb */
+    int32_t agc_mode;             /* agc_wdsp_conf.mode */
+    int32_t agc_slope;            /* agc_wdsp_conf.slope */
+    int32_t agc_thresh;           /* agc_wdsp_conf.thresh */
+    int32_t agc_hang_enable;      /* agc_wdsp_conf.hang_enable */
+    int32_t agc_hang_time;        /* agc_wdsp_conf.hang_time (500) */
+    int32_t agc_hang_thresh;      /* agc_wdsp_conf.hang_thresh (45) */
+    int32_t agc_tau_decay[6];     /* agc_wdsp_conf.tau_decay[] */
+    int32_t agc_tau_hang_decay;   /* agc_wdsp_conf.tau_hang_decay */
+    int32_t reserved[16];
+} uhsdr_rx_config;
+
+/* AudioAgc_SetupAgcWdsp() results (audio_agc.c:126-339) */
+typedef struct uhsdr_agc_plan
+{
+    int32_t mode;                 /* 5 == fixed gain (AGC off) */
+    int32_t hang_enable;
+    int32_t remove_dc;
+    int32_t ring_buffsize;        /* 192 */
+    int32_t attack_buffsize;      /* ceilf(rate * n_tau * tau_attack): 49 at 12 ksps */
+    int32_t out_index0;           /* -1 */
+    int32_t in_index0;            /* (attack_buffsize + out_index0) % ring_buffsize */
+    int32_t hang_counter_init;    /* (int)(hangtime * sample_rate) */
+    float   sample_rate;
+    float   fixed_gain, attack_mult, decay_mult, fast_decay_mult, fast_backmult;
+    float   onemfast_backmult, hang_backmult, onemhang_backmult, hang_decay_mult;
+    float   pop_ratio, hang_level, min_volts, inv_max_input, out_target, slope_constant;
+    float   hangtime, hang_thresh, var_gain, max_gain, inv_out_target;
+} uhsdr_agc_plan;
+
+/*
+ * Resolved processing chain (what SetProcessingChain leaves in the driver's instances).
+ * Built on the host; uploaded once per handle; read-only for the kernels.
+ */
+typedef struct uhsdr_rx_plan
+{
+    int32_t dmod_mode, filter_path, lsb;
+    int32_t decimation_rate;      /* ads.decimation_rate */
+    int32_t decimated_freq;       /* ads.decimated_freq */
+    int32_t use_decimated_iq;     /* audio_driver.c:2718-2720 */
+    int32_t iq_auto_correction;
+    float   iq_gain_i, iq_gain_q, iq_phase_balance;
+    int32_t freq_shift_hz;        /* AudioDriver_GetTranslateFreq(), audio_driver.c:445-464 */
+    int32_t shift_kind;           /* 0 none, 1 Fs/4 exchange, 2 recursive oscillator */
+    int32_t shift_up;             /* dir == FREQ_SHIFT_UP (freq_shift.c:324) */
+    float   osc_cos, osc_sin;     /* FreqShift_Approx_Prepare, freq_shift.c:40-52 */
+    int32_t hilbert_taps;         /* 0 => Hilbert skipped (AM/SAM) */
+    float   hilbert_i[UHSDR_MAX_FIR_TAPS];
+    float   hilbert_q[UHSDR_MAX_FIR_TAPS];
+    int32_t dec_taps;
+    float   dec[UHSDR_MAX_DEC_TAPS];
+    int32_t pre_stages;
+    float   pre_k[UHSDR_MAX_LATTICE];
+    float   pre_v[UHSDR_MAX_LATTICE + 1];
+    int32_t interp_L, interp_phase;  /* INTERPOLATE_RX: L, phaseLength (quirk: numTaps/L) */
+    float   interp[UHSDR_MAX_INTERP];
+    int32_t aa_stages;
+    float   aa_k[UHSDR_MAX_LATTICE];
+    float   aa_v[UHSDR_MAX_LATTICE + 1];
+    float   biquad1[20];          /* IIR_biquad_1: 4 stages {b0,b1,b2,a1,a2} */
+    float   biquad2[5];           /* IIR_biquad_2: 1 stage */
+    float   post_agc_scale;       /* audio_driver.c:2513-2524 */
+    float   line_out_scale;       /* LINE_OUT_SCALING_FACTOR, audio_driver.h:396 */
+    uhsdr_agc_plan agc;
+    int32_t reserved[64];
+} uhsdr_rx_plan;
+
+typedef struct uhsdr_rx_s* uhsdr_rx_handle;
+
+/* ---- host setup layer ---- */
+void         uhsdr_rx_config_default(uhsdr_rx_config* cfg);
+uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* plan);
+/* 1 if the device chain implements this plan, 0 otherwise */
+int          uhsdr_rx_plan_supported(const uhsdr_rx_plan* plan);
+
+/* ---- batched device chain ---- */
+/* stream: hipStream_t to order all work of this handle on (NULL = default stream). */
+uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t num_channels, int32_t frames_per_call,
+                             void* stream, uhsdr_rx_handle* out);
+uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h);
+/* iq, audio, dst: device pointers ([C][N][2] int32, [C][N] f32, [C][N][2] int32).
+   audio or dst may be NULL (not written).  Asynchronous on the handle's stream. */
+uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, int32_t* dst);
+/* Same with host buffers: copies in, processes, copies out, synchronises. */
+uhsdr_status uhsdr_rx_process_host(uhsdr_rx_handle h, const int32_t* iq, float* audio, int32_t* dst);
+uhsdr_status uhsdr_rx_get_plan(uhsdr_rx_handle h, uhsdr_rx_plan* plan);
+uhsdr_status uhsdr_rx_set_stream(uhsdr_rx_handle h, void* stream);
+uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h);
+
+/* ---- diagnostics ---- */
+const char*  uhsdr_version(void);
+/* sizeof(uhsdr_rx_config), sizeof(uhsdr_rx_plan): lets FFI bindings check their layouts */
+int32_t      uhsdr_sizeof_config(void);
+int32_t      uhsdr_sizeof_plan(void);
+const char*  uhsdr_last_error(void);
+/* number of kernels one uhsdr_rx_process call enqueues */
+int32_t      uhsdr_rx_kernel_count(uhsdr_rx_handle h);
+/* Per-kernel device timing: while enabled, every uhsdr_rx_process brackets each kernel with
+   hipEvents on the handle's stream.  uhsdr_rx_kernel_times() synchronises the stream and
+   returns, per kernel, the summed milliseconds and launch count since the last enable. */
+uhsdr_status uhsdr_rx_enable_timing(uhsdr_rx_handle h, int32_t enable);
+int32_t      uhsdr_rx_kernel_times(uhsdr_rx_handle h, float* total_ms, int32_t* launches, int32_t max_kernels);
+const char*  uhsdr_rx_kernel_name(int32_t index);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UHSDR_H */

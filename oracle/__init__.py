@@ -1,0 +1,58 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+ctypes loader for oracle/build/libuhsdr_oracle.so, the clean-room CPU restatement of the
+reference RX chain (oracle/uhsdr_oracle.c).  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg may import this module, and only as the checker / CPU baseline.
+The product (libuhsdr_amd.so) never links or calls it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libuhsdr_oracle.so")
+REF_BIN = os.path.join(HERE, "_ref", "uhsdr_ref")
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run `make`")
+        lib = C.CDLL(LIB_PATH)
+        lib.uo_rx_state_size.restype = C.c_size_t
+        lib.uo_rx_state_init.argtypes = [C.c_void_p, C.c_void_p]
+        lib.uo_rx_process.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        lib.uo_rx_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                            C.c_void_p, C.c_void_p, C.c_int]
+        _lib = lib
+    return _lib
+
+
+class OracleRx:
+    """C channels of the reference RX chain on the CPU, state carried across calls."""
+
+    def __init__(self, plan, channels: int):
+        self.lib = load()
+        self.plan = plan
+        self.channels = channels
+        self.ssize = self.lib.uo_rx_state_size()
+        self.states = (C.c_char * (self.ssize * channels))()
+        for c in range(channels):
+            self.lib.uo_rx_state_init(C.byref(plan), C.byref(self.states, c * self.ssize))
+
+    def process(self, iq: np.ndarray, threads: int = 1):
+        iq = np.ascontiguousarray(iq, dtype=np.int32)
+        Cn, n, _ = iq.shape
+        assert Cn == self.channels
+        a1 = np.empty((Cn, n), np.float32)
+        dst = np.empty((Cn, n, 2), np.int32)
+        st = self.lib.uo_rx_process_batch(C.byref(self.plan), self.states, Cn, iq.ctypes.data_as(C.c_void_p), n,
+                                          a1.ctypes.data_as(C.c_void_p), dst.ctypes.data_as(C.c_void_p), threads)
+        if st != 0:
+            raise RuntimeError(f"uo_rx_process_batch status {st}")
+        return a1, dst

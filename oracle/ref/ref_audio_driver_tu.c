@@ -1,0 +1,23 @@
+/*
+ * ORACLE TEST INFRASTRUCTURE -- compiles the reference's own audio driver for the x86 host.
+ *
+ * The reference translation unit is included from where it lies under /root/reference
+ * (drivers/audio/audio_driver.c); nothing is copied.  Two things are done around it:
+ *  - USE_PENDSV_FOR_HIGHPRIO_TASKS is undefined: the ISR tail at audio_driver.c:3045-3048
+ *    pokes the Cortex-M SCB->ICSR register, which is not memory on x86.
+ *  - read-only accessors expose the driver's file-static filter instances so that the
+ *    oracle can dump the exact coefficients / state lengths the firmware configured
+ *    (used to pin the product's host setup layer bit-for-bit).
+ */
+#include "uhsdr_board_config.h"
+#undef USE_PENDSV_FOR_HIGHPRIO_TASKS
+#include "audio_driver.c"
+
+const arm_biquad_casd_df1_inst_f32* oracle_ref_biquad1(void) { return &IIR_biquad_1[0]; }
+const arm_biquad_casd_df1_inst_f32* oracle_ref_biquad2(void) { return &IIR_biquad_2[0]; }
+const arm_iir_lattice_instance_f32* oracle_ref_prefilter(void) { return &IIR_PreFilter[0]; }
+const arm_iir_lattice_instance_f32* oracle_ref_antialias(void) { return &IIR_AntiAlias[0]; }
+const arm_fir_interpolate_instance_f32* oracle_ref_interpolate(void) { return &INTERPOLATE_RX[0]; }
+
+/* layout fingerprint of TransceiverState as audio_driver.c sees it */
+unsigned long oracle_driver_layout(void) { return (unsigned long)sizeof(TransceiverState) * 100000ul + (unsigned long)((char*)&ts.dsp.active - (char*)&ts); }

@@ -1,0 +1,213 @@
+/*
+ * ORACLE TEST INFRASTRUCTURE -- command-line driver for the reference RX chain.
+ *
+ * Runs ONE channel through the reference firmware's own entry points, exactly as the
+ * radio does at boot and per DMA interrupt:
+ *     AudioDriver_Init();                       audio_driver.c:677-704
+ *     AudioDriver_SetProcessingChain(mode,0);   audio_driver.c:1093-1251
+ *     AudioDriver_I2SCallback(dst, iq, 0, 32)   audio_driver.c:2962-3049, once per 32 frames
+ * One process = one channel, because the driver keeps its DSP state in globals and
+ * function-local statics (e.g. FreqShift's NCO, audio_agc.c:578 `wold`).
+ *
+ * usage: uhsdr_ref key=value ...
+ *   in=<file>      int32 I/Q frames {l,r} (IqSample_t, audio_driver.h:44-52)
+ *   n=<frames>     number of frames (multiple of 32)
+ *   out_a=<file>   f32 adb.a_buffer[1] after each call (audio_driver.h:147-157)
+ *   out_dst=<file> int32 codec frames {l,r} (AudioSample_t)
+ *   mode= path= iqmode= agc_mode= agc_thresh= agc_slope= agc_hang= bass= treble=
+ *   iq_auto= gain_i= gain_q= phase= dsp= notch= peak= sam_sb= pll_fmax= zeta= omegan=
+ *   fade= sql= fm5k= block=
+ *   dump=setup     print the configured chain (coefficients as raw bits) as JSON
+ *   dump=paths     print FilterPathInfo[] (audio_filter.c:147-922) as JSON
+ */
+/* reference headers first (see ref_harness.c on `bool`) */
+#include "uhsdr_board.h"
+#include "audio_driver.h"
+#include "audio_filter.h"
+#include "audio_agc.h"
+#include "ui_spectrum.h"
+#include "filters.h"
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdint.h>
+
+extern __IO TransceiverState ts;
+extern SpectrumDisplay sd;
+extern AudioDriverState ads;
+extern AudioDriverBuffer adb;
+const arm_biquad_casd_df1_inst_f32* oracle_ref_biquad1(void);
+const arm_biquad_casd_df1_inst_f32* oracle_ref_biquad2(void);
+const arm_iir_lattice_instance_f32* oracle_ref_prefilter(void);
+const arm_iir_lattice_instance_f32* oracle_ref_antialias(void);
+const arm_fir_interpolate_instance_f32* oracle_ref_interpolate(void);
+void oracle_ref_agc_dump(void);
+unsigned long oracle_harness_layout(void);
+unsigned long oracle_driver_layout(void);
+extern arm_fir_instance_f32 Fir_Rx_Hilbert_I, Fir_Rx_Hilbert_Q;
+extern arm_fir_decimate_instance_f32 DECIMATE_RX_I, DECIMATE_RX_Q;
+
+static const char* arg(int argc, char** argv, const char* key, const char* dflt)
+{
+    size_t k = strlen(key);
+    for (int i = 1; i < argc; i++)
+        if (strncmp(argv[i], key, k) == 0 && argv[i][k] == '=') return argv[i] + k + 1;
+    return dflt;
+}
+static long iarg(int argc, char** argv, const char* key, long dflt)
+{
+    const char* v = arg(argc, argv, key, NULL);
+    return v ? strtol(v, NULL, 0) : dflt;
+}
+static float farg(int argc, char** argv, const char* key, float dflt)
+{
+    const char* v = arg(argc, argv, key, NULL);
+    return v ? strtof(v, NULL) : dflt;
+}
+
+static uint32_t bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static void print_fvec(const char* name, const float* p, int n, int last)
+{
+    printf("  \"%s\": [", name);
+    for (int i = 0; i < n; i++) printf("%s%u", i ? "," : "", p ? bits(p[i]) : 0u);
+    printf("]%s\n", last ? "" : ",");
+}
+
+static void dump_paths(void)
+{
+    printf("[\n");
+    for (int i = 0; i < AUDIO_FILTER_PATH_NUM; i++)
+    {
+        const FilterPathDescriptor* f = &FilterPathInfo[i];
+        printf("{\"index\":%d,\"id\":%u,\"name\":\"%s\",\"mode\":%u,\"select\":%u,\"fir_taps\":%u,"
+               "\"sample_rate_dec\":%u,\"offset\":%u,\n", i, f->id, f->name ? f->name : "", f->mode,
+               f->filter_select_id, f->FIR_numTaps, f->sample_rate_dec, f->offset);
+        print_fvec("fir_i", f->FIR_I_coeff_file, f->FIR_I_coeff_file ? f->FIR_numTaps : 0, 0);
+        print_fvec("fir_q", f->FIR_Q_coeff_file, f->FIR_Q_coeff_file ? f->FIR_numTaps : 0, 0);
+        print_fvec("dec", f->dec ? f->dec->pCoeffs : NULL, f->dec ? f->dec->numTaps : 0, 0);
+        print_fvec("pre_k", f->pre_instance ? f->pre_instance->pkCoeffs : NULL, f->pre_instance ? f->pre_instance->numStages : 0, 0);
+        print_fvec("pre_v", f->pre_instance ? f->pre_instance->pvCoeffs : NULL, f->pre_instance ? f->pre_instance->numStages + 1 : 0, 0);
+        print_fvec("interp", f->interpolate ? f->interpolate->pCoeffs : NULL, f->interpolate ? f->interpolate->phaseLength : 0, 0);
+        print_fvec("aa_k", f->iir_instance ? f->iir_instance->pkCoeffs : NULL, f->iir_instance ? f->iir_instance->numStages : 0, 0);
+        print_fvec("aa_v", f->iir_instance ? f->iir_instance->pvCoeffs : NULL, f->iir_instance ? f->iir_instance->numStages + 1 : 0, 1);
+        printf("}%s\n", i + 1 < AUDIO_FILTER_PATH_NUM ? "," : "");
+    }
+    printf("]\n");
+}
+
+static void dump_setup(void)
+{
+    const arm_biquad_casd_df1_inst_f32* b1 = oracle_ref_biquad1();
+    const arm_biquad_casd_df1_inst_f32* b2 = oracle_ref_biquad2();
+    const arm_iir_lattice_instance_f32* pre = oracle_ref_prefilter();
+    const arm_iir_lattice_instance_f32* aa = oracle_ref_antialias();
+    const arm_fir_interpolate_instance_f32* ip = oracle_ref_interpolate();
+    printf("{\n");
+    printf("  \"filter_path\": %u, \"decimation_rate\": %u, \"decimated_freq\": %u,\n",
+           ts.filter_path, ads.decimation_rate, (unsigned)ads.decimated_freq);
+    printf("  \"hilbert_taps\": %u, \"decim_taps\": %u, \"pre_stages\": %u, \"aa_stages\": %u,"
+           " \"interp_L\": %u, \"interp_phase\": %u,\n", Fir_Rx_Hilbert_I.numTaps, DECIMATE_RX_I.numTaps,
+           pre->numStages, aa->numStages, ip->L, ip->phaseLength);
+    print_fvec("biquad1", b1->pCoeffs, 5 * b1->numStages, 0);
+    print_fvec("biquad2", b2->pCoeffs, 5 * b2->numStages, 0);
+    print_fvec("interp", ip->pCoeffs, ip->phaseLength * ip->L, 0);
+    print_fvec("hilbert_i", Fir_Rx_Hilbert_I.pCoeffs, Fir_Rx_Hilbert_I.numTaps, 0);
+    print_fvec("hilbert_q", Fir_Rx_Hilbert_Q.pCoeffs, Fir_Rx_Hilbert_Q.numTaps, 0);
+    print_fvec("decim", DECIMATE_RX_I.pCoeffs, DECIMATE_RX_I.numTaps, 0);
+    print_fvec("pre_k", pre->pkCoeffs, pre->numStages, 0);
+    print_fvec("pre_v", pre->pvCoeffs, pre->numStages ? pre->numStages + 1 : 0, 0);
+    print_fvec("aa_k", aa->pkCoeffs, aa->numStages, 0);
+    print_fvec("aa_v", aa->pvCoeffs, aa->numStages ? aa->numStages + 1 : 0, 1);
+    printf("}\n");
+}
+
+int main(int argc, char** argv)
+{
+    const unsigned long mine = (unsigned long)sizeof(TransceiverState) * 100000ul +
+                               (unsigned long)((char*)&ts.dsp.active - (char*)&ts);
+    if (mine != oracle_driver_layout() || mine != oracle_harness_layout())
+    {
+        fprintf(stderr, "TransceiverState layout mismatch between TUs (%lu %lu %lu)\n", mine,
+                oracle_driver_layout(), oracle_harness_layout());
+        return 3;
+    }
+    const char* dump = arg(argc, argv, "dump", "");
+    if (strcmp(dump, "paths") == 0) { dump_paths(); return 0; }
+
+    const int mode = (int)iarg(argc, argv, "mode", DEMOD_USB);
+    const int path = (int)iarg(argc, argv, "path", 0);
+    const int block = (int)iarg(argc, argv, "block", IQ_BLOCK_SIZE);
+
+    /* settings the firmware loads from its config store before AudioDriver_Init
+       (drivers/ui/ui_configuration.c:70-230 defaults unless overridden) */
+    ts.txrx_mode = TRX_MODE_RX;                    /* src/uhsdr_main.c:181-182 */
+    ts.samp_rate = IQ_SAMPLE_RATE;
+    ts.beep_frequency = DEFAULT_BEEP_FREQUENCY;    /* ui_configuration.c defaults */
+    ts.beep_loudness = DEFAULT_BEEP_LOUDNESS;
+    ts.dmod_mode = mode;
+    ts.rx_iq_source = RX_IQ_CODEC;
+    ts.tx_audio_source = TX_AUDIO_MIC;
+    ts.iq_freq_mode = iarg(argc, argv, "iqmode", FREQ_IQ_CONV_M12KHZ);
+    ts.iq_auto_correction = iarg(argc, argv, "iq_auto", 0);
+    ts.rx_adj_gain_var.i = farg(argc, argv, "gain_i", 1.0f);
+    ts.rx_adj_gain_var.q = farg(argc, argv, "gain_q", 1.0f);
+    ads.iq_phase_balance_rx = farg(argc, argv, "phase", 0.0f);
+    ts.dsp.active = iarg(argc, argv, "dsp", 0);
+    ts.dsp.notch_frequency = iarg(argc, argv, "notch", 800);
+    ts.dsp.peak_frequency = iarg(argc, argv, "peak", 750);
+    ts.dsp.bass_gain = iarg(argc, argv, "bass", 2);
+    ts.dsp.treble_gain = iarg(argc, argv, "treble", 0);
+    ts.stereo_enable = false;
+    ts.cw_keyer_mode = CW_KEYER_MODE_STRAIGHT;
+    ts.fm_sql_threshold = iarg(argc, argv, "sql", FM_SQUELCH_DEFAULT);
+    if (iarg(argc, argv, "fm5k", 0)) ts.flags2 |= FLAGS2_FM_MODE_DEVIATION_5KHZ;
+    ads.sam_sideband = iarg(argc, argv, "sam_sb", SAM_SIDEBAND_BOTH);
+    ads.pll_fmax_int = iarg(argc, argv, "pll_fmax", 2500);
+    ads.zeta_int = iarg(argc, argv, "zeta", 65);
+    ads.omegaN_int = iarg(argc, argv, "omegan", 250);
+    ads.fade_leveler = iarg(argc, argv, "fade", 1);
+    agc_wdsp_conf.mode = iarg(argc, argv, "agc_mode", 2);
+    agc_wdsp_conf.hang_enable = iarg(argc, argv, "agc_hang", 0);
+    agc_wdsp_conf.thresh = iarg(argc, argv, "agc_thresh", 20);
+    agc_wdsp_conf.slope = iarg(argc, argv, "agc_slope", 70);
+    agc_wdsp_conf.tau_decay[0] = 4000;
+    agc_wdsp_conf.tau_decay[1] = 2000;
+    agc_wdsp_conf.tau_decay[2] = 500;
+    agc_wdsp_conf.tau_decay[3] = 250;
+    agc_wdsp_conf.tau_decay[4] = 50;
+    agc_wdsp_conf.tau_hang_decay = 500;
+    sd.fft_iq_len = 0;          /* spectrum tap off for the audio oracle */
+
+    ts.filter_path_mem[AudioFilter_GetFilterModeFromDemodMode(mode)][0] = path;
+
+    AudioDriver_Init();
+    AudioDriver_SetProcessingChain(mode, false);
+
+    if (strcmp(dump, "setup") == 0) { dump_setup(); return 0; }
+    if (strcmp(dump, "agc") == 0) { oracle_ref_agc_dump(); return 0; }
+
+    const long n = iarg(argc, argv, "n", 0);
+    const char* in = arg(argc, argv, "in", NULL);
+    const char* out_a = arg(argc, argv, "out_a", NULL);
+    const char* out_dst = arg(argc, argv, "out_dst", NULL);
+    if (!in || n <= 0 || (n % block) != 0) { fprintf(stderr, "need in= and n= (multiple of %d)\n", block); return 2; }
+
+    IqSample_t* iq = malloc(sizeof(IqSample_t) * n);
+    AudioSample_t* dst = calloc(n, sizeof(AudioSample_t));
+    float* a1 = calloc(n, sizeof(float));
+    FILE* f = fopen(in, "rb");
+    if (!f || fread(iq, sizeof(IqSample_t), n, f) != (size_t)n) { fprintf(stderr, "read %s failed\n", in); return 2; }
+    fclose(f);
+
+    IqSample_t blk[IQ_BLOCK_SIZE];
+    for (long off = 0; off < n; off += block)
+    {
+        memcpy(blk, iq + off, sizeof(IqSample_t) * block);   /* the ISR's DMA half-buffer */
+        AudioDriver_I2SCallback(dst + off, blk, NULL, block);
+        memcpy(a1 + off, adb.a_buffer[1], sizeof(float) * block);
+    }
+    if (out_a) { f = fopen(out_a, "wb"); fwrite(a1, sizeof(float), n, f); fclose(f); }
+    if (out_dst) { f = fopen(out_dst, "wb"); fwrite(dst, sizeof(AudioSample_t), n, f); fclose(f); }
+    free(iq); free(dst); free(a1);
+    return 0;
+}

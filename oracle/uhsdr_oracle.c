@@ -1,0 +1,447 @@
+/*
+ * ORACLE -- TEST INFRASTRUCTURE ONLY (see uhsdr_oracle.h).  Compile without FP contraction
+ * (-ffp-contract=off, no -march): every float operation below is one IEEE-754 binary32
+ * rounding in the reference's order, so results are bit-identical to the reference firmware
+ * built for x86.
+ *
+ * Processing is per 32-frame call, the ISR granularity of AudioDriver_I2SCallback
+ * (audio_driver.c:2962-3049), because several state updates happen once per call
+ * (auto I/Q statistics, oscillator gain renormalisation).
+ */
+#include <math.h>
+#include <string.h>
+#include <pthread.h>
+#include "uhsdr_oracle.h"
+
+#define BLK UHSDR_IQ_BLOCK_SIZE
+#define IQ_BIT_SCALE_DOWN 0.0000152587890625f   /* audio_driver.h:596 (2^-16) */
+
+size_t uo_rx_state_size(void) { return sizeof(uo_rx_state); }
+
+void uo_rx_state_init(const uhsdr_rx_plan* p, uo_rx_state* s)
+{
+    memset(s, 0, sizeof *s);
+    s->osc_vi = 0.0f;          /* FreqShift_Approx_Prepare, freq_shift.c:48-49 */
+    s->osc_vq = 1.0f;
+    s->out_index = p->agc.out_index0;
+    s->in_index = p->agc.in_index0;
+}
+
+/* ---- CMSIS-DSP f32 kernels, restated (generic code paths; the CM7 unrolled versions
+        accumulate in the same order) ---- */
+
+/* arm_fir_f32.c:482-560: y[n] = sum_k c[k]*s[n+k], acc from 0.0f in tap order.
+   hist holds the T-1 most recent inputs. */
+static void fir(const float* c, int T, float* hist, const float* x, float* y, int n)
+{
+    float st[UHSDR_MAX_FIR_TAPS + BLK];
+    memcpy(st, hist, sizeof(float) * (T - 1));
+    memcpy(st + T - 1, x, sizeof(float) * n);
+    for (int i = 0; i < n; i++)
+    {
+        float acc = 0.0f;
+        for (int k = 0; k < T; k++) acc += st[i + k] * c[k];
+        y[i] = acc;
+    }
+    memcpy(hist, st + n, sizeof(float) * (T - 1));
+}
+
+/* arm_fir_decimate_f32.c:440-518: one output per M inputs, same dot product. */
+static void fir_decimate(const float* c, int T, int M, float* hist, const float* x, float* y, int n)
+{
+    float st[UHSDR_MAX_DEC_TAPS + BLK];
+    memcpy(st, hist, sizeof(float) * (T - 1));
+    memcpy(st + T - 1, x, sizeof(float) * n);
+    for (int m = 0; m < n / M; m++)
+    {
+        float sum = 0.0f;
+        for (int k = 0; k < T; k++) sum += st[m * M + k] * c[k];
+        y[m] = sum;
+    }
+    memcpy(hist, st + n, sizeof(float) * (T - 1));
+}
+
+/* arm_fir_interpolate_f32.c:482-575: polyphase, output j of input m uses phase L-1-j. */
+static void fir_interpolate(const float* c, int L, int P, float* hist, const float* x, float* y, int n)
+{
+    float st[UHSDR_MAX_INTERP + BLK];
+    memcpy(st, hist, sizeof(float) * (P - 1));
+    memcpy(st + P - 1, x, sizeof(float) * n);
+    for (int m = 0; m < n; m++)
+    {
+        for (int i = L; i > 0; i--)
+        {
+            float sum = 0.0f;
+            for (int t = 0; t < P; t++) sum += st[m + t] * c[(i - 1) + t * L];
+            *y++ = sum;
+        }
+    }
+    if (P > 1) memcpy(hist, st + n, sizeof(float) * (P - 1));
+}
+
+/* arm_iir_lattice_f32.c:348-447 (see the state hand-over: stage i of the next sample
+   reads what stage i+1 wrote, the last one reads the final forward value). */
+static void iir_lattice(const float* k, const float* v, int S, float* g, const float* x, float* y, int n)
+{
+    for (int m = 0; m < n; m++)
+    {
+        float fcurr = x[m], fnext = 0.0f, acc = 0.0f;
+        float gn[UHSDR_MAX_LATTICE];
+        for (int i = 0; i < S; i++)
+        {
+            const float gcurr = g[i];
+            fnext = fcurr - (k[i] * gcurr);
+            const float gnext = (fnext * k[i]) + gcurr;
+            acc += (gnext * v[i]);
+            gn[i] = gnext;
+            fcurr = fnext;
+        }
+        acc += (fnext * v[S]);
+        for (int i = 0; i < S - 1; i++) g[i] = gn[i + 1];
+        g[S - 1] = fnext;
+        y[m] = acc;
+    }
+}
+
+/* arm_biquad_cascade_df1_f32.c:349-418, state per stage {x1, x2, y1, y2}. */
+static void biquad_df1(const float* coeffs, int stages, float* st, float* x, int n)
+{
+    for (int s = 0; s < stages; s++)
+    {
+        const float b0 = coeffs[5 * s], b1 = coeffs[5 * s + 1], b2 = coeffs[5 * s + 2];
+        const float a1 = coeffs[5 * s + 3], a2 = coeffs[5 * s + 4];
+        float Xn1 = st[4 * s], Xn2 = st[4 * s + 1], Yn1 = st[4 * s + 2], Yn2 = st[4 * s + 3];
+        for (int i = 0; i < n; i++)
+        {
+            const float Xn = x[i];
+            const float acc = (b0 * Xn) + (b1 * Xn1) + (b2 * Xn2) + (a1 * Yn1) + (a2 * Yn2);
+            x[i] = acc;
+            Xn2 = Xn1; Xn1 = Xn; Yn2 = Yn1; Yn1 = acc;
+        }
+        st[4 * s] = Xn1; st[4 * s + 1] = Xn2; st[4 * s + 2] = Yn1; st[4 * s + 3] = Yn2;
+    }
+}
+
+/* Math_log10f_fast, misc/uhsdr_math.c:26-39 */
+static float log10f_fast(float X)
+{
+    float Y, F;
+    int E;
+    F = frexpf(fabsf(X), &E);
+    Y = 1.23149591368684f;
+    Y *= F;
+    Y += -4.11852516267426f;
+    Y *= F;
+    Y += 6.02197014179219f;
+    Y *= F;
+    Y += -3.13396450166353f;
+    Y += E;
+    return (Y * 0.3010299956639812f);
+}
+
+static float sign_new(float x) { return (x < 0) ? -1.0 : ((x > 0) ? 1.0 : 0.0); }  /* uhsdr_math.c:84-87 */
+
+/* AudioAgc_RunAgcWdsp, audio_agc.c:349-595 (mono) */
+static void agc_run(const uhsdr_agc_plan* a, uo_rx_state* s, float* buf, int n)
+{
+    if (a->mode == 5)
+    {
+        for (int i = 0; i < n; i++) buf[i] = buf[i] * a->fixed_gain;
+        return;
+    }
+    for (int i = 0; i < n; i++)
+    {
+        if (++s->out_index >= a->ring_buffsize) s->out_index -= a->ring_buffsize;
+        if (++s->in_index >= a->ring_buffsize) s->in_index -= a->ring_buffsize;
+        const float out_sample = s->ring[s->out_index];
+        const float abs_out_sample = s->abs_ring[s->out_index];
+        s->ring[s->in_index] = buf[i];
+        s->abs_ring[s->in_index] = fabsf(buf[i]);
+
+        s->fast_backaverage = a->fast_backmult * abs_out_sample + a->onemfast_backmult * s->fast_backaverage;
+        s->hang_backaverage = a->hang_backmult * abs_out_sample + a->onemhang_backmult * s->hang_backaverage;
+
+        if ((abs_out_sample >= s->ring_max) && (abs_out_sample > 0.0))
+        {
+            s->ring_max = 0.0;
+            int k = s->out_index;
+            for (int j = 0; j < a->attack_buffsize; j++)
+            {
+                if (++k == a->ring_buffsize) k = 0;
+                if (s->abs_ring[k] > s->ring_max) s->ring_max = s->abs_ring[k];
+            }
+        }
+        if (s->abs_ring[s->in_index] > s->ring_max) s->ring_max = s->abs_ring[s->in_index];
+
+        if (s->hang_counter > 0) --s->hang_counter;
+
+        switch (s->state)
+        {
+        case 0:
+            if (s->ring_max >= s->volts)
+                s->volts += (s->ring_max - s->volts) * a->attack_mult;
+            else if (s->volts > a->pop_ratio * s->fast_backaverage)
+            {
+                s->state = 1;
+                s->volts += (s->ring_max - s->volts) * a->fast_decay_mult;
+            }
+            else if (a->hang_enable && (s->hang_backaverage > a->hang_level))
+            {
+                s->state = 2;
+                s->hang_counter = a->hang_counter_init;
+                s->decay_type = 1;
+            }
+            else
+            {
+                s->state = 3;
+                s->volts += (s->ring_max - s->volts) * a->decay_mult;
+                s->decay_type = 0;
+            }
+            break;
+        case 1:
+            if (s->ring_max >= s->volts)
+            {
+                s->state = 0;
+                s->volts += (s->ring_max - s->volts) * a->attack_mult;
+            }
+            else if (s->volts > s->save_volts)
+                s->volts += (s->ring_max - s->volts) * a->fast_decay_mult;
+            else if (s->hang_counter > 0)
+                s->state = 2;
+            else if (s->decay_type == 0)
+            {
+                s->state = 3;
+                s->volts += (s->ring_max - s->volts) * a->decay_mult;
+            }
+            else
+            {
+                s->state = 4;
+                s->volts += (s->ring_max - s->volts) * a->hang_decay_mult;
+            }
+            break;
+        case 2:
+            if (s->ring_max >= s->volts)
+            {
+                s->state = 0;
+                s->save_volts = s->volts;
+                s->volts += (s->ring_max - s->volts) * a->attack_mult;
+            }
+            else if (s->hang_counter == 0)
+            {
+                s->state = 4;
+                s->volts += (s->ring_max - s->volts) * a->hang_decay_mult;
+            }
+            break;
+        case 3:
+            if (s->ring_max >= s->volts)
+            {
+                s->state = 0;
+                s->save_volts = s->volts;
+                s->volts += (s->ring_max - s->volts) * a->attack_mult;
+            }
+            else
+                s->volts += (s->ring_max - s->volts) * a->decay_mult;
+            break;
+        case 4:
+            if (s->ring_max >= s->volts)
+            {
+                s->state = 0;
+                s->save_volts = s->volts;
+                s->volts += (s->ring_max - s->volts) * a->attack_mult;
+            }
+            else
+                s->volts += (s->ring_max - s->volts) * a->hang_decay_mult;
+            break;
+        }
+        if (s->volts < a->min_volts) s->volts = a->min_volts;
+
+        float vo = log10f_fast(a->inv_max_input * s->volts);
+        if (vo > 0.0) vo = 0.0;
+        const float mult = (a->out_target - a->slope_constant * vo) / s->volts;
+        buf[i] = out_sample * mult;
+    }
+    if (a->remove_dc)
+    {
+        for (int i = 0; i < n; i++)
+        {
+            const float w = buf[i] + s->wold * 0.9999;
+            buf[i] = w - s->wold;
+            s->wold = w;
+        }
+    }
+}
+
+/* float -> int32 as x86 cvttss2si does it (out of range / NaN -> INT32_MIN), then the
+   firmware's << AUDIO_BIT_SHIFT (audio_driver.c:2911-2923) in two's complement. */
+static int32_t to_dma(float f)
+{
+    int32_t v = (f > -2147483904.0f && f < 2147483648.0f) ? (int32_t)f : INT32_MIN;
+    return (int32_t)((uint32_t)v << 16);
+}
+
+/* one AudioDriver_RxProcessor call on BLK frames, audio_driver.c:2603-2942 */
+static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, float* out_a1, int32_t* dst)
+{
+    float ib[BLK], qb[BLK], a0[BLK], a1[BLK];
+    const int n = BLK;
+    for (int i = 0; i < n; i++)
+    {
+        ib[i] = iq[2 * i];
+        qb[i] = iq[2 * i + 1];
+    }
+    for (int i = 0; i < n; i++) ib[i] = ib[i] * IQ_BIT_SCALE_DOWN;
+    for (int i = 0; i < n; i++) qb[i] = qb[i] * IQ_BIT_SCALE_DOWN;
+
+    /* AudioDriver_RxHandleIqCorrection, audio_driver.c:2254-2316 */
+    if (!p->iq_auto_correction)
+    {
+        for (int i = 0; i < n; i++) ib[i] = ib[i] * p->iq_gain_i;
+        for (int i = 0; i < n; i++) qb[i] = qb[i] * p->iq_gain_q;
+        const float ph = p->iq_phase_balance;       /* AudioDriver_IQPhaseAdjust :1776-1801 */
+        if (ph < 0)
+            for (int i = 0; i < n; i++) { const float e = ib[i] * ph; qb[i] = qb[i] + e; }
+        else if (ph > 0)
+            for (int i = 0; i < n; i++) { const float e = qb[i] * ph; ib[i] = ib[i] + e; }
+    }
+    else
+    {
+        float t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
+        for (int i = 0; i < n; i++)
+        {
+            t1 += sign_new(ib[i]) * qb[i];
+            t2 += sign_new(ib[i]) * ib[i];
+            t3 += sign_new(qb[i]) * qb[i];
+        }
+        t1 = -0.003 * (t1 / n) + 0.997 * s->teta1_old;
+        t2 = 0.003 * (t2 / n) + 0.997 * s->teta2_old;
+        t3 = 0.003 * (t3 / n) + 0.997 * s->teta3_old;
+        const float M_c1 = (t2 != 0.0) ? t1 / t2 : 0.0;
+        float help = (t2 * t2);
+        if (help > 0.0) help = (t3 * t3 - t1 * t1) / help;
+        const float M_c2 = (help > 0.0) ? sqrtf(help) : 1.0;
+        s->teta1_old = t1;
+        s->teta2_old = t2;
+        s->teta3_old = t3;
+        for (int i = 0; i < n; i++) qb[i] += M_c1 * ib[i];
+        for (int i = 0; i < n; i++) ib[i] = ib[i] * M_c2;
+    }
+
+    /* FreqShift, freq_shift.c:275-334 */
+    if (p->freq_shift_hz != 0)
+    {
+        float* ip = p->shift_up ? ib : qb;
+        float* qp = p->shift_up ? qb : ib;
+        if (p->shift_kind == 1)
+        {
+            for (int i = 0; i < n; i += 4)   /* FreqShift_QuarterFs :219-262 */
+            {
+                float h1 = qp[i + 1], h2 = -ip[i + 1];
+                ip[i + 1] = h1; qp[i + 1] = h2;
+                h1 = -ip[i + 2]; h2 = -qp[i + 2];
+                ip[i + 2] = h1; qp[i + 2] = h2;
+                h1 = -qp[i + 3]; h2 = ip[i + 3];
+                ip[i + 3] = h1; qp[i + 3] = h2;
+            }
+        }
+        else
+        {
+            for (int i = 0; i < n; i++)      /* FreqShift_Approx :57-101 */
+            {
+                const float oq = (s->osc_vq * p->osc_cos) - (s->osc_vi * p->osc_sin);
+                const float oi = (s->osc_vi * p->osc_cos) + (s->osc_vq * p->osc_sin);
+                const float qt = qp[i], it = ip[i];
+                qp[i] = (qt * oq) - (it * oi);
+                ip[i] = (it * oq) + (qt * oi);
+                s->osc_vq = oq;
+                s->osc_vi = oi;
+            }
+            const float g = (3 - ((s->osc_vq * s->osc_vq) + (s->osc_vi * s->osc_vi))) / 2;
+            s->osc_vq = g * s->osc_vq;
+            s->osc_vi = g * s->osc_vi;
+        }
+    }
+
+    const int nd = n / p->decimation_rate;
+    const int niq = p->use_decimated_iq ? nd : n;
+    if (p->use_decimated_iq)
+    {
+        fir_decimate(p->dec, p->dec_taps, p->decimation_rate, s->dec_i, ib, ib, n);
+        fir_decimate(p->dec, p->dec_taps, p->decimation_rate, s->dec_q, qb, qb, n);
+    }
+    if (p->hilbert_taps)
+    {
+        fir(p->hilbert_i, p->hilbert_taps, s->hil_i, ib, ib, niq);
+        fir(p->hilbert_q, p->hilbert_taps, s->hil_q, qb, qb, niq);
+    }
+    if (p->lsb)
+        for (int i = 0; i < niq; i++) a0[i] = ib[i] - qb[i];
+    else
+        for (int i = 0; i < niq; i++) a0[i] = ib[i] + qb[i];
+
+    if (!p->use_decimated_iq)
+        fir_decimate(p->dec, p->dec_taps, p->decimation_rate, s->dec_i, a0, a0, niq);
+
+    /* RxProcessor_DemodAudioPostprocessing, audio_driver.c:2436-2592 */
+    if (p->pre_stages > 0) iir_lattice(p->pre_k, p->pre_v, p->pre_stages, s->pre, a0, a0, nd);
+    agc_run(&p->agc, s, a0, nd);
+    for (int i = 0; i < nd; i++) a0[i] = a0[i] * p->post_agc_scale;
+    biquad_df1(p->biquad1, 4, s->bq1, a0, nd);
+    if (p->interp_phase > 0) fir_interpolate(p->interp, p->interp_L, p->interp_phase, s->interp, a0, a1, nd);
+    if (p->aa_stages > 0) iir_lattice(p->aa_k, p->aa_v, p->aa_stages, s->aa, a1, a1, n);
+
+    biquad_df1(p->biquad2, 1, s->bq2, a1, n);          /* audio_driver.c:2832 */
+    for (int i = 0; i < n; i++) a1[i] = a1[i] * p->line_out_scale;   /* :2860 (OVI40) */
+    for (int i = 0; i < n; i++)
+    {
+        out_a1[i] = a1[i];
+        const int32_t d = to_dma(a1[i]);                /* a_buffer[0] is a copy, :2868 */
+        if (dst) { dst[2 * i] = d; dst[2 * i + 1] = d; }
+    }
+}
+
+int uo_rx_process(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, int n, float* a1, int32_t* dst)
+{
+    if (n % BLK) return UHSDR_LENGTH_ERROR;
+    for (int off = 0; off < n; off += BLK)
+        rx_call(p, s, iq + 2 * off, a1 + off, dst ? dst + 2 * off : NULL);
+    return UHSDR_OK;
+}
+
+typedef struct
+{
+    const uhsdr_rx_plan* p;
+    uo_rx_state* states;
+    const int32_t* iq;
+    float* a1;
+    int32_t* dst;
+    int c0, c1, n;
+} uo_job;
+
+static void* uo_worker(void* arg)
+{
+    uo_job* j = (uo_job*)arg;
+    for (int c = j->c0; c < j->c1; c++)
+        uo_rx_process(j->p, &j->states[c], j->iq + (size_t)c * j->n * 2, j->n, j->a1 + (size_t)c * j->n,
+                      j->dst ? j->dst + (size_t)c * j->n * 2 : NULL);
+    return NULL;
+}
+
+int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
+                        float* a1, int32_t* dst, int threads)
+{
+    if (n % BLK) return UHSDR_LENGTH_ERROR;
+    if (threads < 1) threads = 1;
+    if (threads > C) threads = C;
+    pthread_t tid[256];
+    uo_job jobs[256];
+    if (threads > 256) threads = 256;
+    for (int t = 0; t < threads; t++)
+    {
+        jobs[t] = (uo_job){ p, states, iq, a1, dst, (int)((long)C * t / threads), (int)((long)C * (t + 1) / threads), n };
+        if (threads == 1) uo_worker(&jobs[t]);
+        else pthread_create(&tid[t], NULL, uo_worker, &jobs[t]);
+    }
+    if (threads > 1)
+        for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+    return UHSDR_OK;
+}

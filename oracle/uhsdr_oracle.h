@@ -1,0 +1,58 @@
+/*
+ * ORACLE -- TEST INFRASTRUCTURE ONLY.  Never linked into libuhsdr_amd.so; only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg load it (as the checker / the
+ * CPU baseline, never as the thing measured or shipped).
+ *
+ * Clean-room CPU restatement of the reference RX chain (AudioDriver_RxProcessor,
+ * drivers/audio/audio_driver.c:2603-2942, and the CMSIS-DSP V1.4.5 f32 kernels under it),
+ * one state struct per channel, driven by the same uhsdr_rx_plan the device consumes.
+ * Pinned bit-for-bit against the reference firmware compiled for x86 (oracle/ref/,
+ * fixtures tests/golden/rx_*.npz) by tests/test_oracle.py.
+ */
+#ifndef UHSDR_ORACLE_H
+#define UHSDR_ORACLE_H
+
+#include <stdint.h>
+#include <stddef.h>
+#include "../include/uhsdr.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct uo_rx_state
+{
+    /* adb.iq_corr (audio_driver.h:125-135) */
+    float teta1_old, teta2_old, teta3_old;
+    /* FreqShift_Approx oscillator (freq_shift.c:22-27) */
+    float osc_vi, osc_vq;
+    /* CMSIS state arrays: history part only (the numTaps-1 / numStages values that
+       survive a call, arm_fir_f32.c:565-580) */
+    float hil_i[UHSDR_MAX_FIR_TAPS];
+    float hil_q[UHSDR_MAX_FIR_TAPS];
+    float dec_i[UHSDR_MAX_DEC_TAPS];
+    float dec_q[UHSDR_MAX_DEC_TAPS];
+    float pre[UHSDR_MAX_LATTICE + 1];
+    float aa[UHSDR_MAX_LATTICE + 1];
+    float bq1[16];
+    float bq2[4];
+    float interp[UHSDR_MAX_INTERP];
+    /* agc_wdsp run-time variables (audio_agc.c:24-94) */
+    float ring[UHSDR_AGC_RING];
+    float abs_ring[UHSDR_AGC_RING];
+    int32_t out_index, in_index, hang_counter, decay_type, state;
+    float ring_max, volts, save_volts, fast_backaverage, hang_backaverage, wold;
+} uo_rx_state;
+
+size_t uo_rx_state_size(void);
+void uo_rx_state_init(const uhsdr_rx_plan* p, uo_rx_state* s);
+/* one channel, n frames (n % 32 == 0): iq [n][2] int32 -> a1 [n] f32, dst [n][2] int32 */
+int uo_rx_process(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, int n, float* a1, int32_t* dst);
+/* C channels, channel-major buffers, `threads` POSIX threads (0 = 1) */
+int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
+                        float* a1, int32_t* dst, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

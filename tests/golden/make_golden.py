@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Generate the golden RX-chain fixtures from the reference firmware itself.
+
+Runs ``oracle/_ref/uhsdr_ref`` -- the reference's own audio_driver.c / audio_agc.c /
+freq_shift.c / CMSIS-DSP compiled for x86 by ``oracle/ref/Makefile`` -- once per channel
+(one process per channel: the firmware keeps DSP state in globals/statics) and stores
+
+    tests/golden/rx_<name>.npz
+        iq      int32 [C, N, 2]   IqSample_t frames fed to AudioDriver_I2SCallback
+        a1      f32   [C, N]      adb.a_buffer[1] after every 32-frame call
+        dst     int32 [C, N, 2]   AudioSample_t frames the driver wrote for the codec
+        setup   json             configured chain, coefficient bits (dump=setup)
+        agc     json             AudioAgc_SetupAgcWdsp parameter block bits (dump=agc)
+        args    json             the uhsdr_ref key=value configuration
+
+plus tests/golden/filter_paths.json (FilterPathInfo[], audio_filter.c:147-922, as raw
+float bits).  Only runs where /root/reference exists (build container); the fixtures
+are committed and the GPU box never needs the reference.
+
+    python tests/golden/make_golden.py [--only NAME]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from uhsdr_amd import synth  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref", "uhsdr_ref")
+NCH = 4
+NFRAMES = 2048
+
+# name -> (uhsdr_ref args, signal kwargs)
+CONFIGS = {
+    "p48_usb": ({"mode": 0, "path": 48}, {}),
+    "p48_lsb": ({"mode": 1, "path": 48}, {"lsb": True}),
+    "p48_c1": ({"mode": 0, "path": 48}, {"kind": "c1"}),
+    "p35_usb": ({"mode": 0, "path": 35}, {}),
+    "p55_usb": ({"mode": 0, "path": 55}, {}),
+    "p61_usb": ({"mode": 0, "path": 61}, {}),
+    "p44_usb": ({"mode": 0, "path": 44}, {}),
+    "p4_cw": ({"mode": 2, "path": 4}, {}),
+    "p48_iqauto": ({"mode": 0, "path": 48, "iq_auto": 1}, {}),
+    "p48_iqman": ({"mode": 0, "path": 48, "gain_i": 1.03125, "gain_q": 0.96875, "phase": -0.0125}, {}),
+    "p48_iqman2": ({"mode": 0, "path": 48, "gain_i": 0.98, "gain_q": 1.01, "phase": 0.02}, {}),
+    "p48_eq": ({"mode": 0, "path": 48, "dsp": 0x30, "bass": -6, "treble": 4, "notch": 1200, "peak": 900}, {}),
+    "p48_agcoff": ({"mode": 0, "path": 48, "agc_mode": 5}, {}),
+    "p48_agcfast": ({"mode": 0, "path": 48, "agc_mode": 4, "agc_thresh": 40, "agc_slope": 30}, {}),
+    "p48_agchang": ({"mode": 0, "path": 48, "agc_mode": 1, "agc_hang": 1}, {}),
+    "p48_agcfrank": ({"mode": 0, "path": 48, "agc_mode": 0}, {}),
+    "p48_p12k": ({"mode": 0, "path": 48, "iqmode": 3}, {"center": -12000.0}),
+    "p48_m6k": ({"mode": 0, "path": 48, "iqmode": 2}, {"center": 6000.0}),
+    "p48_p6k": ({"mode": 0, "path": 48, "iqmode": 1}, {"center": -6000.0}),
+    "p48_off": ({"mode": 0, "path": 48, "iqmode": 0}, {"center": 0.0}),
+}
+
+
+def run_ref(args: dict, iq: np.ndarray):
+    n = iq.shape[0]
+    with tempfile.TemporaryDirectory() as td:
+        fin, fa, fd = (os.path.join(td, x) for x in ("in.bin", "a.bin", "d.bin"))
+        iq.astype(np.int32).tofile(fin)
+        cmd = [REF, f"in={fin}", f"n={n}", f"out_a={fa}", f"out_dst={fd}"]
+        cmd += [f"{k}={v}" for k, v in args.items()]
+        subprocess.run(cmd, check=True)
+        a1 = np.fromfile(fa, dtype=np.float32)
+        dst = np.fromfile(fd, dtype=np.int32).reshape(n, 2)
+    return a1, dst
+
+
+def ref_json(args: dict, what: str):
+    cmd = [REF, f"dump={what}"] + [f"{k}={v}" for k, v in args.items()]
+    return json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True).stdout)
+
+
+def make(name: str):
+    args, sig = CONFIGS[name]
+    sig = dict(sig)
+    center = sig.pop("center", None)
+    iq = synth.ssb_iq(np.arange(NCH), 0, NFRAMES, carrier=center if center is not None else 12000.0, **sig)
+    a1 = np.empty((NCH, NFRAMES), np.float32)
+    dst = np.empty((NCH, NFRAMES, 2), np.int32)
+    for c in range(NCH):
+        a1[c], dst[c] = run_ref(args, iq[c])
+    np.savez_compressed(os.path.join(HERE, f"rx_{name}.npz"), iq=iq, a1=a1, dst=dst,
+                        setup=json.dumps(ref_json(args, "setup")), agc=json.dumps(ref_json(args, "agc")),
+                        args=json.dumps(args))
+    peak = float(np.abs(a1).max())
+    print(f"{name:14s} peak|a1|={peak:9.1f}  rms={float(np.sqrt((a1.astype(np.float64)**2).mean())):9.1f}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    if not os.path.exists(REF):
+        sys.exit(f"{REF} missing: run `make -C oracle/ref` (needs /root/reference)")
+    paths = subprocess.run([REF, "dump=paths"], check=True, capture_output=True, text=True).stdout
+    with open(os.path.join(HERE, "filter_paths.json"), "w") as f:
+        json.dump(json.loads(paths), f, separators=(",", ":"))
+    for name in CONFIGS:
+        if a.only and name != a.only:
+            continue
+        make(name)
+
+
+if __name__ == "__main__":
+    main()

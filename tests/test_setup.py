@@ -1,0 +1,53 @@
+"""The product's host setup layer (uhsdr_rx_plan_build, uhsdr_amd/csrc/uhsdr_setup.c) reproduces
+what AudioDriver_SetProcessingChain / AudioAgc_SetupAgcWdsp leave in the firmware, bit for bit
+(dumps of the reference build stored with every golden fixture)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import uhsdr_amd as U
+from golden_util import golden_files, load
+
+
+def fbits(arr, n=None):
+    a = np.frombuffer(bytes(arr), dtype=np.uint32)
+    return a if n is None else a[:n]
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("rx_")[-1][:-4])
+def test_plan_matches_reference_setup(path):
+    g = load(path)
+    s, agc = g["setup"], g["agc"]
+    p = U.build_plan(U.config_from_ref_args(g["args"]))
+    assert p.filter_path == s["filter_path"]
+    assert p.decimation_rate == s["decimation_rate"] and p.decimated_freq == s["decimated_freq"]
+    assert p.hilbert_taps == s["hilbert_taps"] and p.dec_taps == s["decim_taps"]
+    assert p.pre_stages == s["pre_stages"] and p.aa_stages == s["aa_stages"]
+    assert p.interp_L == s["interp_L"] and p.interp_phase == s["interp_phase"]
+    for field, key, n in [("biquad1", "biquad1", 20), ("biquad2", "biquad2", 5),
+                          ("hilbert_i", "hilbert_i", p.hilbert_taps), ("hilbert_q", "hilbert_q", p.hilbert_taps),
+                          ("dec", "decim", p.dec_taps), ("pre_k", "pre_k", p.pre_stages),
+                          ("pre_v", "pre_v", p.pre_stages + 1 if p.pre_stages else 0),
+                          ("aa_k", "aa_k", p.aa_stages), ("aa_v", "aa_v", p.aa_stages + 1 if p.aa_stages else 0),
+                          ("interp", "interp", p.interp_L * p.interp_phase)]:
+        np.testing.assert_array_equal(fbits(getattr(p, field), n), np.array(s[key], dtype=np.uint32), err_msg=field)
+    a = p.agc
+    assert a.attack_buffsize == agc["attack_buffsize"] and a.ring_buffsize == agc["ring_buffsize"]
+    assert a.in_index0 == agc["in_index"] and a.out_index0 == agc["out_index"]
+    assert a.remove_dc == agc["remove_dc"] and a.mode == agc["mode"] and a.hang_enable == agc["hang_enable"]
+    for f in ["fixed_gain", "attack_mult", "decay_mult", "fast_decay_mult", "fast_backmult", "onemfast_backmult",
+              "hang_backmult", "onemhang_backmult", "hang_decay_mult", "pop_ratio", "hang_level", "min_volts",
+              "inv_max_input", "out_target", "slope_constant", "hangtime", "hang_thresh", "var_gain", "max_gain",
+              "inv_out_target", "sample_rate"]:
+        mine = np.array([getattr(a, f)], dtype=np.float32).view(np.uint32)[0]
+        assert mine == agc[f], f"agc.{f}: {getattr(a, f)!r}"
+
+
+def test_plan_rejects_bad_config():
+    lib = U.load()
+    plan = U.RxPlan()
+    for over in [dict(filter_path=0), dict(filter_path=87), dict(dmod_mode=9),
+                 dict(filter_path=1)]:   # FM-only path for USB
+        cfg = U.default_config(**over)
+        assert lib.uhsdr_rx_plan_build(C.byref(cfg), C.byref(plan)) == -1, over

@@ -1,0 +1,8 @@
+"""uhsdr_amd -- MI355X (gfx950) batched implementation of the UHSDR per-block RX DSP chain.
+
+The product is ``uhsdr_amd/lib/libuhsdr_amd.so`` (C ABI: ``include/uhsdr.h``).  This
+package is the thin host-side mirror used by tests and the benchmark.
+"""
+from ._abi import (RxConfig, RxPlan, build_plan, config_from_ref_args, default_config, load,  # noqa: F401
+                   DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI)
+from .rx import RxChain  # noqa: F401

@@ -1,0 +1,152 @@
+"""ctypes view of include/uhsdr.h (the C ABI of libuhsdr_amd.so).
+
+Python is only the test / benchmark driver here: every call below crosses the same C ABI
+that firmware-side C code links against.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libuhsdr_amd.so")
+
+MAX_FIR_TAPS = 200
+MAX_DEC_TAPS = 96
+MAX_LATTICE = 10
+MAX_INTERP = 16
+IQ_BLOCK_SIZE = 32
+FILTER_PATH_NUM = 87
+
+UHSDR_OK = 0
+UHSDR_ARGUMENT_ERROR = -1
+UHSDR_LENGTH_ERROR = -2
+UHSDR_UNSUPPORTED = -10
+UHSDR_DEVICE_ERROR = -11
+
+DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI = range(7)
+
+
+class RxConfig(C.Structure):
+    _fields_ = [
+        ("dmod_mode", C.c_int32), ("filter_path", C.c_int32), ("iq_freq_mode", C.c_int32),
+        ("iq_auto_correction", C.c_int32), ("iq_gain_i", C.c_float), ("iq_gain_q", C.c_float),
+        ("iq_phase_balance", C.c_float), ("dsp_active", C.c_int32), ("notch_frequency", C.c_int32),
+        ("peak_frequency", C.c_int32), ("bass_gain", C.c_int32), ("treble_gain", C.c_int32),
+        ("cw_lsb", C.c_int32), ("digi_lsb", C.c_int32), ("agc_mode", C.c_int32), ("agc_slope", C.c_int32),
+        ("agc_thresh", C.c_int32), ("agc_hang_enable", C.c_int32), ("agc_hang_time", C.c_int32),
+        ("agc_hang_thresh", C.c_int32), ("agc_tau_decay", C.c_int32 * 6), ("agc_tau_hang_decay", C.c_int32),
+        ("reserved", C.c_int32 * 16),
+    ]
+
+
+_AGC_INT = ["mode", "hang_enable", "remove_dc", "ring_buffsize", "attack_buffsize", "out_index0",
+            "in_index0", "hang_counter_init"]
+_AGC_FLT = ["sample_rate", "fixed_gain", "attack_mult", "decay_mult", "fast_decay_mult", "fast_backmult",
+            "onemfast_backmult", "hang_backmult", "onemhang_backmult", "hang_decay_mult", "pop_ratio",
+            "hang_level", "min_volts", "inv_max_input", "out_target", "slope_constant", "hangtime",
+            "hang_thresh", "var_gain", "max_gain", "inv_out_target"]
+
+
+class AgcPlan(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in _AGC_INT] + [(n, C.c_float) for n in _AGC_FLT]
+
+
+class RxPlan(C.Structure):
+    _fields_ = [
+        ("dmod_mode", C.c_int32), ("filter_path", C.c_int32), ("lsb", C.c_int32),
+        ("decimation_rate", C.c_int32), ("decimated_freq", C.c_int32), ("use_decimated_iq", C.c_int32),
+        ("iq_auto_correction", C.c_int32), ("iq_gain_i", C.c_float), ("iq_gain_q", C.c_float),
+        ("iq_phase_balance", C.c_float), ("freq_shift_hz", C.c_int32), ("shift_kind", C.c_int32),
+        ("shift_up", C.c_int32), ("osc_cos", C.c_float), ("osc_sin", C.c_float),
+        ("hilbert_taps", C.c_int32), ("hilbert_i", C.c_float * MAX_FIR_TAPS), ("hilbert_q", C.c_float * MAX_FIR_TAPS),
+        ("dec_taps", C.c_int32), ("dec", C.c_float * MAX_DEC_TAPS),
+        ("pre_stages", C.c_int32), ("pre_k", C.c_float * MAX_LATTICE), ("pre_v", C.c_float * (MAX_LATTICE + 1)),
+        ("interp_L", C.c_int32), ("interp_phase", C.c_int32), ("interp", C.c_float * MAX_INTERP),
+        ("aa_stages", C.c_int32), ("aa_k", C.c_float * MAX_LATTICE), ("aa_v", C.c_float * (MAX_LATTICE + 1)),
+        ("biquad1", C.c_float * 20), ("biquad2", C.c_float * 5),
+        ("post_agc_scale", C.c_float), ("line_out_scale", C.c_float),
+        ("agc", AgcPlan), ("reserved", C.c_int32 * 64),
+    ]
+
+
+# every exported entry point of include/uhsdr.h: name -> (restype, argtypes)
+SIGNATURES = {
+    "uhsdr_rx_config_default": (None, [C.POINTER(RxConfig)]),
+    "uhsdr_rx_plan_build": (C.c_int, [C.POINTER(RxConfig), C.POINTER(RxPlan)]),
+    "uhsdr_rx_plan_supported": (C.c_int, [C.POINTER(RxPlan)]),
+    "uhsdr_rx_create": (C.c_int, [C.POINTER(RxConfig), C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]),
+    "uhsdr_rx_reset": (C.c_int, [C.c_void_p]),
+    "uhsdr_rx_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "uhsdr_rx_process_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "uhsdr_rx_get_plan": (C.c_int, [C.c_void_p, C.POINTER(RxPlan)]),
+    "uhsdr_rx_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "uhsdr_rx_destroy": (C.c_int, [C.c_void_p]),
+    "uhsdr_version": (C.c_char_p, []),
+    "uhsdr_last_error": (C.c_char_p, []),
+    "uhsdr_sizeof_config": (C.c_int32, []),
+    "uhsdr_sizeof_plan": (C.c_int32, []),
+    "uhsdr_rx_kernel_count": (C.c_int32, [C.c_void_p]),
+    "uhsdr_rx_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_rx_kernel_times": (C.c_int32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int32), C.c_int32]),
+    "uhsdr_rx_kernel_name": (C.c_char_p, [C.c_int32]),
+}
+
+_lib = None
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load libuhsdr_amd.so (built in-tree by `make`); raises if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"{p} not built: run `make` (or __graft_entry__.build())")
+    lib = C.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.uhsdr_sizeof_config() != C.sizeof(RxConfig) or lib.uhsdr_sizeof_plan() != C.sizeof(RxPlan):
+        raise RuntimeError("ctypes layout of uhsdr_rx_config / uhsdr_rx_plan does not match include/uhsdr.h")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status != UHSDR_OK:
+        err = load().uhsdr_last_error().decode()
+        raise RuntimeError(f"{what} failed with status {status}: {err}")
+
+
+def default_config(**overrides) -> RxConfig:
+    cfg = RxConfig()
+    load().uhsdr_rx_config_default(C.byref(cfg))
+    for k, v in overrides.items():
+        if k == "agc_tau_decay":
+            for i, x in enumerate(v):
+                cfg.agc_tau_decay[i] = x
+        else:
+            setattr(cfg, k, v)
+    return cfg
+
+
+def build_plan(cfg: RxConfig) -> RxPlan:
+    plan = RxPlan()
+    check(load().uhsdr_rx_plan_build(C.byref(cfg), C.byref(plan)), "uhsdr_rx_plan_build")
+    return plan
+
+
+# uhsdr_ref key=value names (tests/golden) -> RxConfig fields
+REF_ARG_MAP = {
+    "mode": "dmod_mode", "path": "filter_path", "iqmode": "iq_freq_mode", "iq_auto": "iq_auto_correction",
+    "gain_i": "iq_gain_i", "gain_q": "iq_gain_q", "phase": "iq_phase_balance", "dsp": "dsp_active",
+    "notch": "notch_frequency", "peak": "peak_frequency", "bass": "bass_gain", "treble": "treble_gain",
+    "agc_mode": "agc_mode", "agc_thresh": "agc_thresh", "agc_slope": "agc_slope", "agc_hang": "agc_hang_enable",
+}
+
+
+def config_from_ref_args(args: dict) -> RxConfig:
+    return default_config(**{REF_ARG_MAP[k]: v for k, v in args.items()})

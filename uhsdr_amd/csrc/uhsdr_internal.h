@@ -1,0 +1,43 @@
+/*
+ * Internal declarations shared by the host setup layer and the device runtime.
+ */
+#ifndef UHSDR_INTERNAL_H
+#define UHSDR_INTERNAL_H
+
+#include <stdint.h>
+#include "../../include/uhsdr.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One FilterPathDescriptor (drivers/audio/audio_filter.h:108-136), tables as raw bits. */
+typedef struct
+{
+    uint8_t id;                 /* FilterInfo index (bandwidth) */
+    uint16_t mode;              /* FILTER_MASK_* of applicable filter modes */
+    uint8_t sample_rate_dec;    /* RX_DECIMATION_RATE_{12,24,48}KHZ == 4, 2, 1 */
+    uint16_t fir_taps;
+    const uint32_t* fir_i;
+    const uint32_t* fir_q;
+    uint16_t dec_taps;
+    const uint32_t* dec;
+    uint16_t pre_stages;
+    const uint32_t* pre_k;
+    const uint32_t* pre_v;
+    uint16_t interp_taps;       /* the descriptor's `phaseLength` field, really numTaps */
+    const uint32_t* interp;
+    uint16_t aa_stages;
+    const uint32_t* aa_k;
+    const uint32_t* aa_v;
+} uhsdr_filter_path_desc;
+
+extern const uhsdr_filter_path_desc uhsdr_filter_paths[UHSDR_FILTER_PATH_NUM];
+
+/* thread-local last error text for uhsdr_last_error() */
+void uhsdr_set_error(const char* fmt, ...);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,382 @@
+/*
+ * Host setup layer: builds a uhsdr_rx_plan exactly as the firmware configures its RX chain.
+ *
+ * Restates (behaviour, types and evaluation order -- this file must be compiled without
+ * FP contraction, like the reference, so every rounding matches):
+ *   AudioDriver_SetProcessingChain       drivers/audio/audio_driver.c:1093-1251
+ *   AudioDriver_SetRxTxAudioProcessingAudioFilters  audio_driver.c:994-1050
+ *   AudioDriver_CalcBandstop/Bandpass/HighShelf/LowShelf  audio_driver.c:831-964
+ *   AudioFilter_SetRxHilbertAndDecimationFIR  drivers/audio/audio_filter.c:1134-1223
+ *   AudioAgc_AgcWdsp_Init / AudioAgc_SetupAgcWdsp  drivers/audio/audio_agc.c:104-339
+ *   FreqShift front end / FreqShift_Approx_Prepare  drivers/audio/freq_shift.c:40-52, 275-334
+ *   AudioDriver_GetTranslateFreq          audio_driver.c:445-464
+ *   RadioManagement_LSBActive             drivers/ui/radio_management.c:1665-1692
+ * The reference's pow10f is glibc's exp10f (identical results; pow10f was only an alias).
+ * Parity of every field is pinned against the reference build by tests/test_setup.py.
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <string.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include "uhsdr_internal.h"
+
+#define CMSIS_PI 3.14159265358979f          /* CMSIS/Include/arm_math.h:334 */
+#define AUDIO_SAMPLE_RATE 48000             /* hardware/uhsdr_board_config.h:208 */
+#define IQ_SAMPLE_RATE 48000
+#define ADC_CLIP_WARN_THRESHOLD 4096        /* audio_driver.h:81 */
+#define POST_AGC_GAIN_SCALING_DECIMATE_4 3.46                               /* audio_driver.h:362 */
+#define POST_AGC_GAIN_SCALING_DECIMATE_2 (POST_AGC_GAIN_SCALING_DECIMATE_4 * 0.6) /* :364 */
+#define LINE_OUT_SCALING_FACTOR 10          /* audio_driver.h:396 */
+#define FILTER_MODE_CW 0
+#define FILTER_MODE_SSB 1
+#define FILTER_MODE_AM 2
+#define FILTER_MODE_FM 3
+
+static __thread char g_err[256];
+void uhsdr_set_error(const char* fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+const char* uhsdr_last_error(void) { return g_err; }
+
+static float fbits(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static void copy_bits(float* dst, const uint32_t* src, int n)
+{
+    for (int i = 0; i < n; i++) dst[i] = fbits(src[i]);
+}
+
+void uhsdr_rx_config_default(uhsdr_rx_config* c)
+{
+    memset(c, 0, sizeof *c);
+    c->dmod_mode = UHSDR_DEMOD_USB;
+    c->filter_path = 48;                       /* "3.8k LPF" SSB path */
+    c->iq_freq_mode = UHSDR_IQ_CONV_M12KHZ;    /* FREQ_IQ_CONV_MODE_DEFAULT */
+    c->iq_auto_correction = 0;
+    c->iq_gain_i = 1.0f;
+    c->iq_gain_q = 1.0f;
+    c->iq_phase_balance = 0.0f;
+    c->notch_frequency = 800;
+    c->peak_frequency = 750;
+    c->bass_gain = 2;
+    c->treble_gain = 0;
+    c->agc_mode = 2;
+    c->agc_slope = 70;
+    c->agc_thresh = 20;
+    c->agc_hang_enable = 0;
+    c->agc_hang_time = 500;                    /* AudioAgc_AgcWdsp_Init, audio_agc.c:116-121 */
+    c->agc_hang_thresh = 45;
+    c->agc_tau_decay[0] = 4000;
+    c->agc_tau_decay[1] = 2000;
+    c->agc_tau_decay[2] = 500;
+    c->agc_tau_decay[3] = 250;
+    c->agc_tau_decay[4] = 50;
+    c->agc_tau_decay[5] = 1;
+    c->agc_tau_hang_decay = 500;
+}
+
+/* AudioFilter_GetFilterModeFromDemodMode, audio_filter.c:929-955 */
+static int filter_mode_of(int dmod)
+{
+    switch (dmod)
+    {
+    case UHSDR_DEMOD_AM: return FILTER_MODE_AM;
+    case UHSDR_DEMOD_FM: return FILTER_MODE_FM;
+    case UHSDR_DEMOD_CW: return FILTER_MODE_CW;
+    case UHSDR_DEMOD_SAM: return FILTER_MODE_AM;
+    default: return FILTER_MODE_SSB;
+    }
+}
+
+/* ---- biquad designers, audio_driver.c:821-964 (B0..A2 = 0..4) ---- */
+static void scale_biquad(float c[5], const float scalingA, const float scalingB)
+{
+    c[3] = c[3] / scalingA;
+    c[4] = c[4] / scalingA;
+    c[0] = c[0] / scalingB;
+    c[1] = c[1] / scalingB;
+    c[2] = c[2] / scalingB;
+}
+
+static void calc_bandstop(float c[5], float f0, float FS)
+{
+    float Q = 10;
+    float w0 = 2 * CMSIS_PI * f0 / FS;
+    float alpha = sinf(w0) / (2 * Q);
+    c[0] = 1;
+    c[1] = -2 * cosf(w0);
+    c[2] = 1;
+    float scaling = 1 + alpha;
+    c[3] = 2 * cosf(w0);
+    c[4] = alpha - 1;
+    scale_biquad(c, scaling, scaling);
+}
+
+static void calc_bandpass(float c[5], float f0, float FS)
+{
+    float Q = 4;
+    float BW = 0.03;
+    float w0 = 2 * CMSIS_PI * f0 / FS;
+    float alpha = sinf(w0) * sinhf(log(2) / 2 * BW * w0 / sinf(w0));
+    c[0] = Q * alpha;
+    c[1] = 0;
+    c[2] = -Q * alpha;
+    float scaling = 1 + alpha;
+    c[3] = 2 * cosf(w0);
+    c[4] = alpha - 1;
+    scale_biquad(c, scaling, scaling);
+}
+
+static void calc_highshelf(float c[5], float f0, float S, float gain, float FS)
+{
+    float w0 = 2 * CMSIS_PI * f0 / FS;
+    float A = exp10f(gain / 40.0);
+    float alpha = sinf(w0) / 2 * sqrtf((A + 1 / A) * (1 / S - 1) + 2);
+    float cosw0 = cosf(w0);
+    float twoAa = 2 * sqrtf(A) * alpha;
+    c[0] = A * ((A + 1) + (A - 1) * cosw0 + twoAa);
+    c[1] = -2 * A * ((A - 1) + (A + 1) * cosw0);
+    c[2] = A * ((A + 1) + (A - 1) * cosw0 - twoAa);
+    float scaling = (A + 1) - (A - 1) * cosw0 + twoAa;
+    c[3] = -2 * ((A - 1) - (A + 1) * cosw0);
+    c[4] = twoAa - (A + 1) + (A - 1) * cosw0;
+    float DCgain = 1.0 * scaling;
+    scale_biquad(c, scaling, DCgain);
+}
+
+static void calc_lowshelf(float c[5], float f0, float S, float gain, float FS)
+{
+    float w0 = 2 * CMSIS_PI * f0 / FS;
+    float A = exp10f(gain / 40.0);
+    float alpha = sinf(w0) / 2 * sqrtf((A + 1 / A) * (1 / S - 1) + 2);
+    float cosw0 = cosf(w0);
+    float twoAa = 2 * sqrtf(A) * alpha;
+    c[0] = A * ((A + 1) - (A - 1) * cosw0 + twoAa);
+    c[1] = 2 * A * ((A - 1) - (A + 1) * cosw0);
+    c[2] = A * ((A + 1) - (A - 1) * cosw0 - twoAa);
+    float scaling = (A + 1) + (A - 1) * cosw0 + twoAa;
+    c[3] = 2 * ((A - 1) + (A + 1) * cosw0);
+    c[4] = twoAa - (A + 1) - (A - 1) * cosw0;
+    float DCgain = 1.0 * scaling;
+    scale_biquad(c, scaling, DCgain);
+}
+
+static const float biquad_passthrough[5] = { 1, 0, 0, 0, 0 };
+
+/* ---- AGC parameter math, audio_agc.c:126-339 (fresh channel: first setup after Init) ---- */
+static void setup_agc(uhsdr_agc_plan* a, const uhsdr_rx_config* cfg, float sample_rate, int remove_dc)
+{
+    memset(a, 0, sizeof *a);
+    a->remove_dc = remove_dc;
+    a->mode = cfg->agc_mode;
+    a->hang_enable = cfg->agc_hang_enable;
+    a->sample_rate = sample_rate;
+    /* one-time initialisation (:176-223) */
+    a->ring_buffsize = UHSDR_AGC_RING;
+    a->out_index0 = -1;
+    float tau_attack = 0.001;
+    int n_tau = 4;
+    float max_input = (float)ADC_CLIP_WARN_THRESHOLD;
+    float out_targ = (float)ADC_CLIP_WARN_THRESHOLD;
+    float tau_fast_backaverage = 0.250;
+    float tau_fast_decay = 0.005;
+    a->pop_ratio = 5.0;
+    float tau_hang_backmult = 0.500;
+
+    a->var_gain = exp10f((float)cfg->agc_slope / 20.0 / 10.0);
+    a->hangtime = (float)cfg->agc_hang_time / 1000.0;
+    /* switch_mode == 1 on the first setup after AudioAgc_AgcWdsp_Init (:232-275) */
+    switch (cfg->agc_mode)
+    {
+    case 5: break;
+    case 1: a->hangtime = 2.000; break;
+    case 2: a->hangtime = 1.000; break;
+    case 3: a->hangtime = 0.250; break;
+    case 4: a->hangtime = 0.100; break;
+    case 0:
+        a->hangtime = 3.000;
+        tau_hang_backmult = 0.500;
+        tau_fast_decay = 0.05;
+        tau_fast_backaverage = 0.250;
+        break;
+    default: break;
+    }
+    float tau_hang_decay = (float)cfg->agc_tau_hang_decay / 1000.0;
+    int dm = cfg->agc_mode;
+    if (dm < 0) dm = 0;
+    if (dm > 5) dm = 5;
+    float tau_decay = (float)cfg->agc_tau_decay[dm] / 1000.0;
+    a->max_gain = exp10f((float)cfg->agc_thresh / 20.0);
+    a->fixed_gain = a->max_gain / 10.0;
+    a->attack_buffsize = ceilf(sample_rate * n_tau * tau_attack);
+    a->in_index0 = a->attack_buffsize + a->out_index0;
+    a->in_index0 %= a->ring_buffsize;
+
+    a->attack_mult = 1.0 - expf(-1.0 / (sample_rate * tau_attack));
+    a->decay_mult = 1.0 - expf(-1.0 / (sample_rate * tau_decay));
+    a->fast_decay_mult = 1.0 - expf(-1.0 / (sample_rate * tau_fast_decay));
+    a->fast_backmult = 1.0 - expf(-1.0 / (sample_rate * tau_fast_backaverage));
+    a->onemfast_backmult = 1.0 - a->fast_backmult;
+
+    a->out_target = out_targ * (1.0 - expf(-(float)n_tau)) * 0.9999;
+    a->min_volts = a->out_target / (a->var_gain * a->max_gain);
+    a->inv_out_target = 1.0 / a->out_target;
+
+    float tmpA = log10f(a->out_target / (max_input * a->var_gain * a->max_gain));
+    if (tmpA == 0.0)
+    {
+        tmpA = 1e-16;
+    }
+    a->slope_constant = (a->out_target * (1.0 - 1.0 / a->var_gain)) / tmpA;
+    a->inv_max_input = 1.0 / max_input;
+
+    if (max_input > a->min_volts)
+    {
+        float convert = exp10f((float)cfg->agc_hang_thresh / 20.0);
+        float tmpB = (convert - a->min_volts) / (max_input - a->min_volts);
+        if (tmpB < 1e-8)
+        {
+            tmpB = 1e-8;
+        }
+        a->hang_thresh = 1.0 + 0.125 * log10f(tmpB);
+    }
+    else
+    {
+        a->hang_thresh = 1.0;
+    }
+    float tmpC = exp10f((a->hang_thresh - 1.0) / 0.125);
+    a->hang_level = (max_input * tmpC + (a->out_target / (a->var_gain * a->max_gain)) * (1.0 - tmpC)) * 0.637;
+    a->hang_backmult = 1.0 - expf(-1.0 / (sample_rate * tau_hang_backmult));
+    a->onemhang_backmult = 1.0 - a->hang_backmult;
+    a->hang_decay_mult = 1.0 - expf(-1.0 / (sample_rate * tau_hang_decay));
+    a->hang_counter_init = (int)(a->hangtime * a->sample_rate);   /* audio_agc.c:469 */
+}
+
+uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
+{
+    if (!cfg || !p) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
+    if (cfg->filter_path <= 0 || cfg->filter_path >= UHSDR_FILTER_PATH_NUM)
+    {
+        uhsdr_set_error("filter_path %d out of range 1..%d", cfg->filter_path, UHSDR_FILTER_PATH_NUM - 1);
+        return UHSDR_ARGUMENT_ERROR;
+    }
+    if (cfg->dmod_mode < UHSDR_DEMOD_USB || cfg->dmod_mode > UHSDR_DEMOD_DIGI)
+    {
+        uhsdr_set_error("dmod_mode %d unknown", cfg->dmod_mode);
+        return UHSDR_ARGUMENT_ERROR;
+    }
+    const uhsdr_filter_path_desc* f = &uhsdr_filter_paths[cfg->filter_path];
+    if ((f->mode & (1u << filter_mode_of(cfg->dmod_mode))) == 0)
+    {
+        /* the firmware only ever selects applicable paths (audio_filter.c:975-1011) */
+        uhsdr_set_error("filter_path %d not applicable to dmod_mode %d", cfg->filter_path, cfg->dmod_mode);
+        return UHSDR_ARGUMENT_ERROR;
+    }
+    memset(p, 0, sizeof *p);
+    const int mode = cfg->dmod_mode;
+    p->dmod_mode = mode;
+    p->filter_path = cfg->filter_path;
+    switch (mode)
+    {
+    case UHSDR_DEMOD_LSB: p->lsb = 1; break;
+    case UHSDR_DEMOD_CW: p->lsb = cfg->cw_lsb != 0; break;
+    case UHSDR_DEMOD_DIGI: p->lsb = cfg->digi_lsb != 0; break;
+    default: p->lsb = 0; break;
+    }
+    p->decimation_rate = f->sample_rate_dec;
+    p->decimated_freq = IQ_SAMPLE_RATE / f->sample_rate_dec;
+
+    /* input stage */
+    p->iq_auto_correction = cfg->iq_auto_correction != 0;
+    p->iq_gain_i = cfg->iq_gain_i;
+    p->iq_gain_q = cfg->iq_gain_q;
+    p->iq_phase_balance = cfg->iq_phase_balance;
+    switch (cfg->iq_freq_mode)
+    {
+    case UHSDR_IQ_CONV_P6KHZ: p->freq_shift_hz = 6000; break;
+    case UHSDR_IQ_CONV_M6KHZ: p->freq_shift_hz = -6000; break;
+    case UHSDR_IQ_CONV_P12KHZ: p->freq_shift_hz = 12000; break;
+    case UHSDR_IQ_CONV_M12KHZ: p->freq_shift_hz = -12000; break;
+    default: p->freq_shift_hz = 0; break;
+    }
+    if (p->freq_shift_hz != 0)
+    {
+        const int32_t conv = p->freq_shift_hz < 0 ? -p->freq_shift_hz : p->freq_shift_hz;
+        const float rate = conv / (float)IQ_SAMPLE_RATE;       /* IQ_SAMPLE_RATE_F */
+        p->shift_kind = (rate == 0.25) ? 1 : 2;                /* freq_shift.c:294-319 */
+        const double r = (2 * M_PI * conv) / (float)IQ_SAMPLE_RATE;
+        p->osc_cos = cos(r);
+        p->osc_sin = sin(r);
+        p->shift_up = !(p->freq_shift_hz > 0);                 /* dir = shift > 0 => DOWN */
+    }
+
+    /* Hilbert / decimation FIRs, audio_filter.c:1134-1223 and audio_driver.c:2718-2720 */
+    const int is_am = (mode == UHSDR_DEMOD_AM || mode == UHSDR_DEMOD_SAM);
+    p->use_decimated_iq = ((f->fir_i == uhsdr_filter_paths[4].fir_i) && mode != UHSDR_DEMOD_FM) || is_am;
+    p->hilbert_taps = is_am ? 0 : f->fir_taps;
+    copy_bits(p->hilbert_i, f->fir_i, f->fir_taps);
+    copy_bits(p->hilbert_q, f->fir_q, f->fir_taps);
+    if (is_am)
+    {
+        p->dec_taps = f->fir_taps;           /* AM/SAM reuse the I table as decimator */
+        copy_bits(p->dec, f->fir_i, f->fir_taps);
+    }
+    else if (f->dec_taps)
+    {
+        p->dec_taps = f->dec_taps;
+        copy_bits(p->dec, f->dec, f->dec_taps);
+    }
+    /* IIR lattice pre-filter and anti-alias filter, audio_driver.c:1112-1151 */
+    p->pre_stages = f->pre_stages;
+    copy_bits(p->pre_k, f->pre_k, f->pre_stages);
+    if (f->pre_stages) copy_bits(p->pre_v, f->pre_v, f->pre_stages + 1);
+    p->aa_stages = f->aa_stages;
+    copy_bits(p->aa_k, f->aa_k, f->aa_stages);
+    if (f->aa_stages) copy_bits(p->aa_v, f->aa_v, f->aa_stages + 1);
+    /* interpolator, audio_driver.c:1209-1224: the descriptor's phaseLength is passed as numTaps */
+    if (f->interp_taps)
+    {
+        p->interp_L = p->decimation_rate;
+        if (f->interp_taps % p->interp_L) { uhsdr_set_error("interpolator length"); return UHSDR_LENGTH_ERROR; }
+        p->interp_phase = f->interp_taps / p->interp_L;
+        copy_bits(p->interp, f->interp, f->interp_taps);
+    }
+
+    /* biquads, audio_driver.c:994-1050 */
+    const float FSdec = AUDIO_SAMPLE_RATE / (f->sample_rate_dec != 0 ? f->sample_rate_dec : 1);
+    float c[5];
+    if (cfg->dsp_active & UHSDR_DSP_MNOTCH_ENABLE) { calc_bandstop(c, cfg->notch_frequency, FSdec); memcpy(p->biquad1 + 0, c, sizeof c); }
+    else memcpy(p->biquad1 + 0, biquad_passthrough, sizeof c);
+    memcpy(p->biquad1 + 15, biquad_passthrough, sizeof c);
+    if (cfg->dsp_active & UHSDR_DSP_MPEAK_ENABLE) { calc_bandpass(c, cfg->peak_frequency, FSdec); memcpy(p->biquad1 + 5, c, sizeof c); }
+    else memcpy(p->biquad1 + 5, biquad_passthrough, sizeof c);
+    calc_lowshelf(c, 250, 0.7, cfg->bass_gain, FSdec);
+    memcpy(p->biquad1 + 10, c, sizeof c);
+    calc_highshelf(c, 3500, 0.9, cfg->treble_gain, AUDIO_SAMPLE_RATE);
+    memcpy(p->biquad2, c, sizeof c);
+
+    /* post-AGC scaling, audio_driver.c:2513-2524 */
+    const float post_agc_gain_scaling = (f->sample_rate_dec == 4) ? POST_AGC_GAIN_SCALING_DECIMATE_4
+                                                                  : POST_AGC_GAIN_SCALING_DECIMATE_2;
+    p->post_agc_scale = post_agc_gain_scaling * (is_am ? 0.5 : 0.333);
+    p->line_out_scale = LINE_OUT_SCALING_FACTOR;
+
+    setup_agc(&p->agc, cfg, (float)p->decimated_freq, is_am);
+    return UHSDR_OK;
+}
+
+int uhsdr_rx_plan_supported(const uhsdr_rx_plan* p)
+{
+    /* device chain: SSB / CW / DIGI demodulation (I +- Q) on every filter path */
+    if (!p) return 0;
+    if (p->dmod_mode == UHSDR_DEMOD_AM || p->dmod_mode == UHSDR_DEMOD_SAM || p->dmod_mode == UHSDR_DEMOD_FM)
+        return 0;
+    return 1;
+}
+
+const char* uhsdr_version(void) { return "uhsdr_amd 0.1 (gfx950)"; }
+int32_t uhsdr_sizeof_config(void) { return (int32_t)sizeof(uhsdr_rx_config); }
+int32_t uhsdr_sizeof_plan(void) { return (int32_t)sizeof(uhsdr_rx_plan); }

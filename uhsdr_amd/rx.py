@@ -1,0 +1,92 @@
+"""Host-side mirror of the reference RX interface for the batched device chain.
+
+    chain = RxChain(config, channels=C, frames=N)    # AudioDriver_Init + SetProcessingChain
+    chain.process(iq_dev, audio_dev, dst_dev)         # N/32 x AudioDriver_I2SCallback per channel
+
+``iq`` is [C][N][2] int32 IqSample_t frames, ``audio`` [C][N] float (adb.a_buffer[1]),
+``dst`` [C][N][2] int32 AudioSample_t frames -- the firmware's DMA formats, channel-major.
+Device tensors are torch tensors on cuda:N (torch only provides memory and the stream);
+all arithmetic runs in the HIP kernels of libuhsdr_amd.so.  Numpy arrays go through
+``process_host`` (copy in, process, copy out).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+
+
+class RxChain:
+    def __init__(self, config: _abi.RxConfig | None = None, channels: int = 1, frames: int = 32,
+                 stream: int | None = None, **overrides):
+        self.lib = _abi.load()
+        self.config = config if config is not None else _abi.default_config(**overrides)
+        self.channels = int(channels)
+        self.frames = int(frames)
+        h = C.c_void_p()
+        _abi.check(self.lib.uhsdr_rx_create(C.byref(self.config), self.channels, self.frames,
+                                            C.c_void_p(stream or 0), C.byref(h)), "uhsdr_rx_create")
+        self.handle = h
+        self.plan = _abi.RxPlan()
+        _abi.check(self.lib.uhsdr_rx_get_plan(h, C.byref(self.plan)), "uhsdr_rx_get_plan")
+
+    def set_stream(self, stream: int) -> None:
+        _abi.check(self.lib.uhsdr_rx_set_stream(self.handle, C.c_void_p(stream)), "uhsdr_rx_set_stream")
+
+    def reset(self) -> None:
+        _abi.check(self.lib.uhsdr_rx_reset(self.handle), "uhsdr_rx_reset")
+
+    def _shape_ok(self, t, last):
+        shp = tuple(t.shape)
+        want = (self.channels, self.frames) + last
+        if shp != want:
+            raise ValueError(f"buffer shape {shp} != {want}")
+
+    def process(self, iq, audio=None, dst=None) -> None:
+        """Device buffers (torch tensors on the GPU, contiguous): enqueue on the handle's stream."""
+        self._shape_ok(iq, (2,))
+        for t in (iq, audio, dst):
+            if t is not None and not t.is_contiguous():
+                raise ValueError("buffers must be contiguous")
+        if audio is not None:
+            self._shape_ok(audio, ())
+        if dst is not None:
+            self._shape_ok(dst, (2,))
+        _abi.check(self.lib.uhsdr_rx_process(
+            self.handle, C.c_void_p(iq.data_ptr()),
+            C.c_void_p(audio.data_ptr() if audio is not None else 0),
+            C.c_void_p(dst.data_ptr() if dst is not None else 0)), "uhsdr_rx_process")
+
+    def process_host(self, iq: np.ndarray):
+        """Host numpy in/out: returns (audio [C][N] f32, dst [C][N][2] int32)."""
+        iq = np.ascontiguousarray(iq, dtype=np.int32)
+        self._shape_ok(iq, (2,))
+        audio = np.empty((self.channels, self.frames), np.float32)
+        dst = np.empty((self.channels, self.frames, 2), np.int32)
+        _abi.check(self.lib.uhsdr_rx_process_host(
+            self.handle, iq.ctypes.data_as(C.c_void_p), audio.ctypes.data_as(C.c_void_p),
+            dst.ctypes.data_as(C.c_void_p)), "uhsdr_rx_process_host")
+        return audio, dst
+
+    def enable_timing(self, enable: bool = True) -> None:
+        _abi.check(self.lib.uhsdr_rx_enable_timing(self.handle, int(enable)), "uhsdr_rx_enable_timing")
+
+    def kernel_times(self):
+        """{kernel name: (total ms, launches)} accumulated since enable_timing()."""
+        ms = (C.c_float * 8)()
+        n = (C.c_int32 * 8)()
+        k = self.lib.uhsdr_rx_kernel_times(self.handle, ms, n, 8)
+        return {self.lib.uhsdr_rx_kernel_name(i).decode(): (ms[i], n[i]) for i in range(k)}
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.uhsdr_rx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -47,7 +47,7 @@ def test_device_matches_reference_firmware(cuda, path):
     np.testing.assert_array_equal(dst, g["dst"])
 
 
-@pytest.mark.parametrize("frames", [32, 64, 96, 2048])
+@pytest.mark.parametrize("frames", [32, 64, 128, 1024, 2048])
 def test_device_call_granularity(cuda, frames):
     g = load(golden_files()[0])
     cfg = U.config_from_ref_args(g["args"])

@@ -78,10 +78,12 @@ def test_device_c2_batch_sampled_channels(cuda):
     assert np.isfinite(a1).all()
 
 
-def test_device_north_star_batch_sampled_channels(cuda):
-    """262144 channels x 64-frame calls (north-star regime): sampled channels vs oracle."""
+@pytest.mark.parametrize("path", [48, 35, 55])
+def test_device_north_star_batch_sampled_channels(cuda, path):
+    """262144 channels x 64-frame calls (north-star regime, R = 16 front blocks): sampled
+    channels vs oracle, for each filter-path family."""
     import torch
-    cfg = U.default_config()
+    cfg = U.default_config(filter_path=path)
     C, n = 262144, 128
     pick = np.array([0, 1, 63, 64, 4095, 65536, 131071, 262143])
     chain = U.RxChain(cfg, channels=C, frames=64)

@@ -34,6 +34,8 @@ typedef struct
 
 extern const uhsdr_filter_path_desc uhsdr_filter_paths[UHSDR_FILTER_PATH_NUM];
 
+int uhsdr_rx_mode_supported(const uhsdr_rx_plan* p);
+
 /* thread-local last error text for uhsdr_last_error() */
 void uhsdr_set_error(const char* fmt, ...);
 

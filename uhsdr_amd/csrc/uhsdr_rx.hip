@@ -3,27 +3,29 @@
 // One uhsdr_rx_process() call == N/32 consecutive AudioDriver_RxProcessor invocations
 // (drivers/audio/audio_driver.c:2603-2942) on each of C independent channels.  Two kernels:
 //
-//  rx_front  (time-parallel, all lanes busy whatever C is)
+//  rx_front  (time-parallel: every lane busy whatever C is)
 //      int32 I/Q -> f32, x 2^-16          audio_driver.c:2660-2685
 //      I/Q correction (manual / auto)     audio_driver.c:2254-2316
 //      FreqShift (Fs/4 or oscillator)     freq_shift.c:219-334
-//      Hilbert FIR pair + I +- Q + decimator, or decimator pair + Hilbert pair + I +- Q
-//                                         audio_driver.c:2718-2810, CMSIS arm_fir_f32 /
-//                                         arm_fir_decimate_f32
-//    -> decimated audio adec[C][N/M] (12 or 24 ksps), FIR delay lines updated.
-//    Workgroup = G channels; their windows (history + block) sit in LDS; each lane computes
-//    R consecutive FIR outputs from a register-resident sliding window.
+//      Hilbert FIR pair -> I +- Q -> decimator        (wide paths, audio_driver.c:2748-2810)
+//      or decimator pair -> Hilbert pair -> I +- Q    (narrow paths, use_decimatedIQ :2718-2753)
+//    -> decimated audio adec[C][N/M] (12 or 24 ksps); FIR delay lines carried in HBM.
+//    Workgroup = G channels.  One LDS window per channel is filled with history + block for
+//    I, then reused for Q; each lane computes R consecutive FIR outputs with the taps fully
+//    unrolled (tap counts are template parameters): the sliding window lives in registers,
+//    every window sample is read from LDS once per pass, coefficients come in via SGPRs.
 //
-//  rx_back   (sequential per channel: one lane == one channel, 64 channels per wave)
-//      IIR lattice pre-filter -> WDSP AGC -> scale -> biquad_1 -> polyphase interpolator
-//      -> anti-alias lattice -> biquad_2 -> line-out scale -> f32 + int32 codec frames
+//  rx_back   (sequential per channel: lane == channel, 64 channels per workgroup)
+//      wave 0: IIR lattice pre-filter -> WDSP AGC -> scale -> biquad_1 -> polyphase interp
+//      wave 1: anti-alias lattice -> biquad_2 -> line-out scale -> f32 / int32 codec frames
 //                                         audio_driver.c:2436-2592, 2832-2923
-//    All recursions run per sample in the reference order; state lives in registers for the
-//    whole launch; the AGC look-ahead ring lives in LDS.
+//    The two waves form a 2-stage pipeline over 32-frame calls (wave 1 works on call k while
+//    wave 0 works on call k+1), halving the serial dependency chain per channel.  All state
+//    sits in registers for the whole launch; the AGC look-ahead ring sits in LDS.
 //
-// Arithmetic: exactly the reference's binary32 operation sequence (this file is compiled
-// with -ffp-contract=off), so the device output is bit-identical to the firmware built for
-// x86 (tests/test_gpu_parity.py).
+// Arithmetic: exactly the reference's binary32 operation sequence (compiled with
+// -ffp-contract=off), so outputs are bit-identical to the firmware built for x86
+// (tests/test_gpu_parity.py).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,150 +38,241 @@
 #define IQ_BIT_SCALE_DOWN 0.0000152587890625f
 
 // ------------------------------------------------------------------------------------
-// LDS window addressing: one pad word every 8 so that lanes reading windows 8 or 16
-// samples apart hit different banks.
-__device__ __forceinline__ int sk(int p) { return p + (p >> 3); }
-__host__ __device__ constexpr int sk_len(int n) { return n + (n >> 3) + 1; }
-
-// y[j] = sum_{k<Tpad} c[k] * win[j*M + k] for j = j0 .. j0+R-1 (coefficients zero padded
-// to a multiple of 8: a +-0 product never changes a finite accumulator that started at +0).
-template <int R, int M>
-__device__ __forceinline__ void fir_run(const float* win, const float* __restrict__ c, int Tpad, int j0,
-                                        float (&acc)[R])
+// LDS window addressing: one pad word every 8 samples, so lanes whose windows start 8/16
+// samples apart land on different banks.  For p0 % 8 == 0, sk(p0 + o) == sk(p0) + sk(o):
+// all tap offsets become immediate ds_read offsets from one per-lane base.
+// Windows whose lane bases are multiples of 4 only (decimated-rate Hilbert) use a pad
+// every 4 (SH = 2) instead.
+template <int SH = 3> __host__ __device__ constexpr int skw(int p) { return p + (p >> SH); }
+__host__ __device__ constexpr int sk(int p) { return skw<3>(p); }
+__host__ __device__ constexpr int sk_len(int n, int sh = 3) { return n + (n >> sh) + 1; }
+__host__ __device__ constexpr int odd_pitch(int n) { return (n & 1) ? n : n + 1; }
+// skew of the stage-2 window: lane bases there are multiples of R/M on decimate-first paths
+__host__ __device__ constexpr int front_sh2(bool decim_first, int R, int M)
 {
+    return !decim_first ? 3 : (R / M >= 8 ? 3 : (R / M == 4 ? 2 : 1));
+}
+// per-channel LDS window pitch: room for the longest pass (stage-2 windows of decimate-first
+// paths use the pad-every-4 skew), rounded to 5 (mod 8): at most 2-way bank conflicts for
+// every lane/channel layout used
+__host__ __device__ constexpr int window_pitch(int T1, int T2, int N1, int N2, int sh2)
+{
+    const int a = sk_len(T1 - 1 + N1 + 8, 3), b = sk_len(T2 - 1 + N2 + 8, sh2);
+    const int n = a > b ? a : b;
+    return n + ((5 - n) & 7);
+}
+
+// acc[r] = sum_{k<T} c[k] * win[r*M + k], r < R; tap order k = 0..T-1 from +0.0f exactly as
+// arm_fir_f32 / arm_fir_decimate_f32 (CMSIS .../arm_fir_f32.c:482-560).  `win` points at
+// the lane's first window sample (already skewed; base a multiple of 2^SH); `c` is the tap
+// table in LDS, zero padded to a multiple of 8 (a +-0 product never changes a finite
+// accumulator that started at +0, so the padding is exact).
+// The chunk loop over 8 taps is deliberately not unrolled: the register window slides by 8
+// samples per chunk and the next chunk's 8 samples are fetched before the current MACs, so
+// the live set stays at R accumulators + one window (a fully unrolled tap loop lets the
+// compiler hoist every window load and spill).
+template <int T, int R, int M, int SH = 3>
+__device__ __forceinline__ void fir_block(const float* win, const float* c, float (&acc)[R])
+{
+    constexpr int W = M * (R - 1) + 8;
+    constexpr int NCH = (T + 7) / 8;
+    float w[W];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-    constexpr int W = 8 + M * (R - 1);
-    const int base = j0 * M;
-    for (int k0 = 0; k0 < Tpad; k0 += 8)
-    {
-        float w[W];
 #pragma unroll
-        for (int q = 0; q < W; ++q) w[q] = win[sk(base + k0 + q)];
+    for (int j = 0; j < W; ++j) w[j] = win[skw<SH>(j)];
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch)
+    {
+        const float* cp = c + 8 * ch;
+        const float4 c0 = *(const float4*)cp;
+        const float4 c1 = *(const float4*)(cp + 4);
+        const float cc[8] = { c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w };
+        float nw[8];
+        const float* np = win + skw<SH>(8 * ch + W);       // 8 * ch + W is a multiple of 8 + W
+#pragma unroll
+        for (int q = 0; q < 8; ++q) nw[q] = np[skw<SH>(8 * ch + W + q) - skw<SH>(8 * ch + W)];
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk)
         {
-            const float cc = c[k0 + kk];
 #pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * cc;
+            for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * cc[kk];
         }
+#pragma unroll
+        for (int j = 0; j < W - 8; ++j) w[j] = w[j + 8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) w[W - 8 + q] = nw[q];
     }
 }
 
 struct FrontArgs
 {
     const uhsdr_rx_plan* plan;
-    const int2* iq;          // [C][N] IqSample_t
-    float* hist1_i;          // [C][T1-1]: stage-1 FIR history (Hilbert, or I decimator)
-    float* hist1_q;          // [C][T1-1]
-    float* hist2_i;          // [C][T2-1]: stage-2 FIR history (audio decimator, or Hilbert I)
-    float* hist2_q;          // [C][T2-1]  (decimated-IQ paths only)
+    const int2* iq;          // frame 0 of this launch; row stride ld frames (IqSample_t)
+    float* hist1_i;          // [C][HS1] stage-1 FIR history (Hilbert, or I decimator), HS = T-1 rounded to 4
+    float* hist1_q;          // [C][HS1]
+    float* hist2_i;          // [C][HS2] stage-2 history (audio decimator, or Hilbert I)
+    float* hist2_q;          // [C][HS2] (decimate-first paths: Hilbert Q)
     float* teta;             // [3][C] auto I/Q correction low-pass state
-    float* osc;              // [2][C] oscillator {I, Q}
-    float* adec;             // [C][Nd] output
-    int C, N, G;
-    int T1, T1pad, T2, T2pad;
+    const float* osc_in;     // [2] oscillator {I, Q} at the start of this launch (shared by all channels)
+    float* osc_out;          // [2] written by workgroup 0
+    float* adec;             // decimated output of this launch; row stride ldd
+    int C, N, ld, ldd;
 };
 
-// Stage-1 window: x[g][0 .. T1-2] history, x[g][T1-1 .. T1-1+N-1] new samples.
-template <int R1, int M2>
-__global__ void __launch_bounds__(256) rx_front(FrontArgs a)
+// converted, corrected, frequency-shifted sample n of a channel (audio_driver.c:2660-2705)
+struct InputStage
+{
+    float gi, gq, ph;
+    int iq_auto, shift, shift_up;
+};
+
+__device__ __forceinline__ void convert_frame(const int2 v, const InputStage& s, int n, const float* m1, const float* m2,
+                                              const float* osc, float& I, float& Q)
+{
+    I = (float)v.x;
+    Q = (float)v.y;
+    I = I * IQ_BIT_SCALE_DOWN;
+    Q = Q * IQ_BIT_SCALE_DOWN;
+    if (!s.iq_auto)
+    {
+        I = I * s.gi;
+        Q = Q * s.gq;
+        if (s.ph < 0) { const float e3 = I * s.ph; Q = Q + e3; }
+        else if (s.ph > 0) { const float e3 = Q * s.ph; I = I + e3; }
+    }
+    else
+    {
+        const int b = n / BLK;
+        Q += m1[b] * I;
+        I = I * m2[b];
+    }
+    if (s.shift)
+    {
+        float ib = s.shift_up ? I : Q;
+        float qb = s.shift_up ? Q : I;
+        if (s.shift == 1)
+        {
+            const float iv = ib, qv = qb;
+            switch (n & 3)
+            {
+            case 0: break;
+            case 1: ib = qv; qb = -iv; break;
+            case 2: ib = -iv; qb = -qv; break;
+            default: ib = -qv; qb = iv; break;
+            }
+        }
+        else
+        {
+            const float oq = osc[2 * n], oi = osc[2 * n + 1];
+            const float qt = qb, it = ib;
+            qb = (qt * oq) - (it * oi);
+            ib = (it * oq) + (qt * oi);
+        }
+        I = s.shift_up ? ib : qb;
+        Q = s.shift_up ? qb : ib;
+    }
+}
+
+// LDS accesses of one wave are processed in order; the fences only stop the compiler from
+// moving a lane's LDS access across a hand-off between lanes of the same wave.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int FRONT_WAVE = 64;
+
+// One wave owns CPW = 64 / (N/R) whole channels: all data exchange stays inside the wave, so
+// there is no workgroup barrier and waves from many workgroups interleave freely on a CU.
+// The wave has one LDS window per channel, reused by every FIR pass:
+//   Hilbert-first (wide paths):  I -> Hilbert-I (regs), Q -> Hilbert-Q, a = I +- Q (regs),
+//                                a -> decimator /M -> adec
+//   decimate-first (narrow):     I -> decimator (regs), Q -> decimator, dI -> Hilbert-I,
+//                                dQ -> Hilbert-Q, a = hI +- hQ -> adec
+// Each pass: history row (HBM) + this call's samples (registers) into the window, history
+// row for the next call back to HBM, then every lane runs its R-output FIR block.
+template <int T1, int T2, int M, bool DECIM_FIRST, int R>
+__global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const uhsdr_rx_plan* __restrict__ P = a.plan;
-    const int N = a.N, G = a.G, C = a.C;
-    const int T1 = a.T1, T2 = a.T2;
-    const int M = P->decimation_rate;
-    const bool decim_iq = P->use_decimated_iq;
-    const int N2 = decim_iq ? N / M : N;                // stage-2 input length
-    const int L1 = sk_len(T1 - 1 + N + 8);             // + 8 zero words read by the padded taps
-    const int L2 = sk_len(T2 - 1 + N2 + 8);
-    float* xi = smem;                                   // [G][L1]
-    float* xq = xi + G * L1;                            // [G][L1]
-    float* yi = xq + G * L1;                            // [G][L2]  stage-2 window(s)
-    float* yq = yi + G * L2;                            // [G][L2]  (decim_iq only)
-    float* mc = yq + (decim_iq ? G * L2 : 0);           // [G][2][N/32] auto-IQ factors
-    const int c0 = blockIdx.x * G;
-    const int tid = threadIdx.x;
+    const int N = a.N, C = a.C;
+    const int lane = threadIdx.x;
+    const int nb = N / R;                            // lanes per channel
+    const int CPW = FRONT_WAVE / nb;                 // channels per wave
+    const int g = lane / nb, b = lane % nb;
+    const int c = blockIdx.x * CPW + g;
+    const bool act = g < CPW;
+    const bool live = act && c < C;
+    const int gs = act ? g : 0;
     const int nblk32 = N / BLK;
+    constexpr int RD = R / M;                        // decimated samples per lane
+    constexpr int HS1 = (T1 - 1 + 3) & ~3, HS2 = (T2 - 1 + 3) & ~3;
+    const int N2 = DECIM_FIRST ? N / M : N;          // stage-2 input samples per channel
+    constexpr int SH2 = front_sh2(DECIM_FIRST, R, M);
+    const int LW = window_pitch(T1, T2, N, N2, SH2);
+    float* win_all = smem;                           // [CPW][LW]
+    float* W = win_all + gs * LW;
+    constexpr int TH = DECIM_FIRST ? T2 : T1, TD = DECIM_FIRST ? T1 : T2;
+    constexpr int TH8 = (TH + 7) & ~7, TD8 = (TD + 7) & ~7;
+    float* c_hi = win_all + ((CPW * LW + 3) & ~3);   // tap tables (wave-uniform broadcast reads)
+    float* c_hq = c_hi + TH8;
+    float* c_dec = c_hq + TH8;
+    float* aux = c_dec + TD8;                        // auto-IQ factors [2][CPW][nblk32], osc [2N]
+    float* m1 = aux;
+    float* m2 = aux + CPW * nblk32;
+    float* osc = aux + (P->iq_auto_correction ? 2 * CPW * nblk32 : 0);
 
-    // ---- zero the window tails, load stage-1 history + convert new I/Q ----
-    for (int e = tid; e < G * 8; e += blockDim.x)
+    for (int k = lane; k < TH8; k += FRONT_WAVE)
     {
-        const int g = e / 8, k = e % 8;
-        xi[g * L1 + sk(T1 - 1 + N + k)] = 0.0f;
-        xq[g * L1 + sk(T1 - 1 + N + k)] = 0.0f;
+        c_hi[k] = k < TH ? P->hilbert_i[k] : 0.0f;
+        c_hq[k] = k < TH ? P->hilbert_q[k] : 0.0f;
     }
-    for (int e = tid; e < G * (T1 - 1); e += blockDim.x)
-    {
-        const int g = e / (T1 - 1), k = e % (T1 - 1);
-        const int c = c0 + g;
-        if (c < C)
-        {
-            xi[g * L1 + sk(k)] = a.hist1_i[(size_t)c * (T1 - 1) + k];
-            xq[g * L1 + sk(k)] = a.hist1_q[(size_t)c * (T1 - 1) + k];
-        }
-    }
-    const float gi = P->iq_gain_i, gq = P->iq_gain_q, ph = P->iq_phase_balance;
-    const bool iq_auto = P->iq_auto_correction;
-    for (int e = tid; e < G * N; e += blockDim.x)
-    {
-        const int g = e / N, n = e % N;
-        const int c = c0 + g;
-        if (c >= C) continue;
-        const int2 v = a.iq[(size_t)c * N + n];
-        float I = (float)v.x, Q = (float)v.y;
-        I = I * IQ_BIT_SCALE_DOWN;
-        Q = Q * IQ_BIT_SCALE_DOWN;
-        if (!iq_auto)
-        {
-            I = I * gi;
-            Q = Q * gq;
-            if (ph < 0) { const float e3 = I * ph; Q = Q + e3; }
-            else if (ph > 0) { const float e3 = Q * ph; I = I + e3; }
-        }
-        xi[g * L1 + sk(T1 - 1 + n)] = I;
-        xq[g * L1 + sk(T1 - 1 + n)] = Q;
-    }
-    __syncthreads();
+    for (int k = lane; k < TD8; k += FRONT_WAVE) c_dec[k] = k < TD ? P->dec[k] : 0.0f;
 
-    // ---- automatic I/Q correction: per-32-frame statistics, sequential low-pass ----
-    if (iq_auto)
+    InputStage in;
+    in.gi = P->iq_gain_i; in.gq = P->iq_gain_q; in.ph = P->iq_phase_balance;
+    in.iq_auto = P->iq_auto_correction;
+    in.shift = P->freq_shift_hz != 0 ? P->shift_kind : 0;
+    in.shift_up = P->shift_up;
+
+    // ---- pre-pass: auto I/Q statistics per 32-frame call; oscillator trajectory ----
+    if (in.iq_auto)
     {
-        float* m1 = mc;                 // [G][nblk32]
-        float* m2 = mc + G * nblk32;    // [G][nblk32]
-        // statistics need the whole block: one lane per (channel, block), sequential sum
-        // (audio_driver.c:2280-2285), then one lane per channel runs the low-pass.
-        float* t1s = yi;                // reuse stage-2 window as scratch (3 x G x nblk32)
-        for (int e = tid; e < G * nblk32; e += blockDim.x)
+        for (int e = lane; e < CPW * nblk32; e += FRONT_WAVE)
         {
-            const int g = e / nblk32, b = e % nblk32;
+            const int gg = e / nblk32, bb = e % nblk32;
+            const int cc = blockIdx.x * CPW + gg;
             float t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
-            for (int i = 0; i < BLK; ++i)
-            {
-                const float I = xi[g * L1 + sk(T1 - 1 + b * BLK + i)];
-                const float Q = xq[g * L1 + sk(T1 - 1 + b * BLK + i)];
-                const float sI = (I < 0) ? -1.0f : ((I > 0) ? 1.0f : 0.0f);
-                const float sQ = (Q < 0) ? -1.0f : ((Q > 0) ? 1.0f : 0.0f);
-                t1 += sI * Q;
-                t2 += sI * I;
-                t3 += sQ * Q;
-            }
-            t1s[(0 * G + g) * nblk32 + b] = t1;
-            t1s[(1 * G + g) * nblk32 + b] = t2;
-            t1s[(2 * G + g) * nblk32 + b] = t3;
+            if (cc < C)
+                for (int i = 0; i < BLK; ++i)
+                {
+                    const int2 v = a.iq[(size_t)cc * a.ld + bb * BLK + i];
+                    const float I = ((float)v.x) * IQ_BIT_SCALE_DOWN;
+                    const float Q = ((float)v.y) * IQ_BIT_SCALE_DOWN;
+                    const float sI = (I < 0) ? -1.0f : ((I > 0) ? 1.0f : 0.0f);
+                    const float sQ = (Q < 0) ? -1.0f : ((Q > 0) ? 1.0f : 0.0f);
+                    t1 += sI * Q;
+                    t2 += sI * I;
+                    t3 += sQ * Q;
+                }
+            m1[e] = t1;
+            m2[e] = t2;
+            win_all[e] = t3;                         // scratch; the windows are filled later
         }
-        __syncthreads();
-        for (int g = tid; g < G; g += blockDim.x)
+        wave_sync();
+        for (int gg = lane; gg < CPW; gg += FRONT_WAVE)
         {
-            const int c = c0 + g;
-            if (c >= C) continue;
-            float o1 = a.teta[c], o2 = a.teta[C + c], o3 = a.teta[2 * C + c];
-            for (int b = 0; b < nblk32; ++b)
+            const int cc = blockIdx.x * CPW + gg;
+            if (cc >= C) continue;
+            float o1 = a.teta[cc], o2 = a.teta[C + cc], o3 = a.teta[2 * C + cc];
+            for (int bb = 0; bb < nblk32; ++bb)
             {
-                float t1 = t1s[(0 * G + g) * nblk32 + b];
-                float t2 = t1s[(1 * G + g) * nblk32 + b];
-                float t3 = t1s[(2 * G + g) * nblk32 + b];
+                const int e = gg * nblk32 + bb;
+                float t1 = m1[e], t2 = m2[e], t3 = win_all[e];
                 t1 = (float)(-0.003 * (double)(t1 / (float)BLK) + 0.997 * (double)o1);
                 t2 = (float)(0.003 * (double)(t2 / (float)BLK) + 0.997 * (double)o2);
                 t3 = (float)(0.003 * (double)(t3 / (float)BLK) + 0.997 * (double)o3);
@@ -187,181 +280,138 @@ __global__ void __launch_bounds__(256) rx_front(FrontArgs a)
                 float help = (t2 * t2);
                 if (help > 0.0f) help = (t3 * t3 - t1 * t1) / help;
                 const float M_c2 = (help > 0.0f) ? sqrtf(help) : 1.0f;
-                m1[g * nblk32 + b] = M_c1;
-                m2[g * nblk32 + b] = M_c2;
+                m1[e] = M_c1;
+                m2[e] = M_c2;
                 o1 = t1; o2 = t2; o3 = t3;
             }
-            a.teta[c] = o1; a.teta[C + c] = o2; a.teta[2 * C + c] = o3;
+            a.teta[cc] = o1; a.teta[C + cc] = o2; a.teta[2 * C + cc] = o3;
         }
-        __syncthreads();
-        for (int e = tid; e < G * N; e += blockDim.x)
-        {
-            const int g = e / N, n = e % N;
-            const int b = n / BLK;
-            const int p = g * L1 + sk(T1 - 1 + n);
-            const float I = xi[p];
-            const float Q = xq[p] + m1[g * nblk32 + b] * I;
-            xq[p] = Q;
-            xi[p] = I * m2[g * nblk32 + b];
-        }
-        __syncthreads();
     }
-
-    // ---- frequency translation ----
-    if (P->freq_shift_hz != 0)
+    if (in.shift == 2 && lane == 0)
     {
-        float* ib = P->shift_up ? xi : xq;
-        float* qb = P->shift_up ? xq : xi;
-        if (P->shift_kind == 1)
+        // FreqShift_Approx (freq_shift.c:57-101): the oscillator does not depend on the data,
+        // so all channels share one trajectory.
+        const float oc = P->osc_cos, os = P->osc_sin;
+        float vi = a.osc_in[0], vq = a.osc_in[1];
+        for (int n = 0; n < N; ++n)
         {
-            for (int e = tid; e < G * N; e += blockDim.x)
+            const float oq = (vq * oc) - (vi * os);
+            const float oi = (vi * oc) + (vq * os);
+            osc[2 * n] = oq;
+            osc[2 * n + 1] = oi;
+            vq = oq; vi = oi;
+            if ((n & (BLK - 1)) == BLK - 1)
             {
-                const int g = e / N, n = e % N;
-                const int p = g * L1 + sk(T1 - 1 + n);
-                const float iv = ib[p], qv = qb[p];
-                switch (n & 3)
-                {
-                case 0: break;
-                case 1: ib[p] = qv; qb[p] = -iv; break;
-                case 2: ib[p] = -iv; qb[p] = -qv; break;
-                case 3: ib[p] = -qv; qb[p] = iv; break;
-                }
+                const float gn = (3 - ((vq * vq) + (vi * vi))) / 2;
+                vq = gn * vq; vi = gn * vi;
             }
         }
-        else
+        if (blockIdx.x == 0) { a.osc_out[0] = vi; a.osc_out[1] = vq; }
+    }
+    wave_sync();
+
+    // ---- this lane's R frames: R/2 independent 16-byte loads; I and Q kept in registers ----
+    float xi[R], xq[R];
+    {
+        int4 raw[R / 2];
+        const int4* src = (const int4*)(a.iq + (size_t)c * a.ld + b * R);
+#pragma unroll
+        for (int j = 0; j < R / 2; ++j) raw[j] = live ? src[j] : make_int4(0, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
         {
-            // recursive quadrature oscillator: sequential in time, one lane per channel
-            const float oc = P->osc_cos, os = P->osc_sin;
-            for (int g = tid; g < G; g += blockDim.x)
-            {
-                const int c = c0 + g;
-                if (c >= C) continue;
-                float vi = a.osc[c], vq = a.osc[C + c];
-                for (int n = 0; n < N; ++n)
-                {
-                    const int p = g * L1 + sk(T1 - 1 + n);
-                    const float oq = (vq * oc) - (vi * os);
-                    const float oi = (vi * oc) + (vq * os);
-                    const float qt = qb[p], it = ib[p];
-                    qb[p] = (qt * oq) - (it * oi);
-                    ib[p] = (it * oq) + (qt * oi);
-                    vq = oq; vi = oi;
-                    if ((n & (BLK - 1)) == BLK - 1)
-                    {
-                        const float gn = (3 - ((vq * vq) + (vi * vi))) / 2;
-                        vq = gn * vq; vi = gn * vi;
-                    }
-                }
-                a.osc[c] = vi; a.osc[C + c] = vq;
-            }
+            const int2 v = (j & 1) ? make_int2(raw[j / 2].z, raw[j / 2].w) : make_int2(raw[j / 2].x, raw[j / 2].y);
+            convert_frame(v, in, b * R + j, m1 + gs * nblk32, m2 + gs * nblk32, osc, xi[j], xq[j]);
         }
-        __syncthreads();
     }
 
-    // ---- save stage-1 history, load stage-2 history ----
-    for (int e = tid; e < G * (T1 - 1); e += blockDim.x)
-    {
-        const int g = e / (T1 - 1), k = e % (T1 - 1);
-        const int c = c0 + g;
-        if (c >= C) continue;
-        a.hist1_i[(size_t)c * (T1 - 1) + k] = xi[g * L1 + sk(N + k)];
-        a.hist1_q[(size_t)c * (T1 - 1) + k] = xq[g * L1 + sk(N + k)];
-    }
-    for (int e = tid; e < G * 8; e += blockDim.x)
-    {
-        const int g = e / 8, k = e % 8;
-        yi[g * L2 + sk(T2 - 1 + N2 + k)] = 0.0f;
-        if (decim_iq) yq[g * L2 + sk(T2 - 1 + N2 + k)] = 0.0f;
-    }
-    for (int e = tid; e < G * (T2 - 1); e += blockDim.x)
-    {
-        const int g = e / (T2 - 1), k = e % (T2 - 1);
-        const int c = c0 + g;
-        if (c >= C) continue;
-        yi[g * L2 + sk(k)] = a.hist2_i[(size_t)c * (T2 - 1) + k];
-        if (decim_iq) yq[g * L2 + sk(k)] = a.hist2_q[(size_t)c * (T2 - 1) + k];
-    }
-    __syncthreads();
+    // One FIR pass over the window: history (T-1, HBM) + NV new samples per lane, history
+    // written back, then the lane's block of outputs.  SH: window skew (2 when lane bases are
+    // multiples of 4 only).
+    auto fill = [&](const float* hist, float* hist_out, int HS, int T, const float* vals, int NV, int SH) {
+        const int nnew = nb * NV;
+        for (int q = b; q < HS / 4; q += nb)
+        {
+            const float4 v = live ? *(const float4*)(hist + (size_t)c * HS + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float vv[4] = { v.x, v.y, v.z, v.w };
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (act && 4 * q + t < T - 1) W[(4 * q + t) + ((4 * q + t) >> SH)] = vv[t];
+        }
+        if (act && b == 0)
+        {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) W[(T - 1 + nnew + t) + ((T - 1 + nnew + t) >> SH)] = 0.0f;
+        }
+        if (act)
+        {
+            for (int j = 0; j < NV; ++j)
+            {
+                const int p = T - 1 + b * NV + j;
+                W[p + (p >> SH)] = vals[j];
+            }
+        }
+        wave_sync();
+        for (int q = b; q < HS / 4; q += nb)
+        {
+            float vv[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+            {
+                const int p = nnew + 4 * q + t;
+                vv[t] = (4 * q + t < T - 1) ? W[p + (p >> SH)] : 0.0f;
+            }
+            if (live) *(float4*)(hist_out + (size_t)c * HS + 4 * q) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+        }
+    };
 
     const bool lsb = P->lsb;
-    if (!decim_iq)
+    float o[RD];
+    if (!DECIM_FIRST)
     {
-        // stage 1: Hilbert pair at 48 ksps, a = I +- Q into the decimator window
-        const int nb = N / R1;
-        for (int e = tid; e < G * nb; e += blockDim.x)
-        {
-            const int g = e / nb, b = e % nb;
-            float hi[R1], hq[R1];
-            fir_run<R1, 1>(xi + g * L1, P->hilbert_i, a.T1pad, b * R1, hi);
-            fir_run<R1, 1>(xq + g * L1, P->hilbert_q, a.T1pad, b * R1, hq);
+        float hi[R], hq[R];
+        fill(a.hist1_i, a.hist1_i, HS1, T1, xi, R, 3);
+        fir_block<T1, R, 1>(W + sk(b * R), c_hi, hi);
+        wave_sync();
+        fill(a.hist1_q, a.hist1_q, HS1, T1, xq, R, 3);
+        fir_block<T1, R, 1>(W + sk(b * R), c_hq, hq);
+        // a = I + Q (USB) or I - Q (LSB), audio_driver.c:2781-2790
 #pragma unroll
-            for (int r = 0; r < R1; ++r)
-                yi[g * L2 + sk(T2 - 1 + b * R1 + r)] = lsb ? (hi[r] - hq[r]) : (hi[r] + hq[r]);
-        }
-        __syncthreads();
-        // stage 2: decimator -> adec
-        const int Nd = N / M;
-        constexpr int R2 = 4;
-        const int nb2 = Nd / R2;
-        for (int e = tid; e < G * nb2; e += blockDim.x)
-        {
-            const int g = e / nb2, b = e % nb2;
-            const int c = c0 + g;
-            float d[R2];
-            fir_run<R2, M2>(yi + g * L2, P->dec, a.T2pad, b * R2, d);
-            if (c < C)
-            {
-#pragma unroll
-                for (int r = 0; r < R2; ++r) a.adec[(size_t)c * Nd + b * R2 + r] = d[r];
-            }
-        }
+        for (int r = 0; r < R; ++r) hi[r] = lsb ? (hi[r] - hq[r]) : (hi[r] + hq[r]);
+        wave_sync();
+        fill(a.hist2_i, a.hist2_i, HS2, T2, hi, R, 3);
+        fir_block<T2, RD, M>(W + sk(b * R), c_dec, o);
     }
     else
     {
-        // stage 1: decimator pair at 48 ksps into the Hilbert windows
-        const int Nd = N / M;
-        constexpr int R2 = 4;
-        const int nb = Nd / R2;
-        for (int e = tid; e < G * nb; e += blockDim.x)
-        {
-            const int g = e / nb, b = e % nb;
-            float di[R2], dq[R2];
-            fir_run<R2, M2>(xi + g * L1, P->dec, a.T1pad, b * R2, di);
-            fir_run<R2, M2>(xq + g * L1, P->dec, a.T1pad, b * R2, dq);
+        float di[RD], dq[RD], hi[RD], hq[RD];
+        fill(a.hist1_i, a.hist1_i, HS1, T1, xi, R, 3);
+        fir_block<T1, RD, M>(W + sk(b * R), c_dec, di);
+        wave_sync();
+        fill(a.hist1_q, a.hist1_q, HS1, T1, xq, R, 3);
+        fir_block<T1, RD, M>(W + sk(b * R), c_dec, dq);
+        wave_sync();
+        fill(a.hist2_i, a.hist2_i, HS2, T2, di, RD, SH2);
+        fir_block<T2, RD, 1, SH2>(W + skw<SH2>(b * RD), c_hi, hi);
+        wave_sync();
+        fill(a.hist2_q, a.hist2_q, HS2, T2, dq, RD, SH2);
+        fir_block<T2, RD, 1, SH2>(W + skw<SH2>(b * RD), c_hq, hq);
 #pragma unroll
-            for (int r = 0; r < R2; ++r)
-            {
-                yi[g * L2 + sk(T2 - 1 + b * R2 + r)] = di[r];
-                yq[g * L2 + sk(T2 - 1 + b * R2 + r)] = dq[r];
-            }
-        }
-        __syncthreads();
-        // stage 2: Hilbert pair at the decimated rate, a = I +- Q -> adec
-        const int nb2 = Nd / R2;
-        for (int e = tid; e < G * nb2; e += blockDim.x)
-        {
-            const int g = e / nb2, b = e % nb2;
-            const int c = c0 + g;
-            float hi[R2], hq[R2];
-            fir_run<R2, 1>(yi + g * L2, P->hilbert_i, a.T2pad, b * R2, hi);
-            fir_run<R2, 1>(yq + g * L2, P->hilbert_q, a.T2pad, b * R2, hq);
-            if (c < C)
-            {
-#pragma unroll
-                for (int r = 0; r < R2; ++r)
-                    a.adec[(size_t)c * Nd + b * R2 + r] = lsb ? (hi[r] - hq[r]) : (hi[r] + hq[r]);
-            }
-        }
+        for (int r = 0; r < RD; ++r) o[r] = lsb ? (hi[r] - hq[r]) : (hi[r] + hq[r]);
     }
-    __syncthreads();
-    // ---- save stage-2 history ----
-    for (int e = tid; e < G * (T2 - 1); e += blockDim.x)
+    if (live)
     {
-        const int g = e / (T2 - 1), k = e % (T2 - 1);
-        const int c = c0 + g;
-        if (c >= C) continue;
-        a.hist2_i[(size_t)c * (T2 - 1) + k] = yi[g * L2 + sk(N2 + k)];
-        if (decim_iq) a.hist2_q[(size_t)c * (T2 - 1) + k] = yq[g * L2 + sk(N2 + k)];
+        float* dst = a.adec + (size_t)c * a.ldd + b * RD;
+        if (RD % 4 == 0)
+        {
+#pragma unroll
+            for (int r = 0; r < RD; r += 4) *(float4*)(dst + r) = make_float4(o[r], o[r + 1], o[r + 2], o[r + 3]);
+        }
+        else
+        {
+#pragma unroll
+            for (int r = 0; r < RD; ++r) dst[r] = o[r];
+        }
     }
 }
 
@@ -376,7 +426,7 @@ struct BackState
     float* bq2;      // [4][C]
     float* interp;   // [15][C]
     float* ring;     // [W][C]   AGC look-ahead ring, slot = sample index mod W
-    float* agc;      // [6][C]   ring_max volts save_volts fast_bavg hang_bavg wold
+    float* agc;      // [6][C]   spare volts save_volts fast_bavg hang_bavg wold
     int* agci;       // [3][C]   hang_counter decay_type state
 };
 
@@ -391,44 +441,39 @@ struct BackArgs
     int ring_phase;      // (decimated samples processed so far) mod W
 };
 
-// arm_iir_lattice_f32 (generic order), one sample
-template <int SMAX>
-__device__ __forceinline__ float lattice_step(float x, float (&g)[SMAX], const float* __restrict__ k,
-                                              const float* __restrict__ v, int S)
+// arm_iir_lattice_f32 (CMSIS .../arm_iir_lattice_f32.c:348-447), one sample, S stages:
+// stage i of the next sample reads the g stage i+1 produced; the last reads the final f.
+template <int S>
+__device__ __forceinline__ float lattice_step(float x, float (&g)[S > 0 ? S : 1], const float* k, const float* v)
 {
     float fcurr = x, fnext = 0.0f, acc = 0.0f;
-    float gn[SMAX];
+    float gn[S > 0 ? S : 1];
 #pragma unroll
-    for (int i = 0; i < SMAX; ++i)
+    for (int i = 0; i < S; ++i)
     {
-        if (i < S)
-        {
-            const float gcurr = g[i];
-            fnext = fcurr - (k[i] * gcurr);
-            const float gnext = (fnext * k[i]) + gcurr;
-            acc += (gnext * v[i]);
-            gn[i] = gnext;
-            fcurr = fnext;
-        }
+        const float gcurr = g[i];
+        fnext = fcurr - (k[i] * gcurr);
+        const float gnext = (fnext * k[i]) + gcurr;
+        acc += (gnext * v[i]);
+        gn[i] = gnext;
+        fcurr = fnext;
     }
     acc += (fnext * v[S]);
 #pragma unroll
-    for (int i = 0; i < SMAX - 1; ++i)
-        if (i < S - 1) g[i] = gn[i + 1];
-#pragma unroll
-    for (int i = 0; i < SMAX; ++i)
-        if (i == S - 1) g[i] = fnext;
+    for (int i = 0; i + 1 < S; ++i) g[i] = gn[i + 1];
+    if (S > 0) g[S - 1] = fnext;
     return acc;
 }
 
-__device__ __forceinline__ float biquad_step(float x, float& x1, float& x2, float& y1, float& y2,
-                                             const float* __restrict__ c)
+// arm_biquad_cascade_df1_f32 (.../arm_biquad_cascade_df1_f32.c:349-418), one stage
+__device__ __forceinline__ float biquad_step(float x, float& x1, float& x2, float& y1, float& y2, const float* c)
 {
     const float acc = (c[0] * x) + (c[1] * x1) + (c[2] * x2) + (c[3] * y1) + (c[4] * y2);
     x2 = x1; x1 = x; y2 = y1; y1 = acc;
     return acc;
 }
 
+// Math_log10f_fast, misc/uhsdr_math.c:26-39
 __device__ __forceinline__ float log10f_fast(float X)
 {
     int E;
@@ -444,217 +489,375 @@ __device__ __forceinline__ float log10f_fast(float X)
     return (Y * 0.3010299956639812f);
 }
 
+// float -> int32 as the x86 reference converts (cvttss2si: out of range / NaN -> INT32_MIN),
+// then << AUDIO_BIT_SHIFT (audio_driver.c:2911-2923)
 __device__ __forceinline__ int to_dma(float f)
 {
     const int v = (f > -2147483904.0f && f < 2147483648.0f) ? (int)f : INT32_MIN;
     return (int)((unsigned)v << 16);
 }
 
-#define BACK_WAVE 64
-#define GROUP 8
+#define BACK_CH 64
 
-__global__ void __launch_bounds__(BACK_WAVE) rx_back(BackArgs a)
+// PRE / AA lattice stages, L interpolation factor, PH polyphase length, W AGC window
+template <int PRE, int AA, int L, int PH, int W>
+__global__ void __launch_bounds__(2 * BACK_CH) rx_back(BackArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const uhsdr_rx_plan* __restrict__ P = a.plan;
-    const uhsdr_agc_plan* __restrict__ A = &P->agc;
-    const int lane = threadIdx.x;
-    const int cbase = blockIdx.x * BACK_WAVE;
-    const int c = cbase + lane;
+    const int lane = threadIdx.x & (BACK_CH - 1);
+    // 0: decimated-rate stage, 1: 48 ksps stage.  readfirstlane makes the role provably
+    // wave-uniform, so the role branches are scalar and plan loads stay on the scalar path.
+    const int role = __builtin_amdgcn_readfirstlane(threadIdx.x / BACK_CH);
+    const int c = blockIdx.x * BACK_CH + lane;
     const bool live = c < a.C;
     const int C = a.C;
-    const int W = A->attack_buffsize;
-    const int NG = (W + GROUP - 1) / GROUP;
-    const int L = P->interp_L, PH = P->interp_phase;
-    const int Nd = a.Nd;
-    const int ndc = BLK / P->decimation_rate;     // decimated samples per 32-frame call
+    constexpr int M = L;                                 // interpolation == decimation rate
+    constexpr int NDC = BLK / M;                         // decimated samples per 32-frame call
+    const int calls = a.N / BLK;
 
-    float* ring = smem;                            // [W][64]
-    float* gmax = ring + W * BACK_WAVE;            // [NG][64]
-    float* ostage = gmax + NG * BACK_WAVE;         // [64][BLK+1]
-    float* istage = ostage + BACK_WAVE * (BLK + 1);// [64][ndc+1]
+    float* ring = smem;                                  // [W][64]   AGC ring
+    float* sfx = ring + W * BACK_CH;                     // [W+1][64] suffix maxima of the previous block
+    float* mid = sfx + (W + 1) * BACK_CH;                // [2][BLK][64] 48 ksps hand-off
 
-    // ---- state in ----
-    float pre[UHSDR_MAX_LATTICE], aa[UHSDR_MAX_LATTICE], bq1[16], bq2[4], ip[UHSDR_MAX_INTERP];
-#pragma unroll
-    for (int i = 0; i < UHSDR_MAX_LATTICE; ++i)
+    if (role == 0)
     {
-        pre[i] = live ? a.s.pre[i * C + c] : 0.0f;
-        aa[i] = live ? a.s.aa[i * C + c] : 0.0f;
-    }
+        // ================= wave 0: lattice, AGC, scale, biquad_1, interpolator =================
+        // plan values copied to registers once (uniform -> SGPRs); reading them through P
+        // inside the loop would reload them every sample (the state stores may alias)
+        const uhsdr_agc_plan A = P->agc;
+        float pk[PRE > 0 ? PRE : 1], pv[PRE + 1], b1[20], ic[L * PH];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) bq1[i] = live ? a.s.bq1[i * C + c] : 0.0f;
+        for (int i = 0; i < PRE; ++i) pk[i] = P->pre_k[i];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bq2[i] = live ? a.s.bq2[i * C + c] : 0.0f;
+        for (int i = 0; i <= PRE; ++i) pv[i] = P->pre_v[i];
 #pragma unroll
-    for (int i = 0; i < UHSDR_MAX_INTERP; ++i) ip[i] = (live && i < 15) ? a.s.interp[i * C + c] : 0.0f;
-    for (int k = 0; k < W; ++k) ring[k * BACK_WAVE + lane] = live ? a.s.ring[(size_t)k * C + c] : 0.0f;
-    for (int gq = 0; gq < NG; ++gq)
-    {
-        float m = 0.0f;
-        for (int k = gq * GROUP; k < min(W, (gq + 1) * GROUP); ++k) m = fmaxf(m, fabsf(ring[k * BACK_WAVE + lane]));
-        gmax[gq * BACK_WAVE + lane] = m;
-    }
-    float ring_max = live ? a.s.agc[0 * C + c] : 0.0f;
-    float volts = live ? a.s.agc[1 * C + c] : 0.0f;
-    float save_volts = live ? a.s.agc[2 * C + c] : 0.0f;
-    float fast_bavg = live ? a.s.agc[3 * C + c] : 0.0f;
-    float hang_bavg = live ? a.s.agc[4 * C + c] : 0.0f;
-    float wold = live ? a.s.agc[5 * C + c] : 0.0f;
-    int hang_counter = live ? a.s.agci[0 * C + c] : 0;
-    int decay_type = live ? a.s.agci[1 * C + c] : 0;
-    int state = live ? a.s.agci[2 * C + c] : 0;
-
-    const int S_pre = P->pre_stages, S_aa = P->aa_stages;
-    const float scale = P->post_agc_scale, lo = P->line_out_scale;
-    int slot = a.ring_phase;
-
-    for (int call = 0; call < a.N / BLK; ++call)
-    {
-        // stage this call's decimated input (coalesced rows of ndc floats)
-        for (int e = lane; e < BACK_WAVE * ndc; e += BACK_WAVE)
+        for (int i = 0; i < 20; ++i) b1[i] = P->biquad1[i];
+#pragma unroll
+        for (int i = 0; i < L * PH; ++i) ic[i] = P->interp[i];
+        float pre[PRE > 0 ? PRE : 1], bq1[16], ip[PH > 1 ? PH - 1 : 1];
+#pragma unroll
+        for (int i = 0; i < PRE; ++i) pre[i] = live ? a.s.pre[i * C + c] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) bq1[i] = live ? a.s.bq1[i * C + c] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < PH - 1; ++i) ip[i] = live ? a.s.interp[i * C + c] : 0.0f;
+        const bool agc_on = A.mode != 5;
+        int slot = a.ring_phase;
+        // AGC look-ahead window maximum, van Herk / Gil-Werman: the ring's slots 0..W-1 form
+        // blocks; pmax = max |x| of the current block so far, sfx[k] = max |x| of the previous
+        // block's slots k..W-1.  max over the W newest = max(pmax, sfx[slot + 1]) -- exactly the
+        // value the reference's incremental rescan (audio_agc.c:409-429) maintains.
+        float pmax = 0.0f;
+        if (agc_on)
         {
-            const int row = e / ndc, col = e % ndc;
-            const int cc = cbase + row;
-            istage[row * (ndc + 1) + col] = (cc < C) ? a.adec[(size_t)cc * Nd + call * ndc + col] : 0.0f;
-        }
-        __syncthreads();
-        int oidx = 0;
-        for (int m = 0; m < ndc; ++m)
-        {
-            float x = istage[lane * (ndc + 1) + m];
-            if (S_pre > 0) x = lattice_step<UHSDR_MAX_LATTICE>(x, pre, P->pre_k, P->pre_v, S_pre);
-
-            // ---- AudioAgc_RunAgcWdsp, audio_agc.c:349-595 ----
-            if (A->mode == 5)
+            for (int k = 0; k < W; ++k)
             {
-                x = x * A->fixed_gain;
+                const float v = live ? a.s.ring[(size_t)k * C + c] : 0.0f;
+                ring[k * BACK_CH + lane] = v;
+                if (k < slot) pmax = fmaxf(pmax, fabsf(v));
             }
-            else
+            float sm = 0.0f;
+            sfx[W * BACK_CH + lane] = 0.0f;
+            for (int k = W - 1; k >= slot; --k)
             {
-                const float out_sample = ring[slot * BACK_WAVE + lane];
-                const float abs_out = fabsf(out_sample);
-                ring[slot * BACK_WAVE + lane] = x;
-                fast_bavg = A->fast_backmult * abs_out + A->onemfast_backmult * fast_bavg;
-                hang_bavg = A->hang_backmult * abs_out + A->onemhang_backmult * hang_bavg;
-                // ring_max == max |x| over the W newest samples (the reference's incremental
-                // rescan maintains exactly this window maximum; max is order independent)
-                const int gsel = slot / GROUP;
-                float gm = 0.0f;
-                for (int k = gsel * GROUP; k < min(W, (gsel + 1) * GROUP); ++k)
-                    gm = fmaxf(gm, fabsf(ring[k * BACK_WAVE + lane]));
-                gmax[gsel * BACK_WAVE + lane] = gm;
-                float rm = 0.0f;
-                for (int gq = 0; gq < NG; ++gq) rm = fmaxf(rm, gmax[gq * BACK_WAVE + lane]);
-                ring_max = rm;
-                if (++slot == W) slot = 0;
+                sm = fmaxf(sm, fabsf(ring[k * BACK_CH + lane]));
+                sfx[k * BACK_CH + lane] = sm;
+            }
+        }
+        float volts = live ? a.s.agc[1 * C + c] : 0.0f;
+        float save_volts = live ? a.s.agc[2 * C + c] : 0.0f;
+        float fast_bavg = live ? a.s.agc[3 * C + c] : 0.0f;
+        float hang_bavg = live ? a.s.agc[4 * C + c] : 0.0f;
+        float wold = live ? a.s.agc[5 * C + c] : 0.0f;
+        int hang_counter = live ? a.s.agci[0 * C + c] : 0;
+        int decay_type = live ? a.s.agci[1 * C + c] : 0;
+        int state = live ? a.s.agci[2 * C + c] : 0;
+        const float scale = P->post_agc_scale;
 
-                if (hang_counter > 0) --hang_counter;
-                const float rv = ring_max - volts;
-                switch (state)
+        // decimated input of call `it` is fetched one call ahead (hides the HBM latency)
+        float xnext[NDC];
+        auto fetch = [&](int call) {
+            const float* src = a.adec + (size_t)c * a.Nd + call * NDC;
+#pragma unroll
+            for (int m = 0; m < NDC; m += 4)
+            {
+                const float4 v = live ? *(const float4*)(src + m) : make_float4(0.f, 0.f, 0.f, 0.f);
+                xnext[m] = v.x; xnext[m + 1] = v.y; xnext[m + 2] = v.z; xnext[m + 3] = v.w;
+            }
+        };
+        fetch(0);
+        for (int it = 0; it <= calls; ++it)
+        {
+            if (it < calls)
+            {
+                float xin[NDC];
+#pragma unroll
+                for (int m = 0; m < NDC; ++m) xin[m] = xnext[m];
+                if (it + 1 < calls) fetch(it + 1);
+                float* mo = mid + (it & 1) * BLK * BACK_CH;
+#pragma unroll
+                for (int m = 0; m < NDC; ++m)
                 {
-                case 0:
-                    if (ring_max >= volts) volts += rv * A->attack_mult;
-                    else if (volts > A->pop_ratio * fast_bavg) { state = 1; volts += rv * A->fast_decay_mult; }
-                    else if (A->hang_enable && (hang_bavg > A->hang_level))
-                    { state = 2; hang_counter = A->hang_counter_init; decay_type = 1; }
-                    else { state = 3; volts += rv * A->decay_mult; decay_type = 0; }
-                    break;
-                case 1:
-                    if (ring_max >= volts) { state = 0; volts += rv * A->attack_mult; }
-                    else if (volts > save_volts) volts += rv * A->fast_decay_mult;
-                    else if (hang_counter > 0) state = 2;
-                    else if (decay_type == 0) { state = 3; volts += rv * A->decay_mult; }
-                    else { state = 4; volts += rv * A->hang_decay_mult; }
-                    break;
-                case 2:
-                    if (ring_max >= volts) { state = 0; save_volts = volts; volts += rv * A->attack_mult; }
-                    else if (hang_counter == 0) { state = 4; volts += rv * A->hang_decay_mult; }
-                    break;
-                case 3:
-                    if (ring_max >= volts) { state = 0; save_volts = volts; volts += rv * A->attack_mult; }
-                    else volts += rv * A->decay_mult;
-                    break;
-                default:
-                    if (ring_max >= volts) { state = 0; save_volts = volts; volts += rv * A->attack_mult; }
-                    else volts += rv * A->hang_decay_mult;
-                    break;
+                    float x = xin[m];
+                    if (PRE > 0) x = lattice_step<PRE>(x, pre, pk, pv);
+
+                    // ---- AudioAgc_RunAgcWdsp, audio_agc.c:349-595 ----
+                    if (!agc_on)
+                    {
+                        x = x * A.fixed_gain;
+                    }
+                    else
+                    {
+                        float* rs = ring + slot * BACK_CH + lane;
+                        const float out_sample = *rs;
+                        const float abs_out = fabsf(out_sample);
+                        *rs = x;
+                        fast_bavg = A.fast_backmult * abs_out + A.onemfast_backmult * fast_bavg;
+                        hang_bavg = A.hang_backmult * abs_out + A.onemhang_backmult * hang_bavg;
+                        pmax = fmaxf(pmax, fabsf(x));
+                        const float ring_max = fmaxf(pmax, sfx[(slot + 1) * BACK_CH + lane]);
+                        if (++slot == W)
+                        {
+                            // block complete: its suffix maxima serve the next W samples
+                            slot = 0;
+                            pmax = 0.0f;
+                            float sm = 0.0f;
+                            for (int k = W - 1; k >= 0; --k)
+                            {
+                                sm = fmaxf(sm, fabsf(ring[k * BACK_CH + lane]));
+                                sfx[k * BACK_CH + lane] = sm;
+                            }
+                        }
+                        if (hang_counter > 0) --hang_counter;
+                        // the 5-state attack / decay / hang machine (audio_agc.c:436-551), as
+                        // selects: m = the multiplier the taken branch applies (0: volts kept)
+                        const float rv = ring_max - volts;
+                        const bool atk = ring_max >= volts;
+                        float m = 0.0f;
+                        bool upd = false, save = false;
+                        int ns = state;
+                        if (state == 0)
+                        {
+                            const bool fast = volts > A.pop_ratio * fast_bavg;
+                            const bool hang = A.hang_enable && (hang_bavg > A.hang_level);
+                            ns = atk ? 0 : fast ? 1 : hang ? 2 : 3;
+                            upd = atk || fast || !hang;
+                            m = atk ? A.attack_mult : fast ? A.fast_decay_mult : A.decay_mult;
+                            if (!atk && !fast)
+                            {
+                                hang_counter = hang ? A.hang_counter_init : hang_counter;
+                                decay_type = hang ? 1 : 0;
+                            }
+                        }
+                        else if (state == 1)
+                        {
+                            const bool fd = volts > save_volts;
+                            const bool hc = hang_counter > 0;
+                            ns = atk ? 0 : fd ? 1 : hc ? 2 : (decay_type == 0) ? 3 : 4;
+                            upd = atk || fd || !hc;
+                            m = atk ? A.attack_mult : fd ? A.fast_decay_mult
+                                                          : (decay_type == 0) ? A.decay_mult : A.hang_decay_mult;
+                        }
+                        else if (state == 2)
+                        {
+                            const bool hz = hang_counter == 0;
+                            ns = atk ? 0 : hz ? 4 : 2;
+                            upd = atk || hz;
+                            save = atk;
+                            m = atk ? A.attack_mult : A.hang_decay_mult;
+                        }
+                        else
+                        {
+                            ns = atk ? 0 : state;
+                            upd = true;
+                            save = atk;
+                            m = atk ? A.attack_mult : (state == 3) ? A.decay_mult : A.hang_decay_mult;
+                        }
+                        state = ns;
+                        if (save) save_volts = volts;
+                        if (upd) volts += rv * m;
+                        if (volts < A.min_volts) volts = A.min_volts;
+                        float vo = log10f_fast(A.inv_max_input * volts);
+                        if (vo > 0.0f) vo = 0.0f;
+                        const float mult = (A.out_target - A.slope_constant * vo) / volts;
+                        x = out_sample * mult;
+                    }
+                    if (A.remove_dc)
+                    {
+                        const float w = (float)((double)x + (double)wold * 0.9999);
+                        x = w - wold;
+                        wold = w;
+                    }
+                    x = x * scale;
+#pragma unroll
+                    for (int st = 0; st < 4; ++st)
+                        x = biquad_step(x, bq1[4 * st], bq1[4 * st + 1], bq1[4 * st + 2], bq1[4 * st + 3], b1 + 5 * st);
+                    // ---- polyphase interpolator: output j uses phase L-1-j (arm_fir_interpolate_f32.c:482-575)
+                    float win[PH];
+#pragma unroll
+                    for (int t = 0; t < PH - 1; ++t) win[t] = ip[t];
+                    win[PH - 1] = x;
+#pragma unroll
+                    for (int i = L; i > 0; --i)
+                    {
+                        float sum = 0.0f;
+#pragma unroll
+                        for (int t = 0; t < PH; ++t) sum += win[t] * ic[(i - 1) + t * L];
+                        mo[(m * L + (L - i)) * BACK_CH + lane] = sum;
+                    }
+#pragma unroll
+                    for (int t = 0; t + 1 < PH; ++t) ip[t] = win[t + 1];
                 }
-                if (volts < A->min_volts) volts = A->min_volts;
-                float vo = log10f_fast(A->inv_max_input * volts);
-                if (vo > 0.0f) vo = 0.0f;
-                const float mult = (A->out_target - A->slope_constant * vo) / volts;
-                x = out_sample * mult;
             }
-            if (A->remove_dc)
-            {
-                const float w = (float)((double)x + (double)wold * 0.9999);
-                x = w - wold;
-                wold = w;
-            }
-            x = x * scale;
-#pragma unroll
-            for (int st = 0; st < 4; ++st)
-                x = biquad_step(x, bq1[4 * st], bq1[4 * st + 1], bq1[4 * st + 2], bq1[4 * st + 3], P->biquad1 + 5 * st);
-
-            // ---- polyphase interpolator (phase L-1-j for output j) ----
-            float win[UHSDR_MAX_INTERP];
-#pragma unroll
-            for (int t = 0; t < UHSDR_MAX_INTERP; ++t) win[t] = (t < PH - 1) ? ip[t] : 0.0f;
-#pragma unroll
-            for (int t = 0; t < UHSDR_MAX_INTERP; ++t)
-                if (t == PH - 1) win[t] = x;
-            for (int i = L; i > 0; --i)
-            {
-                float sum = 0.0f;
-#pragma unroll
-                for (int t = 0; t < UHSDR_MAX_INTERP; ++t)
-                    if (t < PH) sum += win[t] * P->interp[(i - 1) + t * L];
-                float y = sum;
-                if (S_aa > 0) y = lattice_step<UHSDR_MAX_LATTICE>(y, aa, P->aa_k, P->aa_v, S_aa);
-                y = biquad_step(y, bq2[0], bq2[1], bq2[2], bq2[3], P->biquad2);
-                y = y * lo;
-                ostage[lane * (BLK + 1) + oidx++] = y;
-            }
-#pragma unroll
-            for (int t = 0; t < UHSDR_MAX_INTERP - 1; ++t)
-                if (t < PH - 1) ip[t] = win[t + 1];
+            __syncthreads();
         }
-        __syncthreads();
-        // coalesced store of this call's 32 frames per channel
-        for (int e = lane; e < BACK_WAVE * BLK; e += BACK_WAVE)
+        if (live)
         {
-            const int row = e / BLK, col = e % BLK;
-            const int cc = cbase + row;
-            if (cc >= C) continue;
-            const float y = ostage[row * (BLK + 1) + col];
-            const size_t o = (size_t)cc * a.N + call * BLK + col;
-            if (a.audio) a.audio[o] = y;
-            if (a.dst) { const int d = to_dma(y); a.dst[o] = make_int2(d, d); }
+#pragma unroll
+            for (int i = 0; i < PRE; ++i) a.s.pre[i * C + c] = pre[i];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) a.s.bq1[i * C + c] = bq1[i];
+#pragma unroll
+            for (int i = 0; i < PH - 1; ++i) a.s.interp[i * C + c] = ip[i];
+            if (agc_on)
+                for (int k = 0; k < W; ++k) a.s.ring[(size_t)k * C + c] = ring[k * BACK_CH + lane];
+            a.s.agc[1 * C + c] = volts;
+            a.s.agc[2 * C + c] = save_volts;
+            a.s.agc[3 * C + c] = fast_bavg;
+            a.s.agc[4 * C + c] = hang_bavg;
+            a.s.agc[5 * C + c] = wold;
+            a.s.agci[0 * C + c] = hang_counter;
+            a.s.agci[1 * C + c] = decay_type;
+            a.s.agci[2 * C + c] = state;
         }
-        __syncthreads();
     }
+    else
+    {
+        // ================= wave 1: anti-alias lattice, biquad_2, line-out scale, store =========
+        float aa[AA > 0 ? AA : 1], bq2[4];
+        float ak[AA > 0 ? AA : 1], av[AA + 1], b2[5];
+#pragma unroll
+        for (int i = 0; i < AA; ++i) ak[i] = P->aa_k[i];
+#pragma unroll
+        for (int i = 0; i <= AA; ++i) av[i] = P->aa_v[i];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) b2[i] = P->biquad2[i];
+#pragma unroll
+        for (int i = 0; i < AA; ++i) aa[i] = live ? a.s.aa[i * C + c] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bq2[i] = live ? a.s.bq2[i * C + c] : 0.0f;
+        const float lo = P->line_out_scale;
+        for (int it = 0; it <= calls; ++it)
+        {
+            if (it > 0)
+            {
+                const int call = it - 1;
+                const float* mi = mid + (call & 1) * BLK * BACK_CH;
+                float* ao = a.audio ? a.audio + (size_t)c * a.N + call * BLK : nullptr;
+                int2* dd = a.dst ? a.dst + (size_t)c * a.N + call * BLK : nullptr;
+#pragma unroll
+                for (int n0 = 0; n0 < BLK; n0 += 4)
+                {
+                    float y[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                    {
+                        float v = mi[(n0 + j) * BACK_CH + lane];
+                        if (AA > 0) v = lattice_step<AA>(v, aa, ak, av);
+                        v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
+                        y[j] = v * lo;
+                    }
+                    if (live)
+                    {
+                        if (ao) *(float4*)(ao + n0) = make_float4(y[0], y[1], y[2], y[3]);
+                        if (dd)
+                        {
+                            const int d0 = to_dma(y[0]), d1 = to_dma(y[1]), d2 = to_dma(y[2]), d3 = to_dma(y[3]);
+                            *(int4*)(dd + n0) = make_int4(d0, d0, d1, d1);
+                            *(int4*)(dd + n0 + 2) = make_int4(d2, d2, d3, d3);
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (live)
+        {
+#pragma unroll
+            for (int i = 0; i < AA; ++i) a.s.aa[i * C + c] = aa[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a.s.bq2[i * C + c] = bq2[i];
+        }
+    }
+}
 
-    // ---- state out ----
-    if (!live) return;
-#pragma unroll
-    for (int i = 0; i < UHSDR_MAX_LATTICE; ++i) { a.s.pre[i * C + c] = pre[i]; a.s.aa[i * C + c] = aa[i]; }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) a.s.bq1[i * C + c] = bq1[i];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a.s.bq2[i * C + c] = bq2[i];
-#pragma unroll
-    for (int i = 0; i < 15; ++i) a.s.interp[i * C + c] = ip[i];
-    for (int k = 0; k < W; ++k) a.s.ring[(size_t)k * C + c] = ring[k * BACK_WAVE + lane];
-    a.s.agc[0 * C + c] = ring_max;
-    a.s.agc[1 * C + c] = volts;
-    a.s.agc[2 * C + c] = save_volts;
-    a.s.agc[3 * C + c] = fast_bavg;
-    a.s.agc[4 * C + c] = hang_bavg;
-    a.s.agc[5 * C + c] = wold;
-    a.s.agci[0 * C + c] = hang_counter;
-    a.s.agci[1 * C + c] = decay_type;
-    a.s.agci[2 * C + c] = state;
+// ------------------------------------------------------------------------------------
+// kernel selection: the filter-path families of FilterPathInfo (audio_filter.c:147-922)
+
+typedef void (*front_fn)(FrontArgs);
+typedef void (*back_fn)(BackArgs);
+
+struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; };
+struct BackVariant { int pre, aa, L, ph, w; back_fn fn; };
+
+// R = FIR outputs per lane: 16 for large batches (more MACs per window load), 8 for small
+// batches (twice the waves in flight)
+static const FrontVariant kFront[] = {
+    { 89, 43, 4, 0, rx_front<89, 43, 4, false, 16>, 16 },     // wide SSB/CW  (P48-54)
+    { 89, 43, 4, 0, rx_front<89, 43, 4, false, 8>, 8 },
+    { 89, 4, 2, 0, rx_front<89, 4, 2, false, 16>, 16 },       // 24 ksps SSB   (P55-65)
+    { 89, 4, 2, 0, rx_front<89, 4, 2, false, 8>, 8 },
+    { 83, 199, 4, 1, rx_front<83, 199, 4, true, 16>, 16 },    // narrow SSB/CW (P4-47)
+    { 83, 199, 4, 1, rx_front<83, 199, 4, true, 8>, 8 },
+};
+
+static const BackVariant kBack[] = {
+    { 10, 6, 4, 1, 49, rx_back<10, 6, 4, 1, 49> },
+    { 10, 0, 4, 4, 49, rx_back<10, 0, 4, 4, 49> },
+    { 0, 0, 2, 8, 97, rx_back<0, 0, 2, 8, 97> },
+    { 0, 6, 2, 2, 97, rx_back<0, 6, 2, 2, 97> },
+    { 10, 0, 2, 8, 97, rx_back<10, 0, 2, 8, 97> },
+    { 8, 0, 2, 8, 97, rx_back<8, 0, 2, 8, 97> },
+    { 8, 6, 2, 2, 97, rx_back<8, 6, 2, 2, 97> },
+};
+
+// frames handled by one front launch: one wave covers a channel's launch block
+static int front_frames(int N, int R) { return N < FRONT_WAVE * R ? N : FRONT_WAVE * R; }
+
+// C, N == 0: any R (support query)
+static const FrontVariant* find_front(const uhsdr_rx_plan& p, long long C = 0, int N = 0)
+{
+    const int t1 = p.use_decimated_iq ? p.dec_taps : p.hilbert_taps;
+    const int t2 = p.use_decimated_iq ? p.hilbert_taps : p.dec_taps;
+    const FrontVariant* best = nullptr;
+    long long best_waves = 0;
+    for (const FrontVariant& v : kFront)
+        if (v.t1 == t1 && v.t2 == t2 && v.m == p.decimation_rate && v.decim_first == p.use_decimated_iq)
+        {
+            if (N && N % v.R) continue;
+            // waves one launch puts on the chip; prefer R = 16 once there are >= 4 per SIMD
+            const int nf = N ? front_frames(N, v.R) : 0;
+            const long long waves = N ? (C + FRONT_WAVE / (nf / v.R) - 1) / (FRONT_WAVE / (nf / v.R)) : 0;
+            if (!best) { best = &v; best_waves = waves; continue; }
+            const bool big_v = waves >= 4096, big_b = best_waves >= 4096;
+            if (N == 0 ? v.R > best->R
+                       : (big_v && big_b ? v.R > best->R : (big_v != big_b ? big_v : waves > best_waves)))
+            {
+                best = &v;
+                best_waves = waves;
+            }
+        }
+    return best;
+}
+
+static const BackVariant* find_back(const uhsdr_rx_plan& p)
+{
+    for (const BackVariant& v : kBack)
+        if (v.pre == p.pre_stages && v.aa == p.aa_stages && v.L == p.interp_L && v.ph == p.interp_phase &&
+            v.w == p.agc.attack_buffsize)
+            return &v;
+    return nullptr;
 }
 
 // ------------------------------------------------------------------------------------
@@ -664,8 +867,10 @@ struct uhsdr_rx_s
 {
     uhsdr_rx_plan plan;
     uhsdr_rx_plan* d_plan;
-    int C, N, Nd, G;
-    int T1, T1pad, T2, T2pad;
+    const FrontVariant* fv;
+    const BackVariant* bv;
+    int C, N, Nd, Nf;        // Nf: frames per front launch (N split into N / Nf launches)
+    int T1, T2;
     hipStream_t stream;
     // front state
     float *hist1_i, *hist1_q, *hist2_i, *hist2_q, *teta, *osc, *adec;
@@ -674,10 +879,11 @@ struct uhsdr_rx_s
     void* arena;
     size_t arena_bytes;
     long long dec_samples;   // decimated samples processed (AGC ring phase)
-    int kernels_last;
+    long long calls_done;
+    long long front_launches; // oscillator ping-pong parity
     // per-kernel timing (uhsdr_rx_enable_timing)
     int timing;
-    int nev;                 // events used
+    int nev;
     int nev_cap;
     hipEvent_t* ev;          // [cap][2 kernels][start, stop]
     float total_ms[2];
@@ -686,11 +892,9 @@ struct uhsdr_rx_s
 
 static const char* kKernelNames[2] = { "rx_front", "rx_back" };
 
-// record event slot (kernel k, 0=start / 1=stop) of the current timed call
 static void time_mark(uhsdr_rx_s* h, int k, int which)
 {
-    if (!h->timing) return;
-    if (h->nev >= h->nev_cap) return;
+    if (!h->timing || h->nev >= h->nev_cap) return;
     (void)hipEventRecord(h->ev[(size_t)h->nev * 4 + 2 * k + which], h->stream);
 }
 
@@ -713,39 +917,42 @@ static void time_harvest(uhsdr_rx_s* h)
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { uhsdr_set_error("%s: %s", #x, hipGetErrorString(e_)); return UHSDR_DEVICE_ERROR; } } while (0)
 
-static int pad8(int t) { return (t + 7) & ~7; }
-
-static size_t front_lds(const uhsdr_rx_s* h, int G)
+// LDS of one front workgroup (one wave): must match the carve-up in rx_front
+static size_t front_lds(const uhsdr_rx_s* h)
 {
-    const int N = h->N;
-    const bool dq = h->plan.use_decimated_iq;
-    const int N2 = dq ? N / h->plan.decimation_rate : N;
-    size_t L1 = sk_len(h->T1 - 1 + N + 8), L2 = sk_len(h->T2 - 1 + N2 + 8);
-    size_t f = 2 * G * L1 + (dq ? 2 : 1) * G * L2 + 2 * G * (N / BLK);
+    const int N = h->Nf;
+    const bool df = h->plan.use_decimated_iq;
+    const int N2 = df ? N / h->plan.decimation_rate : N;
+    const int cpw = FRONT_WAVE / (N / h->fv->R);
+    size_t f = ((size_t)cpw * window_pitch(h->T1, h->T2, N, N2, front_sh2(df, h->fv->R, h->plan.decimation_rate)) + 3) & ~(size_t)3;
+    const int th = df ? h->T2 : h->T1, td = df ? h->T1 : h->T2;
+    f += 2 * ((th + 7) & ~7) + ((td + 7) & ~7);
+    if (h->plan.iq_auto_correction) f += 2 * cpw * (N / BLK);
+    if (h->plan.freq_shift_hz != 0 && h->plan.shift_kind == 2) f += 2 * N;
     return f * sizeof(float);
 }
 
 static size_t back_lds(const uhsdr_rx_s* h)
 {
-    const int W = h->plan.agc.attack_buffsize > 0 ? h->plan.agc.attack_buffsize : 1;
-    const int NG = (W + GROUP - 1) / GROUP;
-    const int ndc = BLK / h->plan.decimation_rate;
-    return sizeof(float) * (size_t)BACK_WAVE * (W + NG + (BLK + 1) + (ndc + 1));
+    return sizeof(float) * (size_t)BACK_CH * (2 * h->bv->w + 1 + 2 * BLK);
+}
+
+extern "C" int uhsdr_rx_plan_supported(const uhsdr_rx_plan* p)
+{
+    return p && uhsdr_rx_mode_supported(p) && find_front(*p) && find_back(*p);
 }
 
 extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
     HIPCHK(hipMemsetAsync(h->arena, 0, h->arena_bytes, h->stream));
-    // oscillator starts at {I=0, Q=1} (freq_shift.c:48-49)
-    float* one = (float*)malloc(sizeof(float) * h->C);
-    for (int i = 0; i < h->C; ++i) one[i] = 1.0f;
-    hipError_t e = hipMemcpyAsync(h->osc + h->C, one, sizeof(float) * h->C, hipMemcpyHostToDevice, h->stream);
-    hipError_t e2 = hipStreamSynchronize(h->stream);
-    free(one);
-    HIPCHK(e);
-    HIPCHK(e2);
+    // oscillator starts at {I=0, Q=1} (freq_shift.c:48-49); both ping-pong copies
+    const float osc0[4] = { 0.0f, 1.0f, 0.0f, 1.0f };
+    HIPCHK(hipMemcpyAsync(h->osc, osc0, sizeof osc0, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
     h->dec_samples = 0;
+    h->calls_done = 0;
+    h->front_launches = 0;
     return UHSDR_OK;
 }
 
@@ -758,28 +965,30 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     uhsdr_rx_s* h = (uhsdr_rx_s*)calloc(1, sizeof(uhsdr_rx_s));
     uhsdr_status st = uhsdr_rx_plan_build(cfg, &h->plan);
     if (st != UHSDR_OK) { free(h); return st; }
-    if (!uhsdr_rx_plan_supported(&h->plan)) { free(h); uhsdr_set_error("demodulation mode %d not supported on device", cfg->dmod_mode); return UHSDR_UNSUPPORTED; }
     const uhsdr_rx_plan& p = h->plan;
+    h->fv = find_front(p, C, N);
+    h->bv = find_back(p);
+    if (!uhsdr_rx_mode_supported(&p) || !h->fv || !h->bv)
+    {
+        free(h);
+        uhsdr_set_error("demodulation mode %d / filter path %d not implemented on the device", cfg->dmod_mode,
+                        cfg->filter_path);
+        return UHSDR_UNSUPPORTED;
+    }
     h->C = C; h->N = N; h->Nd = N / p.decimation_rate;
     h->stream = (hipStream_t)stream;
-    if (p.use_decimated_iq) { h->T1 = p.dec_taps; h->T2 = p.hilbert_taps; }
-    else { h->T1 = p.hilbert_taps; h->T2 = p.dec_taps; }
-    h->T1pad = pad8(h->T1); h->T2pad = pad8(h->T2);
-    // channels per front workgroup: enough FIR blocks for 256 lanes, LDS <= 64 KiB
-    int G = (256 * 8) / N;
-    if (G < 1) G = 1;
-    if (G > 64) G = 64;
-    while (G > 1 && front_lds(h, G) > 64 * 1024) --G;
-    if (front_lds(h, G) > 160 * 1024) { free(h); uhsdr_set_error("block too long for LDS"); return UHSDR_LENGTH_ERROR; }
-    h->G = G;
-    const int W = p.agc.attack_buffsize > 0 ? p.agc.attack_buffsize : 1;
+    h->T1 = h->fv->t1; h->T2 = h->fv->t2;
+    h->Nf = front_frames(N, h->fv->R);
+    if (N % h->Nf) { free(h); uhsdr_set_error("frames_per_call %d not a multiple of %d", N, h->Nf); return UHSDR_LENGTH_ERROR; }
+    if (front_lds(h) > 64 * 1024) { free(h); uhsdr_set_error("frames_per_call too long for LDS"); return UHSDR_LENGTH_ERROR; }
+    const int W = h->bv->w;
 
-    // one arena: [front histories][teta][osc][back state]; adec separate (not state)
     size_t fl = 0;
     auto take = [&](size_t n) { size_t o = fl; fl += (n + 63) & ~(size_t)63; return o; };
-    const size_t o_h1i = take((size_t)C * (h->T1 - 1)), o_h1q = take((size_t)C * (h->T1 - 1));
-    const size_t o_h2i = take((size_t)C * (h->T2 - 1)), o_h2q = take((size_t)C * (h->T2 - 1));
-    const size_t o_teta = take((size_t)3 * C), o_osc = take((size_t)2 * C);
+    const size_t hs1 = (h->T1 - 1 + 3) & ~3, hs2 = (h->T2 - 1 + 3) & ~3;   // padded history rows
+    const size_t o_h1i = take((size_t)C * hs1), o_h1q = take((size_t)C * hs1);
+    const size_t o_h2i = take((size_t)C * hs2), o_h2q = take((size_t)C * hs2);
+    const size_t o_teta = take((size_t)3 * C), o_osc = take(4);
     const size_t o_pre = take((size_t)10 * C), o_aa = take((size_t)10 * C), o_bq1 = take((size_t)16 * C);
     const size_t o_bq2 = take((size_t)4 * C), o_ip = take((size_t)15 * C), o_ring = take((size_t)W * C);
     const size_t o_agc = take((size_t)6 * C), o_agci = take((size_t)3 * C);
@@ -818,23 +1027,25 @@ extern "C" uhsdr_status uhsdr_rx_set_stream(uhsdr_rx_handle h, void* stream)
 extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, int32_t* dst)
 {
     if (!h || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
-    const uhsdr_rx_plan& p = h->plan;
-    FrontArgs fa;
-    fa.plan = h->d_plan;
-    fa.iq = (const int2*)iq;
-    fa.hist1_i = h->hist1_i; fa.hist1_q = h->hist1_q; fa.hist2_i = h->hist2_i; fa.hist2_q = h->hist2_q;
-    fa.teta = h->teta; fa.osc = h->osc; fa.adec = h->adec;
-    fa.C = h->C; fa.N = h->N; fa.G = h->G;
-    fa.T1 = h->T1; fa.T1pad = h->T1pad; fa.T2 = h->T2; fa.T2pad = h->T2pad;
-    const dim3 fgrid((h->C + h->G - 1) / h->G);
-    const size_t flds = front_lds(h, h->G);
     if (h->timing && h->nev >= h->nev_cap) time_harvest(h);
     time_mark(h, 0, 0);
-    if (p.decimation_rate == 4)
-        hipLaunchKernelGGL((rx_front<8, 4>), fgrid, dim3(256), flds, h->stream, fa);
-    else
-        hipLaunchKernelGGL((rx_front<8, 2>), fgrid, dim3(256), flds, h->stream, fa);
-    HIPCHK(hipGetLastError());
+    const int cpw = FRONT_WAVE / (h->Nf / h->fv->R);
+    const size_t lds = front_lds(h);
+    for (int f0 = 0; f0 < h->N; f0 += h->Nf)
+    {
+        FrontArgs fa;
+        fa.plan = h->d_plan;
+        fa.iq = (const int2*)iq + f0;
+        fa.hist1_i = h->hist1_i; fa.hist1_q = h->hist1_q; fa.hist2_i = h->hist2_i; fa.hist2_q = h->hist2_q;
+        fa.teta = h->teta;
+        fa.osc_in = h->osc + 2 * (h->front_launches & 1);     // ping-pong: read one copy, write the other
+        fa.osc_out = h->osc + 2 * ((h->front_launches + 1) & 1);
+        fa.adec = h->adec + f0 / h->plan.decimation_rate;
+        fa.C = h->C; fa.N = h->Nf; fa.ld = h->N; fa.ldd = h->Nd;
+        hipLaunchKernelGGL(h->fv->fn, dim3((h->C + cpw - 1) / cpw), dim3(FRONT_WAVE), lds, h->stream, fa);
+        HIPCHK(hipGetLastError());
+        h->front_launches += 1;
+    }
     time_mark(h, 0, 1);
 
     BackArgs ba;
@@ -844,15 +1055,14 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
     ba.dst = (int2*)dst;
     ba.s = h->bs;
     ba.C = h->C; ba.N = h->N; ba.Nd = h->Nd;
-    const int W = p.agc.attack_buffsize > 0 ? p.agc.attack_buffsize : 1;
-    ba.ring_phase = (int)(h->dec_samples % W);
+    ba.ring_phase = (int)(h->dec_samples % h->bv->w);
     time_mark(h, 1, 0);
-    hipLaunchKernelGGL(rx_back, dim3((h->C + BACK_WAVE - 1) / BACK_WAVE), dim3(BACK_WAVE), back_lds(h), h->stream, ba);
+    hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(2 * BACK_CH), back_lds(h), h->stream, ba);
     HIPCHK(hipGetLastError());
     time_mark(h, 1, 1);
     if (h->timing) h->nev++;
     h->dec_samples += h->Nd;
-    h->kernels_last = 2;
+    h->calls_done += 1;
     return UHSDR_OK;
 }
 

@@ -368,13 +368,13 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
     return UHSDR_OK;
 }
 
-int uhsdr_rx_plan_supported(const uhsdr_rx_plan* p)
+/* uhsdr_rx_plan_supported() lives with the device kernels (uhsdr_rx.hip): it answers
+   whether a kernel variant exists for the plan's filter-path family. */
+int uhsdr_rx_mode_supported(const uhsdr_rx_plan* p)
 {
-    /* device chain: SSB / CW / DIGI demodulation (I +- Q) on every filter path */
+    /* device chain: SSB / CW / DIGI demodulation (I +- Q) */
     if (!p) return 0;
-    if (p->dmod_mode == UHSDR_DEMOD_AM || p->dmod_mode == UHSDR_DEMOD_SAM || p->dmod_mode == UHSDR_DEMOD_FM)
-        return 0;
-    return 1;
+    return !(p->dmod_mode == UHSDR_DEMOD_AM || p->dmod_mode == UHSDR_DEMOD_SAM || p->dmod_mode == UHSDR_DEMOD_FM);
 }
 
 const char* uhsdr_version(void) { return "uhsdr_amd 0.1 (gfx950)"; }

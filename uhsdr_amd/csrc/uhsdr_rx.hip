@@ -418,6 +418,17 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
 // ------------------------------------------------------------------------------------
 // rx_back: per-channel recursions.  State arrays are [field][C] (lane-coalesced).
 
+// AGC look-ahead window (AudioAgc_RunAgcWdsp, audio_agc.c:365-429): the sample leaving the
+// ring is the one W = attack_buffsize samples old, and ring_max is the maximum |x| of the W
+// newest samples.  With B decimated samples per 32-frame call, W = Q*B + 1 for both rates
+// (12 ksps: 49 = 6*8 + 1; 24 ksps: 97 = 6*16 + 1), so for sample j of call k the window is
+//   prefix of call k [0..j]  +  calls k-1 .. k-Q+1 whole  +  suffix of call k-Q [j..B-1]
+// and the leaving sample is call k-Q's sample j-1 (j > 0) or call k-Q-1's last sample.
+// Per channel the kernel keeps in HBM the last Q calls' AGC inputs ([Q][B][C]: call k
+// overwrites the slot of call k-Q after reading it), the Q-1 whole-call maxima and call
+// k-Q-1's last sample.  max() is exact, so this equals the reference's incremental rescan.
+constexpr int AGC_Q = 6;
+
 struct BackState
 {
     float* pre;      // [10][C]
@@ -425,8 +436,8 @@ struct BackState
     float* bq1;      // [16][C]
     float* bq2;      // [4][C]
     float* interp;   // [15][C]
-    float* ring;     // [W][C]   AGC look-ahead ring, slot = sample index mod W
-    float* agc;      // [6][C]   spare volts save_volts fast_bavg hang_bavg wold
+    float* ring;     // [AGC_Q][B][C]  AGC inputs of the last AGC_Q calls
+    float* agc;      // [6 + AGC_Q][C]  spare volts save_volts fast_bavg hang_bavg wold | call maxima[Q-1], leaving sample
     int* agci;       // [3][C]   hang_counter decay_type state
 };
 
@@ -438,7 +449,7 @@ struct BackArgs
     int2* dst;           // [C][N]  or null
     BackState s;
     int C, N, Nd;
-    int ring_phase;      // (decimated samples processed so far) mod W
+    int ring_phase;      // (32-frame calls processed so far) mod AGC_Q
 };
 
 // arm_iir_lattice_f32 (CMSIS .../arm_iir_lattice_f32.c:348-447), one sample, S stages:
@@ -498,298 +509,352 @@ __device__ __forceinline__ int to_dma(float f)
 }
 
 #define BACK_CH 64
+#define BACK_ROLES 3
 
-// PRE / AA lattice stages, L interpolation factor, PH polyphase length, W AGC window
-template <int PRE, int AA, int L, int PH, int W>
-__global__ void __launch_bounds__(2 * BACK_CH) rx_back(BackArgs a)
+// The back end of one channel group runs as a 3-stage pipeline over 32-frame calls, one wave
+// per stage (lane == channel); stage s works on call it - s in iteration it and hands its
+// results to stage s+1 through double-buffered LDS, one workgroup barrier per iteration:
+//   role 0  lattice pre-filter -> WDSP AGC                    (decimated rate)
+//   role 1  post-AGC scale -> biquad_1 -> polyphase interp    (decimated rate -> 48 ksps)
+//   role 2  anti-alias lattice -> biquad_2 -> line-out scale -> f32 / int32 stores (48 ksps)
+// Splitting the serial chain three ways shortens the critical path per call (small batches)
+// and keeps each wave's coefficients + state small enough for 4 waves per SIMD (large ones).
+struct BackLds
 {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const uhsdr_rx_plan* __restrict__ P = a.plan;
-    const int lane = threadIdx.x & (BACK_CH - 1);
-    // 0: decimated-rate stage, 1: 48 ksps stage.  readfirstlane makes the role provably
-    // wave-uniform, so the role branches are scalar and plan loads stay on the scalar path.
-    const int role = __builtin_amdgcn_readfirstlane(threadIdx.x / BACK_CH);
-    const int c = blockIdx.x * BACK_CH + lane;
-    const bool live = c < a.C;
-    const int C = a.C;
-    constexpr int M = L;                                 // interpolation == decimation rate
-    constexpr int NDC = BLK / M;                         // decimated samples per 32-frame call
-    const int calls = a.N / BLK;
+    float* agc;   // [2][NDC][64]  role 0 -> role 1
+    float* mid;   // [2][BLK][64]  role 1 -> role 2
+};
 
-    float* ring = smem;                                  // [W][64]   AGC ring
-    float* sfx = ring + W * BACK_CH;                     // [W+1][64] suffix maxima of the previous block
-    float* mid = sfx + (W + 1) * BACK_CH;                // [2][BLK][64] 48 ksps hand-off
+template <int NDC>
+__device__ __forceinline__ BackLds back_lds_carve(float* smem)
+{
+    BackLds l;
+    l.mid = smem;
+    l.agc = smem + 2 * BLK * BACK_CH;
+    return l;
+}
 
-    if (role == 0)
-    {
-        // ================= wave 0: lattice, AGC, scale, biquad_1, interpolator =================
-        // plan values copied to registers once (uniform -> SGPRs); reading them through P
-        // inside the loop would reload them every sample (the state stores may alias)
-        const uhsdr_agc_plan A = P->agc;
-        float pk[PRE > 0 ? PRE : 1], pv[PRE + 1], b1[20], ic[L * PH];
+#define BACK_PROLOGUE                                                                          \
+    const uhsdr_rx_plan* __restrict__ P = a.plan;                                              \
+    const int lane = threadIdx.x & (BACK_CH - 1);                                              \
+    const int c = blockIdx.x * BACK_CH + lane;                                                 \
+    const bool live = c < a.C;                                                                 \
+    const int cl = live ? c : a.C - 1; /* loads clamped: no exec-masked load branches */       \
+    const int C = a.C;                                                                         \
+    constexpr int NDC = BLK / L;       /* decimated samples per 32-frame call */               \
+    const int calls = a.N / BLK;                                                               \
+    (void)P; (void)live;
+
+// ---- role 0: IIR lattice pre-filter (audio_driver.c:2473-2482) + AudioAgc_RunAgcWdsp ----
+template <int PRE, int L, int W>
+__device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
+{
+    BACK_PROLOGUE
+    static_assert(W == AGC_Q * NDC + 1, "AGC window must be AGC_Q calls + 1 sample");
+    // plan values copied to registers once (uniform -> SGPRs); reading them through P
+    // inside the loop would reload them every sample (the state stores may alias)
+    const uhsdr_agc_plan A = P->agc;
+    float pk[PRE > 0 ? PRE : 1], pv[PRE + 1];
 #pragma unroll
-        for (int i = 0; i < PRE; ++i) pk[i] = P->pre_k[i];
+    for (int i = 0; i < PRE; ++i) pk[i] = P->pre_k[i];
 #pragma unroll
-        for (int i = 0; i <= PRE; ++i) pv[i] = P->pre_v[i];
+    for (int i = 0; i <= PRE; ++i) pv[i] = P->pre_v[i];
+    float pre[PRE > 0 ? PRE : 1];
 #pragma unroll
-        for (int i = 0; i < 20; ++i) b1[i] = P->biquad1[i];
+    for (int i = 0; i < PRE; ++i) pre[i] = a.s.pre[i * C + cl];
+    const bool agc_on = A.mode != 5;
+    float volts = a.s.agc[1 * C + cl];
+    float save_volts = a.s.agc[2 * C + cl];
+    float fast_bavg = a.s.agc[3 * C + cl];
+    float hang_bavg = a.s.agc[4 * C + cl];
+    float wold = a.s.agc[5 * C + cl];
+    float cmax[AGC_Q - 1];                               // maxima of calls k-Q+1 .. k-1 (oldest first)
 #pragma unroll
-        for (int i = 0; i < L * PH; ++i) ic[i] = P->interp[i];
-        float pre[PRE > 0 ? PRE : 1], bq1[16], ip[PH > 1 ? PH - 1 : 1];
+    for (int i = 0; i < AGC_Q - 1; ++i) cmax[i] = a.s.agc[(6 + i) * C + cl];
+    float leave_last = a.s.agc[(5 + AGC_Q) * C + cl];   // last sample of call k-Q-1
+    int hang_counter = a.s.agci[0 * C + cl];
+    int decay_type = a.s.agci[1 * C + cl];
+    int state = a.s.agci[2 * C + cl];
+
+    // the decimated input and the ring slot of call `it` are fetched one call ahead
+    float xnext[NDC], rnext[NDC];
+    auto fetch = [&](int call) {
+        const float* src = a.adec + (size_t)cl * a.Nd + call * NDC;
 #pragma unroll
-        for (int i = 0; i < PRE; ++i) pre[i] = live ? a.s.pre[i * C + c] : 0.0f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) bq1[i] = live ? a.s.bq1[i * C + c] : 0.0f;
-#pragma unroll
-        for (int i = 0; i < PH - 1; ++i) ip[i] = live ? a.s.interp[i * C + c] : 0.0f;
-        const bool agc_on = A.mode != 5;
-        int slot = a.ring_phase;
-        // AGC look-ahead window maximum, van Herk / Gil-Werman: the ring's slots 0..W-1 form
-        // blocks; pmax = max |x| of the current block so far, sfx[k] = max |x| of the previous
-        // block's slots k..W-1.  max over the W newest = max(pmax, sfx[slot + 1]) -- exactly the
-        // value the reference's incremental rescan (audio_agc.c:409-429) maintains.
-        float pmax = 0.0f;
+        for (int m = 0; m < NDC; m += 4)
+        {
+            const float4 v = *(const float4*)(src + m);
+            xnext[m] = v.x; xnext[m + 1] = v.y; xnext[m + 2] = v.z; xnext[m + 3] = v.w;
+        }
         if (agc_on)
         {
-            for (int k = 0; k < W; ++k)
-            {
-                const float v = live ? a.s.ring[(size_t)k * C + c] : 0.0f;
-                ring[k * BACK_CH + lane] = v;
-                if (k < slot) pmax = fmaxf(pmax, fabsf(v));
-            }
-            float sm = 0.0f;
-            sfx[W * BACK_CH + lane] = 0.0f;
-            for (int k = W - 1; k >= slot; --k)
-            {
-                sm = fmaxf(sm, fabsf(ring[k * BACK_CH + lane]));
-                sfx[k * BACK_CH + lane] = sm;
-            }
+            const int slot = (a.ring_phase + call) % AGC_Q;
+            const float* rs = a.s.ring + (size_t)slot * NDC * C + cl;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) rnext[m] = rs[(size_t)m * C];
         }
-        float volts = live ? a.s.agc[1 * C + c] : 0.0f;
-        float save_volts = live ? a.s.agc[2 * C + c] : 0.0f;
-        float fast_bavg = live ? a.s.agc[3 * C + c] : 0.0f;
-        float hang_bavg = live ? a.s.agc[4 * C + c] : 0.0f;
-        float wold = live ? a.s.agc[5 * C + c] : 0.0f;
-        int hang_counter = live ? a.s.agci[0 * C + c] : 0;
-        int decay_type = live ? a.s.agci[1 * C + c] : 0;
-        int state = live ? a.s.agci[2 * C + c] : 0;
-        const float scale = P->post_agc_scale;
-
-        // decimated input of call `it` is fetched one call ahead (hides the HBM latency)
-        float xnext[NDC];
-        auto fetch = [&](int call) {
-            const float* src = a.adec + (size_t)c * a.Nd + call * NDC;
-#pragma unroll
-            for (int m = 0; m < NDC; m += 4)
-            {
-                const float4 v = live ? *(const float4*)(src + m) : make_float4(0.f, 0.f, 0.f, 0.f);
-                xnext[m] = v.x; xnext[m + 1] = v.y; xnext[m + 2] = v.z; xnext[m + 3] = v.w;
-            }
-        };
-        fetch(0);
-        for (int it = 0; it <= calls; ++it)
+    };
+    fetch(0);
+    for (int it = 0; it < calls + BACK_ROLES - 1; ++it)
+    {
+        if (it < calls)
         {
-            if (it < calls)
+            float xin[NDC], old[NDC];
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) { xin[m] = xnext[m]; old[m] = rnext[m]; }
+            if (it + 1 < calls) fetch(it + 1);
+            // suffix maxima of call k-Q; maximum of the whole calls k-Q+1 .. k-1
+            float sfx[NDC];
+            sfx[NDC - 1] = fabsf(old[NDC - 1]);
+#pragma unroll
+            for (int m = NDC - 2; m >= 0; --m) sfx[m] = fmaxf(sfx[m + 1], fabsf(old[m]));
+            float wmax = cmax[0];
+#pragma unroll
+            for (int i = 1; i < AGC_Q - 1; ++i) wmax = fmaxf(wmax, cmax[i]);
+            float pmax = 0.0f;
+            float* ring_out = a.s.ring + (size_t)((a.ring_phase + it) % AGC_Q) * NDC * C + c;
+            float* ao = lds.agc + (it & 1) * NDC * BACK_CH + lane;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m)
             {
-                float xin[NDC];
-#pragma unroll
-                for (int m = 0; m < NDC; ++m) xin[m] = xnext[m];
-                if (it + 1 < calls) fetch(it + 1);
-                float* mo = mid + (it & 1) * BLK * BACK_CH;
-#pragma unroll
-                for (int m = 0; m < NDC; ++m)
+                float x = xin[m];
+                if (PRE > 0) x = lattice_step<PRE>(x, pre, pk, pv);
+                // ---- AudioAgc_RunAgcWdsp, audio_agc.c:349-595 ----
+                if (!agc_on)
                 {
-                    float x = xin[m];
-                    if (PRE > 0) x = lattice_step<PRE>(x, pre, pk, pv);
-
-                    // ---- AudioAgc_RunAgcWdsp, audio_agc.c:349-595 ----
-                    if (!agc_on)
+                    x = x * A.fixed_gain;
+                }
+                else
+                {
+                    const float out_sample = m ? old[m - 1] : leave_last;
+                    const float abs_out = fabsf(out_sample);
+                    if (live) ring_out[(size_t)m * C] = x;
+                    fast_bavg = A.fast_backmult * abs_out + A.onemfast_backmult * fast_bavg;
+                    hang_bavg = A.hang_backmult * abs_out + A.onemhang_backmult * hang_bavg;
+                    pmax = fmaxf(pmax, fabsf(x));
+                    const float ring_max = fmaxf(fmaxf(pmax, wmax), sfx[m]);
+                    if (hang_counter > 0) --hang_counter;
+                    // the 5-state attack / decay / hang machine (audio_agc.c:436-551), as
+                    // selects: mu = the multiplier the taken branch applies
+                    const float rv = ring_max - volts;
+                    const bool atk = ring_max >= volts;
+                    float mu = 0.0f;
+                    bool upd = false, save = false;
+                    int ns = state;
+                    if (state == 0)
                     {
-                        x = x * A.fixed_gain;
+                        const bool fast = volts > A.pop_ratio * fast_bavg;
+                        const bool hang = A.hang_enable && (hang_bavg > A.hang_level);
+                        ns = atk ? 0 : fast ? 1 : hang ? 2 : 3;
+                        upd = atk || fast || !hang;
+                        mu = atk ? A.attack_mult : fast ? A.fast_decay_mult : A.decay_mult;
+                        if (!atk && !fast)
+                        {
+                            hang_counter = hang ? A.hang_counter_init : hang_counter;
+                            decay_type = hang ? 1 : 0;
+                        }
+                    }
+                    else if (state == 1)
+                    {
+                        const bool fd = volts > save_volts;
+                        const bool hc = hang_counter > 0;
+                        ns = atk ? 0 : fd ? 1 : hc ? 2 : (decay_type == 0) ? 3 : 4;
+                        upd = atk || fd || !hc;
+                        mu = atk ? A.attack_mult : fd ? A.fast_decay_mult
+                                                       : (decay_type == 0) ? A.decay_mult : A.hang_decay_mult;
+                    }
+                    else if (state == 2)
+                    {
+                        const bool hz = hang_counter == 0;
+                        ns = atk ? 0 : hz ? 4 : 2;
+                        upd = atk || hz;
+                        save = atk;
+                        mu = atk ? A.attack_mult : A.hang_decay_mult;
                     }
                     else
                     {
-                        float* rs = ring + slot * BACK_CH + lane;
-                        const float out_sample = *rs;
-                        const float abs_out = fabsf(out_sample);
-                        *rs = x;
-                        fast_bavg = A.fast_backmult * abs_out + A.onemfast_backmult * fast_bavg;
-                        hang_bavg = A.hang_backmult * abs_out + A.onemhang_backmult * hang_bavg;
-                        pmax = fmaxf(pmax, fabsf(x));
-                        const float ring_max = fmaxf(pmax, sfx[(slot + 1) * BACK_CH + lane]);
-                        if (++slot == W)
-                        {
-                            // block complete: its suffix maxima serve the next W samples
-                            slot = 0;
-                            pmax = 0.0f;
-                            float sm = 0.0f;
-                            for (int k = W - 1; k >= 0; --k)
-                            {
-                                sm = fmaxf(sm, fabsf(ring[k * BACK_CH + lane]));
-                                sfx[k * BACK_CH + lane] = sm;
-                            }
-                        }
-                        if (hang_counter > 0) --hang_counter;
-                        // the 5-state attack / decay / hang machine (audio_agc.c:436-551), as
-                        // selects: m = the multiplier the taken branch applies (0: volts kept)
-                        const float rv = ring_max - volts;
-                        const bool atk = ring_max >= volts;
-                        float m = 0.0f;
-                        bool upd = false, save = false;
-                        int ns = state;
-                        if (state == 0)
-                        {
-                            const bool fast = volts > A.pop_ratio * fast_bavg;
-                            const bool hang = A.hang_enable && (hang_bavg > A.hang_level);
-                            ns = atk ? 0 : fast ? 1 : hang ? 2 : 3;
-                            upd = atk || fast || !hang;
-                            m = atk ? A.attack_mult : fast ? A.fast_decay_mult : A.decay_mult;
-                            if (!atk && !fast)
-                            {
-                                hang_counter = hang ? A.hang_counter_init : hang_counter;
-                                decay_type = hang ? 1 : 0;
-                            }
-                        }
-                        else if (state == 1)
-                        {
-                            const bool fd = volts > save_volts;
-                            const bool hc = hang_counter > 0;
-                            ns = atk ? 0 : fd ? 1 : hc ? 2 : (decay_type == 0) ? 3 : 4;
-                            upd = atk || fd || !hc;
-                            m = atk ? A.attack_mult : fd ? A.fast_decay_mult
-                                                          : (decay_type == 0) ? A.decay_mult : A.hang_decay_mult;
-                        }
-                        else if (state == 2)
-                        {
-                            const bool hz = hang_counter == 0;
-                            ns = atk ? 0 : hz ? 4 : 2;
-                            upd = atk || hz;
-                            save = atk;
-                            m = atk ? A.attack_mult : A.hang_decay_mult;
-                        }
-                        else
-                        {
-                            ns = atk ? 0 : state;
-                            upd = true;
-                            save = atk;
-                            m = atk ? A.attack_mult : (state == 3) ? A.decay_mult : A.hang_decay_mult;
-                        }
-                        state = ns;
-                        if (save) save_volts = volts;
-                        if (upd) volts += rv * m;
-                        if (volts < A.min_volts) volts = A.min_volts;
-                        float vo = log10f_fast(A.inv_max_input * volts);
-                        if (vo > 0.0f) vo = 0.0f;
-                        const float mult = (A.out_target - A.slope_constant * vo) / volts;
-                        x = out_sample * mult;
+                        ns = atk ? 0 : state;
+                        upd = true;
+                        save = atk;
+                        mu = atk ? A.attack_mult : (state == 3) ? A.decay_mult : A.hang_decay_mult;
                     }
-                    if (A.remove_dc)
-                    {
-                        const float w = (float)((double)x + (double)wold * 0.9999);
-                        x = w - wold;
-                        wold = w;
-                    }
-                    x = x * scale;
-#pragma unroll
-                    for (int st = 0; st < 4; ++st)
-                        x = biquad_step(x, bq1[4 * st], bq1[4 * st + 1], bq1[4 * st + 2], bq1[4 * st + 3], b1 + 5 * st);
-                    // ---- polyphase interpolator: output j uses phase L-1-j (arm_fir_interpolate_f32.c:482-575)
-                    float win[PH];
-#pragma unroll
-                    for (int t = 0; t < PH - 1; ++t) win[t] = ip[t];
-                    win[PH - 1] = x;
-#pragma unroll
-                    for (int i = L; i > 0; --i)
-                    {
-                        float sum = 0.0f;
-#pragma unroll
-                        for (int t = 0; t < PH; ++t) sum += win[t] * ic[(i - 1) + t * L];
-                        mo[(m * L + (L - i)) * BACK_CH + lane] = sum;
-                    }
-#pragma unroll
-                    for (int t = 0; t + 1 < PH; ++t) ip[t] = win[t + 1];
+                    state = ns;
+                    if (save) save_volts = volts;
+                    if (upd) volts += rv * mu;
+                    if (volts < A.min_volts) volts = A.min_volts;
+                    float vo = log10f_fast(A.inv_max_input * volts);
+                    if (vo > 0.0f) vo = 0.0f;
+                    const float mult = (A.out_target - A.slope_constant * vo) / volts;
+                    x = out_sample * mult;
                 }
-            }
-            __syncthreads();
-        }
-        if (live)
-        {
-#pragma unroll
-            for (int i = 0; i < PRE; ++i) a.s.pre[i * C + c] = pre[i];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) a.s.bq1[i * C + c] = bq1[i];
-#pragma unroll
-            for (int i = 0; i < PH - 1; ++i) a.s.interp[i * C + c] = ip[i];
-            if (agc_on)
-                for (int k = 0; k < W; ++k) a.s.ring[(size_t)k * C + c] = ring[k * BACK_CH + lane];
-            a.s.agc[1 * C + c] = volts;
-            a.s.agc[2 * C + c] = save_volts;
-            a.s.agc[3 * C + c] = fast_bavg;
-            a.s.agc[4 * C + c] = hang_bavg;
-            a.s.agc[5 * C + c] = wold;
-            a.s.agci[0 * C + c] = hang_counter;
-            a.s.agci[1 * C + c] = decay_type;
-            a.s.agci[2 * C + c] = state;
-        }
-    }
-    else
-    {
-        // ================= wave 1: anti-alias lattice, biquad_2, line-out scale, store =========
-        float aa[AA > 0 ? AA : 1], bq2[4];
-        float ak[AA > 0 ? AA : 1], av[AA + 1], b2[5];
-#pragma unroll
-        for (int i = 0; i < AA; ++i) ak[i] = P->aa_k[i];
-#pragma unroll
-        for (int i = 0; i <= AA; ++i) av[i] = P->aa_v[i];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) b2[i] = P->biquad2[i];
-#pragma unroll
-        for (int i = 0; i < AA; ++i) aa[i] = live ? a.s.aa[i * C + c] : 0.0f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) bq2[i] = live ? a.s.bq2[i * C + c] : 0.0f;
-        const float lo = P->line_out_scale;
-        for (int it = 0; it <= calls; ++it)
-        {
-            if (it > 0)
-            {
-                const int call = it - 1;
-                const float* mi = mid + (call & 1) * BLK * BACK_CH;
-                float* ao = a.audio ? a.audio + (size_t)c * a.N + call * BLK : nullptr;
-                int2* dd = a.dst ? a.dst + (size_t)c * a.N + call * BLK : nullptr;
-#pragma unroll
-                for (int n0 = 0; n0 < BLK; n0 += 4)
+                if (A.remove_dc)
                 {
-                    float y[4];
+                    const float w = (float)((double)x + (double)wold * 0.9999);
+                    x = w - wold;
+                    wold = w;
+                }
+                ao[m * BACK_CH] = x;
+            }
+            leave_last = old[NDC - 1];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+            for (int i = 0; i + 1 < AGC_Q - 1; ++i) cmax[i] = cmax[i + 1];
+            cmax[AGC_Q - 2] = pmax;
+        }
+        __syncthreads();
+    }
+    if (live)
+    {
+#pragma unroll
+        for (int i = 0; i < PRE; ++i) a.s.pre[i * C + c] = pre[i];
+        a.s.agc[1 * C + c] = volts;
+        a.s.agc[2 * C + c] = save_volts;
+        a.s.agc[3 * C + c] = fast_bavg;
+        a.s.agc[4 * C + c] = hang_bavg;
+        a.s.agc[5 * C + c] = wold;
+#pragma unroll
+        for (int i = 0; i < AGC_Q - 1; ++i) a.s.agc[(6 + i) * C + c] = cmax[i];
+        a.s.agc[(5 + AGC_Q) * C + c] = leave_last;
+        a.s.agci[0 * C + c] = hang_counter;
+        a.s.agci[1 * C + c] = decay_type;
+        a.s.agci[2 * C + c] = state;
+    }
+}
+
+// ---- role 1: post-AGC scale (audio_driver.c:2513-2524), biquad_1 (:2527), interpolator (:2560-2577)
+template <int L, int PH>
+__device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
+{
+    BACK_PROLOGUE
+    float b1[20], ic[L * PH];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) b1[i] = P->biquad1[i];
+#pragma unroll
+    for (int i = 0; i < L * PH; ++i) ic[i] = P->interp[i];
+    const float scale = P->post_agc_scale;
+    float bq1[16], ip[PH > 1 ? PH - 1 : 1];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bq1[i] = a.s.bq1[i * C + cl];
+#pragma unroll
+    for (int i = 0; i < PH - 1; ++i) ip[i] = a.s.interp[i * C + cl];
+    for (int it = 0; it < calls + BACK_ROLES - 1; ++it)
+    {
+        const int call = it - 1;
+        if (call >= 0 && call < calls)
+        {
+            const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + lane;
+            float* mo = lds.mid + (call & 1) * BLK * BACK_CH + lane;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m)
+            {
+                float x = ai[m * BACK_CH];
+                x = x * scale;
+#pragma unroll
+                for (int st = 0; st < 4; ++st)
+                    x = biquad_step(x, bq1[4 * st], bq1[4 * st + 1], bq1[4 * st + 2], bq1[4 * st + 3], b1 + 5 * st);
+                // polyphase interpolator: output j uses phase L-1-j (arm_fir_interpolate_f32.c:482-575)
+                float win[PH];
+#pragma unroll
+                for (int t = 0; t < PH - 1; ++t) win[t] = ip[t];
+                win[PH - 1] = x;
+#pragma unroll
+                for (int i = L; i > 0; --i)
+                {
+                    float sum = 0.0f;
+#pragma unroll
+                    for (int t = 0; t < PH; ++t) sum += win[t] * ic[(i - 1) + t * L];
+                    mo[(m * L + (L - i)) * BACK_CH] = sum;
+                }
+#pragma unroll
+                for (int t = 0; t + 1 < PH; ++t) ip[t] = win[t + 1];
+            }
+        }
+        __syncthreads();
+    }
+    if (live)
+    {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a.s.bq1[i * C + c] = bq1[i];
+#pragma unroll
+        for (int i = 0; i < PH - 1; ++i) a.s.interp[i * C + c] = ip[i];
+    }
+}
+
+// ---- role 2: anti-alias lattice (audio_driver.c:2581-2590), biquad_2 (:2832), line-out scale
+//      (:2860), f32 audio and int32 codec frames (:2911-2923) ----
+template <int AA, int L>
+__device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
+{
+    BACK_PROLOGUE
+    float aa[AA > 0 ? AA : 1], bq2[4];
+    float ak[AA > 0 ? AA : 1], av[AA + 1], b2[5];
+#pragma unroll
+    for (int i = 0; i < AA; ++i) ak[i] = P->aa_k[i];
+#pragma unroll
+    for (int i = 0; i <= AA; ++i) av[i] = P->aa_v[i];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) b2[i] = P->biquad2[i];
+#pragma unroll
+    for (int i = 0; i < AA; ++i) aa[i] = a.s.aa[i * C + cl];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bq2[i] = a.s.bq2[i * C + cl];
+    const float lo = P->line_out_scale;
+    for (int it = 0; it < calls + BACK_ROLES - 1; ++it)
+    {
+        const int call = it - 2;
+        if (call >= 0)
+        {
+            const float* mi = lds.mid + (call & 1) * BLK * BACK_CH + lane;
+            float* ao = a.audio ? a.audio + (size_t)c * a.N + call * BLK : nullptr;
+            int2* dd = a.dst ? a.dst + (size_t)c * a.N + call * BLK : nullptr;
+#pragma unroll 2
+            for (int n0 = 0; n0 < BLK; n0 += 4)
+            {
+                float y[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                {
+                    float v = mi[(n0 + j) * BACK_CH];
+                    if (AA > 0) v = lattice_step<AA>(v, aa, ak, av);
+                    v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
+                    y[j] = v * lo;
+                }
+                if (live)
+                {
+                    if (ao) *(float4*)(ao + n0) = make_float4(y[0], y[1], y[2], y[3]);
+                    if (dd)
                     {
-                        float v = mi[(n0 + j) * BACK_CH + lane];
-                        if (AA > 0) v = lattice_step<AA>(v, aa, ak, av);
-                        v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
-                        y[j] = v * lo;
-                    }
-                    if (live)
-                    {
-                        if (ao) *(float4*)(ao + n0) = make_float4(y[0], y[1], y[2], y[3]);
-                        if (dd)
-                        {
-                            const int d0 = to_dma(y[0]), d1 = to_dma(y[1]), d2 = to_dma(y[2]), d3 = to_dma(y[3]);
-                            *(int4*)(dd + n0) = make_int4(d0, d0, d1, d1);
-                            *(int4*)(dd + n0 + 2) = make_int4(d2, d2, d3, d3);
-                        }
+                        const int d0 = to_dma(y[0]), d1 = to_dma(y[1]), d2 = to_dma(y[2]), d3 = to_dma(y[3]);
+                        *(int4*)(dd + n0) = make_int4(d0, d0, d1, d1);
+                        *(int4*)(dd + n0 + 2) = make_int4(d2, d2, d3, d3);
                     }
                 }
             }
-            __syncthreads();
         }
-        if (live)
-        {
-#pragma unroll
-            for (int i = 0; i < AA; ++i) a.s.aa[i * C + c] = aa[i];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) a.s.bq2[i * C + c] = bq2[i];
-        }
+        __syncthreads();
     }
+    if (live)
+    {
+#pragma unroll
+        for (int i = 0; i < AA; ++i) a.s.aa[i * C + c] = aa[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a.s.bq2[i * C + c] = bq2[i];
+    }
+}
+
+// PRE / AA lattice stages, L interpolation factor, PH polyphase length, W AGC window
+template <int PRE, int AA, int L, int PH, int W>
+__global__ void __launch_bounds__(BACK_ROLES * BACK_CH) rx_back(BackArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const BackLds lds = back_lds_carve<BLK / L>(smem);
+    // readfirstlane makes the role provably wave-uniform (scalar branches)
+    const int role = __builtin_amdgcn_readfirstlane(threadIdx.x / BACK_CH);
+    if (role == 0)
+        rx_back_agc<PRE, L, W>(a, lds);
+    else if (role == 1)
+        rx_back_audio<L, PH>(a, lds);
+    else
+        rx_back_output<AA, L>(a, lds);
 }
 
 // ------------------------------------------------------------------------------------
@@ -934,7 +999,7 @@ static size_t front_lds(const uhsdr_rx_s* h)
 
 static size_t back_lds(const uhsdr_rx_s* h)
 {
-    return sizeof(float) * (size_t)BACK_CH * (2 * h->bv->w + 1 + 2 * BLK);
+    return sizeof(float) * (size_t)BACK_CH * 2 * (BLK + BLK / h->plan.interp_L);
 }
 
 extern "C" int uhsdr_rx_plan_supported(const uhsdr_rx_plan* p)
@@ -990,8 +1055,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const size_t o_h2i = take((size_t)C * hs2), o_h2q = take((size_t)C * hs2);
     const size_t o_teta = take((size_t)3 * C), o_osc = take(4);
     const size_t o_pre = take((size_t)10 * C), o_aa = take((size_t)10 * C), o_bq1 = take((size_t)16 * C);
-    const size_t o_bq2 = take((size_t)4 * C), o_ip = take((size_t)15 * C), o_ring = take((size_t)W * C);
-    const size_t o_agc = take((size_t)6 * C), o_agci = take((size_t)3 * C);
+    const size_t o_bq2 = take((size_t)4 * C), o_ip = take((size_t)15 * C), o_ring = take((size_t)(W - 1) * C);
+    const size_t o_agc = take((size_t)(6 + AGC_Q) * C), o_agci = take((size_t)3 * C);
     h->arena_bytes = fl * sizeof(float);
     if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess ||
         hipMalloc((void**)&h->adec, sizeof(float) * (size_t)C * h->Nd) != hipSuccess ||
@@ -1055,14 +1120,14 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
     ba.dst = (int2*)dst;
     ba.s = h->bs;
     ba.C = h->C; ba.N = h->N; ba.Nd = h->Nd;
-    ba.ring_phase = (int)(h->dec_samples % h->bv->w);
+    ba.ring_phase = (int)(h->calls_done % AGC_Q);
     time_mark(h, 1, 0);
-    hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(2 * BACK_CH), back_lds(h), h->stream, ba);
+    hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_ROLES * BACK_CH), back_lds(h), h->stream, ba);
     HIPCHK(hipGetLastError());
     time_mark(h, 1, 1);
     if (h->timing) h->nev++;
     h->dec_samples += h->Nd;
-    h->calls_done += 1;
+    h->calls_done += h->N / BLK;
     return UHSDR_OK;
 }
 

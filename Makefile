@@ -11,7 +11,7 @@ HIPCC   ?= /opt/rocm/bin/hipcc
 CC      ?= gcc
 ARCH    ?= gfx950
 HOSTCFLAGS := -O2 -fPIC -ffp-contract=off -std=gnu11 -Wall -Wno-unused-function
-HIPFLAGS   := --offload-arch=$(ARCH) -O3 -fPIC -ffp-contract=off -std=c++17 -Wno-unused-result
+HIPFLAGS   := --offload-arch=$(ARCH) -O3 -fPIC -ffp-contract=off -fno-slp-vectorize -std=c++17 -Wno-unused-result
 
 LIB     := uhsdr_amd/lib/libuhsdr_amd.so
 ORACLE  := oracle/build/libuhsdr_oracle.so

@@ -37,61 +37,56 @@
 #define BLK UHSDR_IQ_BLOCK_SIZE
 #define IQ_BIT_SCALE_DOWN 0.0000152587890625f
 
-// ------------------------------------------------------------------------------------
-// LDS window addressing: one pad word every 8 samples, so lanes whose windows start 8/16
-// samples apart land on different banks.  For p0 % 8 == 0, sk(p0 + o) == sk(p0) + sk(o):
-// all tap offsets become immediate ds_read offsets from one per-lane base.
-// Windows whose lane bases are multiples of 4 only (decimated-rate Hilbert) use a pad
-// every 4 (SH = 2) instead.
-template <int SH = 3> __host__ __device__ constexpr int skw(int p) { return p + (p >> SH); }
-__host__ __device__ constexpr int sk(int p) { return skw<3>(p); }
-__host__ __device__ constexpr int sk_len(int n, int sh = 3) { return n + (n >> sh) + 1; }
-__host__ __device__ constexpr int odd_pitch(int n) { return (n & 1) ? n : n + 1; }
-// skew of the stage-2 window: lane bases there are multiples of R/M on decimate-first paths
-__host__ __device__ constexpr int front_sh2(bool decim_first, int R, int M)
+// acc[r] = sum_{k<T} c[k] * win[r*M + k], r < R; tap order k = 0..T-1 from +0.0f exactly as
+// arm_fir_f32 / arm_fir_decimate_f32 (CMSIS .../arm_fir_f32.c:482-560).  `win` is the lane's
+// first window sample in LDS (16-byte aligned); `c` the tap table in the plan (global, read
+// with scalar loads: the index is wave-uniform), zero beyond T up to a multiple of 8 (a +-0
+// product never changes a finite accumulator that started at +0, so the padding is exact).
+// The chunk loop over 8 taps is deliberately not unrolled: the register window (WA samples,
+// a multiple of 8) slides by 8 samples per chunk and the next 8 samples (two ds_read_b128)
+// and the next 8 taps are fetched before the current MACs, so the live set stays at R
+// accumulators + one window.  Reads run up to 22 samples past the last one used (zeroed).
+// LDS load of V (4 or 2) consecutive floats into w[j..j+V)
+template <int V, int N>
+__device__ __forceinline__ void lds_vec(const float* p, float (&w)[N], int j)
 {
-    return !decim_first ? 3 : (R / M >= 8 ? 3 : (R / M == 4 ? 2 : 1));
-}
-// per-channel LDS window pitch: room for the longest pass (stage-2 windows of decimate-first
-// paths use the pad-every-4 skew), rounded to 5 (mod 8): at most 2-way bank conflicts for
-// every lane/channel layout used
-__host__ __device__ constexpr int window_pitch(int T1, int T2, int N1, int N2, int sh2)
-{
-    const int a = sk_len(T1 - 1 + N1 + 8, 3), b = sk_len(T2 - 1 + N2 + 8, sh2);
-    const int n = a > b ? a : b;
-    return n + ((5 - n) & 7);
+    if (V == 4)
+    {
+        const float4 v = *(const float4*)p;
+        w[j] = v.x; w[j + 1] = v.y; w[j + 2] = v.z; w[j + 3] = v.w;
+    }
+    else
+    {
+        const float2 v = *(const float2*)p;
+        w[j] = v.x; w[j + 1] = v.y;
+    }
 }
 
-// acc[r] = sum_{k<T} c[k] * win[r*M + k], r < R; tap order k = 0..T-1 from +0.0f exactly as
-// arm_fir_f32 / arm_fir_decimate_f32 (CMSIS .../arm_fir_f32.c:482-560).  `win` points at
-// the lane's first window sample (already skewed; base a multiple of 2^SH); `c` is the tap
-// table in LDS, zero padded to a multiple of 8 (a +-0 product never changes a finite
-// accumulator that started at +0, so the padding is exact).
-// The chunk loop over 8 taps is deliberately not unrolled: the register window slides by 8
-// samples per chunk and the next chunk's 8 samples are fetched before the current MACs, so
-// the live set stays at R accumulators + one window (a fully unrolled tap loop lets the
-// compiler hoist every window load and spill).
-template <int T, int R, int M, int SH = 3>
-__device__ __forceinline__ void fir_block(const float* win, const float* c, float (&acc)[R])
+// tap tables are read through the constant address space: wave-uniform indices then become
+// scalar loads (SGPR operands for the MACs) instead of vector loads
+typedef const __attribute__((address_space(4))) float ctaps_t;
+__device__ __forceinline__ ctaps_t* as_taps(const float* p) { return (ctaps_t*)p; }
+
+// V: LDS read width in floats (the lane base is 4V bytes aligned)
+template <int T, int R, int M, int V = 4>
+__device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&acc)[R])
 {
-    constexpr int W = M * (R - 1) + 8;
+    constexpr int WA = (M * (R - 1) + 8 + 7) & ~7;
     constexpr int NCH = (T + 7) / 8;
-    float w[W];
+    float w[WA];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.0f;
 #pragma unroll
-    for (int j = 0; j < W; ++j) w[j] = win[skw<SH>(j)];
+    for (int j = 0; j < WA; j += V) lds_vec<V>(win + j, w, j);
 #pragma unroll 1
     for (int ch = 0; ch < NCH; ++ch)
     {
-        const float* cp = c + 8 * ch;
-        const float4 c0 = *(const float4*)cp;
-        const float4 c1 = *(const float4*)(cp + 4);
-        const float cc[8] = { c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w };
-        float nw[8];
-        const float* np = win + skw<SH>(8 * ch + W);       // 8 * ch + W is a multiple of 8 + W
+        float cc[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) nw[q] = np[skw<SH>(8 * ch + W + q) - skw<SH>(8 * ch + W)];
+        for (int q = 0; q < 8; ++q) cc[q] = c[8 * ch + q];
+        float nw[8];
+#pragma unroll
+        for (int q = 0; q < 8; q += V) lds_vec<V>(win + 8 * ch + WA + q, nw, q);
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk)
         {
@@ -99,11 +94,14 @@ __device__ __forceinline__ void fir_block(const float* win, const float* c, floa
             for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * cc[kk];
         }
 #pragma unroll
-        for (int j = 0; j < W - 8; ++j) w[j] = w[j + 8];
+        for (int j = 0; j < WA - 8; ++j) w[j] = w[j + 8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) w[W - 8 + q] = nw[q];
+        for (int q = 0; q < 8; ++q) w[WA - 8 + q] = nw[q];
     }
 }
+
+// samples zeroed after the end of a window (fir_block over-read, see above)
+constexpr int FRONT_TAIL = 24;
 
 struct FrontArgs
 {
@@ -118,6 +116,8 @@ struct FrontArgs
     float* osc_out;          // [2] written by workgroup 0
     float* adec;             // decimated output of this launch; row stride ldd
     int C, N, ld, ldd;
+    int lw;                  // LDS window pitch per channel (floats, multiple of 4; host picks it
+                             // for conflict-free ds_read_b128, front_window_pitch)
 };
 
 // converted, corrected, frequency-shifted sample n of a channel (audio_driver.c:2660-2705)
@@ -185,6 +185,96 @@ __device__ __forceinline__ void wave_sync()
 
 constexpr int FRONT_WAVE = 64;
 
+// history rows: HS = T-1 rounded up to 4 floats; lane b of a channel loads float4s b, b+nb, ...
+__host__ __device__ constexpr int hist_stride(int T) { return (T - 1 + 3) & ~3; }
+// float4s of a T-tap history row prefetched per lane (all of it when nb >= 8 lanes per channel;
+// with fewer lanes the rest is loaded when the window is filled)
+__host__ __device__ constexpr int hist_q(int T) { return (hist_stride(T) / 4 + 7) / 8; }
+
+// native 4-float vector: arrays of HIP's float4 (a struct with a union) loaded from global
+// memory defeat SROA and end up in scratch
+typedef float vf4 __attribute__((ext_vector_type(4)));
+
+// history row of a T-tap filter for channel cl: lane b of nb loads float4s b, b+nb, ... (HQ per lane)
+template <int T, int HQM>
+__device__ __forceinline__ void front_load_row(const float* row, int cl, int b, int nb, vf4 (&buf)[HQM])
+{
+    constexpr int hs4 = hist_stride(T) / 4, HQ = hist_q(T);
+    const vf4* h = (const vf4*)(row + (size_t)cl * (hs4 * 4));
+#pragma unroll
+    for (int i = 0; i < HQ; ++i)
+    {
+        const int q = b + nb * i;
+        buf[i] = h[q < hs4 ? q : hs4 - 1];
+    }
+}
+
+// One FIR pass's window: history row (registers) + NV new samples per lane, tail zeroed, and
+// the history row of the next call (window samples nnew .. nnew+T-2) written back to HBM.
+template <int T, int HQM>
+__device__ __forceinline__ void front_fill(float* W, float* row, int c, bool act, bool live, int b, int nb,
+                                           const vf4 (&buf)[HQM], const float* vals, int NV)
+{
+    constexpr int hs4 = hist_stride(T) / 4, HQ = hist_q(T);
+    const int nnew = nb * NV;
+    if (act)
+    {
+        // the row's pad floats (T-1 .. HS-1) land where the new samples go: written first,
+        // overwritten below (one wave's LDS accesses are processed in order)
+#pragma unroll
+        for (int i = 0; i < HQ; ++i)
+        {
+            const int q = b + nb * i;
+            if (q < hs4) *(vf4*)(W + 4 * q) = buf[i];
+        }
+        const vf4* h = (const vf4*)(row + (size_t)(live ? c : 0) * (hs4 * 4));
+        for (int q = b + nb * HQ; q < hs4; q += nb) *(vf4*)(W + 4 * q) = h[q];
+    }
+    wave_sync();
+    if (act)
+    {
+        for (int j = 0; j < NV; ++j) W[T - 1 + b * NV + j] = vals[j];
+        for (int t = b; t < FRONT_TAIL; t += nb) W[T - 1 + nnew + t] = 0.0f;
+    }
+    wave_sync();
+    float* ho = row + (size_t)c * (hs4 * 4);
+    for (int q = b; q < hs4; q += nb)
+    {
+        const float4 v = *(const float4*)(W + nnew + 4 * q);
+        if (live) *(float4*)(ho + 4 * q) = v;
+    }
+}
+
+// Lane -> (channel g, block b) of a front wave.  Window reads are ds_read_b128 at g*lw + b*S
+// (S = R floats), serviced in four 16-lane groups (MI355X_MICROARCH.md §LDS).  A run of
+// K = 64/S consecutive blocks of one channel covers one bank in four of every S; S/4
+// consecutive channels with lw = 4 (mod S) interleave into all 64 banks.  So each 16-lane group
+// gets S/4 (channel, run) pairs of consecutive channels: conflict-free.  Batches whose shape
+// does not allow that (nb not a power of two, too few channels or blocks) use g = l / nb.
+__host__ __device__ inline void front_lane(int l, int nb, int S, int& g, int& b)
+{
+    const int cpw = 64 / nb, K = 64 / S, cpg = S / 4;
+    if ((nb & (nb - 1)) || nb < K || cpw < cpg)
+    {
+        g = l / nb;
+        b = l % nb;
+        return;
+    }
+    // b128 groups: {0-3,12-15,20-27}, {4-11,16-19,28-31}, then the same + 32
+    const int h = l & 31;
+    int k, j;
+    if (h < 4) { k = 0; j = h; }
+    else if (h < 12) { k = 1; j = h - 4; }
+    else if (h < 16) { k = 0; j = h - 8; }
+    else if (h < 20) { k = 1; j = h - 8; }
+    else if (h < 28) { k = 0; j = h - 12; }
+    else { k = 1; j = h - 16; }
+    k += (l >> 5) * 2;
+    const int pr = k * cpg + j / K;          // (channel, run) pair
+    g = pr % cpw;
+    b = (pr / cpw) * K + j % K;
+}
+
 // One wave owns CPW = 64 / (N/R) whole channels: all data exchange stays inside the wave, so
 // there is no workgroup barrier and waves from many workgroups interleave freely on a CU.
 // The wave has one LDS window per channel, reused by every FIR pass:
@@ -192,8 +282,11 @@ constexpr int FRONT_WAVE = 64;
 //                                a -> decimator /M -> adec
 //   decimate-first (narrow):     I -> decimator (regs), Q -> decimator, dI -> Hilbert-I,
 //                                dQ -> Hilbert-Q, a = hI +- hQ -> adec
-// Each pass: history row (HBM) + this call's samples (registers) into the window, history
-// row for the next call back to HBM, then every lane runs its R-output FIR block.
+// Each pass: history row + this call's samples (registers) into the window, history row for
+// the next call back to HBM, then every lane runs its R-output FIR block.  All global loads
+// are issued early: the I/Q frames and the first two history rows at entry, and the row of
+// pass p+2 as soon as pass p has put its row into LDS (double-buffered registers), so each
+// pass's HBM latency hides behind the previous pass's FIR.
 template <int T1, int T2, int M, bool DECIM_FIRST, int R>
 __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
 {
@@ -201,37 +294,36 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     const int N = a.N, C = a.C;
     const int lane = threadIdx.x;
-    const int nb = N / R;                            // lanes per channel
+    const int nb = N / R;                            // lanes per channel (>= 4)
     const int CPW = FRONT_WAVE / nb;                 // channels per wave
-    const int g = lane / nb, b = lane % nb;
+    int g, b;
+    front_lane(lane, nb, R, g, b);
     const int c = blockIdx.x * CPW + g;
     const bool act = g < CPW;
     const bool live = act && c < C;
     const int gs = act ? g : 0;
+    const int cl = c < C ? c : C - 1;                // loads clamped: no exec-masked load branches
     const int nblk32 = N / BLK;
     constexpr int RD = R / M;                        // decimated samples per lane
-    constexpr int HS1 = (T1 - 1 + 3) & ~3, HS2 = (T2 - 1 + 3) & ~3;
-    const int N2 = DECIM_FIRST ? N / M : N;          // stage-2 input samples per channel
-    constexpr int SH2 = front_sh2(DECIM_FIRST, R, M);
-    const int LW = window_pitch(T1, T2, N, N2, SH2);
-    float* win_all = smem;                           // [CPW][LW]
-    float* W = win_all + gs * LW;
-    constexpr int TH = DECIM_FIRST ? T2 : T1, TD = DECIM_FIRST ? T1 : T2;
-    constexpr int TH8 = (TH + 7) & ~7, TD8 = (TD + 7) & ~7;
-    float* c_hi = win_all + ((CPW * LW + 3) & ~3);   // tap tables (wave-uniform broadcast reads)
-    float* c_hq = c_hi + TH8;
-    float* c_dec = c_hq + TH8;
-    float* aux = c_dec + TD8;                        // auto-IQ factors [2][CPW][nblk32], osc [2N]
+    constexpr int HQ1 = hist_q(T1), HQ2 = hist_q(T2);
+    constexpr int HQM = HQ1 > HQ2 ? HQ1 : HQ2;
+    const int LW = a.lw;
+    float* W = smem + gs * LW;                       // this channel's window
+    float* aux = smem + CPW * LW;                    // auto-IQ factors [2][CPW][nblk32], osc [2N]
     float* m1 = aux;
     float* m2 = aux + CPW * nblk32;
     float* osc = aux + (P->iq_auto_correction ? 2 * CPW * nblk32 : 0);
 
-    for (int k = lane; k < TH8; k += FRONT_WAVE)
+    // ---- entry: issue the I/Q frames and the history rows of passes 0 and 1 ----
+    int4 raw[R / 2];
     {
-        c_hi[k] = k < TH ? P->hilbert_i[k] : 0.0f;
-        c_hq[k] = k < TH ? P->hilbert_q[k] : 0.0f;
+        const int4* src = (const int4*)(a.iq + (size_t)cl * a.ld + b * R);
+#pragma unroll
+        for (int j = 0; j < R / 2; ++j) raw[j] = src[j];
     }
-    for (int k = lane; k < TD8; k += FRONT_WAVE) c_dec[k] = k < TD ? P->dec[k] : 0.0f;
+    vf4 hA[HQM], hB[HQM];
+    front_load_row<T1>(a.hist1_i, cl, b, nb, hA);
+    front_load_row<T1>(a.hist1_q, cl, b, nb, hB);
 
     InputStage in;
     in.gi = P->iq_gain_i; in.gq = P->iq_gain_q; in.ph = P->iq_phase_balance;
@@ -261,7 +353,7 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
                 }
             m1[e] = t1;
             m2[e] = t2;
-            win_all[e] = t3;                         // scratch; the windows are filled later
+            smem[e] = t3;                            // scratch; the windows are filled later
         }
         wave_sync();
         for (int gg = lane; gg < CPW; gg += FRONT_WAVE)
@@ -272,7 +364,7 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
             for (int bb = 0; bb < nblk32; ++bb)
             {
                 const int e = gg * nblk32 + bb;
-                float t1 = m1[e], t2 = m2[e], t3 = win_all[e];
+                float t1 = m1[e], t2 = m2[e], t3 = smem[e];
                 t1 = (float)(-0.003 * (double)(t1 / (float)BLK) + 0.997 * (double)o1);
                 t2 = (float)(0.003 * (double)(t2 / (float)BLK) + 0.997 * (double)o2);
                 t3 = (float)(0.003 * (double)(t3 / (float)BLK) + 0.997 * (double)o3);
@@ -310,92 +402,50 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
     }
     wave_sync();
 
-    // ---- this lane's R frames: R/2 independent 16-byte loads; I and Q kept in registers ----
+    // ---- this lane's R frames, converted; I and Q kept in registers ----
     float xi[R], xq[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j)
     {
-        int4 raw[R / 2];
-        const int4* src = (const int4*)(a.iq + (size_t)c * a.ld + b * R);
-#pragma unroll
-        for (int j = 0; j < R / 2; ++j) raw[j] = live ? src[j] : make_int4(0, 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < R; ++j)
-        {
-            const int2 v = (j & 1) ? make_int2(raw[j / 2].z, raw[j / 2].w) : make_int2(raw[j / 2].x, raw[j / 2].y);
-            convert_frame(v, in, b * R + j, m1 + gs * nblk32, m2 + gs * nblk32, osc, xi[j], xq[j]);
-        }
+        const int2 v = (j & 1) ? make_int2(raw[j / 2].z, raw[j / 2].w) : make_int2(raw[j / 2].x, raw[j / 2].y);
+        convert_frame(v, in, b * R + j, m1 + gs * nblk32, m2 + gs * nblk32, osc, xi[j], xq[j]);
     }
-
-    // One FIR pass over the window: history (T-1, HBM) + NV new samples per lane, history
-    // written back, then the lane's block of outputs.  SH: window skew (2 when lane bases are
-    // multiples of 4 only).
-    auto fill = [&](const float* hist, float* hist_out, int HS, int T, const float* vals, int NV, int SH) {
-        const int nnew = nb * NV;
-        for (int q = b; q < HS / 4; q += nb)
-        {
-            const float4 v = live ? *(const float4*)(hist + (size_t)c * HS + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float vv[4] = { v.x, v.y, v.z, v.w };
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (act && 4 * q + t < T - 1) W[(4 * q + t) + ((4 * q + t) >> SH)] = vv[t];
-        }
-        if (act && b == 0)
-        {
-#pragma unroll
-            for (int t = 0; t < 8; ++t) W[(T - 1 + nnew + t) + ((T - 1 + nnew + t) >> SH)] = 0.0f;
-        }
-        if (act)
-        {
-            for (int j = 0; j < NV; ++j)
-            {
-                const int p = T - 1 + b * NV + j;
-                W[p + (p >> SH)] = vals[j];
-            }
-        }
-        wave_sync();
-        for (int q = b; q < HS / 4; q += nb)
-        {
-            float vv[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-            {
-                const int p = nnew + 4 * q + t;
-                vv[t] = (4 * q + t < T - 1) ? W[p + (p >> SH)] : 0.0f;
-            }
-            if (live) *(float4*)(hist_out + (size_t)c * HS + 4 * q) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-        }
-    };
 
     const bool lsb = P->lsb;
     float o[RD];
     if (!DECIM_FIRST)
     {
         float hi[R], hq[R];
-        fill(a.hist1_i, a.hist1_i, HS1, T1, xi, R, 3);
-        fir_block<T1, R, 1>(W + sk(b * R), c_hi, hi);
+        front_fill<T1>(W, a.hist1_i, c, act, live, b, nb, hA, xi, R);
+        front_load_row<T2>(a.hist2_i, cl, b, nb, hA);
+        fir_block<T1, R, 1>(W + b * R, as_taps(P->hilbert_i), hi);
         wave_sync();
-        fill(a.hist1_q, a.hist1_q, HS1, T1, xq, R, 3);
-        fir_block<T1, R, 1>(W + sk(b * R), c_hq, hq);
+        front_fill<T1>(W, a.hist1_q, c, act, live, b, nb, hB, xq, R);
+        fir_block<T1, R, 1>(W + b * R, as_taps(P->hilbert_q), hq);
         // a = I + Q (USB) or I - Q (LSB), audio_driver.c:2781-2790
 #pragma unroll
         for (int r = 0; r < R; ++r) hi[r] = lsb ? (hi[r] - hq[r]) : (hi[r] + hq[r]);
         wave_sync();
-        fill(a.hist2_i, a.hist2_i, HS2, T2, hi, R, 3);
-        fir_block<T2, RD, M>(W + sk(b * R), c_dec, o);
+        front_fill<T2>(W, a.hist2_i, c, act, live, b, nb, hA, hi, R);
+        fir_block<T2, RD, M>(W + b * R, as_taps(P->dec), o);
     }
     else
     {
+        constexpr int V2 = RD % 4 == 0 ? 4 : 2;
         float di[RD], dq[RD], hi[RD], hq[RD];
-        fill(a.hist1_i, a.hist1_i, HS1, T1, xi, R, 3);
-        fir_block<T1, RD, M>(W + sk(b * R), c_dec, di);
+        front_fill<T1>(W, a.hist1_i, c, act, live, b, nb, hA, xi, R);
+        front_load_row<T2>(a.hist2_i, cl, b, nb, hA);
+        fir_block<T1, RD, M>(W + b * R, as_taps(P->dec), di);
         wave_sync();
-        fill(a.hist1_q, a.hist1_q, HS1, T1, xq, R, 3);
-        fir_block<T1, RD, M>(W + sk(b * R), c_dec, dq);
+        front_fill<T1>(W, a.hist1_q, c, act, live, b, nb, hB, xq, R);
+        front_load_row<T2>(a.hist2_q, cl, b, nb, hB);
+        fir_block<T1, RD, M>(W + b * R, as_taps(P->dec), dq);
         wave_sync();
-        fill(a.hist2_i, a.hist2_i, HS2, T2, di, RD, SH2);
-        fir_block<T2, RD, 1, SH2>(W + skw<SH2>(b * RD), c_hi, hi);
+        front_fill<T2>(W, a.hist2_i, c, act, live, b, nb, hA, di, RD);
+        fir_block<T2, RD, 1, V2>(W + b * RD, as_taps(P->hilbert_i), hi);
         wave_sync();
-        fill(a.hist2_q, a.hist2_q, HS2, T2, dq, RD, SH2);
-        fir_block<T2, RD, 1, SH2>(W + skw<SH2>(b * RD), c_hq, hq);
+        front_fill<T2>(W, a.hist2_q, c, act, live, b, nb, hB, dq, RD);
+        fir_block<T2, RD, 1, V2>(W + b * RD, as_taps(P->hilbert_q), hq);
 #pragma unroll
         for (int r = 0; r < RD; ++r) o[r] = lsb ? (hi[r] - hq[r]) : (hi[r] + hq[r]);
     }
@@ -890,28 +940,22 @@ static const BackVariant kBack[] = {
 // frames handled by one front launch: one wave covers a channel's launch block
 static int front_frames(int N, int R) { return N < FRONT_WAVE * R ? N : FRONT_WAVE * R; }
 
-// C, N == 0: any R (support query)
+// C, N == 0: support query.  R = 8 by default: more waves per batch, and its 8+ lanes per
+// channel prefetch whole history rows; UHSDR_FRONT_R=16 selects the 16-output blocks
+// (benchmarking knob).
 static const FrontVariant* find_front(const uhsdr_rx_plan& p, long long C = 0, int N = 0)
 {
+    (void)C;
     const int t1 = p.use_decimated_iq ? p.dec_taps : p.hilbert_taps;
     const int t2 = p.use_decimated_iq ? p.hilbert_taps : p.dec_taps;
+    const char* env = getenv("UHSDR_FRONT_R");
+    const int want = env ? atoi(env) : 8;
     const FrontVariant* best = nullptr;
-    long long best_waves = 0;
     for (const FrontVariant& v : kFront)
         if (v.t1 == t1 && v.t2 == t2 && v.m == p.decimation_rate && v.decim_first == p.use_decimated_iq)
         {
-            if (N && N % v.R) continue;
-            // waves one launch puts on the chip; prefer R = 16 once there are >= 4 per SIMD
-            const int nf = N ? front_frames(N, v.R) : 0;
-            const long long waves = N ? (C + FRONT_WAVE / (nf / v.R) - 1) / (FRONT_WAVE / (nf / v.R)) : 0;
-            if (!best) { best = &v; best_waves = waves; continue; }
-            const bool big_v = waves >= 4096, big_b = best_waves >= 4096;
-            if (N == 0 ? v.R > best->R
-                       : (big_v && big_b ? v.R > best->R : (big_v != big_b ? big_v : waves > best_waves)))
-            {
-                best = &v;
-                best_waves = waves;
-            }
+            if (N && (N % v.R || front_frames(N, v.R) / v.R < 4)) continue;   // >= 4 lanes per channel
+            if (!best || (v.R == want && best->R != want)) best = &v;
         }
     return best;
 }
@@ -935,6 +979,7 @@ struct uhsdr_rx_s
     const FrontVariant* fv;
     const BackVariant* bv;
     int C, N, Nd, Nf;        // Nf: frames per front launch (N split into N / Nf launches)
+    int lw;                  // front LDS window pitch (floats)
     int T1, T2;
     hipStream_t stream;
     // front state
@@ -982,16 +1027,65 @@ static void time_harvest(uhsdr_rx_s* h)
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { uhsdr_set_error("%s: %s", #x, hipGetErrorString(e_)); return UHSDR_DEVICE_ERROR; } } while (0)
 
+// ds_read_b128 lane groups (one LDS cycle each, MI355X_MICROARCH.md §LDS); ds_read_b64: halves
+static const int kB128Groups[4][16] = {
+    { 0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27 },
+    { 4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31 },
+    { 32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59 },
+    { 36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63 } };
+
+// extra LDS cycles of one FIR window read for lane bases g*lw + b*stride (dwords), vec 4 or 2
+static int window_conflicts(int lw, int nb, int cpw, int R, int stride, int vec)
+{
+    int cost = 0;
+    const int ngroups = vec == 4 ? 4 : 2, glen = vec == 4 ? 16 : 32;
+    for (int gi = 0; gi < ngroups; ++gi)
+    {
+        int load[64] = { 0 };
+        for (int k = 0; k < glen; ++k)
+        {
+            const int l = vec == 4 ? kB128Groups[gi][k] : gi * 32 + k;
+            int g, b;
+            front_lane(l, nb, R, g, b);
+            if (g >= cpw) continue;
+            const int addr = g * lw + b * stride;
+            for (int d = 0; d < vec; ++d) load[(addr + d) & 63] += 1;
+        }
+        int mx = 0;
+        for (int k = 0; k < 64; ++k) mx = load[k] > mx ? load[k] : mx;
+        cost += mx - 1;
+    }
+    return cost;
+}
+
+// LDS window pitch per channel: room for every pass (T-1 history + new samples + tail),
+// a multiple of 4 floats, chosen among 16 candidates for the fewest ds_read bank conflicts
+static int front_window_pitch(const uhsdr_rx_s* h)
+{
+    const int N = h->Nf, R = h->fv->R, M = h->plan.decimation_rate;
+    const bool df = h->plan.use_decimated_iq;
+    const int nb = N / R, cpw = FRONT_WAVE / nb;
+    const int n2 = df ? N / M : N;
+    int need = h->T1 - 1 + N + FRONT_TAIL;
+    const int need2 = h->T2 - 1 + n2 + FRONT_TAIL;
+    need = ((need > need2 ? need : need2) + 3) & ~3;
+    const int rd = R / M;
+    int best = need, best_cost = 1 << 30;
+    for (int lw = need; lw < need + 64; lw += 4)
+    {
+        int cost = window_conflicts(lw, nb, cpw, R, R, 4);
+        if (df) cost += window_conflicts(lw, nb, cpw, R, rd, rd % 4 == 0 ? 4 : 2);
+        if (cost < best_cost) { best_cost = cost; best = lw; }
+    }
+    return best;
+}
+
 // LDS of one front workgroup (one wave): must match the carve-up in rx_front
 static size_t front_lds(const uhsdr_rx_s* h)
 {
     const int N = h->Nf;
-    const bool df = h->plan.use_decimated_iq;
-    const int N2 = df ? N / h->plan.decimation_rate : N;
     const int cpw = FRONT_WAVE / (N / h->fv->R);
-    size_t f = ((size_t)cpw * window_pitch(h->T1, h->T2, N, N2, front_sh2(df, h->fv->R, h->plan.decimation_rate)) + 3) & ~(size_t)3;
-    const int th = df ? h->T2 : h->T1, td = df ? h->T1 : h->T2;
-    f += 2 * ((th + 7) & ~7) + ((td + 7) & ~7);
+    size_t f = (size_t)cpw * h->lw;
     if (h->plan.iq_auto_correction) f += 2 * cpw * (N / BLK);
     if (h->plan.freq_shift_hz != 0 && h->plan.shift_kind == 2) f += 2 * N;
     return f * sizeof(float);
@@ -1044,6 +1138,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->stream = (hipStream_t)stream;
     h->T1 = h->fv->t1; h->T2 = h->fv->t2;
     h->Nf = front_frames(N, h->fv->R);
+    h->lw = front_window_pitch(h);
     if (N % h->Nf) { free(h); uhsdr_set_error("frames_per_call %d not a multiple of %d", N, h->Nf); return UHSDR_LENGTH_ERROR; }
     if (front_lds(h) > 64 * 1024) { free(h); uhsdr_set_error("frames_per_call too long for LDS"); return UHSDR_LENGTH_ERROR; }
     const int W = h->bv->w;
@@ -1107,6 +1202,7 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
         fa.osc_out = h->osc + 2 * ((h->front_launches + 1) & 1);
         fa.adec = h->adec + f0 / h->plan.decimation_rate;
         fa.C = h->C; fa.N = h->Nf; fa.ld = h->N; fa.ldd = h->Nd;
+        fa.lw = h->lw;
         hipLaunchKernelGGL(h->fv->fn, dim3((h->C + cpw - 1) / cpw), dim3(FRONT_WAVE), lds, h->stream, fa);
         HIPCHK(hipGetLastError());
         h->front_launches += 1;

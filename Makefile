@@ -23,7 +23,9 @@ HOST_OBJS := $(patsubst uhsdr_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS  := $(patsubst uhsdr_amd/csrc/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
 HDRS := include/uhsdr.h uhsdr_amd/csrc/uhsdr_internal.h
 
-all: $(LIB) $(ORACLE)
+EXAMPLE := examples/build/rx_batch
+
+all: $(LIB) $(ORACLE) $(EXAMPLE)
 
 $(OBJDIR) uhsdr_amd/lib oracle/build:
 	mkdir -p $@
@@ -40,10 +42,17 @@ $(LIB): $(HOST_OBJS) $(HIP_OBJS) | uhsdr_amd/lib
 $(ORACLE): oracle/uhsdr_oracle.c oracle/uhsdr_oracle.h include/uhsdr.h | oracle/build
 	$(CC) $(HOSTCFLAGS) -shared -o $@ $< -lm -lpthread
 
+examples/build:
+	mkdir -p $@
+
+# plain C host against the C ABI: gcc only, no HIP headers
+$(EXAMPLE): examples/rx_batch.c include/uhsdr.h $(LIB) | examples/build
+	$(CC) -O2 -std=gnu11 -Wall -Iinclude -o $@ $< -Luhsdr_amd/lib -luhsdr_amd -Wl,-rpath,'$$ORIGIN/../../uhsdr_amd/lib'
+
 ref:
 	$(MAKE) -C oracle/ref
 
 clean:
-	rm -rf $(OBJDIR) uhsdr_amd/lib oracle/build
+	rm -rf $(OBJDIR) uhsdr_amd/lib oracle/build examples/build
 
 .PHONY: all ref clean

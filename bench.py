@@ -37,8 +37,18 @@ WORKLOADS = {
 }
 
 
+AGC_Q = 6   # AGC look-ahead ring: the last 6 calls of AGC inputs (uhsdr_rx.hip, rx_back_agc)
+
+
 def algorithmic_bytes(plan, C: int, N: int, write_dst: bool):
-    """Bytes each kernel must move per launch, from the live state sizes."""
+    """Bytes each kernel must move per launch, from the live state sizes.
+
+    Per channel and launch: the I/Q frames in (8 B/frame), f32 audio out (4 B/frame, +8 B for
+    int32 codec frames), every persistent state word read once and written once, except the
+    AGC look-ahead ring, of which a launch reads and rewrites only the Nd decimated samples it
+    advances.  The decimated hand-off between the two kernels (adec) counts for the kernels
+    but not for the chain: it is an artefact of the split, not of the algorithm.
+    """
     M = plan.decimation_rate
     Nd = N // M
     if plan.use_decimated_iq:
@@ -47,14 +57,36 @@ def algorithmic_bytes(plan, C: int, N: int, write_dst: bool):
         fir_hist = 2 * (plan.hilbert_taps - 1) + (plan.dec_taps - 1)
     if plan.iq_auto_correction:
         fir_hist += 3
+    # lattice pre/aa, biquad_1/2 state, interpolator history, 5 AGC floats, 5 call maxima,
+    # the leaving sample, 3 AGC ints
     back_state = (plan.pre_stages + plan.aa_stages + 16 + 4 + max(plan.interp_phase - 1, 0)
-                  + plan.agc.attack_buffsize + 9)
+                  + 5 + (AGC_Q - 1) + 1 + 3)
+    ring = 2 * 4 * Nd if plan.agc.mode != 5 else 0
     out_b = 4 + (8 if write_dst else 0)
     front = C * (8 * N + 4 * Nd + 2 * 4 * fir_hist)
-    back = C * (4 * Nd + out_b * N + 2 * 4 * back_state)
-    chain = C * ((8 + out_b) * N + 2 * 4 * (fir_hist + back_state))   # adec round trip excluded
-    return {"rx_front": front, "rx_back": back, "chain": chain,
-            "s_live_bytes": 4 * (fir_hist + back_state)}
+    back = C * (4 * Nd + out_b * N + 2 * 4 * back_state + ring)
+    chain = C * ((8 + out_b) * N + 2 * 4 * (fir_hist + back_state) + ring)
+    s_live = 4 * (fir_hist + back_state + (AGC_Q * (BLK // M) if plan.agc.mode != 5 else 0))
+    return {"rx_front": front, "rx_back": back, "chain": chain, "s_live_bytes": s_live}
+
+
+BLK = 32
+
+
+def pmc_traffic(workload: str):
+    """HBM bytes per launch per kernel from the committed rocprofv3 PMC summary of this
+    workload (profiles/pmc_<workload>.json, tools/pmc_summary.py: FETCH_SIZE x 2 per the gfx950
+    correction of MI355X_MICROARCH.md §HBM, + WRITE_SIZE), or None."""
+    f = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    try:
+        d = json.load(open(f))
+    except (OSError, ValueError):
+        return None
+    out = {}
+    for k, v in d.items():
+        if "hbm_read_bytes_corrected" in v and "hbm_write_bytes" in v:
+            out[k] = v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]
+    return out or None
 
 
 def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
@@ -89,6 +121,98 @@ def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
                       f"{threads} threads, channels split evenly; host CPU: {model}"}
 
 
+def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, pool, want_dst):
+    """W untimed + K timed steps of one RxChain on this rank; returns (max-rank seconds,
+    per-kernel (total ms, launches) from HIP events on the library's stream, plan, finite)."""
+    cfg = U.default_config()
+    stream = torch.cuda.current_stream(dev)
+    chain = U.RxChain(cfg, channels=C, frames=N, stream=stream.cuda_stream)
+    plan = chain.plan
+    # inputs resident in HBM before timing: a pool of consecutive blocks, cycled
+    c0 = shard.channel_range(C, rank)[0]          # weak scaling: rank r owns channels [r*C, (r+1)*C)
+    inputs = [synth.ssb_iq_torch(c0, C, k * N, N, dev) for k in range(pool)]
+    audio = torch.empty((C, N), dtype=torch.float32, device=dev)
+    dst = torch.empty((C, N, 2), dtype=torch.int32, device=dev) if want_dst else None
+    torch.cuda.synchronize(dev)
+    for s in range(warmup):
+        chain.process(inputs[s % pool], audio, dst)
+    torch.cuda.synchronize(dev)
+    chain.enable_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(steps):
+        chain.process(inputs[s % pool], audio, dst)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ktimes = chain.kernel_times()
+    chain.enable_timing(False)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ok = bool(torch.isfinite(audio).all().item())
+    chain.close()
+    del inputs
+    return float(t.item()), ktimes, plan, ok, audio
+
+
+def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup):
+    """The same chain with every launch's f32 audio gathered to rank 0 over RCCL (SURVEY.md
+    §8(e) e1; RCCL has no gather primitive, torch.distributed.gather issues grouped send/recv,
+    so rank 0 receives from every peer over its own xGMI link): the gather of launch k runs on
+    a communication stream while launch k+1 computes (double-buffered outputs).  Returns
+    max-rank seconds for `steps` steps."""
+    cfg = U.default_config()
+    comp = torch.cuda.current_stream(dev)
+    comm = torch.cuda.Stream(dev)
+    chain = U.RxChain(cfg, channels=C, frames=N, stream=comp.cuda_stream)
+    x = synth.ssb_iq_torch(shard.channel_range(C, rank)[0], C, 0, N, dev)
+    outs = [torch.empty((C, N), dtype=torch.float32, device=dev) for _ in range(2)]
+    recv = [[torch.empty((C, N), dtype=torch.float32, device=dev) for _ in range(world)] if rank == 0 else None
+            for _ in range(2)]
+    done = [torch.cuda.Event() for _ in range(2)]
+    gdone = [torch.cuda.Event() for _ in range(2)]
+
+    def step(s):
+        k = s & 1
+        if s >= 2:
+            comp.wait_event(gdone[k])                  # buffer k's previous gather has finished
+        chain.process(x, outs[k], None)
+        done[k].record(comp)
+        with torch.cuda.stream(comm):
+            comm.wait_event(done[k])
+            dist.gather(outs[k], gather_list=recv[k], dst=0)
+            gdone[k].record(comm)
+    for s in range(warmup):
+        step(s)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        step(s)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    chain.close()
+    return float(t.item())
+
+
+def roofline_of(ab, ktimes, traffic):
+    kms = {k: v[0] / max(v[1], 1) for k, v in ktimes.items()}       # mean ms per launch
+    dominant = max(kms, key=kms.get)
+    achieved = ab[dominant] / (kms[dominant] * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": int(traffic[dominant]) if traffic and dominant in traffic else None,
+            "kernel": dominant, "alg_bytes_per_launch": ab[dominant],
+            "mean_launch_ms": round(kms[dominant], 5)}
+    return roof, kms
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -99,6 +223,8 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="override frames per call")
     ap.add_argument("--dst", action="store_true", help="also write int32 codec frames")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-northstar", action="store_true", help="skip the 1M-channel north-star leg")
+    ap.add_argument("--no-gather", action="store_true", help="skip the RCCL gather leg (N > 1)")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--pool", type=int, default=8, help="distinct input blocks cycled through")
     args = ap.parse_args()
@@ -106,7 +232,7 @@ def main():
     import torch
     import torch.distributed as dist
     import uhsdr_amd as U
-    from uhsdr_amd import synth
+    from uhsdr_amd import shard, synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -120,42 +246,33 @@ def main():
     wl = WORKLOADS[args.workload]
     C = args.channels or wl["channels"]
     N = args.frames or wl["frames"]
-    cfg = U.default_config()
-    stream = torch.cuda.current_stream(dev)
-    chain = U.RxChain(cfg, channels=C, frames=N, stream=stream.cuda_stream)
-    plan = chain.plan
+    elapsed, ktimes, plan, ok, _ = timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, args.steps,
+                                             args.warmup, max(1, args.pool), args.dst)
 
-    # inputs resident in HBM before timing: a pool of consecutive blocks, cycled
-    pool = max(1, args.pool)
-    inputs = [synth.ssb_iq_torch(rank * C, C, k * N, N, dev) for k in range(pool)]
-    audio = torch.empty((C, N), dtype=torch.float32, device=dev)
-    dst = torch.empty((C, N, 2), dtype=torch.int32, device=dev) if args.dst else None
-    torch.cuda.synchronize(dev)
+    gather = None
+    if world > 1 and not args.no_gather:
+        gs = max(10, args.steps // 4)
+        gt = gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, gs, 5)
+        gather = {"value": round(world * C * N * gs / gt / 1e6, 2), "unit": "Msamples/s", "steps": gs,
+                  "ms_per_step": round(gt / gs * 1e3, 5),
+                  "how": "every launch's f32 audio gathered to rank 0 (torch.distributed.gather = grouped RCCL "
+                         "send/recv over xGMI) on a comm stream, overlapped with the next launch (double-buffered)"}
 
-    for s in range(args.warmup):
-        chain.process(inputs[s % pool], audio, dst)
-    torch.cuda.synchronize(dev)
+    ns = None
+    if world == 1 and not args.no_northstar and args.workload != "northstar" and not (args.channels or args.frames):
+        nw = WORKLOADS["northstar"]
+        n_el, n_kt, n_plan, n_ok, _ = timed_run(U, synth, shard, torch, dist, dev, 1, 0, nw["channels"], nw["frames"],
+                                                20, 3, 3, False)
+        n_ab = algorithmic_bytes(n_plan, nw["channels"], nw["frames"], False)
+        n_roof, n_kms = roofline_of(n_ab, n_kt, pmc_traffic("northstar"))
+        n_dev = sum(n_kms.values())
+        ns = {"workload": nw["desc"], "value": round(nw["channels"] * nw["frames"] * 20 / n_el / 1e6, 2),
+              "unit": "Msamples/s", "steps": 20, "ms_per_step": round(n_el / 20 * 1e3, 5), "roofline": n_roof,
+              "kernel_ms": {k: round(v, 5) for k, v in n_kms.items()},
+              "chain_hbm_frac": round(n_ab["chain"] / (n_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+              "alg_bytes_per_sample": round(n_ab["chain"] / (nw["channels"] * nw["frames"]), 2),
+              "outputs_finite": n_ok}
 
-    chain.enable_timing(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        chain.process(inputs[s % pool], audio, dst)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ktimes = chain.kernel_times()
-    chain.enable_timing(False)
-
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-
-    ok = bool(torch.isfinite(audio).all().item())
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -165,14 +282,8 @@ def main():
     total_samples = world * C * N * args.steps
     value = total_samples / elapsed / 1e6
     ab = algorithmic_bytes(plan, C, N, args.dst)
-    kms = {k: v[0] / max(v[1], 1) for k, v in ktimes.items()}       # mean ms per launch
-    dominant = max(kms, key=kms.get)
-    achieved = ab[dominant] / (kms[dominant] * 1e-3) / 1e9
+    roofline, kms = roofline_of(ab, ktimes, pmc_traffic(args.workload) if not (args.channels or args.frames) else None)
     chain_dev_ms = sum(kms.values())
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": dominant, "alg_bytes_per_launch": ab[dominant],
-                "mean_launch_ms": round(kms[dominant], 5)}
     chain_gbs = ab["chain"] / (chain_dev_ms * 1e-3) / 1e9
     out = {
         "metric": "Msamples/s through full SSB-RX chain (node); % of HBM-roofline per GPU",
@@ -191,9 +302,14 @@ def main():
                   "alg_bytes_per_sample": round(ab["chain"] / (C * N), 2),
                   "s_live_bytes_per_channel": ab["s_live_bytes"],
                   "hbm_frac": round(chain_gbs / HBM_PEAK_GBS, 4),
-                  "fp32_ops_note": "see DESIGN.md: the chain is VALU-bound at this size"},
+                  "note": "C2 (4096 channels) is latency-bound: one lane per channel for the recursive "
+                          "stages leaves most of the 256 CUs idle; see DESIGN.md and north_star"},
         "outputs_finite": ok,
     }
+    if ns:
+        out["north_star"] = ns
+    if gather:
+        out["with_gather"] = gather
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(plan, N, args.cpu_budget)
     print(json.dumps(out), flush=True)

@@ -178,6 +178,15 @@ uhsdr_status uhsdr_rx_get_plan(uhsdr_rx_handle h, uhsdr_rx_plan* plan);
 uhsdr_status uhsdr_rx_set_stream(uhsdr_rx_handle h, void* stream);
 uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h);
 
+/* Wait until every call enqueued on the handle's stream has finished. */
+uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h);
+
+/* ---- device memory for plain-C hosts (no HIP headers needed) ---- */
+void*        uhsdr_device_alloc(uint64_t bytes);             /* NULL on failure */
+void         uhsdr_device_free(void* p);
+uhsdr_status uhsdr_copy_to_device(void* dst, const void* src, uint64_t bytes);
+uhsdr_status uhsdr_copy_to_host(void* dst, const void* src, uint64_t bytes);
+
 /* ---- diagnostics ---- */
 const char*  uhsdr_version(void);
 /* sizeof(uhsdr_rx_config), sizeof(uhsdr_rx_plan): lets FFI bindings check their layouts */

@@ -53,3 +53,13 @@ def test_unsupported_modes_are_reported():
     assert lib.uhsdr_rx_plan_supported(C.byref(plan)) == 0
     plan = U.build_plan(U.default_config())
     assert lib.uhsdr_rx_plan_supported(C.byref(plan)) == 1
+
+
+def test_plain_c_host_links_against_the_abi():
+    """examples/rx_batch.c (gcc, no HIP headers) links against libuhsdr_amd.so; run without
+    arguments it only prints usage (no device call)."""
+    import subprocess
+    exe = os.path.join(ROOT, "examples", "build", "rx_batch")
+    assert os.path.exists(exe), "run `make` first"
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 2 and "uhsdr_amd" in r.stderr

@@ -120,3 +120,21 @@ def test_device_host_entry_point(cuda):
     a1, dst = chain.process_host(g["iq"])
     assert_bitexact(a1, g["a1"], "process_host")
     np.testing.assert_array_equal(dst, g["dst"])
+
+
+def test_plain_c_host_matches_reference_firmware(cuda, tmp_path):
+    """The gcc-built C host (examples/rx_batch.c) through the C ABI: bit-exact vs the
+    reference firmware's fixture."""
+    import os
+    import subprocess
+    g = load(golden_files()[0])
+    C, n, _ = g["iq"].shape
+    src, out = tmp_path / "iq.bin", tmp_path / "audio.bin"
+    np.ascontiguousarray(g["iq"], dtype=np.int32).tofile(src)
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "build", "rx_batch")
+    cfg = U.config_from_ref_args(g["args"])
+    r = subprocess.run([exe, str(src), str(out), str(C), str(n), "256", str(cfg.filter_path), str(cfg.dmod_mode)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(out, dtype=np.float32).reshape(C, n)
+    assert_bitexact(got, g["a1"], "rx_batch.c")

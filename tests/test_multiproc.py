@@ -1,0 +1,64 @@
+"""N > 1 path on CPU: world_size-2 gloo ranks, each owning a contiguous channel range (the
+sharding bench.py uses on the GPU box), gathering their audio to rank 0.  The per-rank chain
+here is the CPU oracle (the checker; the GPU path is the same code with the HIP chain and
+RCCL): rank 0's gathered result must equal one process running all channels, bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+import uhsdr_amd as U
+from uhsdr_amd import shard, synth
+
+PER_RANK, FRAMES = 6, 256
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard.channel_range(PER_RANK, rank)
+    plan = U.build_plan(U.default_config())
+    iq = synth.ssb_iq(np.arange(lo, hi), 0, FRAMES)
+    a1, _ = oracle.OracleRx(plan, hi - lo).process(iq)
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)           # bench.py's max-over-ranks timing
+    full = shard.gather_to_root(torch.from_numpy(a1), dist, world, rank)
+    if rank == 0:
+        assert float(t.item()) == float(world)
+        np.save(out_path, full.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_shard_and_gather(tmp_path):
+    world = 2
+    out = str(tmp_path / "gathered.npy")
+    mp.start_processes(_rank_main, args=(world, _free_port(), out), nprocs=world, start_method="spawn")
+    got = np.load(out)
+    plan = U.build_plan(U.default_config())
+    iq = synth.ssb_iq(np.arange(world * PER_RANK), 0, FRAMES)
+    ref, _ = oracle.OracleRx(plan, world * PER_RANK).process(iq)
+    assert got.shape == ref.shape
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("total,world", [(10, 3), (4096, 8), (7, 8)])
+def test_split_range_covers(total, world):
+    ranges = [shard.split_range(total, world, r) for r in range(world)]
+    assert ranges[0][0] == 0 and ranges[-1][1] == total
+    for (a, b), (c, d) in zip(ranges, ranges[1:]):
+        assert b == c and b - a >= d - c

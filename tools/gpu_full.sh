@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round evidence on one GPU box: parity tests, smoke, the default bench line, kernel-trace
+# stats (C2 and north-star), PMC passes (FETCH_SIZE / WRITE_SIZE and SQ counters).
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+tag=${1:-cur}
+step() { echo "=== $1 ($(date +%T))"; }
+step "pytest gpu"
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+tail -3 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || { echo "pytest gpu failed rc=$rc"; tail -60 gpurun_out/pytest_gpu.log; exit $rc; }
+step "smoke"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+step "bench (default)"
+timeout -k 10 400 python bench.py > gpurun_out/bench_${tag}.json 2> gpurun_out/bench_${tag}.err || { tail -30 gpurun_out/bench_${tag}.err; exit 1; }
+cat gpurun_out/bench_${tag}.json
+step "rocprof kernel trace c2"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2_${tag} -o prof --output-format csv -- python bench.py --steps 200 --warmup 20 --no-cpu --no-northstar > gpurun_out/prof_c2_${tag}.log 2>&1 || { tail -20 gpurun_out/prof_c2_${tag}.log; exit 1; }
+step "rocprof kernel trace northstar"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ns_${tag} -o prof --output-format csv -- python bench.py --workload northstar --steps 20 --warmup 3 --no-cpu > gpurun_out/prof_ns_${tag}.log 2>&1 || { tail -20 gpurun_out/prof_ns_${tag}.log; exit 1; }
+step "pmc northstar"
+bash tools/gpu_pmc.sh ns_${tag} --workload northstar --steps 5 --warmup 2 || exit 1
+step "pmc c2"
+bash tools/gpu_pmc.sh c2_${tag} --steps 20 --warmup 5 --no-northstar || exit 1
+python tools/pmc_summary.py ns_${tag} > gpurun_out/pmc_northstar_${tag}.json
+python tools/pmc_summary.py c2_${tag} > gpurun_out/pmc_c2_${tag}.json
+echo DONE

@@ -13,6 +13,6 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD S
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   echo "=== pass $i: $grp"
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_$tag/p$i -o pmc -- python bench.py --no-cpu "$@" > gpurun_out/pmc_$tag/p$i.log 2>&1 || { echo "pass $i failed"; tail -20 gpurun_out/pmc_$tag/p$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_$tag/p$i -o pmc -- python bench.py --no-cpu --no-northstar "$@" > gpurun_out/pmc_$tag/p$i.log 2>&1 || { echo "pass $i failed"; tail -20 gpurun_out/pmc_$tag/p$i.log; exit 1; }
 done
 echo PMC_DONE

@@ -90,6 +90,11 @@ SIGNATURES = {
     "uhsdr_rx_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_rx_kernel_times": (C.c_int32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int32), C.c_int32]),
     "uhsdr_rx_kernel_name": (C.c_char_p, [C.c_int32]),
+    "uhsdr_rx_synchronize": (C.c_int, [C.c_void_p]),
+    "uhsdr_device_alloc": (C.c_void_p, [C.c_uint64]),
+    "uhsdr_device_free": (None, [C.c_void_p]),
+    "uhsdr_copy_to_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "uhsdr_copy_to_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
 }
 
 _lib = None

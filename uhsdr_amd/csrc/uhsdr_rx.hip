@@ -1249,6 +1249,36 @@ extern "C" uhsdr_status uhsdr_rx_process_host(uhsdr_rx_handle h, const int32_t* 
     return st;
 }
 
+extern "C" uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return UHSDR_OK;
+}
+
+extern "C" void* uhsdr_device_alloc(uint64_t bytes)
+{
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) { uhsdr_set_error("hipMalloc(%llu) failed", (unsigned long long)bytes); return nullptr; }
+    return p;
+}
+
+extern "C" void uhsdr_device_free(void* p) { if (p) (void)hipFree(p); }
+
+extern "C" uhsdr_status uhsdr_copy_to_device(void* dst, const void* src, uint64_t bytes)
+{
+    if (!dst || !src) return UHSDR_ARGUMENT_ERROR;
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_copy_to_host(void* dst, const void* src, uint64_t bytes)
+{
+    if (!dst || !src) return UHSDR_ARGUMENT_ERROR;
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return UHSDR_OK;
+}
+
 extern "C" uhsdr_status uhsdr_rx_get_plan(uhsdr_rx_handle h, uhsdr_rx_plan* plan)
 {
     if (!h || !plan) return UHSDR_ARGUMENT_ERROR;

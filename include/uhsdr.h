@@ -49,6 +49,9 @@ typedef enum
     UHSDR_DEVICE_ERROR = -11      /* HIP runtime error */
 } uhsdr_status;
 
+/* sam_sideband_t, drivers/audio/audio_driver.h:181-190 */
+enum { UHSDR_SAM_SIDEBAND_BOTH = 0, UHSDR_SAM_SIDEBAND_LSB = 1, UHSDR_SAM_SIDEBAND_USB = 2 };
+
 /* DemodModes_t, hardware/uhsdr_board.h:72-85 */
 enum { UHSDR_DEMOD_USB = 0, UHSDR_DEMOD_LSB = 1, UHSDR_DEMOD_CW = 2, UHSDR_DEMOD_AM = 3,
        UHSDR_DEMOD_SAM = 4, UHSDR_DEMOD_FM = 5, UHSDR_DEMOD_DIGI = 6 };
@@ -98,7 +101,12 @@ typedef struct uhsdr_rx_config
     int32_t agc_hang_thresh;      /* agc_wdsp_conf.hang_thresh (45) */
     int32_t agc_tau_decay[6];     /* agc_wdsp_conf.tau_decay[] */
     int32_t agc_tau_hang_decay;   /* agc_wdsp_conf.tau_hang_decay */
-    int32_t reserved[16];
+    int32_t sam_sideband;         /* ads.sam_sideband: 0 both, 1 LSB, 2 USB (audio_driver.h:181-190) */
+    int32_t sam_pll_fmax;         /* ads.pll_fmax_int (2500) */
+    int32_t sam_zeta;             /* ads.zeta_int, zeta x 100 (65) */
+    int32_t sam_omega_n;          /* ads.omegaN_int (250) */
+    int32_t fade_leveler;         /* ads.fade_leveler (1) */
+    int32_t reserved[11];
 } uhsdr_rx_config;
 
 /* AudioAgc_SetupAgcWdsp() results (audio_agc.c:126-339) */
@@ -153,6 +161,12 @@ typedef struct uhsdr_rx_plan
     float   post_agc_scale;       /* audio_driver.c:2513-2524 */
     float   line_out_scale;       /* LINE_OUT_SCALING_FACTOR, audio_driver.h:396 */
     uhsdr_agc_plan agc;
+    /* AM / SAM (AudioDriver_DemodSAM, audio_driver.c:1990-2166) */
+    float   dec_q[UHSDR_MAX_DEC_TAPS];  /* DECIMATE_RX_Q taps: the path's Q table for AM/SAM (audio_filter.c:1167-1176) */
+    int32_t sam_sideband, fade_leveler;
+    /* AudioDriver_SetSamPllParameters, audio_driver.c:709-745 */
+    float   sam_omega_min, sam_omega_max, sam_g1, sam_g2;
+    float   fade_mtauR, fade_onem_mtauR, fade_mtauI, fade_onem_mtauI;
     int32_t reserved[64];
 } uhsdr_rx_plan;
 

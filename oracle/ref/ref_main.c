@@ -114,6 +114,12 @@ static void dump_setup(void)
     print_fvec("hilbert_i", Fir_Rx_Hilbert_I.pCoeffs, Fir_Rx_Hilbert_I.numTaps, 0);
     print_fvec("hilbert_q", Fir_Rx_Hilbert_Q.pCoeffs, Fir_Rx_Hilbert_Q.numTaps, 0);
     print_fvec("decim", DECIMATE_RX_I.pCoeffs, DECIMATE_RX_I.numTaps, 0);
+    print_fvec("decim_q", DECIMATE_RX_Q.pCoeffs, DECIMATE_RX_Q.numTaps, 0);
+    {
+        const float sam[8] = { adb.sam.omega_min, adb.sam.omega_max, adb.sam.g1, adb.sam.g2,
+                               adb.sam.mtauR, adb.sam.onem_mtauR, adb.sam.mtauI, adb.sam.onem_mtauI };
+        print_fvec("sam", sam, 8, 0);
+    }
     print_fvec("pre_k", pre->pkCoeffs, pre->numStages, 0);
     print_fvec("pre_v", pre->pvCoeffs, pre->numStages ? pre->numStages + 1 : 0, 0);
     print_fvec("aa_k", aa->pkCoeffs, aa->numStages, 0);

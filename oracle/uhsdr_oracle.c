@@ -1,3 +1,4 @@
+#define _GNU_SOURCE
 /*
  * ORACLE -- TEST INFRASTRUCTURE ONLY (see uhsdr_oracle.h).  Compile without FP contraction
  * (-ffp-contract=off, no -march): every float operation below is one IEEE-754 binary32
@@ -15,6 +16,7 @@
 
 #define BLK UHSDR_IQ_BLOCK_SIZE
 #define IQ_BIT_SCALE_DOWN 0.0000152587890625f   /* audio_driver.h:596 (2^-16) */
+#define CMSIS_PI 3.14159265358979f              /* PI, CMSIS/Include/arm_math.h:334 */
 
 size_t uo_rx_state_size(void) { return sizeof(uo_rx_state); }
 
@@ -271,6 +273,91 @@ static void agc_run(const uhsdr_agc_plan* a, uo_rx_state* s, float* buf, int n)
     }
 }
 
+/* AudioDriver_FadeLeveler, audio_driver.c:1911-1923 (channel 0) */
+static float fade_leveler(const uhsdr_rx_plan* p, uo_rx_state* s, float audio, float corr)
+{
+    s->fade_dc27 = p->fade_mtauR * s->fade_dc27 + p->fade_onem_mtauR * audio;
+    s->fade_dc_insert = p->fade_mtauI * s->fade_dc_insert + p->fade_onem_mtauI * corr;
+    audio = audio + s->fade_dc_insert - s->fade_dc27;
+    return audio;
+}
+
+/* the 7-stage allpass pair of the SAM sideband selector, demod_sam_const (audio_driver.c:1931-1953) */
+static const float sam_c0[7] = { -0.328201924180698, -0.744171491539427, -0.923022915444215, -0.978490468768238,
+                                 -0.994128272402075, -0.998458978159551, -0.999790306259206 };
+static const float sam_c1[7] = { -0.0991227952747244, -0.565619728761389, -0.857467122550052, -0.959123933111275,
+                                 -0.988739372718090, -0.996959189310611, -0.999282492800792 };
+
+/* AudioDriver_DemodSAM, audio_driver.c:1990-2166 (mono; the display-only carrier estimate
+   at :2150-2162 does not touch the audio and is not restated) */
+static void demod_sam(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, const float* qb, float* a0, int n)
+{
+    if (p->dmod_mode == UHSDR_DEMOD_AM)
+    {
+        for (int i = 0; i < n; i++)
+        {
+            const float in = ib[i] * ib[i] + qb[i] * qb[i];
+            float audio = (in >= 0.0f) ? sqrtf(in) : 0.0f;      /* arm_sqrt_f32, arm_math.h:5745-5771 */
+            if (p->fade_leveler) audio = fade_leveler(p, s, audio, 0);
+            a0[i] = audio;
+        }
+        return;
+    }
+    for (int i = 0; i < n; i++)
+    {
+        float Sin, Cos;
+        sincosf(s->sam_phs, &Sin, &Cos);
+        const float ai = Cos * ib[i];
+        const float bi = Sin * ib[i];
+        const float aq = Cos * qb[i];
+        const float bq = Sin * qb[i];
+        float audio;
+        const float corr[2] = { ai + bq, -bi + aq };
+        if (p->sam_sideband != UHSDR_SAM_SIDEBAND_BOTH)
+        {
+            s->sam_a[0] = s->sam_dsI;
+            s->sam_b[0] = bi;
+            s->sam_c[0] = s->sam_dsQ;
+            s->sam_d[0] = aq;
+            s->sam_dsI = ai;
+            s->sam_dsQ = bq;
+            for (int j = 0; j < 7; j++)
+            {
+                const int k = 3 * j;
+                s->sam_a[k + 3] = sam_c0[j] * (s->sam_a[k] - s->sam_a[k + 5]) + s->sam_a[k + 2];
+                s->sam_b[k + 3] = sam_c1[j] * (s->sam_b[k] - s->sam_b[k + 5]) + s->sam_b[k + 2];
+                s->sam_c[k + 3] = sam_c0[j] * (s->sam_c[k] - s->sam_c[k + 5]) + s->sam_c[k + 2];
+                s->sam_d[k + 3] = sam_c1[j] * (s->sam_d[k] - s->sam_d[k + 5]) + s->sam_d[k + 2];
+            }
+            const float ai_ps = s->sam_a[21], bi_ps = s->sam_b[21], bq_ps = s->sam_c[21], aq_ps = s->sam_d[21];
+            for (int j = 23; j > 0; j--)
+            {
+                s->sam_a[j] = s->sam_a[j - 1];
+                s->sam_b[j] = s->sam_b[j - 1];
+                s->sam_c[j] = s->sam_c[j - 1];
+                s->sam_d[j] = s->sam_d[j - 1];
+            }
+            if (p->sam_sideband == UHSDR_SAM_SIDEBAND_LSB) audio = (ai_ps + bi_ps) - (aq_ps - bq_ps);
+            else audio = (ai_ps - bi_ps) + (aq_ps + bq_ps);
+        }
+        else
+        {
+            audio = corr[0];
+        }
+        if (p->fade_leveler) audio = fade_leveler(p, s, audio, corr[0]);
+        a0[i] = audio;
+        const float phzerror = atan2f(corr[1], corr[0]);
+        const float del_out = s->sam_fil_out;
+        s->sam_omega2 = s->sam_omega2 + p->sam_g2 * phzerror;
+        if (s->sam_omega2 < p->sam_omega_min) s->sam_omega2 = p->sam_omega_min;
+        else if (s->sam_omega2 > p->sam_omega_max) s->sam_omega2 = p->sam_omega_max;
+        s->sam_fil_out = p->sam_g1 * phzerror + s->sam_omega2;
+        s->sam_phs = s->sam_phs + del_out;
+        while (s->sam_phs >= 2.0 * CMSIS_PI) s->sam_phs -= (2.0 * CMSIS_PI);
+        while (s->sam_phs < 0.0) s->sam_phs += (2.0 * CMSIS_PI);
+    }
+}
+
 /* float -> int32 as x86 cvttss2si does it (out of range / NaN -> INT32_MIN), then the
    firmware's << AUDIO_BIT_SHIFT (audio_driver.c:2911-2923) in two's complement. */
 static int32_t to_dma(float f)
@@ -363,17 +450,20 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
 
     const int nd = n / p->decimation_rate;
     const int niq = p->use_decimated_iq ? nd : n;
+    const int am = p->dmod_mode == UHSDR_DEMOD_AM || p->dmod_mode == UHSDR_DEMOD_SAM;
     if (p->use_decimated_iq)
     {
         fir_decimate(p->dec, p->dec_taps, p->decimation_rate, s->dec_i, ib, ib, n);
-        fir_decimate(p->dec, p->dec_taps, p->decimation_rate, s->dec_q, qb, qb, n);
+        fir_decimate(am ? p->dec_q : p->dec, p->dec_taps, p->decimation_rate, s->dec_q, qb, qb, n);
     }
     if (p->hilbert_taps)
     {
         fir(p->hilbert_i, p->hilbert_taps, s->hil_i, ib, ib, niq);
         fir(p->hilbert_q, p->hilbert_taps, s->hil_q, qb, qb, niq);
     }
-    if (p->lsb)
+    if (am)
+        demod_sam(p, s, ib, qb, a0, niq);
+    else if (p->lsb)
         for (int i = 0; i < niq; i++) a0[i] = ib[i] - qb[i];
     else
         for (int i = 0; i < niq; i++) a0[i] = ib[i] + qb[i];

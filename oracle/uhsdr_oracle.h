@@ -42,6 +42,10 @@ typedef struct uo_rx_state
     float abs_ring[UHSDR_AGC_RING];
     int32_t out_index, in_index, hang_counter, decay_type, state;
     float ring_max, volts, save_volts, fast_backaverage, hang_backaverage, wold;
+    /* sam_data (audio_driver.c:1955-1976) and the fade leveler statics (:1911-1923) */
+    float sam_phs, sam_omega2, sam_fil_out, sam_dsI, sam_dsQ;
+    float sam_a[24], sam_b[24], sam_c[24], sam_d[24];
+    float fade_dc27, fade_dc_insert;
 } uo_rx_state;
 
 size_t uo_rx_state_size(void);

@@ -61,6 +61,17 @@ CONFIGS = {
     "p48_m6k": ({"mode": 0, "path": 48, "iqmode": 2}, {"center": 6000.0}),
     "p48_p6k": ({"mode": 0, "path": 48, "iqmode": 1}, {"center": -6000.0}),
     "p48_off": ({"mode": 0, "path": 48, "iqmode": 0}, {"center": 0.0}),
+    # AM / SAM (C3): AM carrier at +12 kHz +- 200 Hz, 50 % modulation with a 1 kHz tone
+    "p70_am": ({"mode": 3, "path": 70}, {"am": True}),
+    "p70_sam": ({"mode": 4, "path": 70}, {"am": True}),
+    "p70_sam_nofade": ({"mode": 4, "path": 70, "fade": 0}, {"am": True}),
+    "p70_sam_dx": ({"mode": 4, "path": 70, "zeta": 20, "omegan": 70, "pll_fmax": 1000}, {"am": True}),
+    "p75_sam": ({"mode": 4, "path": 75}, {"am": True}),
+    "p83_am": ({"mode": 3, "path": 83}, {"am": True}),
+    "p86_sam": ({"mode": 4, "path": 86}, {"am": True}),
+    "p70_sam_agcoff": ({"mode": 4, "path": 70, "agc_mode": 5}, {"am": True}),
+    "p70_sam_usb": ({"mode": 4, "path": 70, "sam_sb": 2}, {"am": True}),
+    "p70_sam_lsb": ({"mode": 4, "path": 70, "sam_sb": 1}, {"am": True}),
 }
 
 
@@ -86,7 +97,10 @@ def make(name: str):
     args, sig = CONFIGS[name]
     sig = dict(sig)
     center = sig.pop("center", None)
-    iq = synth.ssb_iq(np.arange(NCH), 0, NFRAMES, carrier=center if center is not None else 12000.0, **sig)
+    if sig.pop("am", False):
+        iq = synth.am_iq(np.arange(NCH), 0, NFRAMES)
+    else:
+        iq = synth.ssb_iq(np.arange(NCH), 0, NFRAMES, carrier=center if center is not None else 12000.0, **sig)
     a1 = np.empty((NCH, NFRAMES), np.float32)
     dst = np.empty((NCH, NFRAMES, 2), np.int32)
     for c in range(NCH):

@@ -1,0 +1,28 @@
+"""uhsdr_amd/csrc/uhsdr_libm.h (the device's sincosf / atan2f) reproduces the host glibc bit for
+bit -- the SAM PLL and FM discriminator of the reference call glibc (audio_driver.c:2039,
+2128, 1581).  tools/libm_check.c is compiled here and run on a strided subset (every 251st
+float of [-2pi, 2pi]) and on 2e6 atan2f operand pairs; the exhaustive run (every float of
+[-2pi, 2pi], 2e8 atan2f pairs) is recorded in tests/golden/libm_pin.txt."""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _build(tmp_path):
+    exe = str(tmp_path / "libm_check")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", exe, os.path.join(ROOT, "tools", "libm_check.c"), "-lm"],
+                   check=True)
+    return exe
+
+
+def test_sincosf_matches_glibc(tmp_path):
+    r = subprocess.run([_build(tmp_path), "sincos", "251"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout
+    assert " 0 of " in r.stdout
+
+
+def test_atan2f_matches_glibc(tmp_path):
+    r = subprocess.run([_build(tmp_path), "atan2", "2000000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout
+    assert " 0 of " in r.stdout

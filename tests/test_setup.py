@@ -22,15 +22,27 @@ def test_plan_matches_reference_setup(path):
     p = U.build_plan(U.config_from_ref_args(g["args"]))
     assert p.filter_path == s["filter_path"]
     assert p.decimation_rate == s["decimation_rate"] and p.decimated_freq == s["decimated_freq"]
-    assert p.hilbert_taps == s["hilbert_taps"] and p.dec_taps == s["decim_taps"]
+    am = p.dmod_mode in (U.DEMOD_AM, U.DEMOD_SAM)
+    # AM / SAM skip the Hilbert FIRs (audio_driver.c:2748): the plan carries none
+    assert p.hilbert_taps == (0 if am else s["hilbert_taps"]) and p.dec_taps == s["decim_taps"]
+    if am:
+        np.testing.assert_array_equal(fbits(p.dec_q, p.dec_taps), np.array(s["decim_q"], dtype=np.uint32))
+    if "sam" in s:
+        mine = [p.sam_omega_min, p.sam_omega_max, p.sam_g1, p.sam_g2, p.fade_mtauR, p.fade_onem_mtauR,
+                p.fade_mtauI, p.fade_onem_mtauI]
+        np.testing.assert_array_equal(np.array(mine, dtype=np.float32).view(np.uint32),
+                                      np.array(s["sam"], dtype=np.uint32), err_msg="sam pll / fade")
     assert p.pre_stages == s["pre_stages"] and p.aa_stages == s["aa_stages"]
     assert p.interp_L == s["interp_L"] and p.interp_phase == s["interp_phase"]
     for field, key, n in [("biquad1", "biquad1", 20), ("biquad2", "biquad2", 5),
-                          ("hilbert_i", "hilbert_i", p.hilbert_taps), ("hilbert_q", "hilbert_q", p.hilbert_taps),
+                          ("hilbert_i", "hilbert_i", 0 if am else p.hilbert_taps),
+                          ("hilbert_q", "hilbert_q", 0 if am else p.hilbert_taps),
                           ("dec", "decim", p.dec_taps), ("pre_k", "pre_k", p.pre_stages),
                           ("pre_v", "pre_v", p.pre_stages + 1 if p.pre_stages else 0),
                           ("aa_k", "aa_k", p.aa_stages), ("aa_v", "aa_v", p.aa_stages + 1 if p.aa_stages else 0),
                           ("interp", "interp", p.interp_L * p.interp_phase)]:
+        if am and field.startswith("hilbert"):
+            continue
         np.testing.assert_array_equal(fbits(getattr(p, field), n), np.array(s[key], dtype=np.uint32), err_msg=field)
     a = p.agc
     assert a.attack_buffsize == agc["attack_buffsize"] and a.ring_buffsize == agc["ring_buffsize"]

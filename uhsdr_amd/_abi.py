@@ -25,6 +25,7 @@ UHSDR_UNSUPPORTED = -10
 UHSDR_DEVICE_ERROR = -11
 
 DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI = range(7)
+SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB = range(3)
 
 
 class RxConfig(C.Structure):
@@ -36,7 +37,8 @@ class RxConfig(C.Structure):
         ("cw_lsb", C.c_int32), ("digi_lsb", C.c_int32), ("agc_mode", C.c_int32), ("agc_slope", C.c_int32),
         ("agc_thresh", C.c_int32), ("agc_hang_enable", C.c_int32), ("agc_hang_time", C.c_int32),
         ("agc_hang_thresh", C.c_int32), ("agc_tau_decay", C.c_int32 * 6), ("agc_tau_hang_decay", C.c_int32),
-        ("reserved", C.c_int32 * 16),
+        ("sam_sideband", C.c_int32), ("sam_pll_fmax", C.c_int32), ("sam_zeta", C.c_int32), ("sam_omega_n", C.c_int32),
+        ("fade_leveler", C.c_int32), ("reserved", C.c_int32 * 11),
     ]
 
 
@@ -66,7 +68,11 @@ class RxPlan(C.Structure):
         ("aa_stages", C.c_int32), ("aa_k", C.c_float * MAX_LATTICE), ("aa_v", C.c_float * (MAX_LATTICE + 1)),
         ("biquad1", C.c_float * 20), ("biquad2", C.c_float * 5),
         ("post_agc_scale", C.c_float), ("line_out_scale", C.c_float),
-        ("agc", AgcPlan), ("reserved", C.c_int32 * 64),
+        ("agc", AgcPlan),
+        ("dec_q", C.c_float * MAX_DEC_TAPS), ("sam_sideband", C.c_int32), ("fade_leveler", C.c_int32),
+        ("sam_omega_min", C.c_float), ("sam_omega_max", C.c_float), ("sam_g1", C.c_float), ("sam_g2", C.c_float),
+        ("fade_mtauR", C.c_float), ("fade_onem_mtauR", C.c_float), ("fade_mtauI", C.c_float),
+        ("fade_onem_mtauI", C.c_float), ("reserved", C.c_int32 * 64),
     ]
 
 
@@ -150,6 +156,8 @@ REF_ARG_MAP = {
     "gain_i": "iq_gain_i", "gain_q": "iq_gain_q", "phase": "iq_phase_balance", "dsp": "dsp_active",
     "notch": "notch_frequency", "peak": "peak_frequency", "bass": "bass_gain", "treble": "treble_gain",
     "agc_mode": "agc_mode", "agc_thresh": "agc_thresh", "agc_slope": "agc_slope", "agc_hang": "agc_hang_enable",
+    "sam_sb": "sam_sideband", "pll_fmax": "sam_pll_fmax", "zeta": "sam_zeta", "omegan": "sam_omega_n",
+    "fade": "fade_leveler",
 }
 
 

@@ -1,0 +1,216 @@
+/*
+ * glibc-exact single-precision libm functions the demodulators call per sample.
+ *
+ * The reference runs AudioDriver_DemodSAM / AudioDriver_DemodFM (drivers/audio/audio_driver.c:
+ * 2021-2147, 1544-1600) against the host's libm: glibc 2.35 here and on the GPU box host
+ * (both x86-64 with FMA).  The SAM PLL feeds every rounding of sincosf / atan2f back into
+ * its phase, so the device must reproduce those functions bit for bit, not merely within an
+ * ulp.  This header restates glibc 2.35's published algorithms:
+ *
+ *   sincosf  sysdeps/ieee754/flt-32/s_sincosf.c + sincosf.h (Szabolcs Nagy, ARM
+ *            optimized-routines, 2018): double-precision polynomials, fast pi/2 reduction;
+ *            the x86-64 build dispatches (IFUNC) to s_sincosf-fma.c, compiled with -mfma,
+ *            so every a + b*c below is one fused multiply-add.  Table values: the
+ *            __sincosf_table of the published source.
+ *   atan2f   sysdeps/ieee754/flt-32/e_atan2f.c + s_atanf.c (fdlibm, Sun 1993): pure binary32
+ *            arithmetic, no IFUNC variant.
+ *
+ * Pinned against the host's libm by tests/test_libm.py (every float in [0, 2*pi] for
+ * sincosf -- the PLL phase range -- plus random and special operands for atan2f).
+ * Compiled by hipcc for the device and by gcc (-ffp-contract=off) for the host check;
+ * the fused operations are explicit fma() calls, so no compiler contraction is involved.
+ */
+#ifndef UHSDR_LIBM_H
+#define UHSDR_LIBM_H
+
+#include <stdint.h>
+#include <string.h>
+#include <math.h>
+
+#ifdef __HIPCC__
+#define UHSDR_LIBM_FN __host__ __device__ static inline
+#else
+#define UHSDR_LIBM_FN static inline
+#endif
+
+UHSDR_LIBM_FN uint32_t ul_asuint(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+UHSDR_LIBM_FN float ul_asfloat(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+/* top 12 bits of |x|: exponent and 3 mantissa bits (s_sincosf.c abstop12) */
+UHSDR_LIBM_FN uint32_t ul_abstop12(float x) { return (ul_asuint(x) >> 20) & 0x7ff; }
+
+/* ---- sincosf, |y| < 120 (the PLL phase is in [0, 2*pi)) ---- */
+typedef struct
+{
+    double sign[4];          /* sign of sine in quadrants 0..3 */
+    double hpi_inv;          /* 2/pi * 2^24 (no round-to-int intrinsics on x86-64) */
+    double hpi;              /* pi/2 */
+    double c0, c1, s1, c2, s2, c3, s3, c4;
+} ul_sincos_t;
+
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+static inline const ul_sincos_t* ul_sincosf_table(int k)
+{
+#ifdef __HIPCC__
+    static __constant__ const ul_sincos_t t[2] = {
+#else
+    static const ul_sincos_t t[2] = {
+#endif
+        { { 1.0, -1.0, -1.0, 1.0 }, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+          0x1p+0, -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
+          0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16 },
+        { { 1.0, -1.0, -1.0, 1.0 }, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+          -0x1p+0, 0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5,
+          0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16 },
+    };
+    return &t[k];
+}
+
+/* sincosf.h sincosf_poly (FMA build) */
+UHSDR_LIBM_FN void ul_sincosf_poly(double x, double x2, const ul_sincos_t* p, int n, float* sinp, float* cosp)
+{
+    const double x4 = x2 * x2;
+    const double x3 = x2 * x;
+    const double c2 = fma(x2, p->c4, p->c3);
+    const double s1 = fma(x2, p->s3, p->s2);
+    const double c1 = fma(x2, p->c1, p->c0);
+    const double x5 = x3 * x2;
+    const double x6 = x4 * x2;
+    const double s = fma(x3, p->s1, x);
+    const double c = fma(x4, p->c2, c1);
+    const float rs = (float)fma(x5, s1, s);
+    const float rc = (float)fma(x6, c2, c);
+    if (n & 1) { *sinp = rc; *cosp = rs; }   /* quadrant swap */
+    else { *sinp = rs; *cosp = rc; }
+}
+
+/* s_sincosf.c for |y| < 120 (callers guarantee the range; the Payne-Hanek branch for huge
+   arguments is not needed by the PLL) */
+UHSDR_LIBM_FN void ul_sincosf(float y, float* sinp, float* cosp)
+{
+    double x = y;
+    const ul_sincos_t* p = ul_sincosf_table(0);
+    if (ul_abstop12(y) < ul_abstop12(0x1.921fb6p-1f))        /* pio4f */
+    {
+        const double x2 = x * x;
+        if (ul_abstop12(y) < ul_abstop12(0x1p-12f))
+        {
+            *sinp = y;
+            *cosp = 1.0f;
+            return;
+        }
+        ul_sincosf_poly(x, x2, p, 0, sinp, cosp);
+    }
+    else
+    {
+        /* reduce_fast, !TOINT_INTRINSICS */
+        const double r = x * p->hpi_inv;
+        const int n = ((int32_t)r + 0x800000) >> 24;
+        x = fma(-(double)n, p->hpi, x);
+        const double s = p->sign[n & 3];
+        if (n & 2) p = ul_sincosf_table(1);
+        ul_sincosf_poly(x * s, x * x, p, n, sinp, cosp);
+    }
+}
+
+/* ---- atanf / atan2f (fdlibm binary32) ---- */
+UHSDR_LIBM_FN float ul_atanf(float x)
+{
+    const float atanhi[4] = { 4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f };
+    const float atanlo[4] = { 5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f };
+    const float aT[11] = { 3.3333334327e-01f, -2.0000000298e-01f, 1.4285714924e-01f, -1.1111110449e-01f,
+                           9.0908870101e-02f, -7.6918758452e-02f, 6.6610731184e-02f, -5.8335702866e-02f,
+                           4.9768779427e-02f, -3.6531571299e-02f, 1.6285819933e-02f };
+    const uint32_t hx = ul_asuint(x);
+    const uint32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000)                               /* |x| >= 2^25 */
+    {
+        if (ix > 0x7f800000) return x + x;              /* NaN */
+        return (hx >> 31) ? -atanhi[3] - atanlo[3] : atanhi[3] + atanlo[3];
+    }
+    if (ix < 0x3ee00000)                                /* |x| < 0.4375 */
+    {
+        if (ix < 0x31000000) return x;                  /* |x| < 2^-29 */
+        id = -1;
+    }
+    else
+    {
+        x = fabsf(x);
+        if (ix < 0x3f980000)                            /* |x| < 1.1875 */
+        {
+            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }   /* 7/16 <= |x| < 11/16 */
+            else { id = 1; x = (x - 1.0f) / (x + 1.0f); }                          /* 11/16 <= |x| < 19/16 */
+        }
+        else
+        {
+            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }   /* |x| < 2.4375 */
+            else { id = 3; x = -1.0f / x; }                                         /* 2.4375 <= |x| < 2^25 */
+        }
+    }
+    const float z = x * x;
+    const float w = z * z;
+    const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const float s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float zz = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return (hx >> 31) ? -zz : zz;
+}
+
+UHSDR_LIBM_FN float ul_atan2f(float y, float x)
+{
+    const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f,
+                pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+    const int32_t hx = (int32_t)ul_asuint(x), hy = (int32_t)ul_asuint(y);
+    const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;   /* NaN */
+    if (hx == 0x3f800000) return ul_atanf(y);               /* x = 1.0 */
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);      /* 2*sign(x) + sign(y) */
+    if (iy == 0)
+    {
+        switch (m)
+        {
+        case 0:
+        case 1: return y;                                   /* atan(+-0, +anything) = +-0 */
+        case 2: return pi + tiny;                           /* atan(+0, -anything) = pi */
+        default: return -pi - tiny;                         /* atan(-0, -anything) = -pi */
+        }
+    }
+    if (ix == 0) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000)
+    {
+        if (iy == 0x7f800000)
+        {
+            switch (m)
+            {
+            case 0: return pi_o_4 + tiny;
+            case 1: return -pi_o_4 - tiny;
+            case 2: return 3.0f * pi_o_4 + tiny;
+            default: return -3.0f * pi_o_4 - tiny;
+            }
+        }
+        switch (m)
+        {
+        case 0: return 0.0f;
+        case 1: return -0.0f;
+        case 2: return pi + tiny;
+        default: return -pi - tiny;
+        }
+    }
+    if (iy == 0x7f800000) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int32_t k = (iy - ix) >> 23;
+    float z;
+    if (k > 26) z = pi_o_2 + 0.5f * pi_lo;                 /* |y/x| > 2^26 */
+    else if (hx < 0 && k < -26) z = 0.0f;                   /* |y|/x < -2^26 */
+    else z = ul_atanf(fabsf(y / x));
+    switch (m)
+    {
+    case 0: return z;
+    case 1: return ul_asfloat(ul_asuint(z) ^ 0x80000000u);
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+    }
+}
+
+#endif /* UHSDR_LIBM_H */

@@ -33,6 +33,7 @@
 #include <stdlib.h>
 #include <math.h>
 #include "uhsdr_internal.h"
+#include "uhsdr_libm.h"
 
 #define BLK UHSDR_IQ_BLOCK_SIZE
 #define IQ_BIT_SCALE_DOWN 0.0000152587890625f
@@ -115,6 +116,7 @@ struct FrontArgs
     const float* osc_in;     // [2] oscillator {I, Q} at the start of this launch (shared by all channels)
     float* osc_out;          // [2] written by workgroup 0
     float* adec;             // decimated output of this launch; row stride ldd
+    float* adec_q;           // AM / SAM: decimated Q (adec holds I)
     int C, N, ld, ldd;
     int lw;                  // LDS window pitch per channel (floats, multiple of 4; host picks it
                              // for conflict-free ds_read_b128, front_window_pitch)
@@ -413,7 +415,25 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
 
     const bool lsb = P->lsb;
     float o[RD];
-    if (!DECIM_FIRST)
+    if constexpr (T2 == 0)
+    {
+        // AM / SAM: decimate I and Q with the path's own tables (DECIMATE_RX_I / _Q,
+        // audio_filter.c:1167-1176, audio_driver.c:2742-2746); no Hilbert (:2748); the
+        // demodulator in rx_back takes both
+        float dq[RD];
+        front_fill<T1>(W, a.hist1_i, c, act, live, b, nb, hA, xi, R);
+        fir_block<T1, RD, M>(W + b * R, as_taps(P->dec), o);
+        wave_sync();
+        front_fill<T1>(W, a.hist1_q, c, act, live, b, nb, hB, xq, R);
+        fir_block<T1, RD, M>(W + b * R, as_taps(P->dec_q), dq);
+        if (live)
+        {
+            float* dst = a.adec_q + (size_t)c * a.ldd + b * RD;
+#pragma unroll
+            for (int r = 0; r < RD; ++r) dst[r] = dq[r];
+        }
+    }
+    else if (!DECIM_FIRST)
     {
         float hi[R], hq[R];
         front_fill<T1>(W, a.hist1_i, c, act, live, b, nb, hA, xi, R);
@@ -489,12 +509,14 @@ struct BackState
     float* ring;     // [AGC_Q][B][C]  AGC inputs of the last AGC_Q calls
     float* agc;      // [6 + AGC_Q][C]  spare volts save_volts fast_bavg hang_bavg wold | call maxima[Q-1], leaving sample
     int* agci;       // [3][C]   hang_counter decay_type state
+    float* sam;      // AM / SAM: [7 + 96][C] phs omega2 fil_out dsI dsQ dc27 dc_insert | allpass a,b,c,d[24]
 };
 
 struct BackArgs
 {
     const uhsdr_rx_plan* plan;
-    const float* adec;   // [C][Nd]
+    const float* adec;   // [C][Nd]  (AM / SAM: decimated I)
+    const float* adec_q; // [C][Nd]  AM / SAM: decimated Q
     float* audio;        // [C][N]  or null
     int2* dst;           // [C][N]  or null
     BackState s;
@@ -559,20 +581,25 @@ __device__ __forceinline__ int to_dma(float f)
 }
 
 #define BACK_CH 64
-#define BACK_ROLES 3
 
-// The back end of one channel group runs as a 3-stage pipeline over 32-frame calls, one wave
-// per stage (lane == channel); stage s works on call it - s in iteration it and hands its
-// results to stage s+1 through double-buffered LDS, one workgroup barrier per iteration:
-//   role 0  lattice pre-filter -> WDSP AGC                    (decimated rate)
-//   role 1  post-AGC scale -> biquad_1 -> polyphase interp    (decimated rate -> 48 ksps)
-//   role 2  anti-alias lattice -> biquad_2 -> line-out scale -> f32 / int32 stores (48 ksps)
-// Splitting the serial chain three ways shortens the critical path per call (small batches)
-// and keeps each wave's coefficients + state small enough for 4 waves per SIMD (large ones).
+// demodulator kinds of rx_back (DM): the SSB/CW/DIGI sum I +- Q happens in rx_front
+enum { DM_NONE = 0, DM_AM = 1, DM_SAM = 2, DM_SAM_SB = 3 /* SAM with the allpass sideband selector */ };
+__host__ __device__ constexpr int back_roles(int dm) { return dm ? 4 : 3; }
+
+// The back end of one channel group runs as a pipeline over 32-frame calls, one wave per
+// stage (lane == channel); stage s works on call it - s in iteration it and hands its results
+// to stage s+1 through double-buffered LDS, one workgroup barrier per iteration:
+//   [demod]  AM envelope / SAM PLL (AM, SAM only)              (decimated rate)
+//   agc      lattice pre-filter -> WDSP AGC                    (decimated rate)
+//   audio    post-AGC scale -> biquad_1 -> polyphase interp    (decimated rate -> 48 ksps)
+//   output   anti-alias lattice -> biquad_2 -> line-out scale -> f32 / int32 stores (48 ksps)
+// Splitting the serial chain shortens the critical path per call (small batches) and keeps
+// each wave's coefficients + state small enough for 3-4 waves per SIMD (large ones).
 struct BackLds
 {
-    float* agc;   // [2][NDC][64]  role 0 -> role 1
-    float* mid;   // [2][BLK][64]  role 1 -> role 2
+    float* dem;   // [2][NDC][64]  demod -> agc
+    float* agc;   // [2][NDC][64]  agc -> audio
+    float* mid;   // [2][BLK][64]  audio -> output
 };
 
 template <int NDC>
@@ -581,6 +608,7 @@ __device__ __forceinline__ BackLds back_lds_carve(float* smem)
     BackLds l;
     l.mid = smem;
     l.agc = smem + 2 * BLK * BACK_CH;
+    l.dem = l.agc + 2 * NDC * BACK_CH;
     return l;
 }
 
@@ -595,11 +623,13 @@ __device__ __forceinline__ BackLds back_lds_carve(float* smem)
     const int calls = a.N / BLK;                                                               \
     (void)P; (void)live;
 
-// ---- role 0: IIR lattice pre-filter (audio_driver.c:2473-2482) + AudioAgc_RunAgcWdsp ----
-template <int PRE, int L, int W>
+// ---- agc role: IIR lattice pre-filter (audio_driver.c:2473-2482) + AudioAgc_RunAgcWdsp ----
+// input: adec from HBM (SSB: rx_front summed I +- Q), or the demod role's LDS output
+template <int PRE, int L, int W, int DM>
 __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
 {
     BACK_PROLOGUE
+    constexpr int ROLES = back_roles(DM), ST = DM ? 1 : 0;
     static_assert(W == AGC_Q * NDC + 1, "AGC window must be AGC_Q calls + 1 sample");
     // plan values copied to registers once (uniform -> SGPRs); reading them through P
     // inside the loop would reload them every sample (the state stores may alias)
@@ -629,12 +659,15 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
     // the decimated input and the ring slot of call `it` are fetched one call ahead
     float xnext[NDC], rnext[NDC];
     auto fetch = [&](int call) {
-        const float* src = a.adec + (size_t)cl * a.Nd + call * NDC;
-#pragma unroll
-        for (int m = 0; m < NDC; m += 4)
+        if (!DM)
         {
-            const float4 v = *(const float4*)(src + m);
-            xnext[m] = v.x; xnext[m + 1] = v.y; xnext[m + 2] = v.z; xnext[m + 3] = v.w;
+            const float* src = a.adec + (size_t)cl * a.Nd + call * NDC;
+#pragma unroll
+            for (int m = 0; m < NDC; m += 4)
+            {
+                const float4 v = *(const float4*)(src + m);
+                xnext[m] = v.x; xnext[m + 1] = v.y; xnext[m + 2] = v.z; xnext[m + 3] = v.w;
+            }
         }
         if (agc_on)
         {
@@ -645,14 +678,21 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
         }
     };
     fetch(0);
-    for (int it = 0; it < calls + BACK_ROLES - 1; ++it)
+    for (int it = 0; it < calls + ROLES - 1; ++it)
     {
-        if (it < calls)
+        const int call = it - ST;
+        if (call >= 0 && call < calls)
         {
             float xin[NDC], old[NDC];
 #pragma unroll
             for (int m = 0; m < NDC; ++m) { xin[m] = xnext[m]; old[m] = rnext[m]; }
-            if (it + 1 < calls) fetch(it + 1);
+            if (DM)
+            {
+                const float* di = lds.dem + (call & 1) * NDC * BACK_CH + lane;
+#pragma unroll
+                for (int m = 0; m < NDC; ++m) xin[m] = di[m * BACK_CH];
+            }
+            if (call + 1 < calls) fetch(call + 1);
             // suffix maxima of call k-Q; maximum of the whole calls k-Q+1 .. k-1
             float sfx[NDC];
             sfx[NDC - 1] = fabsf(old[NDC - 1]);
@@ -662,8 +702,8 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
 #pragma unroll
             for (int i = 1; i < AGC_Q - 1; ++i) wmax = fmaxf(wmax, cmax[i]);
             float pmax = 0.0f;
-            float* ring_out = a.s.ring + (size_t)((a.ring_phase + it) % AGC_Q) * NDC * C + c;
-            float* ao = lds.agc + (it & 1) * NDC * BACK_CH + lane;
+            float* ring_out = a.s.ring + (size_t)((a.ring_phase + call) % AGC_Q) * NDC * C + c;
+            float* ao = lds.agc + (call & 1) * NDC * BACK_CH + lane;
 #pragma unroll
             for (int m = 0; m < NDC; ++m)
             {
@@ -737,7 +777,7 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
                     const float mult = (A.out_target - A.slope_constant * vo) / volts;
                     x = out_sample * mult;
                 }
-                if (A.remove_dc)
+                if (agc_on && A.remove_dc)                      // mode 5 returns first (audio_agc.c:354-365)
                 {
                     const float w = (float)((double)x + (double)wold * 0.9999);
                     x = w - wold;
@@ -770,11 +810,12 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
     }
 }
 
-// ---- role 1: post-AGC scale (audio_driver.c:2513-2524), biquad_1 (:2527), interpolator (:2560-2577)
-template <int L, int PH>
+// ---- audio role: post-AGC scale (audio_driver.c:2513-2524), biquad_1 (:2527), interpolator (:2560-2577)
+template <int L, int PH, int DM>
 __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
 {
     BACK_PROLOGUE
+    constexpr int ROLES = back_roles(DM), ST = DM ? 2 : 1;
     float b1[20], ic[L * PH];
 #pragma unroll
     for (int i = 0; i < 20; ++i) b1[i] = P->biquad1[i];
@@ -786,9 +827,9 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
     for (int i = 0; i < 16; ++i) bq1[i] = a.s.bq1[i * C + cl];
 #pragma unroll
     for (int i = 0; i < PH - 1; ++i) ip[i] = a.s.interp[i * C + cl];
-    for (int it = 0; it < calls + BACK_ROLES - 1; ++it)
+    for (int it = 0; it < calls + ROLES - 1; ++it)
     {
-        const int call = it - 1;
+        const int call = it - ST;
         if (call >= 0 && call < calls)
         {
             const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + lane;
@@ -829,12 +870,13 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
     }
 }
 
-// ---- role 2: anti-alias lattice (audio_driver.c:2581-2590), biquad_2 (:2832), line-out scale
-//      (:2860), f32 audio and int32 codec frames (:2911-2923) ----
-template <int AA, int L>
+// ---- output role: anti-alias lattice (audio_driver.c:2581-2590), biquad_2 (:2832), line-out
+//      scale (:2860), f32 audio and int32 codec frames (:2911-2923) ----
+template <int AA, int L, int DM>
 __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
 {
     BACK_PROLOGUE
+    constexpr int ROLES = back_roles(DM), ST = DM ? 3 : 2;
     float aa[AA > 0 ? AA : 1], bq2[4];
     float ak[AA > 0 ? AA : 1], av[AA + 1], b2[5];
 #pragma unroll
@@ -848,9 +890,9 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
 #pragma unroll
     for (int i = 0; i < 4; ++i) bq2[i] = a.s.bq2[i * C + cl];
     const float lo = P->line_out_scale;
-    for (int it = 0; it < calls + BACK_ROLES - 1; ++it)
+    for (int it = 0; it < calls + ROLES - 1; ++it)
     {
-        const int call = it - 2;
+        const int call = it - ST;
         if (call >= 0)
         {
             const float* mi = lds.mid + (call & 1) * BLK * BACK_CH + lane;
@@ -891,20 +933,161 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
     }
 }
 
-// PRE / AA lattice stages, L interpolation factor, PH polyphase length, W AGC window
-template <int PRE, int AA, int L, int PH, int W>
-__global__ void __launch_bounds__(BACK_ROLES * BACK_CH) rx_back(BackArgs a)
+// ---- demod role: AudioDriver_DemodSAM (audio_driver.c:1990-2166): AM envelope
+//      (:2008-2020) or the SAM PLL (:2021-2147), fade leveler (:1911-1923) ----
+template <int L, int DM>
+__device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
+{
+    BACK_PROLOGUE
+    constexpr int ROLES = back_roles(DM);
+    const bool fade = P->fade_leveler;
+    const float mtauR = P->fade_mtauR, onem_mtauR = P->fade_onem_mtauR;
+    const float mtauI = P->fade_mtauI, onem_mtauI = P->fade_onem_mtauI;
+    const float g1 = P->sam_g1, g2 = P->sam_g2, omega_min = P->sam_omega_min, omega_max = P->sam_omega_max;
+    const bool lsb_sb = P->sam_sideband == UHSDR_SAM_SIDEBAND_LSB;
+    float phs = a.s.sam[0 * C + cl], omega2 = a.s.sam[1 * C + cl], fil_out = a.s.sam[2 * C + cl];
+    float dsI = a.s.sam[3 * C + cl], dsQ = a.s.sam[4 * C + cl];
+    float dc27 = a.s.sam[5 * C + cl], dc_insert = a.s.sam[6 * C + cl];
+    constexpr int NA = DM == DM_SAM_SB ? 24 : 1;         // allpass delay lines (sam_data.a..d)
+    float ap[4][NA];
+    if (DM == DM_SAM_SB)
+    {
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+            for (int j = 0; j < NA; ++j) ap[f][j] = a.s.sam[(7 + f * 24 + j) * C + cl];
+    }
+    // demod_sam_const (audio_driver.c:1931-1953), binary32 as the firmware stores them
+    const float sc0[7] = { -0.328201924180698f, -0.744171491539427f, -0.923022915444215f, -0.978490468768238f,
+                           -0.994128272402075f, -0.998458978159551f, -0.999790306259206f };
+    const float sc1[7] = { -0.0991227952747244f, -0.565619728761389f, -0.857467122550052f, -0.959123933111275f,
+                           -0.988739372718090f, -0.996959189310611f, -0.999282492800792f };
+    const double two_pi = 2.0 * (double)3.14159265358979f;   // 2.0 * PI (CMSIS/Include/arm_math.h:334)
+
+    auto fade_leveler = [&](float audio, float corr) {
+        dc27 = mtauR * dc27 + onem_mtauR * audio;
+        dc_insert = mtauI * dc_insert + onem_mtauI * corr;
+        return audio + dc_insert - dc27;
+    };
+
+    float inext[NDC], qnext[NDC];
+    auto fetch = [&](int call) {
+        const float* si = a.adec + (size_t)cl * a.Nd + call * NDC;
+        const float* sq = a.adec_q + (size_t)cl * a.Nd + call * NDC;
+#pragma unroll
+        for (int m = 0; m < NDC; m += 4)
+        {
+            const float4 v = *(const float4*)(si + m);
+            const float4 w = *(const float4*)(sq + m);
+            inext[m] = v.x; inext[m + 1] = v.y; inext[m + 2] = v.z; inext[m + 3] = v.w;
+            qnext[m] = w.x; qnext[m + 1] = w.y; qnext[m + 2] = w.z; qnext[m + 3] = w.w;
+        }
+    };
+    fetch(0);
+    for (int it = 0; it < calls + ROLES - 1; ++it)
+    {
+        if (it < calls)
+        {
+            float xi[NDC], xq[NDC];
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) { xi[m] = inext[m]; xq[m] = qnext[m]; }
+            if (it + 1 < calls) fetch(it + 1);
+            float* dout = lds.dem + (it & 1) * NDC * BACK_CH + lane;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m)
+            {
+                float audio;
+                if (DM == DM_AM)
+                {
+                    const float in = xi[m] * xi[m] + xq[m] * xq[m];
+                    audio = (in >= 0.0f) ? sqrtf(in) : 0.0f;      // arm_sqrt_f32, arm_math.h:5745-5771
+                    if (fade) audio = fade_leveler(audio, 0.0f);
+                }
+                else
+                {
+                    float Sin, Cos;
+                    ul_sincosf(phs, &Sin, &Cos);                   // glibc-exact (uhsdr_libm.h)
+                    const float ai = Cos * xi[m];
+                    const float bi = Sin * xi[m];
+                    const float aq = Cos * xq[m];
+                    const float bq = Sin * xq[m];
+                    const float corr0 = ai + bq, corr1 = -bi + aq;
+                    if (DM == DM_SAM_SB)
+                    {
+                        // 7-stage allpass pair per path (audio_driver.c:2059-2097)
+                        ap[0][0] = dsI; ap[1][0] = bi; ap[2][0] = dsQ; ap[3][0] = aq;
+                        dsI = ai; dsQ = bq;
+#pragma unroll
+                        for (int j = 0; j < 7; ++j)
+                        {
+                            const int k = 3 * j;
+#pragma unroll
+                            for (int f = 0; f < 4; ++f)
+                            {
+                                const float cc = (f & 1) ? sc1[j] : sc0[j];
+                                ap[f][k + 3] = cc * (ap[f][k] - ap[f][k + 5]) + ap[f][k + 2];
+                            }
+                        }
+                        const float ai_ps = ap[0][21], bi_ps = ap[1][21], bq_ps = ap[2][21], aq_ps = ap[3][21];
+#pragma unroll
+                        for (int j = NA - 1; j > 0; --j)
+#pragma unroll
+                            for (int f = 0; f < 4; ++f) ap[f][j] = ap[f][j - 1];
+                        audio = lsb_sb ? (ai_ps + bi_ps) - (aq_ps - bq_ps) : (ai_ps - bi_ps) + (aq_ps + bq_ps);
+                    }
+                    else
+                    {
+                        audio = corr0;
+                    }
+                    if (fade) audio = fade_leveler(audio, corr0);
+                    // PLL (audio_driver.c:2128-2147)
+                    const float phzerror = ul_atan2f(corr1, corr0);
+                    const float del_out = fil_out;
+                    omega2 = omega2 + g2 * phzerror;
+                    if (omega2 < omega_min) omega2 = omega_min;
+                    else if (omega2 > omega_max) omega2 = omega_max;
+                    fil_out = g1 * phzerror + omega2;
+                    phs = phs + del_out;
+                    while ((double)phs >= two_pi) phs = (float)((double)phs - two_pi);
+                    while ((double)phs < 0.0) phs = (float)((double)phs + two_pi);
+                }
+                dout[m * BACK_CH] = audio;
+            }
+        }
+        __syncthreads();
+    }
+    if (live)
+    {
+        a.s.sam[0 * C + c] = phs; a.s.sam[1 * C + c] = omega2; a.s.sam[2 * C + c] = fil_out;
+        a.s.sam[3 * C + c] = dsI; a.s.sam[4 * C + c] = dsQ;
+        a.s.sam[5 * C + c] = dc27; a.s.sam[6 * C + c] = dc_insert;
+        if (DM == DM_SAM_SB)
+        {
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int j = 0; j < NA; ++j) a.s.sam[(7 + f * 24 + j) * C + c] = ap[f][j];
+        }
+    }
+}
+
+// PRE / AA lattice stages, L interpolation factor, PH polyphase length, W AGC window,
+// DM demodulator (DM_NONE: SSB/CW/DIGI)
+template <int PRE, int AA, int L, int PH, int W, int DM>
+__global__ void __launch_bounds__(4 * BACK_CH) rx_back(BackArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const BackLds lds = back_lds_carve<BLK / L>(smem);
     // readfirstlane makes the role provably wave-uniform (scalar branches)
-    const int role = __builtin_amdgcn_readfirstlane(threadIdx.x / BACK_CH);
-    if (role == 0)
-        rx_back_agc<PRE, L, W>(a, lds);
+    const int role = __builtin_amdgcn_readfirstlane(threadIdx.x / BACK_CH) - (DM ? 1 : 0);
+    if (role < 0)
+        rx_back_demod<L, DM>(a, lds);
+    else if (role == 0)
+        rx_back_agc<PRE, L, W, DM>(a, lds);
     else if (role == 1)
-        rx_back_audio<L, PH>(a, lds);
+        rx_back_audio<L, PH, DM>(a, lds);
     else
-        rx_back_output<AA, L>(a, lds);
+        rx_back_output<AA, L, DM>(a, lds);
 }
 
 // ------------------------------------------------------------------------------------
@@ -914,7 +1097,7 @@ typedef void (*front_fn)(FrontArgs);
 typedef void (*back_fn)(BackArgs);
 
 struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; };
-struct BackVariant { int pre, aa, L, ph, w; back_fn fn; };
+struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; };
 
 // R = FIR outputs per lane: 16 for large batches (more MACs per window load), 8 for small
 // batches (twice the waves in flight)
@@ -925,17 +1108,34 @@ static const FrontVariant kFront[] = {
     { 89, 4, 2, 0, rx_front<89, 4, 2, false, 8>, 8 },
     { 83, 199, 4, 1, rx_front<83, 199, 4, true, 16>, 16 },    // narrow SSB/CW (P4-47)
     { 83, 199, 4, 1, rx_front<83, 199, 4, true, 8>, 8 },
+    { 89, 0, 4, 1, rx_front<89, 0, 4, true, 16>, 16 },        // AM / SAM, 12 ksps (P66-82)
+    { 89, 0, 4, 1, rx_front<89, 0, 4, true, 8>, 8 },
+    { 89, 0, 2, 1, rx_front<89, 0, 2, true, 16>, 16 },        // AM / SAM, 24 ksps (P83-86)
+    { 89, 0, 2, 1, rx_front<89, 0, 2, true, 8>, 8 },
 };
 
+#define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm> }
 static const BackVariant kBack[] = {
-    { 10, 6, 4, 1, 49, rx_back<10, 6, 4, 1, 49> },
-    { 10, 0, 4, 4, 49, rx_back<10, 0, 4, 4, 49> },
-    { 0, 0, 2, 8, 97, rx_back<0, 0, 2, 8, 97> },
-    { 0, 6, 2, 2, 97, rx_back<0, 6, 2, 2, 97> },
-    { 10, 0, 2, 8, 97, rx_back<10, 0, 2, 8, 97> },
-    { 8, 0, 2, 8, 97, rx_back<8, 0, 2, 8, 97> },
-    { 8, 6, 2, 2, 97, rx_back<8, 6, 2, 2, 97> },
+    // SSB / CW / DIGI
+    BACK_V(10, 6, 4, 1, 49, DM_NONE), BACK_V(10, 0, 4, 4, 49, DM_NONE), BACK_V(0, 0, 2, 8, 97, DM_NONE),
+    BACK_V(0, 6, 2, 2, 97, DM_NONE), BACK_V(10, 0, 2, 8, 97, DM_NONE), BACK_V(8, 0, 2, 8, 97, DM_NONE),
+    BACK_V(8, 6, 2, 2, 97, DM_NONE),
+    // AM / SAM paths P66-86
+    BACK_V(10, 0, 4, 4, 49, DM_AM), BACK_V(10, 6, 4, 1, 49, DM_AM), BACK_V(10, 0, 2, 8, 97, DM_AM),
+    BACK_V(8, 0, 2, 8, 97, DM_AM), BACK_V(8, 6, 2, 2, 97, DM_AM),
+    BACK_V(10, 0, 4, 4, 49, DM_SAM), BACK_V(10, 6, 4, 1, 49, DM_SAM), BACK_V(10, 0, 2, 8, 97, DM_SAM),
+    BACK_V(8, 0, 2, 8, 97, DM_SAM), BACK_V(8, 6, 2, 2, 97, DM_SAM),
+    BACK_V(10, 0, 4, 4, 49, DM_SAM_SB), BACK_V(10, 6, 4, 1, 49, DM_SAM_SB), BACK_V(10, 0, 2, 8, 97, DM_SAM_SB),
+    BACK_V(8, 0, 2, 8, 97, DM_SAM_SB), BACK_V(8, 6, 2, 2, 97, DM_SAM_SB),
 };
+#undef BACK_V
+
+static int plan_dm(const uhsdr_rx_plan& p)
+{
+    if (p.dmod_mode == UHSDR_DEMOD_AM) return DM_AM;
+    if (p.dmod_mode == UHSDR_DEMOD_SAM) return p.sam_sideband == UHSDR_SAM_SIDEBAND_BOTH ? DM_SAM : DM_SAM_SB;
+    return DM_NONE;
+}
 
 // frames handled by one front launch: one wave covers a channel's launch block
 static int front_frames(int N, int R) { return N < FRONT_WAVE * R ? N : FRONT_WAVE * R; }
@@ -964,7 +1164,7 @@ static const BackVariant* find_back(const uhsdr_rx_plan& p)
 {
     for (const BackVariant& v : kBack)
         if (v.pre == p.pre_stages && v.aa == p.aa_stages && v.L == p.interp_L && v.ph == p.interp_phase &&
-            v.w == p.agc.attack_buffsize)
+            v.w == p.agc.attack_buffsize && v.dm == plan_dm(p))
             return &v;
     return nullptr;
 }
@@ -983,7 +1183,7 @@ struct uhsdr_rx_s
     int T1, T2;
     hipStream_t stream;
     // front state
-    float *hist1_i, *hist1_q, *hist2_i, *hist2_q, *teta, *osc, *adec;
+    float *hist1_i, *hist1_q, *hist2_i, *hist2_q, *teta, *osc, *adec, *adec_q;
     // back state
     BackState bs;
     void* arena;
@@ -1093,7 +1293,7 @@ static size_t front_lds(const uhsdr_rx_s* h)
 
 static size_t back_lds(const uhsdr_rx_s* h)
 {
-    return sizeof(float) * (size_t)BACK_CH * 2 * (BLK + BLK / h->plan.interp_L);
+    return sizeof(float) * (size_t)BACK_CH * 2 * (BLK + 2 * (BLK / h->plan.interp_L));
 }
 
 extern "C" int uhsdr_rx_plan_supported(const uhsdr_rx_plan* p)
@@ -1152,6 +1352,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const size_t o_pre = take((size_t)10 * C), o_aa = take((size_t)10 * C), o_bq1 = take((size_t)16 * C);
     const size_t o_bq2 = take((size_t)4 * C), o_ip = take((size_t)15 * C), o_ring = take((size_t)(W - 1) * C);
     const size_t o_agc = take((size_t)(6 + AGC_Q) * C), o_agci = take((size_t)3 * C);
+    const bool am = h->bv->dm != DM_NONE;
+    const size_t o_sam = take(am ? (size_t)(7 + 96) * C : 0), o_adq = take(am ? (size_t)C * h->Nd : 0);
     h->arena_bytes = fl * sizeof(float);
     if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess ||
         hipMalloc((void**)&h->adec, sizeof(float) * (size_t)C * h->Nd) != hipSuccess ||
@@ -1168,6 +1370,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->teta = A + o_teta; h->osc = A + o_osc;
     h->bs.pre = A + o_pre; h->bs.aa = A + o_aa; h->bs.bq1 = A + o_bq1; h->bs.bq2 = A + o_bq2;
     h->bs.interp = A + o_ip; h->bs.ring = A + o_ring; h->bs.agc = A + o_agc; h->bs.agci = (int*)(A + o_agci);
+    h->bs.sam = am ? A + o_sam : nullptr;
+    h->adec_q = am ? A + o_adq : nullptr;
     if (hipMemcpy(h->d_plan, &h->plan, sizeof(uhsdr_rx_plan), hipMemcpyHostToDevice) != hipSuccess)
     {
         uhsdr_set_error("plan upload failed");
@@ -1201,6 +1405,7 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
         fa.osc_in = h->osc + 2 * (h->front_launches & 1);     // ping-pong: read one copy, write the other
         fa.osc_out = h->osc + 2 * ((h->front_launches + 1) & 1);
         fa.adec = h->adec + f0 / h->plan.decimation_rate;
+        fa.adec_q = h->adec_q ? h->adec_q + f0 / h->plan.decimation_rate : nullptr;
         fa.C = h->C; fa.N = h->Nf; fa.ld = h->N; fa.ldd = h->Nd;
         fa.lw = h->lw;
         hipLaunchKernelGGL(h->fv->fn, dim3((h->C + cpw - 1) / cpw), dim3(FRONT_WAVE), lds, h->stream, fa);
@@ -1212,13 +1417,14 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
     BackArgs ba;
     ba.plan = h->d_plan;
     ba.adec = h->adec;
+    ba.adec_q = h->adec_q;
     ba.audio = audio;
     ba.dst = (int2*)dst;
     ba.s = h->bs;
     ba.C = h->C; ba.N = h->N; ba.Nd = h->Nd;
     ba.ring_phase = (int)(h->calls_done % AGC_Q);
     time_mark(h, 1, 0);
-    hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_ROLES * BACK_CH), back_lds(h), h->stream, ba);
+    hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH), back_lds(h), h->stream, ba);
     HIPCHK(hipGetLastError());
     time_mark(h, 1, 1);
     if (h->timing) h->nev++;

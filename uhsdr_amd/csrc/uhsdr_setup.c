@@ -76,6 +76,11 @@ void uhsdr_rx_config_default(uhsdr_rx_config* c)
     c->agc_tau_decay[4] = 50;
     c->agc_tau_decay[5] = 1;
     c->agc_tau_hang_decay = 500;
+    c->sam_sideband = UHSDR_SAM_SIDEBAND_BOTH;   /* ui_configuration.c:214-219 */
+    c->sam_pll_fmax = 2500;
+    c->sam_zeta = 65;
+    c->sam_omega_n = 250;
+    c->fade_leveler = 1;
 }
 
 /* AudioFilter_GetFilterModeFromDemodMode, audio_filter.c:929-955 */
@@ -321,8 +326,9 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
     copy_bits(p->hilbert_q, f->fir_q, f->fir_taps);
     if (is_am)
     {
-        p->dec_taps = f->fir_taps;           /* AM/SAM reuse the I table as decimator */
+        p->dec_taps = f->fir_taps;           /* AM/SAM: the path's I / Q tables as decimators */
         copy_bits(p->dec, f->fir_i, f->fir_taps);
+        copy_bits(p->dec_q, f->fir_q, f->fir_taps);
     }
     else if (f->dec_taps)
     {
@@ -365,6 +371,27 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
     p->line_out_scale = LINE_OUT_SCALING_FACTOR;
 
     setup_agc(&p->agc, cfg, (float)p->decimated_freq, is_am);
+
+    /* AudioDriver_SetSamPllParameters, audio_driver.c:709-745 (PI = 3.14159265358979f) */
+    p->sam_sideband = cfg->sam_sideband;
+    p->fade_leveler = cfg->fade_leveler != 0;
+    {
+        const float decimSampleRate = p->decimated_freq;
+        const float pll_fmax = cfg->sam_pll_fmax;
+        const float omegaN = cfg->sam_omega_n;
+        const float zeta = (float)cfg->sam_zeta / 100.0;
+        p->sam_omega_min = -(2.0 * CMSIS_PI * pll_fmax / decimSampleRate);
+        p->sam_omega_max = (2.0 * CMSIS_PI * pll_fmax / decimSampleRate);
+        p->sam_g1 = (1.0 - expf(-2.0 * omegaN * zeta / decimSampleRate));
+        p->sam_g2 = (-p->sam_g1 + 2.0 * (1 - expf(-omegaN * zeta / decimSampleRate)
+                     * cosf(omegaN / decimSampleRate * sqrtf(1.0 - zeta * zeta))));
+        const float tauR = 0.02;
+        const float tauI = 1.4;
+        p->fade_mtauR = (expf(-1 / (decimSampleRate * tauR)));
+        p->fade_onem_mtauR = (1.0 - p->fade_mtauR);
+        p->fade_mtauI = (expf(-1 / (decimSampleRate * tauI)));
+        p->fade_onem_mtauI = (1.0 - p->fade_mtauI);
+    }
     return UHSDR_OK;
 }
 
@@ -372,9 +399,9 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
    whether a kernel variant exists for the plan's filter-path family. */
 int uhsdr_rx_mode_supported(const uhsdr_rx_plan* p)
 {
-    /* device chain: SSB / CW / DIGI demodulation (I +- Q) */
+    /* device chain: SSB / CW / DIGI (I +- Q), AM, SAM; FM not yet */
     if (!p) return 0;
-    return !(p->dmod_mode == UHSDR_DEMOD_AM || p->dmod_mode == UHSDR_DEMOD_SAM || p->dmod_mode == UHSDR_DEMOD_FM);
+    return p->dmod_mode != UHSDR_DEMOD_FM;
 }
 
 const char* uhsdr_version(void) { return "uhsdr_amd 0.1 (gfx950)"; }

@@ -86,6 +86,44 @@ def ssb_iq(channels, start: int, nframes: int, kind: str = "ssb2tone",
     return out
 
 
+def _noise(channels, start, nframes, noise_sigma):
+    ch = channels.astype(np.uint64)[:, None]
+    idx = np.arange(start, start + nframes, dtype=np.uint64)[None, :]
+    key = ((np.uint64(SEED_BASE) + ch) << np.uint64(40)) ^ (idx << np.uint64(1))
+    u1 = _uniform(key)
+    u2 = _uniform(key ^ np.uint64(1))
+    r = np.sqrt(-2.0 * np.log(u1)) * noise_sigma
+    return r * np.cos(2.0 * np.pi * u2), r * np.sin(2.0 * np.pi * u2)
+
+
+def _frames(i_sig, q_sig):
+    out = np.empty(i_sig.shape + (2,), dtype=np.int32)
+    out[..., 0] = np.clip(np.rint(i_sig), -32768, 32767).astype(np.int32) << 16
+    out[..., 1] = np.clip(np.rint(q_sig), -32768, 32767).astype(np.int32) << 16
+    return out
+
+
+def am_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier: float = 12000.0,
+          depth: float = 0.5, tone: float = 1000.0, amplitude: float = 2000.0, offset_hz: float = 200.0):
+    """C3: AM, carrier at `carrier` + U(-offset_hz, offset_hz) Hz per channel,
+    `depth` modulation with a `tone` Hz audio tone, peak carrier `amplitude` LSB16, plus noise.
+    The SAM PLL has to acquire and track each channel's carrier offset."""
+    channels = np.asarray(channels, dtype=np.int64)
+    ch = channels.astype(np.uint64)
+    base = (np.uint64(SEED_BASE) + ch) << np.uint64(20)
+    off = offset_hz * (2.0 * _uniform(base + np.uint64(7)) - 1.0)
+    ph_c = 2.0 * np.pi * _uniform(base + np.uint64(8))
+    ph_m = 2.0 * np.pi * _uniform(base + np.uint64(9))
+    n = np.arange(start, start + nframes, dtype=np.float64)[None, :]
+    env = amplitude * (1.0 + depth * np.cos(2.0 * np.pi * tone / FS * n + ph_m[:, None]))
+    ph = 2.0 * np.pi * (carrier + off[:, None]) / FS * n + ph_c[:, None]
+    i_sig, q_sig = env * np.cos(ph), env * np.sin(ph)
+    if noise_sigma > 0:
+        ni, nq = _noise(channels, start, nframes, noise_sigma)
+        i_sig, q_sig = i_sig + ni, q_sig + nq
+    return _frames(i_sig, q_sig)
+
+
 def ssb_iq_torch(c0: int, nch: int, start: int, nframes: int, device, noise_sigma: float = 30.0):
     """Same signal model as ``ssb_iq`` (kind "ssb2tone"), generated on the GPU for large
     benchmark batches: channels c0 .. c0+nch-1.  Tone parameters and noise come from the

@@ -106,7 +106,9 @@ typedef struct uhsdr_rx_config
     int32_t sam_zeta;             /* ads.zeta_int, zeta x 100 (65) */
     int32_t sam_omega_n;          /* ads.omegaN_int (250) */
     int32_t fade_leveler;         /* ads.fade_leveler (1) */
-    int32_t reserved[11];
+    int32_t fm_sql_threshold;     /* ts.fm_sql_threshold (FM_SQUELCH_DEFAULT 12, audio_driver.h:449) */
+    int32_t fm_deviation_5k;      /* FLAGS2_FM_MODE_DEVIATION_5KHZ (RadioManagement_FmDevIs5khz) */
+    int32_t reserved[9];
 } uhsdr_rx_config;
 
 /* AudioAgc_SetupAgcWdsp() results (audio_agc.c:126-339) */
@@ -167,6 +169,12 @@ typedef struct uhsdr_rx_plan
     /* AudioDriver_SetSamPllParameters, audio_driver.c:709-745 */
     float   sam_omega_min, sam_omega_max, sam_g1, sam_g2;
     float   fade_mtauR, fade_onem_mtauR, fade_mtauI, fade_onem_mtauI;
+    /* FM (AudioDriver_DemodFM, audio_driver.c:1544-1737) */
+    float   fm_scale;             /* FM_RX_SCALING_2K5 10000 or _5K 5000 (audio_driver.c:1494-1495) */
+    int32_t fm_sql_threshold;
+    int32_t sq_stages;            /* IIR_Squelch_HPF = IIR_15k_hpf (audio_driver.c:481-484) */
+    float   sq_k[UHSDR_MAX_LATTICE];
+    float   sq_v[UHSDR_MAX_LATTICE + 1];
     int32_t reserved[64];
 } uhsdr_rx_plan;
 

@@ -21,3 +21,4 @@ const arm_fir_interpolate_instance_f32* oracle_ref_interpolate(void) { return &I
 
 /* layout fingerprint of TransceiverState as audio_driver.c sees it */
 unsigned long oracle_driver_layout(void) { return (unsigned long)sizeof(TransceiverState) * 100000ul + (unsigned long)((char*)&ts.dsp.active - (char*)&ts); }
+const arm_iir_lattice_instance_f32* oracle_ref_squelch(void) { return &IIR_Squelch_HPF; }

@@ -41,6 +41,7 @@ const arm_biquad_casd_df1_inst_f32* oracle_ref_biquad2(void);
 const arm_iir_lattice_instance_f32* oracle_ref_prefilter(void);
 const arm_iir_lattice_instance_f32* oracle_ref_antialias(void);
 const arm_fir_interpolate_instance_f32* oracle_ref_interpolate(void);
+const arm_iir_lattice_instance_f32* oracle_ref_squelch(void);
 void oracle_ref_agc_dump(void);
 unsigned long oracle_harness_layout(void);
 unsigned long oracle_driver_layout(void);
@@ -123,7 +124,10 @@ static void dump_setup(void)
     print_fvec("pre_k", pre->pkCoeffs, pre->numStages, 0);
     print_fvec("pre_v", pre->pvCoeffs, pre->numStages ? pre->numStages + 1 : 0, 0);
     print_fvec("aa_k", aa->pkCoeffs, aa->numStages, 0);
-    print_fvec("aa_v", aa->pvCoeffs, aa->numStages ? aa->numStages + 1 : 0, 1);
+    print_fvec("aa_v", aa->pvCoeffs, aa->numStages ? aa->numStages + 1 : 0, 0);
+    const arm_iir_lattice_instance_f32* sq = oracle_ref_squelch();   /* FM squelch HPF, audio_driver.c:481-484 */
+    print_fvec("squelch_k", sq->pkCoeffs, sq->numStages, 0);
+    print_fvec("squelch_v", sq->pvCoeffs, sq->numStages + 1, 1);
     printf("}\n");
 }
 

@@ -27,6 +27,7 @@ void uo_rx_state_init(const uhsdr_rx_plan* p, uo_rx_state* s)
     s->osc_vq = 1.0f;
     s->out_index = p->agc.out_index0;
     s->in_index = p->agc.in_index0;
+    s->fm_squelched = 1;       /* AudioDriver_FM_Rx_Init: "we start squelched" (audio_driver.c:475) */
 }
 
 /* ---- CMSIS-DSP f32 kernels, restated (generic code paths; the CM7 unrolled versions
@@ -358,6 +359,61 @@ static void demod_sam(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, c
     }
 }
 
+/* AudioDriver_DemodFM, audio_driver.c:1544-1737 (subaudible tone detection off); returns
+   signal_active = !squelched after this call's squelch update */
+static int demod_fm(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, const float* qb, float* a0, int n)
+{
+    float sq[BLK];
+    if (p->freq_shift_hz == 0) return !s->fm_squelched;      /* bails out without translation (:1548) */
+    for (int i = 0; i < n; i++)
+    {
+        const float y = (s->fm_i_prev * qb[i]) - (ib[i] * s->fm_q_prev);
+        const float x = (s->fm_i_prev * ib[i]) + (qb[i] * s->fm_q_prev);
+        const float angle = atan2f(y, x);
+        sq[i] = angle;
+        const float a = s->fm_lpf_prev + (0.05 * (angle - s->fm_lpf_prev));     /* FM_RX_LPF_ALPHA */
+        s->fm_lpf_prev = a;
+        if (!s->fm_squelched || !p->fm_sql_threshold)
+        {
+            const float b = 0.96 * (s->fm_hpf_prev_b + a - s->fm_hpf_prev_a);  /* FM_RX_HPF_ALPHA */
+            s->fm_hpf_prev_a = a;
+            s->fm_hpf_prev_b = b;
+            a0[i] = b;
+        }
+        else
+        {
+            a0[i] = 0;
+        }
+        s->fm_q_prev = qb[i];
+        s->fm_i_prev = ib[i];
+    }
+    iir_lattice(p->sq_k, p->sq_v, p->sq_stages, s->fm_sq, sq, sq, n);
+    s->fm_sql_avg = ((1 - 0.005) * s->fm_sql_avg) + (0.005 * sqrtf(fabsf(sq[0])));   /* FM_RX_SQL_SMOOTHING */
+    s->fm_count = (s->fm_count + 1) % 200;                                            /* FM_SQUELCH_PROC_DECIMATION */
+    if (s->fm_count == 0)
+    {
+        if (s->fm_sql_avg > 0.175) s->fm_sql_avg = 0.175;
+        float scaled_sql_avg = s->fm_sql_avg * 172;
+        if (scaled_sql_avg > 24) scaled_sql_avg = 24;
+        scaled_sql_avg = 22 - scaled_sql_avg;
+        const int thr = p->fm_sql_threshold;
+        if (thr == 0) s->fm_squelched = 0;
+        else if (s->fm_squelched)
+        {
+            if (scaled_sql_avg >= (float)(thr + 3)) s->fm_squelched = 0;           /* FM_SQUELCH_HYSTERESIS */
+        }
+        else if (thr > 3)
+        {
+            if (scaled_sql_avg < (float)(thr - 3)) s->fm_squelched = 1;
+        }
+        else if (scaled_sql_avg < (float)thr)
+        {
+            s->fm_squelched = 1;
+        }
+    }
+    return !s->fm_squelched;
+}
+
 /* float -> int32 as x86 cvttss2si does it (out of range / NaN -> INT32_MIN), then the
    firmware's << AUDIO_BIT_SHIFT (audio_driver.c:2911-2923) in two's complement. */
 static int32_t to_dma(float f)
@@ -460,6 +516,22 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
     {
         fir(p->hilbert_i, p->hilbert_taps, s->hil_i, ib, ib, niq);
         fir(p->hilbert_q, p->hilbert_taps, s->hil_q, qb, qb, niq);
+    }
+    if (p->dmod_mode == UHSDR_DEMOD_FM)
+    {
+        /* FM: no decimation / post-processing; audio = demod x FM_RX_SCALING (audio_driver.c:2818-2828),
+           the AGC run there only rewrites a_buffer[0], which the output stage overwrites */
+        const int active = demod_fm(p, s, ib, qb, a0, n);
+        for (int i = 0; i < n; i++) a1[i] = a0[i] * p->fm_scale;
+        biquad_df1(p->biquad2, 1, s->bq2, a1, n);      /* audio_driver.c:2832 */
+        for (int i = 0; i < n; i++)
+        {
+            const float v = active ? a1[i] * p->line_out_scale : 0.0f;    /* mute when squelched, :2843-2850 */
+            out_a1[i] = v;
+            const int32_t d = active ? to_dma(v) : 0;
+            if (dst) { dst[2 * i] = d; dst[2 * i + 1] = d; }
+        }
+        return;
     }
     if (am)
         demod_sam(p, s, ib, qb, a0, niq);

@@ -46,6 +46,10 @@ typedef struct uo_rx_state
     float sam_phs, sam_omega2, sam_fil_out, sam_dsI, sam_dsQ;
     float sam_a[24], sam_b[24], sam_c[24], sam_d[24];
     float fade_dc27, fade_dc_insert;
+    /* fm_data (audio_driver.c:1515-1531), ads.fm_conf squelch (:470-486), IIR_Squelch_HPF state */
+    float fm_i_prev, fm_q_prev, fm_lpf_prev, fm_hpf_prev_a, fm_hpf_prev_b, fm_sql_avg;
+    float fm_sq[UHSDR_MAX_LATTICE + 1];
+    int32_t fm_squelched, fm_count;
 } uo_rx_state;
 
 size_t uo_rx_state_size(void);

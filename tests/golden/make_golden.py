@@ -72,6 +72,12 @@ CONFIGS = {
     "p70_sam_agcoff": ({"mode": 4, "path": 70, "agc_mode": 5}, {"am": True}),
     "p70_sam_usb": ({"mode": 4, "path": 70, "sam_sb": 2}, {"am": True}),
     "p70_sam_lsb": ({"mode": 4, "path": 70, "sam_sb": 1}, {"am": True}),
+    # FM (C4): 1 kHz tone at 2.5 kHz deviation; 8192 frames = 256 calls, so the squelch
+    # (evaluated every 200 calls, audio_driver.c:1605) decides once inside the fixture
+    "p1_fm": ({"mode": 5, "path": 1}, {"fm": True, "frames": 8192}),
+    "p1_fm_sql0": ({"mode": 5, "path": 1, "sql": 0}, {"fm": True, "frames": 8192}),
+    "p2_fm5k": ({"mode": 5, "path": 2, "sql": 2, "fm5k": 1}, {"fm": True, "frames": 8192, "deviation": 5000.0}),
+    "p3_fm_noise": ({"mode": 5, "path": 3, "sql": 18}, {"fm": True, "frames": 8192, "amplitude": 40.0}),
 }
 
 
@@ -97,12 +103,15 @@ def make(name: str):
     args, sig = CONFIGS[name]
     sig = dict(sig)
     center = sig.pop("center", None)
-    if sig.pop("am", False):
+    nframes = sig.pop("frames", NFRAMES)
+    if sig.pop("fm", False):
+        iq = synth.fm_iq(np.arange(NCH), 0, nframes, **sig)
+    elif sig.pop("am", False):
         iq = synth.am_iq(np.arange(NCH), 0, NFRAMES)
     else:
         iq = synth.ssb_iq(np.arange(NCH), 0, NFRAMES, carrier=center if center is not None else 12000.0, **sig)
-    a1 = np.empty((NCH, NFRAMES), np.float32)
-    dst = np.empty((NCH, NFRAMES, 2), np.int32)
+    a1 = np.empty((NCH, iq.shape[1]), np.float32)
+    dst = np.empty((NCH, iq.shape[1], 2), np.int32)
     for c in range(NCH):
         a1[c], dst[c] = run_ref(args, iq[c])
     np.savez_compressed(os.path.join(HERE, f"rx_{name}.npz"), iq=iq, a1=a1, dst=dst,

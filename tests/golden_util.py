@@ -12,6 +12,10 @@ def golden_files():
     return sorted(glob.glob(os.path.join(GOLDEN, "rx_*.npz")))
 
 
+def golden_file(name):
+    return os.path.join(GOLDEN, f"rx_{name}.npz")
+
+
 def load(path):
     d = np.load(path)
     return {

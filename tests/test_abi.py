@@ -49,8 +49,11 @@ def test_create_rejects_bad_lengths_without_touching_the_device():
 
 def test_unsupported_modes_are_reported():
     lib = U.load()
-    plan = U.build_plan(U.default_config(dmod_mode=U.DEMOD_FM, filter_path=1))
+    # FM without the I/Q translation: the reference demodulator bails out (audio_driver.c:1548)
+    plan = U.build_plan(U.default_config(dmod_mode=U.DEMOD_FM, filter_path=1, iq_freq_mode=0))
     assert lib.uhsdr_rx_plan_supported(C.byref(plan)) == 0
+    plan = U.build_plan(U.default_config(dmod_mode=U.DEMOD_FM, filter_path=1))
+    assert lib.uhsdr_rx_plan_supported(C.byref(plan)) == 1
     plan = U.build_plan(U.default_config())
     assert lib.uhsdr_rx_plan_supported(C.byref(plan)) == 1
 

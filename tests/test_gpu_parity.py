@@ -13,7 +13,7 @@ import pytest
 
 import oracle
 import uhsdr_amd as U
-from golden_util import assert_bitexact, golden_files, load
+from golden_util import assert_bitexact, golden_file, golden_files, load
 from uhsdr_amd import synth
 
 pytestmark = pytest.mark.gpu
@@ -49,7 +49,7 @@ def test_device_matches_reference_firmware(cuda, path):
 
 @pytest.mark.parametrize("frames", [32, 64, 128, 1024, 2048])
 def test_device_call_granularity(cuda, frames):
-    g = load(golden_files()[0])
+    g = load(golden_file("p48_usb"))
     cfg = U.config_from_ref_args(g["args"])
     a1, _ = run_device(cfg, g["iq"], frames, want_dst=False)
     assert_bitexact(a1, g["a1"], f"frames={frames}")
@@ -101,7 +101,7 @@ def test_device_north_star_batch_sampled_channels(cuda, path):
 
 def test_device_reset_restarts_stream(cuda):
     import torch
-    g = load(golden_files()[0])
+    g = load(golden_file("p48_usb"))
     cfg = U.config_from_ref_args(g["args"])
     chain = U.RxChain(cfg, channels=4, frames=256)
     audio = torch.empty((4, 256), dtype=torch.float32, device="cuda")
@@ -115,7 +115,7 @@ def test_device_reset_restarts_stream(cuda):
 
 
 def test_device_host_entry_point(cuda):
-    g = load(golden_files()[0])
+    g = load(golden_file("p48_usb"))
     chain = U.RxChain(U.config_from_ref_args(g["args"]), channels=4, frames=2048)
     a1, dst = chain.process_host(g["iq"])
     assert_bitexact(a1, g["a1"], "process_host")
@@ -127,7 +127,7 @@ def test_plain_c_host_matches_reference_firmware(cuda, tmp_path):
     reference firmware's fixture."""
     import os
     import subprocess
-    g = load(golden_files()[0])
+    g = load(golden_file("p48_usb"))
     C, n, _ = g["iq"].shape
     src, out = tmp_path / "iq.bin", tmp_path / "audio.bin"
     np.ascontiguousarray(g["iq"], dtype=np.int32).tofile(src)
@@ -169,3 +169,14 @@ def test_device_c3_sam_batch_sampled_channels(cuda):
     chain.close()
     ref, _ = oracle.OracleRx(U.build_plan(cfg), len(pick)).process(synth.am_iq(pick, 0, n))
     assert_bitexact(got, ref, "C3 sampled")
+
+
+@pytest.mark.parametrize("path,sql,channels", [(1, 12, 200), (1, 0, 77), (3, 2, 65)])
+def test_device_fm_matches_oracle(cuda, path, sql, channels):
+    """FM-RX (C4 row a10): 8192 frames so the squelch decides inside the run."""
+    cfg = U.default_config(filter_path=path, dmod_mode=U.DEMOD_FM, fm_sql_threshold=sql)
+    iq = synth.fm_iq(np.arange(channels), 0, 8192)
+    a1, dst = run_device(cfg, iq, 512)
+    ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), channels).process(iq, threads=8)
+    assert_bitexact(a1, ref_a1, f"FM P{path} sql={sql} C={channels}")
+    np.testing.assert_array_equal(dst, ref_dst)

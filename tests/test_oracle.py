@@ -8,7 +8,7 @@ import pytest
 
 import oracle
 import uhsdr_amd as U
-from golden_util import assert_bitexact, golden_files, load
+from golden_util import assert_bitexact, golden_file, golden_files, load
 
 
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("rx_")[-1][:-4])
@@ -25,7 +25,7 @@ def test_oracle_matches_reference(path):
 def test_oracle_call_granularity(chunk):
     """Splitting the stream into calls of any multiple of 32 frames gives the same samples
     (state is carried exactly as across ISR invocations)."""
-    g = load(golden_files()[0])
+    g = load(golden_file("p48_usb"))
     plan = U.build_plan(U.config_from_ref_args(g["args"]))
     o = oracle.OracleRx(plan, g["iq"].shape[0])
     outs = []
@@ -36,7 +36,7 @@ def test_oracle_call_granularity(chunk):
 
 
 def test_oracle_threads_equal_single():
-    g = load(golden_files()[0])
+    g = load(golden_file("p48_usb"))
     plan = U.build_plan(U.config_from_ref_args(g["args"]))
     a = oracle.OracleRx(plan, 4).process(g["iq"], threads=1)[0]
     b = oracle.OracleRx(plan, 4).process(g["iq"], threads=4)[0]

@@ -32,6 +32,9 @@ def test_plan_matches_reference_setup(path):
                 p.fade_mtauI, p.fade_onem_mtauI]
         np.testing.assert_array_equal(np.array(mine, dtype=np.float32).view(np.uint32),
                                       np.array(s["sam"], dtype=np.uint32), err_msg="sam pll / fade")
+    if "squelch_k" in s:
+        np.testing.assert_array_equal(fbits(p.sq_k, p.sq_stages), np.array(s["squelch_k"], dtype=np.uint32))
+        np.testing.assert_array_equal(fbits(p.sq_v, p.sq_stages + 1), np.array(s["squelch_v"], dtype=np.uint32))
     assert p.pre_stages == s["pre_stages"] and p.aa_stages == s["aa_stages"]
     assert p.interp_L == s["interp_L"] and p.interp_phase == s["interp_phase"]
     for field, key, n in [("biquad1", "biquad1", 20), ("biquad2", "biquad2", 5),

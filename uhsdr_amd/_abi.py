@@ -38,7 +38,8 @@ class RxConfig(C.Structure):
         ("agc_thresh", C.c_int32), ("agc_hang_enable", C.c_int32), ("agc_hang_time", C.c_int32),
         ("agc_hang_thresh", C.c_int32), ("agc_tau_decay", C.c_int32 * 6), ("agc_tau_hang_decay", C.c_int32),
         ("sam_sideband", C.c_int32), ("sam_pll_fmax", C.c_int32), ("sam_zeta", C.c_int32), ("sam_omega_n", C.c_int32),
-        ("fade_leveler", C.c_int32), ("reserved", C.c_int32 * 11),
+        ("fade_leveler", C.c_int32), ("fm_sql_threshold", C.c_int32), ("fm_deviation_5k", C.c_int32),
+        ("reserved", C.c_int32 * 9),
     ]
 
 
@@ -72,7 +73,9 @@ class RxPlan(C.Structure):
         ("dec_q", C.c_float * MAX_DEC_TAPS), ("sam_sideband", C.c_int32), ("fade_leveler", C.c_int32),
         ("sam_omega_min", C.c_float), ("sam_omega_max", C.c_float), ("sam_g1", C.c_float), ("sam_g2", C.c_float),
         ("fade_mtauR", C.c_float), ("fade_onem_mtauR", C.c_float), ("fade_mtauI", C.c_float),
-        ("fade_onem_mtauI", C.c_float), ("reserved", C.c_int32 * 64),
+        ("fade_onem_mtauI", C.c_float),
+        ("fm_scale", C.c_float), ("fm_sql_threshold", C.c_int32), ("sq_stages", C.c_int32),
+        ("sq_k", C.c_float * MAX_LATTICE), ("sq_v", C.c_float * (MAX_LATTICE + 1)), ("reserved", C.c_int32 * 64),
     ]
 
 
@@ -157,7 +160,7 @@ REF_ARG_MAP = {
     "notch": "notch_frequency", "peak": "peak_frequency", "bass": "bass_gain", "treble": "treble_gain",
     "agc_mode": "agc_mode", "agc_thresh": "agc_thresh", "agc_slope": "agc_slope", "agc_hang": "agc_hang_enable",
     "sam_sb": "sam_sideband", "pll_fmax": "sam_pll_fmax", "zeta": "sam_zeta", "omegan": "sam_omega_n",
-    "fade": "fade_leveler",
+    "fade": "fade_leveler", "sql": "fm_sql_threshold", "fm5k": "fm_deviation_5k",
 }
 
 

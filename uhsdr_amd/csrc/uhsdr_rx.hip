@@ -418,14 +418,15 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
     if constexpr (T2 == 0)
     {
         // AM / SAM: decimate I and Q with the path's own tables (DECIMATE_RX_I / _Q,
-        // audio_filter.c:1167-1176, audio_driver.c:2742-2746); no Hilbert (:2748); the
-        // demodulator in rx_back takes both
+        // audio_filter.c:1167-1176, audio_driver.c:2742-2746), no Hilbert (:2748);
+        // FM: the Hilbert / low-pass pair at 48 ksps (:2748-2753), no decimation.
+        // The demodulator in rx_back / rx_fm takes both I and Q.
         float dq[RD];
         front_fill<T1>(W, a.hist1_i, c, act, live, b, nb, hA, xi, R);
-        fir_block<T1, RD, M>(W + b * R, as_taps(P->dec), o);
+        fir_block<T1, RD, M>(W + b * R, as_taps(DECIM_FIRST ? P->dec : P->hilbert_i), o);
         wave_sync();
         front_fill<T1>(W, a.hist1_q, c, act, live, b, nb, hB, xq, R);
-        fir_block<T1, RD, M>(W + b * R, as_taps(P->dec_q), dq);
+        fir_block<T1, RD, M>(W + b * R, as_taps(DECIM_FIRST ? P->dec_q : P->hilbert_q), dq);
         if (live)
         {
             float* dst = a.adec_q + (size_t)c * a.ldd + b * RD;
@@ -583,8 +584,9 @@ __device__ __forceinline__ int to_dma(float f)
 #define BACK_CH 64
 
 // demodulator kinds of rx_back (DM): the SSB/CW/DIGI sum I +- Q happens in rx_front
-enum { DM_NONE = 0, DM_AM = 1, DM_SAM = 2, DM_SAM_SB = 3 /* SAM with the allpass sideband selector */ };
-__host__ __device__ constexpr int back_roles(int dm) { return dm ? 4 : 3; }
+enum { DM_NONE = 0, DM_AM = 1, DM_SAM = 2, DM_SAM_SB = 3 /* SAM with the allpass sideband selector */,
+       DM_FM = 4 /* separate kernel, rx_fm */ };
+__host__ __device__ constexpr int back_roles(int dm) { return dm == DM_FM ? 2 : dm ? 4 : 3; }
 
 // The back end of one channel group runs as a pipeline over 32-frame calls, one wave per
 // stage (lane == channel); stage s works on call it - s in iteration it and hands its results
@@ -1090,6 +1092,181 @@ __global__ void __launch_bounds__(4 * BACK_CH) rx_back(BackArgs a)
         rx_back_output<AA, L, DM>(a, lds);
 }
 
+
+// ------------------------------------------------------------------------------------
+// rx_fm: FM receive after the Hilbert pair (AudioDriver_DemodFM, audio_driver.c:1544-1737,
+// and the FM branch of AudioDriver_RxProcessor, :2818-2850).  Two waves over 64 channels:
+//   wave 0  discriminator atan2f -> de-emphasis LPF -> HPF (or 0 when squelched) per sample;
+//           squelch noise lattice (IIR_15k_hpf) over the call, averaged energy of its first
+//           output, squelch decision every FM_SQUELCH_PROC_DECIMATION = 200 calls
+//   wave 1  x FM_RX_SCALING, biquad_2 (:2832), mute when squelched / line-out x10 (:2843-2860),
+//           f32 audio and int32 codec frames
+// The AGC the reference runs on a_buffer[0] in FM (:2827) is not run: the output stage
+// overwrites that buffer with the line-out copy (:2868), so it never reaches the audio.
+// Subaudible tone detection (:1665-1734) is off (ui_configuration.c default); a plan with it
+// on is not offered to this kernel.  FM state: [field][C] in BackState.sam:
+//   0 i_prev 1 q_prev 2 lpf_prev 3 hpf_prev_a 4 hpf_prev_b 5 sql_avg 6 open (!squelched) 7.. lattice
+template <int SQ>
+__global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    const int lane = threadIdx.x & (BACK_CH - 1);
+    const int role = __builtin_amdgcn_readfirstlane(threadIdx.x / BACK_CH);
+    const int c = blockIdx.x * BACK_CH + lane;
+    const bool live = c < a.C;
+    const int cl = live ? c : a.C - 1;
+    const int C = a.C;
+    const int calls = a.N / BLK;
+    float* dem = smem;                                   // [2][BLK][64] demodulated audio
+    float* act = smem + 2 * BLK * BACK_CH;               // [2][64] signal_active of the call
+    float* S = a.s.sam;
+    if (role == 0)
+    {
+        float sk[SQ], sv[SQ + 1], g[SQ];
+#pragma unroll
+        for (int i = 0; i < SQ; ++i) sk[i] = P->sq_k[i];
+#pragma unroll
+        for (int i = 0; i <= SQ; ++i) sv[i] = P->sq_v[i];
+#pragma unroll
+        for (int i = 0; i < SQ; ++i) g[i] = S[(7 + i) * C + cl];
+        float i_prev = S[0 * C + cl], q_prev = S[1 * C + cl], lpf_prev = S[2 * C + cl];
+        float hpf_a = S[3 * C + cl], hpf_b = S[4 * C + cl], sql_avg = S[5 * C + cl];
+        bool squelched = S[6 * C + cl] == 0.0f;          // field 6 = "open": zeroed state starts squelched (:475)
+        const int thr = P->fm_sql_threshold;
+        const bool translate = P->freq_shift_hz != 0;   // no translation: the demod bails out (:1548)
+        float inext[BLK], qnext[BLK];
+        auto fetch = [&](int call) {
+            const float* si = a.adec + (size_t)cl * a.Nd + call * BLK;
+            const float* sq = a.adec_q + (size_t)cl * a.Nd + call * BLK;
+#pragma unroll
+            for (int m = 0; m < BLK; m += 4)
+            {
+                const float4 v = *(const float4*)(si + m);
+                const float4 w = *(const float4*)(sq + m);
+                inext[m] = v.x; inext[m + 1] = v.y; inext[m + 2] = v.z; inext[m + 3] = v.w;
+                qnext[m] = w.x; qnext[m + 1] = w.y; qnext[m + 2] = w.z; qnext[m + 3] = w.w;
+            }
+        };
+        fetch(0);
+        for (int it = 0; it <= calls; ++it)
+        {
+            if (it < calls)
+            {
+                float xi[BLK], xq[BLK];
+#pragma unroll
+                for (int m = 0; m < BLK; ++m) { xi[m] = inext[m]; xq[m] = qnext[m]; }
+                if (it + 1 < calls) fetch(it + 1);
+                float* out = dem + (it & 1) * BLK * BACK_CH + lane;
+                if (translate)
+                {
+                    const bool pass = !squelched || !thr;
+                    float sq0 = 0.0f;
+#pragma unroll 4
+                    for (int m = 0; m < BLK; ++m)
+                    {
+                        const float y = (i_prev * xq[m]) - (xi[m] * q_prev);
+                        const float x = (i_prev * xi[m]) + (xq[m] * q_prev);
+                        const float angle = ul_atan2f(y, x);
+                        const float aa = (float)((double)lpf_prev + (0.05 * (double)(angle - lpf_prev)));
+                        lpf_prev = aa;
+                        float o = 0.0f;
+                        if (pass)
+                        {
+                            const float bb = (float)(0.96 * (double)(hpf_b + aa - hpf_a));
+                            hpf_a = aa;
+                            hpf_b = bb;
+                            o = bb;
+                        }
+                        out[m * BACK_CH] = o;
+                        q_prev = xq[m];
+                        i_prev = xi[m];
+                        const float sqo = lattice_step<SQ>(angle, g, sk, sv);   // squelch HPF (:1594)
+                        if (m == 0) sq0 = sqo;
+                    }
+                    sql_avg = (float)(((1 - 0.005) * (double)sql_avg) + (0.005 * (double)sqrtf(fabsf(sq0))));
+                    if ((a.ring_phase + it + 1) % 200 == 0)     // fm_data.count (:1604-1605)
+                    {
+                        if ((double)sql_avg > 0.175) sql_avg = 0.175f;
+                        float scaled = sql_avg * 172;
+                        if (scaled > 24) scaled = 24;
+                        scaled = 22 - scaled;
+                        if (thr == 0) squelched = false;
+                        else if (squelched) { if (scaled >= (float)(thr + 3)) squelched = false; }
+                        else if (thr > 3) { if (scaled < (float)(thr - 3)) squelched = true; }
+                        else if (scaled < (float)thr) squelched = true;
+                    }
+                }
+                else
+                {
+                    // a_buffer[0] keeps its previous contents in the reference; not offered
+#pragma unroll
+                    for (int m = 0; m < BLK; ++m) out[m * BACK_CH] = 0.0f;
+                }
+                act[(it & 1) * BACK_CH + lane] = squelched ? 0.0f : 1.0f;
+            }
+            __syncthreads();
+        }
+        if (live)
+        {
+            S[0 * C + c] = i_prev; S[1 * C + c] = q_prev; S[2 * C + c] = lpf_prev;
+            S[3 * C + c] = hpf_a; S[4 * C + c] = hpf_b; S[5 * C + c] = sql_avg;
+            S[6 * C + c] = squelched ? 0.0f : 1.0f;
+#pragma unroll
+            for (int i = 0; i < SQ; ++i) S[(7 + i) * C + c] = g[i];
+        }
+    }
+    else
+    {
+        float bq2[4], b2[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) b2[i] = P->biquad2[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bq2[i] = a.s.bq2[i * C + cl];
+        const float lo = P->line_out_scale, fs = P->fm_scale;
+        for (int it = 0; it <= calls; ++it)
+        {
+            if (it > 0)
+            {
+                const int call = it - 1;
+                const float* mi = dem + (call & 1) * BLK * BACK_CH + lane;
+                const bool on = act[(call & 1) * BACK_CH + lane] != 0.0f;
+                float* ao = a.audio ? a.audio + (size_t)c * a.N + call * BLK : nullptr;
+                int2* dd = a.dst ? a.dst + (size_t)c * a.N + call * BLK : nullptr;
+#pragma unroll 2
+                for (int n0 = 0; n0 < BLK; n0 += 4)
+                {
+                    float y[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                    {
+                        float v = mi[(n0 + j) * BACK_CH] * fs;
+                        v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
+                        y[j] = on ? v * lo : 0.0f;
+                    }
+                    if (live)
+                    {
+                        if (ao) *(float4*)(ao + n0) = make_float4(y[0], y[1], y[2], y[3]);
+                        if (dd)
+                        {
+                            const int d0 = on ? to_dma(y[0]) : 0, d1 = on ? to_dma(y[1]) : 0;
+                            const int d2 = on ? to_dma(y[2]) : 0, d3 = on ? to_dma(y[3]) : 0;
+                            *(int4*)(dd + n0) = make_int4(d0, d0, d1, d1);
+                            *(int4*)(dd + n0 + 2) = make_int4(d2, d2, d3, d3);
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (live)
+        {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a.s.bq2[i * C + c] = bq2[i];
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // kernel selection: the filter-path families of FilterPathInfo (audio_filter.c:147-922)
 
@@ -1112,6 +1289,8 @@ static const FrontVariant kFront[] = {
     { 89, 0, 4, 1, rx_front<89, 0, 4, true, 8>, 8 },
     { 89, 0, 2, 1, rx_front<89, 0, 2, true, 16>, 16 },        // AM / SAM, 24 ksps (P83-86)
     { 89, 0, 2, 1, rx_front<89, 0, 2, true, 8>, 8 },
+    { 89, 0, 1, 0, rx_front<89, 0, 1, false, 16>, 16 },       // FM, 48 ksps Hilbert pair (P1-3)
+    { 89, 0, 1, 0, rx_front<89, 0, 1, false, 8>, 8 },
 };
 
 #define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm> }
@@ -1128,10 +1307,13 @@ static const BackVariant kBack[] = {
     BACK_V(10, 0, 4, 4, 49, DM_SAM_SB), BACK_V(10, 6, 4, 1, 49, DM_SAM_SB), BACK_V(10, 0, 2, 8, 97, DM_SAM_SB),
     BACK_V(8, 0, 2, 8, 97, DM_SAM_SB), BACK_V(8, 6, 2, 2, 97, DM_SAM_SB),
 };
+// FM: its own kernel (squelch lattice stages)
+static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6> };
 #undef BACK_V
 
 static int plan_dm(const uhsdr_rx_plan& p)
 {
+    if (p.dmod_mode == UHSDR_DEMOD_FM) return DM_FM;
     if (p.dmod_mode == UHSDR_DEMOD_AM) return DM_AM;
     if (p.dmod_mode == UHSDR_DEMOD_SAM) return p.sam_sideband == UHSDR_SAM_SIDEBAND_BOTH ? DM_SAM : DM_SAM_SB;
     return DM_NONE;
@@ -1162,6 +1344,7 @@ static const FrontVariant* find_front(const uhsdr_rx_plan& p, long long C = 0, i
 
 static const BackVariant* find_back(const uhsdr_rx_plan& p)
 {
+    if (p.dmod_mode == UHSDR_DEMOD_FM) return p.sq_stages == 6 ? &kBackFm : nullptr;
     for (const BackVariant& v : kBack)
         if (v.pre == p.pre_stages && v.aa == p.aa_stages && v.L == p.interp_L && v.ph == p.interp_phase &&
             v.w == p.agc.attack_buffsize && v.dm == plan_dm(p))
@@ -1293,6 +1476,7 @@ static size_t front_lds(const uhsdr_rx_s* h)
 
 static size_t back_lds(const uhsdr_rx_s* h)
 {
+    if (h->bv->dm == DM_FM) return sizeof(float) * (size_t)BACK_CH * 2 * (BLK + 1);
     return sizeof(float) * (size_t)BACK_CH * 2 * (BLK + 2 * (BLK / h->plan.interp_L));
 }
 
@@ -1350,7 +1534,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const size_t o_h2i = take((size_t)C * hs2), o_h2q = take((size_t)C * hs2);
     const size_t o_teta = take((size_t)3 * C), o_osc = take(4);
     const size_t o_pre = take((size_t)10 * C), o_aa = take((size_t)10 * C), o_bq1 = take((size_t)16 * C);
-    const size_t o_bq2 = take((size_t)4 * C), o_ip = take((size_t)15 * C), o_ring = take((size_t)(W - 1) * C);
+    const size_t o_bq2 = take((size_t)4 * C), o_ip = take((size_t)15 * C), o_ring = take(W > 0 ? (size_t)(W - 1) * C : 0);
     const size_t o_agc = take((size_t)(6 + AGC_Q) * C), o_agci = take((size_t)3 * C);
     const bool am = h->bv->dm != DM_NONE;
     const size_t o_sam = take(am ? (size_t)(7 + 96) * C : 0), o_adq = take(am ? (size_t)C * h->Nd : 0);
@@ -1422,7 +1606,7 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
     ba.dst = (int2*)dst;
     ba.s = h->bs;
     ba.C = h->C; ba.N = h->N; ba.Nd = h->Nd;
-    ba.ring_phase = (int)(h->calls_done % AGC_Q);
+    ba.ring_phase = (int)(h->calls_done % (h->bv->dm == DM_FM ? 200 : AGC_Q));   // FM: fm_data.count phase
     time_mark(h, 1, 0);
     hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH), back_lds(h), h->stream, ba);
     HIPCHK(hipGetLastError());

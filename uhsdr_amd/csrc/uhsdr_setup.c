@@ -81,7 +81,15 @@ void uhsdr_rx_config_default(uhsdr_rx_config* c)
     c->sam_zeta = 65;
     c->sam_omega_n = 250;
     c->fade_leveler = 1;
+    c->fm_sql_threshold = 12;                    /* FM_SQUELCH_DEFAULT, audio_driver.h:449 */
+    c->fm_deviation_5k = 0;
 }
+
+/* IIR_15k_hpf (drivers/audio/filters/iir_15k_hpf_fm_squelch.c): 6-stage lattice high-pass of
+   the FM squelch noise detector, as raw binary32 bits (pinned against the reference build by
+   tests/test_setup.py) */
+static const uint32_t squelch_k_bits[6] = { 0x3dafcf3cu, 0x3e98cf2fu, 0x3f1b1449u, 0x3f362601u, 0x3f451263u, 0x3f49b75cu };
+static const uint32_t squelch_v_bits[7] = { 0x3bb81eb1u, 0xbcd76eb4u, 0x3d8c17f0u, 0xbdea21a5u, 0x3def82c3u, 0xbd953da8u, 0x3ccfa56fu };
 
 /* AudioFilter_GetFilterModeFromDemodMode, audio_filter.c:929-955 */
 static int filter_mode_of(int dmod)
@@ -392,6 +400,12 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
         p->fade_mtauI = (expf(-1 / (decimSampleRate * tauI)));
         p->fade_onem_mtauI = (1.0 - p->fade_mtauI);
     }
+    /* FM: AudioDriver_DemodFM (audio_driver.c:1544-1737), FM_RX_SCALING_* (:1494-1495) */
+    p->fm_scale = cfg->fm_deviation_5k ? 5000 : 10000;
+    p->fm_sql_threshold = cfg->fm_sql_threshold;
+    p->sq_stages = 6;
+    copy_bits(p->sq_k, squelch_k_bits, 6);
+    copy_bits(p->sq_v, squelch_v_bits, 7);
     return UHSDR_OK;
 }
 
@@ -399,9 +413,10 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
    whether a kernel variant exists for the plan's filter-path family. */
 int uhsdr_rx_mode_supported(const uhsdr_rx_plan* p)
 {
-    /* device chain: SSB / CW / DIGI (I +- Q), AM, SAM; FM not yet */
+    /* device chain: SSB / CW / DIGI (I +- Q), AM, SAM, FM (FM needs the I/Q translation: without
+       it AudioDriver_DemodFM leaves a_buffer[0] untouched, audio_driver.c:1548) */
     if (!p) return 0;
-    return p->dmod_mode != UHSDR_DEMOD_FM;
+    return p->dmod_mode != UHSDR_DEMOD_FM || p->freq_shift_hz != 0;
 }
 
 const char* uhsdr_version(void) { return "uhsdr_amd 0.1 (gfx950)"; }

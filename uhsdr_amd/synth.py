@@ -124,6 +124,25 @@ def am_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier
     return _frames(i_sig, q_sig)
 
 
+def fm_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier: float = 12000.0,
+          deviation: float = 2500.0, tone: float = 1000.0, amplitude: float = 3000.0):
+    """C4 FM-RX: carrier at `carrier` Hz, a `tone` Hz audio tone at
+    `deviation` Hz peak deviation, `amplitude` LSB16, plus noise."""
+    channels = np.asarray(channels, dtype=np.int64)
+    ch = channels.astype(np.uint64)
+    base = (np.uint64(SEED_BASE) + ch) << np.uint64(20)
+    ph_c = 2.0 * np.pi * _uniform(base + np.uint64(10))
+    ph_m = 2.0 * np.pi * _uniform(base + np.uint64(11))
+    n = np.arange(start, start + nframes, dtype=np.float64)[None, :]
+    ph = (2.0 * np.pi * carrier / FS * n + ph_c[:, None]
+          + (deviation / tone) * np.sin(2.0 * np.pi * tone / FS * n + ph_m[:, None]))
+    i_sig, q_sig = amplitude * np.cos(ph), amplitude * np.sin(ph)
+    if noise_sigma > 0:
+        ni, nq = _noise(channels, start, nframes, noise_sigma)
+        i_sig, q_sig = i_sig + ni, q_sig + nq
+    return _frames(i_sig, q_sig)
+
+
 def ssb_iq_torch(c0: int, nch: int, start: int, nframes: int, device, noise_sigma: float = 30.0):
     """Same signal model as ``ssb_iq`` (kind "ssb2tone"), generated on the GPU for large
     benchmark batches: channels c0 .. c0+nch-1.  Tone parameters and noise come from the

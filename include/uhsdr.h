@@ -209,6 +209,77 @@ void         uhsdr_device_free(void* p);
 uhsdr_status uhsdr_copy_to_device(void* dst, const void* src, uint64_t bytes);
 uhsdr_status uhsdr_copy_to_host(void* dst, const void* src, uint64_t bytes);
 
+/* ================================ transmit ================================
+ * TxProcessor_Run (drivers/audio/tx_processor.c:891-1078) for SSB (USB / LSB) voice:
+ *   codec audio frames -> mic gain -> TX band-pass lattice -> bass/treble biquads ->
+ *   ALC compressor with its 288-sample look-ahead delay -> 201-tap Hilbert pair ->
+ *   FreqShift -> I/Q gain + phase -> int32 IQ frames for the DAC.
+ * One uhsdr_tx_process call == N/32 TX-mode AudioDriver_I2SCallback invocations per channel.
+ */
+#define UHSDR_TX_HILBERT_TAPS 201    /* iq_tx_wide, drivers/audio/filters/iq_tx_filter.h:22 */
+#define UHSDR_TX_DELAY 320           /* AUDIO_DELAY_BUFSIZE, audio_driver.h:516 */
+
+/* TX_AUDIO_*, hardware/uhsdr_board.h:128-131 */
+enum { UHSDR_TX_AUDIO_MIC = 0, UHSDR_TX_AUDIO_LINEIN_L = 1, UHSDR_TX_AUDIO_LINEIN_R = 2, UHSDR_TX_AUDIO_DIG = 3 };
+
+typedef struct uhsdr_tx_config
+{
+    int32_t dmod_mode;            /* ts.dmod_mode: UHSDR_DEMOD_USB or UHSDR_DEMOD_LSB */
+    int32_t iq_freq_mode;         /* ts.iq_freq_mode */
+    int32_t audio_source;         /* ts.tx_audio_source: MIC, LINEIN_L, LINEIN_R */
+    int32_t mic_gain_mult;        /* ts.tx_mic_gain_mult (codec.c:313-321) */
+    int32_t mic_boost;            /* ts.tx_mic_boost */
+    int32_t comp_level;           /* ts.tx_comp_level: -1 off, 0..12 presets, 13 = stored values */
+    int32_t alc_decay;            /* ts.alc_decay (EEPROM, used by comp_level 13) */
+    int32_t alc_postfilt_gain;    /* ts.alc_tx_postfilt_gain (EEPROM, used by comp_level 13) */
+    int32_t tx_filter;            /* ts.tx_filter: 0/1 soprano, 2 tenor, 3 bass */
+    int32_t bass_gain;            /* ts.dsp.tx_bass_gain */
+    int32_t treble_gain;          /* ts.dsp.tx_treble_gain */
+    int32_t filter_disable;       /* FLAGS1_SSB_TX_FILTER_DISABLE */
+    float   power_factor;         /* ts.tx_power_factor */
+    float   gain_i, gain_q;       /* ts.tx_adj_gain_var[trans].i / .q */
+    float   phase_balance;        /* ads.iq_phase_balance_tx[trans] */
+    int32_t reserved[16];
+} uhsdr_tx_config;
+
+typedef struct uhsdr_tx_plan
+{
+    int32_t dmod_mode, lsb, audio_source;
+    float   in_gain;              /* gain_calc of TxProcessor_AudioBufferFill (tx_processor.c:354-381) */
+    int32_t apply_in_gain;        /* gain_calc != 1.0 */
+    int32_t run_lattice, run_biquad;
+    int32_t lat_stages;
+    float   lat_k[UHSDR_MAX_LATTICE];
+    float   lat_v[UHSDR_MAX_LATTICE + 1];
+    float   biquad[15];           /* IIR_TX_biquad: treble shelf 1700 Hz, bass shelf 300 Hz, passthrough */
+    int32_t comp_on;              /* ts.tx_comp_level > -1 */
+    float   postfilt_gain;        /* alc_tx_postfilt_gain_var / 2.0 + 0.5 */
+    float   alc_decay;            /* ads.alc_decay (audio_management.c:15-19) */
+    float   alc_gain_scaling;     /* SSB_ALC_GAIN_CORRECTION */
+    float   hilbert_i[UHSDR_TX_HILBERT_TAPS + 7];   /* already swapped for LSB (tx_processor.c:477-478) */
+    float   hilbert_q[UHSDR_TX_HILBERT_TAPS + 7];
+    int32_t freq_shift_hz, shift_kind, shift_up;
+    float   osc_cos, osc_sin;
+    float   final_i_gain, final_q_gain;   /* tx_power_factor * tx_adj_gain_var * SSB_GAIN_COMP * 2^16 */
+    float   phase_balance;
+    int32_t reserved[32];
+} uhsdr_tx_plan;
+
+typedef struct uhsdr_tx_s* uhsdr_tx_handle;
+
+void         uhsdr_tx_config_default(uhsdr_tx_config* cfg);
+uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* plan);
+/* audio: device AudioSample_t [C][N][2] int32 in; iq: device IqSample_t [C][N][2] int32 out;
+   a0: optional device f32 [C][N], the compressed audio (adb.a_buffer[0]) */
+uhsdr_status uhsdr_tx_create(const uhsdr_tx_config* cfg, int32_t num_channels, int32_t frames_per_call,
+                             void* stream, uhsdr_tx_handle* out);
+uhsdr_status uhsdr_tx_reset(uhsdr_tx_handle h);
+uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio, int32_t* iq, float* a0);
+uhsdr_status uhsdr_tx_get_plan(uhsdr_tx_handle h, uhsdr_tx_plan* plan);
+uhsdr_status uhsdr_tx_destroy(uhsdr_tx_handle h);
+int32_t      uhsdr_sizeof_tx_config(void);
+int32_t      uhsdr_sizeof_tx_plan(void);
+
 /* ---- diagnostics ---- */
 const char*  uhsdr_version(void);
 /* sizeof(uhsdr_rx_config), sizeof(uhsdr_rx_plan): lets FFI bindings check their layouts */

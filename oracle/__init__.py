@@ -29,6 +29,10 @@ def load():
         lib.uo_rx_process.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         lib.uo_rx_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                             C.c_void_p, C.c_void_p, C.c_int]
+        lib.uo_tx_state_size.restype = C.c_size_t
+        lib.uo_tx_state_init.argtypes = [C.c_void_p, C.c_void_p]
+        lib.uo_tx_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                            C.c_void_p, C.c_void_p, C.c_int]
         _lib = lib
     return _lib
 
@@ -56,3 +60,29 @@ class OracleRx:
         if st != 0:
             raise RuntimeError(f"uo_rx_process_batch status {st}")
         return a1, dst
+
+
+class OracleTx:
+    """C channels of the reference SSB transmit chain on the CPU, state carried across calls."""
+
+    def __init__(self, plan, channels: int):
+        self.lib = load()
+        self.plan = plan
+        self.channels = channels
+        self.ssize = self.lib.uo_tx_state_size()
+        self.states = (C.c_char * (self.ssize * channels))()
+        for c in range(channels):
+            self.lib.uo_tx_state_init(C.byref(plan), C.byref(self.states, c * self.ssize))
+
+    def process(self, audio: np.ndarray, threads: int = 1):
+        """audio: int32 [C][n][2] codec frames -> (iq int32 [C][n][2], a0 f32 [C][n])"""
+        audio = np.ascontiguousarray(audio, dtype=np.int32)
+        Cn, n, _ = audio.shape
+        assert Cn == self.channels
+        iq = np.empty((Cn, n, 2), np.int32)
+        a0 = np.empty((Cn, n), np.float32)
+        st = self.lib.uo_tx_process_batch(C.byref(self.plan), self.states, Cn, audio.ctypes.data_as(C.c_void_p), n,
+                                          iq.ctypes.data_as(C.c_void_p), a0.ctypes.data_as(C.c_void_p), threads)
+        if st != 0:
+            raise RuntimeError(f"uo_tx_process_batch status {st}")
+        return iq, a0

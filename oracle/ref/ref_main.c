@@ -17,6 +17,9 @@
  *   mode= path= iqmode= agc_mode= agc_thresh= agc_slope= agc_hang= bass= treble=
  *   iq_auto= gain_i= gain_q= phase= dsp= notch= peak= sam_sb= pll_fmax= zeta= omegan=
  *   fade= sql= fm5k= block=
+ *   tx=1           transmit: in= holds codec audio frames {l,r}, out_dst= gets the IQ frames
+ *                  TxProcessor_Run writes (tx_processor.c:891-1078), out_a= a_buffer[0]
+ *   micmult= boost= comp= txfilter= txbass= txtreble= txpwr= txgi= txgq= txphase=
  *   dump=setup     print the configured chain (coefficients as raw bits) as JSON
  *   dump=paths     print FilterPathInfo[] (audio_filter.c:147-922) as JSON
  */
@@ -42,6 +45,9 @@ const arm_iir_lattice_instance_f32* oracle_ref_prefilter(void);
 const arm_iir_lattice_instance_f32* oracle_ref_antialias(void);
 const arm_fir_interpolate_instance_f32* oracle_ref_interpolate(void);
 const arm_iir_lattice_instance_f32* oracle_ref_squelch(void);
+const arm_iir_lattice_instance_f32* oracle_ref_tx_lattice(void);
+const arm_biquad_casd_df1_inst_f32* oracle_ref_tx_biquad(void);
+extern arm_fir_instance_f32 Fir_Tx_Hilbert_I, Fir_Tx_Hilbert_Q;
 void oracle_ref_agc_dump(void);
 unsigned long oracle_harness_layout(void);
 unsigned long oracle_driver_layout(void);
@@ -127,7 +133,19 @@ static void dump_setup(void)
     print_fvec("aa_v", aa->pvCoeffs, aa->numStages ? aa->numStages + 1 : 0, 0);
     const arm_iir_lattice_instance_f32* sq = oracle_ref_squelch();   /* FM squelch HPF, audio_driver.c:481-484 */
     print_fvec("squelch_k", sq->pkCoeffs, sq->numStages, 0);
-    print_fvec("squelch_v", sq->pvCoeffs, sq->numStages + 1, 1);
+    print_fvec("squelch_v", sq->pvCoeffs, sq->numStages + 1, 0);
+    /* transmit chain (TxProcessor_Set, tx_processor.c:72-120; AudioManagement_CalcTxCompLevel) */
+    const arm_iir_lattice_instance_f32* txl = oracle_ref_tx_lattice();
+    const arm_biquad_casd_df1_inst_f32* txb = oracle_ref_tx_biquad();
+    print_fvec("tx_k", txl->pkCoeffs, txl->numStages, 0);
+    print_fvec("tx_v", txl->pvCoeffs, txl->numStages + 1, 0);
+    print_fvec("tx_biquad", txb->pCoeffs, 5 * txb->numStages, 0);
+    print_fvec("tx_hilbert_i", Fir_Tx_Hilbert_I.pCoeffs, Fir_Tx_Hilbert_I.numTaps, 0);
+    print_fvec("tx_hilbert_q", Fir_Tx_Hilbert_Q.pCoeffs, Fir_Tx_Hilbert_Q.numTaps, 0);
+    {
+        const float alc[2] = { ads.alc_decay, (float)ts.alc_tx_postfilt_gain_var };
+        print_fvec("tx_alc", alc, 2, 1);
+    }
     printf("}\n");
 }
 
@@ -187,6 +205,20 @@ int main(int argc, char** argv)
     agc_wdsp_conf.tau_decay[4] = 50;
     agc_wdsp_conf.tau_hang_decay = 500;
     sd.fft_iq_len = 0;          /* spectrum tap off for the audio oracle */
+    /* transmit settings (hardware/uhsdr_board.h:301-460, defaults ui_configuration.c) */
+    const int tx = (int)iarg(argc, argv, "tx", 0);
+    ts.tx_mic_gain_mult = iarg(argc, argv, "micmult", 15);
+    ts.tx_mic_boost = iarg(argc, argv, "boost", 0);
+    ts.tx_comp_level = iarg(argc, argv, "comp", TX_AUDIO_COMPRESSION_DEFAULT);
+    ts.alc_decay = ALC_DECAY_DEFAULT;
+    ts.alc_tx_postfilt_gain = ALC_POSTFILT_GAIN_DEFAULT;
+    ts.tx_filter = iarg(argc, argv, "txfilter", 0);
+    ts.dsp.tx_bass_gain = iarg(argc, argv, "txbass", 4);
+    ts.dsp.tx_treble_gain = iarg(argc, argv, "txtreble", 4);
+    ts.tx_power_factor = farg(argc, argv, "txpwr", 0.5f);
+    ts.tx_adj_gain_var[IQ_TRANS_ON].i = ts.tx_adj_gain_var[IQ_TRANS_OFF].i = farg(argc, argv, "txgi", 1.0f);
+    ts.tx_adj_gain_var[IQ_TRANS_ON].q = ts.tx_adj_gain_var[IQ_TRANS_OFF].q = farg(argc, argv, "txgq", 1.0f);
+    ads.iq_phase_balance_tx[IQ_TRANS_ON] = ads.iq_phase_balance_tx[IQ_TRANS_OFF] = farg(argc, argv, "txphase", 0.0f);
 
     ts.filter_path_mem[AudioFilter_GetFilterModeFromDemodMode(mode)][0] = path;
 
@@ -210,6 +242,22 @@ int main(int argc, char** argv)
     fclose(f);
 
     IqSample_t blk[IQ_BLOCK_SIZE];
+    if (tx)
+    {
+        /* TX: the codec's audio frames in, IQ frames out (AudioDriver_I2SCallback TX branch,
+           audio_driver.c:3010-3036 -> TxProcessor_Run); the sidetone goes to a scratch buffer */
+        ts.txrx_mode = TRX_MODE_TX;
+        AudioSample_t ablk[IQ_BLOCK_SIZE], side[IQ_BLOCK_SIZE];
+        IqSample_t oblk[IQ_BLOCK_SIZE];
+        for (long off = 0; off < n; off += block)
+        {
+            memcpy(ablk, iq + off, sizeof(AudioSample_t) * block);
+            AudioDriver_I2SCallback(ablk, oblk, side, block);
+            memcpy(dst + off, oblk, sizeof(IqSample_t) * block);
+            memcpy(a1 + off, adb.a_buffer[0], sizeof(float) * block);
+        }
+    }
+    else
     for (long off = 0; off < n; off += block)
     {
         memcpy(blk, iq + off, sizeof(IqSample_t) * block);   /* the ISR's DMA half-buffer */

@@ -607,3 +607,152 @@ int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, cons
         for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
     return UHSDR_OK;
 }
+
+/* ================================ transmit ================================ */
+
+size_t uo_tx_state_size(void) { return sizeof(uo_tx_state); }
+
+void uo_tx_state_init(const uhsdr_tx_plan* p, uo_tx_state* s)
+{
+    (void)p;
+    memset(s, 0, sizeof *s);
+    s->alc_val = 1;             /* TxProcessor_Init, tx_processor.c:137 */
+    s->osc_vi = 0.0f;           /* FreqShift_Approx_Prepare, freq_shift.c:48-49 */
+    s->osc_vq = 1.0f;
+}
+
+static int32_t to_int32(float f)     /* float -> int32 as x86 cvttss2si (out of range -> INT32_MIN) */
+{
+    return (f > -2147483904.0f && f < 2147483648.0f) ? (int32_t)f : INT32_MIN;
+}
+
+/* one TxProcessor_Run call (SSB voice) on BLK frames */
+static void tx_call(const uhsdr_tx_plan* p, uo_tx_state* s, const int32_t* audio, int32_t* iq, float* a0)
+{
+    const int n = BLK;
+    float a[BLK], ib[BLK], qb[BLK], valbuf[BLK];
+    /* TxProcessor_AudioBufferFill (tx_processor.c:339-405) */
+    for (int i = 0; i < n; i++) a[i] = (p->audio_source == UHSDR_TX_AUDIO_LINEIN_R) ? audio[2 * i + 1] : audio[2 * i];
+    if (p->apply_in_gain)
+        for (int i = 0; i < n; i++) a[i] = a[i] * p->in_gain;
+    /* TxProcessor_FilterAudio (:416-429) */
+    if (p->run_lattice) iir_lattice(p->lat_k, p->lat_v, p->lat_stages, s->lat, a, a, n);
+    if (p->run_biquad) biquad_df1(p->biquad, 3, s->bq, a, n);
+    /* TxProcessor_VoiceCompressor (:173-242) */
+    if (p->comp_on)
+    {
+        for (int i = 0; i < n; i++) a[i] = a[i] * p->postfilt_gain;
+        for (int i = 0; i < n; i++)
+        {
+            const float alc_var = fabsf(a[i] * s->alc_val) / 30000 - 1.0;        /* ALC_KNEE */
+            if (alc_var < 0)
+            {
+                s->alc_val -= s->alc_val * p->alc_decay * alc_var;
+            }
+            else
+            {
+                s->alc_val -= s->alc_val * 0.1 * alc_var;                        /* ALC_ATTACK */
+                if (s->alc_val < 0.001) s->alc_val = 0.001;                      /* ALC_VAL_MIN */
+            }
+            if (s->alc_val > 1) s->alc_val = 1;                                 /* ALC_VAL_MAX */
+            valbuf[i] = (s->alc_val * p->alc_gain_scaling);
+        }
+        s->delay_in += n;
+        int out = s->delay_in + n;
+        s->delay_in %= UHSDR_TX_DELAY;
+        out %= UHSDR_TX_DELAY;
+        memcpy(&s->delay[s->delay_in], a, sizeof(float) * n);
+        memcpy(a, &s->delay[out], sizeof(float) * n);
+        for (int i = 0; i < n; i++) a[i] = a[i] * valbuf[i];
+    }
+    if (a0) memcpy(a0, a, sizeof(float) * n);
+    /* TxProcessor_SSB (:467-490): Hilbert pair, then FreqShift */
+    fir(p->hilbert_i, UHSDR_TX_HILBERT_TAPS, s->hil_i, a, ib, n);
+    fir(p->hilbert_q, UHSDR_TX_HILBERT_TAPS, s->hil_q, a, qb, n);
+    if (p->freq_shift_hz != 0)
+    {
+        float* ip = p->shift_up ? ib : qb;
+        float* qp = p->shift_up ? qb : ib;
+        if (p->shift_kind == 1)
+        {
+            for (int i = 0; i < n; i += 4)
+            {
+                float h1 = qp[i + 1], h2 = -ip[i + 1];
+                ip[i + 1] = h1; qp[i + 1] = h2;
+                h1 = -ip[i + 2]; h2 = -qp[i + 2];
+                ip[i + 2] = h1; qp[i + 2] = h2;
+                h1 = -qp[i + 3]; h2 = ip[i + 3];
+                ip[i + 3] = h1; qp[i + 3] = h2;
+            }
+        }
+        else
+        {
+            for (int i = 0; i < n; i++)
+            {
+                const float oq = (s->osc_vq * p->osc_cos) - (s->osc_vi * p->osc_sin);
+                const float oi = (s->osc_vi * p->osc_cos) + (s->osc_vq * p->osc_sin);
+                const float qt = qp[i], it = ip[i];
+                qp[i] = (qt * oq) - (it * oi);
+                ip[i] = (it * oq) + (qt * oi);
+                s->osc_vq = oq;
+                s->osc_vi = oi;
+            }
+            const float g = (3 - ((s->osc_vq * s->osc_vq) + (s->osc_vi * s->osc_vi))) / 2;
+            s->osc_vq = g * s->osc_vq;
+            s->osc_vi = g * s->osc_vi;
+        }
+    }
+    /* TxProcessor_IqFinalProcessing (:282-330) */
+    for (int i = 0; i < n; i++) ib[i] = ib[i] * p->final_i_gain;
+    for (int i = 0; i < n; i++) qb[i] = qb[i] * p->final_q_gain;
+    const float ph = p->phase_balance;                 /* AudioDriver_IQPhaseAdjust, audio_driver.c:1776-1801 */
+    if (ph < 0)
+        for (int i = 0; i < n; i++) { const float e = ib[i] * ph; qb[i] = qb[i] + e; }
+    else if (ph > 0)
+        for (int i = 0; i < n; i++) { const float e = qb[i] * ph; ib[i] = ib[i] + e; }
+    for (int i = 0; i < n; i++)
+    {
+        iq[2 * i] = to_int32(ib[i]);
+        iq[2 * i + 1] = to_int32(qb[i]);
+    }
+}
+
+typedef struct
+{
+    const uhsdr_tx_plan* p;
+    uo_tx_state* states;
+    const int32_t* audio;
+    int32_t* iq;
+    float* a0;
+    int c0, c1, n;
+} uo_tx_job;
+
+static void* uo_tx_worker(void* arg)
+{
+    uo_tx_job* j = (uo_tx_job*)arg;
+    for (int c = j->c0; c < j->c1; c++)
+        for (int off = 0; off < j->n; off += BLK)
+            tx_call(j->p, &j->states[c], j->audio + ((size_t)c * j->n + off) * 2, j->iq + ((size_t)c * j->n + off) * 2,
+                    j->a0 ? j->a0 + (size_t)c * j->n + off : NULL);
+    return NULL;
+}
+
+int uo_tx_process_batch(const uhsdr_tx_plan* p, uo_tx_state* states, int C, const int32_t* audio, int n,
+                        int32_t* iq, float* a0, int threads)
+{
+    if (n % BLK) return UHSDR_LENGTH_ERROR;
+    if (threads < 1) threads = 1;
+    if (threads > C) threads = C;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    uo_tx_job jobs[256];
+    for (int t = 0; t < threads; t++)
+    {
+        jobs[t] = (uo_tx_job){ p, states, audio, iq, a0, (int)((long)C * t / threads), (int)((long)C * (t + 1) / threads), n };
+        if (threads == 1) uo_tx_worker(&jobs[t]);
+        else pthread_create(&tid[t], NULL, uo_tx_worker, &jobs[t]);
+    }
+    if (threads > 1)
+        for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+    return UHSDR_OK;
+}

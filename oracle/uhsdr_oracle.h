@@ -60,6 +60,23 @@ int uo_rx_process(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, int
 int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
                         float* a1, int32_t* dst, int threads);
 
+/* transmit: TxProcessor_Run SSB voice path (drivers/audio/tx_processor.c:891-1078) */
+typedef struct uo_tx_state
+{
+    float lat[UHSDR_MAX_LATTICE + 1];        /* IIR_TXFilter state */
+    float bq[12];                             /* IIR_TX_biquad state */
+    float alc_val;                            /* ads.alc_val (TxProcessor_Init: 1) */
+    float delay[UHSDR_TX_DELAY];              /* audio_delay_buffer */
+    int32_t delay_in;                         /* alc_delay_inbuf (function static) */
+    float hil_i[UHSDR_TX_HILBERT_TAPS], hil_q[UHSDR_TX_HILBERT_TAPS];
+    float osc_vi, osc_vq;
+} uo_tx_state;
+
+size_t uo_tx_state_size(void);
+void uo_tx_state_init(const uhsdr_tx_plan* p, uo_tx_state* s);
+int uo_tx_process_batch(const uhsdr_tx_plan* p, uo_tx_state* states, int C, const int32_t* audio, int n,
+                        int32_t* iq, float* a0, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -80,6 +80,43 @@ CONFIGS = {
     "p3_fm_noise": ({"mode": 5, "path": 3, "sql": 18}, {"fm": True, "frames": 8192, "amplitude": 40.0}),
 }
 
+# SSB transmit (C4, TxProcessor_Run): microphone two-tone in, IQ frames out (tests/golden/tx_*.npz)
+TX_CONFIGS = {
+    "usb": {"mode": 0, "path": 48},
+    "lsb": {"mode": 1, "path": 48},
+    "usb_bass": {"mode": 0, "path": 48, "txfilter": 3, "txbass": -4, "txtreble": 2},
+    "usb_tenor": {"mode": 0, "path": 48, "txfilter": 2, "comp": 5},
+    "usb_comp_off": {"mode": 0, "path": 48, "comp": -1},
+    "usb_comp_hi": {"mode": 0, "path": 48, "comp": 11, "micmult": 40, "boost": 1},
+    "usb_iqadj": {"mode": 0, "path": 48, "txgi": 0.97, "txgq": 1.02, "txphase": -0.015, "txpwr": 0.8},
+    "usb_m6k": {"mode": 0, "path": 48, "iqmode": 2},
+    "usb_off": {"mode": 0, "path": 48, "iqmode": 0, "txphase": 0.01},
+}
+
+
+def make_tx(name: str):
+    args = dict(TX_CONFIGS[name], tx=1)
+    audio = synth.tx_audio(np.arange(NCH), 0, NFRAMES)
+    a0 = np.empty((NCH, NFRAMES), np.float32)
+    iq = np.empty((NCH, NFRAMES, 2), np.int32)
+    for c in range(NCH):
+        a0[c], iq[c] = run_ref(args, audio[c])
+    np.savez_compressed(os.path.join(HERE, f"tx_{name}.npz"), audio=audio, a0=a0, iq=iq,
+                        setup=json.dumps(ref_json(args, "setup")), args=json.dumps(args))
+    print(f"tx_{name:12s} peak|iq|={int(np.abs(iq).max()):11d}  peak|a0|={float(np.abs(a0).max()):9.1f}")
+
+
+def tx_tables():
+    """TX lattice band-pass per voice profile (TxProcessor_Set, tx_processor.c:88-107) and the
+    201-tap TX Hilbert pair, as raw bits from the compiled reference."""
+    out = {"lattice": {}}
+    for f in (1, 2, 3):
+        d = ref_json({"mode": 0, "path": 48, "tx": 1, "txfilter": f}, "setup")
+        out["lattice"][str(f)] = {"k": d["tx_k"], "v": d["tx_v"]}
+        out["hilbert_i"], out["hilbert_q"] = d["tx_hilbert_i"], d["tx_hilbert_q"]
+    with open(os.path.join(HERE, "tx_tables.json"), "w") as fo:
+        json.dump(out, fo, separators=(",", ":"))
+
 
 def run_ref(args: dict, iq: np.ndarray):
     n = iq.shape[0]
@@ -130,10 +167,15 @@ def main():
     paths = subprocess.run([REF, "dump=paths"], check=True, capture_output=True, text=True).stdout
     with open(os.path.join(HERE, "filter_paths.json"), "w") as f:
         json.dump(json.loads(paths), f, separators=(",", ":"))
+    tx_tables()
     for name in CONFIGS:
         if a.only and name != a.only:
             continue
         make(name)
+    for name in TX_CONFIGS:
+        if a.only and f"tx_{name}" != a.only:
+            continue
+        make_tx(name)
 
 
 if __name__ == "__main__":

@@ -79,6 +79,33 @@ class RxPlan(C.Structure):
     ]
 
 
+TX_HILBERT_TAPS = 201
+TX_AUDIO_MIC, TX_AUDIO_LINEIN_L, TX_AUDIO_LINEIN_R, TX_AUDIO_DIG = range(4)
+
+
+class TxConfig(C.Structure):
+    _fields_ = [
+        ("dmod_mode", C.c_int32), ("iq_freq_mode", C.c_int32), ("audio_source", C.c_int32),
+        ("mic_gain_mult", C.c_int32), ("mic_boost", C.c_int32), ("comp_level", C.c_int32), ("alc_decay", C.c_int32),
+        ("alc_postfilt_gain", C.c_int32), ("tx_filter", C.c_int32), ("bass_gain", C.c_int32),
+        ("treble_gain", C.c_int32), ("filter_disable", C.c_int32), ("power_factor", C.c_float),
+        ("gain_i", C.c_float), ("gain_q", C.c_float), ("phase_balance", C.c_float), ("reserved", C.c_int32 * 16),
+    ]
+
+
+class TxPlan(C.Structure):
+    _fields_ = [
+        ("dmod_mode", C.c_int32), ("lsb", C.c_int32), ("audio_source", C.c_int32), ("in_gain", C.c_float),
+        ("apply_in_gain", C.c_int32), ("run_lattice", C.c_int32), ("run_biquad", C.c_int32),
+        ("lat_stages", C.c_int32), ("lat_k", C.c_float * MAX_LATTICE), ("lat_v", C.c_float * (MAX_LATTICE + 1)),
+        ("biquad", C.c_float * 15), ("comp_on", C.c_int32), ("postfilt_gain", C.c_float), ("alc_decay", C.c_float),
+        ("alc_gain_scaling", C.c_float), ("hilbert_i", C.c_float * (TX_HILBERT_TAPS + 7)),
+        ("hilbert_q", C.c_float * (TX_HILBERT_TAPS + 7)), ("freq_shift_hz", C.c_int32), ("shift_kind", C.c_int32),
+        ("shift_up", C.c_int32), ("osc_cos", C.c_float), ("osc_sin", C.c_float), ("final_i_gain", C.c_float),
+        ("final_q_gain", C.c_float), ("phase_balance", C.c_float), ("reserved", C.c_int32 * 32),
+    ]
+
+
 # every exported entry point of include/uhsdr.h: name -> (restype, argtypes)
 SIGNATURES = {
     "uhsdr_rx_config_default": (None, [C.POINTER(RxConfig)]),
@@ -104,6 +131,15 @@ SIGNATURES = {
     "uhsdr_device_free": (None, [C.c_void_p]),
     "uhsdr_copy_to_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "uhsdr_copy_to_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "uhsdr_tx_config_default": (None, [C.POINTER(TxConfig)]),
+    "uhsdr_tx_plan_build": (C.c_int, [C.POINTER(TxConfig), C.POINTER(TxPlan)]),
+    "uhsdr_tx_create": (C.c_int, [C.POINTER(TxConfig), C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]),
+    "uhsdr_tx_reset": (C.c_int, [C.c_void_p]),
+    "uhsdr_tx_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "uhsdr_tx_get_plan": (C.c_int, [C.c_void_p, C.POINTER(TxPlan)]),
+    "uhsdr_tx_destroy": (C.c_int, [C.c_void_p]),
+    "uhsdr_sizeof_tx_config": (C.c_int32, []),
+    "uhsdr_sizeof_tx_plan": (C.c_int32, []),
 }
 
 _lib = None
@@ -124,6 +160,8 @@ def load(path: str | None = None) -> C.CDLL:
         fn.argtypes = args
     if lib.uhsdr_sizeof_config() != C.sizeof(RxConfig) or lib.uhsdr_sizeof_plan() != C.sizeof(RxPlan):
         raise RuntimeError("ctypes layout of uhsdr_rx_config / uhsdr_rx_plan does not match include/uhsdr.h")
+    if lib.uhsdr_sizeof_tx_config() != C.sizeof(TxConfig) or lib.uhsdr_sizeof_tx_plan() != C.sizeof(TxPlan):
+        raise RuntimeError("ctypes layout of uhsdr_tx_config / uhsdr_tx_plan does not match include/uhsdr.h")
     if path is None:
         _lib = lib
     return lib
@@ -166,3 +204,29 @@ REF_ARG_MAP = {
 
 def config_from_ref_args(args: dict) -> RxConfig:
     return default_config(**{REF_ARG_MAP[k]: v for k, v in args.items()})
+
+
+# uhsdr_ref TX key=value names (tests/golden/tx_*.npz) -> TxConfig fields
+TX_ARG_MAP = {
+    "mode": "dmod_mode", "iqmode": "iq_freq_mode", "micmult": "mic_gain_mult", "boost": "mic_boost",
+    "comp": "comp_level", "txfilter": "tx_filter", "txbass": "bass_gain", "txtreble": "treble_gain",
+    "txpwr": "power_factor", "txgi": "gain_i", "txgq": "gain_q", "txphase": "phase_balance",
+}
+
+
+def default_tx_config(**overrides) -> TxConfig:
+    cfg = TxConfig()
+    load().uhsdr_tx_config_default(C.byref(cfg))
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def tx_config_from_ref_args(args: dict) -> TxConfig:
+    return default_tx_config(**{TX_ARG_MAP[k]: v for k, v in args.items() if k in TX_ARG_MAP})
+
+
+def build_tx_plan(cfg: TxConfig) -> TxPlan:
+    plan = TxPlan()
+    check(load().uhsdr_tx_plan_build(C.byref(cfg), C.byref(plan)), "uhsdr_tx_plan_build")
+    return plan

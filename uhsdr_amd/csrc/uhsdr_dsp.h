@@ -1,0 +1,249 @@
+/*
+ * Device DSP building blocks shared by the receive (uhsdr_rx.hip) and transmit (uhsdr_tx.hip)
+ * kernels: the CMSIS-DSP f32 primitives restated in the reference's operation order
+ * (arm_fir_f32 / arm_fir_decimate_f32 as register-window FIR blocks over LDS windows,
+ * arm_iir_lattice_f32, arm_biquad_cascade_df1_f32) and the time-parallel FIR window plumbing
+ * (history rows, lane map, LDS pitch model).
+ */
+#ifndef UHSDR_DSP_H
+#define UHSDR_DSP_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "uhsdr_internal.h"
+
+#define BLK UHSDR_IQ_BLOCK_SIZE
+#define IQ_BIT_SCALE_DOWN 0.0000152587890625f
+
+// acc[r] = sum_{k<T} c[k] * win[r*M + k], r < R; tap order k = 0..T-1 from +0.0f exactly as
+// arm_fir_f32 / arm_fir_decimate_f32 (CMSIS .../arm_fir_f32.c:482-560).  `win` is the lane's
+// first window sample in LDS (16-byte aligned); `c` the tap table in the plan (global, read
+// with scalar loads: the index is wave-uniform), zero beyond T up to a multiple of 8 (a +-0
+// product never changes a finite accumulator that started at +0, so the padding is exact).
+// The chunk loop over 8 taps is deliberately not unrolled: the register window (WA samples,
+// a multiple of 8) slides by 8 samples per chunk and the next 8 samples (two ds_read_b128)
+// and the next 8 taps are fetched before the current MACs, so the live set stays at R
+// accumulators + one window.  Reads run up to 22 samples past the last one used (zeroed).
+// LDS load of V (4 or 2) consecutive floats into w[j..j+V)
+template <int V, int N>
+__device__ __forceinline__ void lds_vec(const float* p, float (&w)[N], int j)
+{
+    if (V == 4)
+    {
+        const float4 v = *(const float4*)p;
+        w[j] = v.x; w[j + 1] = v.y; w[j + 2] = v.z; w[j + 3] = v.w;
+    }
+    else
+    {
+        const float2 v = *(const float2*)p;
+        w[j] = v.x; w[j + 1] = v.y;
+    }
+}
+
+// tap tables are read through the constant address space: wave-uniform indices then become
+// scalar loads (SGPR operands for the MACs) instead of vector loads
+typedef const __attribute__((address_space(4))) float ctaps_t;
+__device__ __forceinline__ ctaps_t* as_taps(const float* p) { return (ctaps_t*)p; }
+
+// V: LDS read width in floats (the lane base is 4V bytes aligned)
+template <int T, int R, int M, int V = 4>
+__device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&acc)[R])
+{
+    constexpr int WA = (M * (R - 1) + 8 + 7) & ~7;
+    constexpr int NCH = (T + 7) / 8;
+    float w[WA];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < WA; j += V) lds_vec<V>(win + j, w, j);
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch)
+    {
+        float cc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cc[q] = c[8 * ch + q];
+        float nw[8];
+#pragma unroll
+        for (int q = 0; q < 8; q += V) lds_vec<V>(win + 8 * ch + WA + q, nw, q);
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+        {
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * cc[kk];
+        }
+#pragma unroll
+        for (int j = 0; j < WA - 8; ++j) w[j] = w[j + 8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) w[WA - 8 + q] = nw[q];
+    }
+}
+
+// samples zeroed after the end of a window (fir_block over-read, see above)
+constexpr int FRONT_TAIL = 24;
+
+// LDS accesses of one wave are processed in order; the fences only stop the compiler from
+// moving a lane's LDS access across a hand-off between lanes of the same wave.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int FRONT_WAVE = 64;
+
+// history rows: HS = T-1 rounded up to 4 floats; lane b of a channel loads float4s b, b+nb, ...
+__host__ __device__ constexpr int hist_stride(int T) { return (T - 1 + 3) & ~3; }
+// float4s of a T-tap history row prefetched per lane (all of it when nb >= 8 lanes per channel;
+// with fewer lanes the rest is loaded when the window is filled)
+__host__ __device__ constexpr int hist_q(int T) { return (hist_stride(T) / 4 + 7) / 8; }
+
+// native 4-float vector: arrays of HIP's float4 (a struct with a union) loaded from global
+// memory defeat SROA and end up in scratch
+typedef float vf4 __attribute__((ext_vector_type(4)));
+
+// history row of a T-tap filter for channel cl: lane b of nb loads float4s b, b+nb, ... (HQ per lane)
+template <int T, int HQM>
+__device__ __forceinline__ void front_load_row(const float* row, int cl, int b, int nb, vf4 (&buf)[HQM])
+{
+    constexpr int hs4 = hist_stride(T) / 4, HQ = hist_q(T);
+    const vf4* h = (const vf4*)(row + (size_t)cl * (hs4 * 4));
+#pragma unroll
+    for (int i = 0; i < HQ; ++i)
+    {
+        const int q = b + nb * i;
+        buf[i] = h[q < hs4 ? q : hs4 - 1];
+    }
+}
+
+// One FIR pass's window: history row (registers) + NV new samples per lane, tail zeroed, and
+// the history row of the next call (window samples nnew .. nnew+T-2) written back to HBM.
+template <int T, int HQM>
+__device__ __forceinline__ void front_fill(float* W, float* row, int c, bool act, bool live, int b, int nb,
+                                           const vf4 (&buf)[HQM], const float* vals, int NV)
+{
+    constexpr int hs4 = hist_stride(T) / 4, HQ = hist_q(T);
+    const int nnew = nb * NV;
+    if (act)
+    {
+        // the row's pad floats (T-1 .. HS-1) land where the new samples go: written first,
+        // overwritten below (one wave's LDS accesses are processed in order)
+#pragma unroll
+        for (int i = 0; i < HQ; ++i)
+        {
+            const int q = b + nb * i;
+            if (q < hs4) *(vf4*)(W + 4 * q) = buf[i];
+        }
+        const vf4* h = (const vf4*)(row + (size_t)(live ? c : 0) * (hs4 * 4));
+        for (int q = b + nb * HQ; q < hs4; q += nb) *(vf4*)(W + 4 * q) = h[q];
+    }
+    wave_sync();
+    if (act)
+    {
+        for (int j = 0; j < NV; ++j) W[T - 1 + b * NV + j] = vals[j];
+        for (int t = b; t < FRONT_TAIL; t += nb) W[T - 1 + nnew + t] = 0.0f;
+    }
+    wave_sync();
+    float* ho = row + (size_t)c * (hs4 * 4);
+    for (int q = b; q < hs4; q += nb)
+    {
+        const float4 v = *(const float4*)(W + nnew + 4 * q);
+        if (live) *(float4*)(ho + 4 * q) = v;
+    }
+}
+
+// Lane -> (channel g, block b) of a front wave.  Window reads are ds_read_b128 at g*lw + b*S
+// (S = R floats), serviced in four 16-lane groups (MI355X_MICROARCH.md §LDS).  A run of
+// K = 64/S consecutive blocks of one channel covers one bank in four of every S; S/4
+// consecutive channels with lw = 4 (mod S) interleave into all 64 banks.  So each 16-lane group
+// gets S/4 (channel, run) pairs of consecutive channels: conflict-free.  Batches whose shape
+// does not allow that (nb not a power of two, too few channels or blocks) use g = l / nb.
+__host__ __device__ inline void front_lane(int l, int nb, int S, int& g, int& b)
+{
+    const int cpw = 64 / nb, K = 64 / S, cpg = S / 4;
+    if ((nb & (nb - 1)) || nb < K || cpw < cpg)
+    {
+        g = l / nb;
+        b = l % nb;
+        return;
+    }
+    // b128 groups: {0-3,12-15,20-27}, {4-11,16-19,28-31}, then the same + 32
+    const int h = l & 31;
+    int k, j;
+    if (h < 4) { k = 0; j = h; }
+    else if (h < 12) { k = 1; j = h - 4; }
+    else if (h < 16) { k = 0; j = h - 8; }
+    else if (h < 20) { k = 1; j = h - 8; }
+    else if (h < 28) { k = 0; j = h - 12; }
+    else { k = 1; j = h - 16; }
+    k += (l >> 5) * 2;
+    const int pr = k * cpg + j / K;          // (channel, run) pair
+    g = pr % cpw;
+    b = (pr / cpw) * K + j % K;
+}
+
+// arm_iir_lattice_f32 (CMSIS .../arm_iir_lattice_f32.c:348-447), one sample, S stages:
+// stage i of the next sample reads the g stage i+1 produced; the last reads the final f.
+template <int S>
+__device__ __forceinline__ float lattice_step(float x, float (&g)[S > 0 ? S : 1], const float* k, const float* v)
+{
+    float fcurr = x, fnext = 0.0f, acc = 0.0f;
+    float gn[S > 0 ? S : 1];
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+    {
+        const float gcurr = g[i];
+        fnext = fcurr - (k[i] * gcurr);
+        const float gnext = (fnext * k[i]) + gcurr;
+        acc += (gnext * v[i]);
+        gn[i] = gnext;
+        fcurr = fnext;
+    }
+    acc += (fnext * v[S]);
+#pragma unroll
+    for (int i = 0; i + 1 < S; ++i) g[i] = gn[i + 1];
+    if (S > 0) g[S - 1] = fnext;
+    return acc;
+}
+
+// arm_biquad_cascade_df1_f32 (.../arm_biquad_cascade_df1_f32.c:349-418), one stage
+__device__ __forceinline__ float biquad_step(float x, float& x1, float& x2, float& y1, float& y2, const float* c)
+{
+    const float acc = (c[0] * x) + (c[1] * x1) + (c[2] * x2) + (c[3] * y1) + (c[4] * y2);
+    x2 = x1; x1 = x; y2 = y1; y1 = acc;
+    return acc;
+}
+
+// ---- host: LDS bank-conflict model of the window reads ----
+// ds_read_b128 lane groups (one LDS cycle each, MI355X_MICROARCH.md §LDS); ds_read_b64: halves
+static const int kB128Groups[4][16] = {
+    { 0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27 },
+    { 4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31 },
+    { 32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59 },
+    { 36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63 } };
+
+// extra LDS cycles of one FIR window read for lane bases g*lw + b*stride (dwords), vec 4 or 2
+static inline int window_conflicts(int lw, int nb, int cpw, int R, int stride, int vec)
+{
+    int cost = 0;
+    const int ngroups = vec == 4 ? 4 : 2, glen = vec == 4 ? 16 : 32;
+    for (int gi = 0; gi < ngroups; ++gi)
+    {
+        int load[64] = { 0 };
+        for (int k = 0; k < glen; ++k)
+        {
+            const int l = vec == 4 ? kB128Groups[gi][k] : gi * 32 + k;
+            int g, b;
+            front_lane(l, nb, R, g, b);
+            if (g >= cpw) continue;
+            const int addr = g * lw + b * stride;
+            for (int d = 0; d < vec; ++d) load[(addr + d) & 63] += 1;
+        }
+        int mx = 0;
+        for (int k = 0; k < 64; ++k) mx = load[k] > mx ? load[k] : mx;
+        cost += mx - 1;
+    }
+    return cost;
+}
+
+#endif /* UHSDR_DSP_H */

@@ -34,6 +34,18 @@ typedef struct
 
 extern const uhsdr_filter_path_desc uhsdr_filter_paths[UHSDR_FILTER_PATH_NUM];
 
+typedef struct
+{
+    uint16_t stages;
+    const uint32_t* k;
+    const uint32_t* v;
+} uhsdr_lattice_desc;
+
+extern const uhsdr_lattice_desc uhsdr_tx_lattices[3];
+extern const uint32_t* const uhsdr_tx_hilbert_i;
+extern const uint32_t* const uhsdr_tx_hilbert_q;
+extern const int uhsdr_tx_hilbert_taps;
+
 int uhsdr_rx_mode_supported(const uhsdr_rx_plan* p);
 
 /* thread-local last error text for uhsdr_last_error() */

@@ -422,3 +422,130 @@ int uhsdr_rx_mode_supported(const uhsdr_rx_plan* p)
 const char* uhsdr_version(void) { return "uhsdr_amd 0.1 (gfx950)"; }
 int32_t uhsdr_sizeof_config(void) { return (int32_t)sizeof(uhsdr_rx_config); }
 int32_t uhsdr_sizeof_plan(void) { return (int32_t)sizeof(uhsdr_rx_plan); }
+
+/* ================================ transmit ================================ */
+
+/* defaults: drivers/ui/ui_configuration.c:91,140-141,161,211-213; codec.c:321 (mic gain 15) */
+void uhsdr_tx_config_default(uhsdr_tx_config* c)
+{
+    memset(c, 0, sizeof *c);
+    c->dmod_mode = UHSDR_DEMOD_USB;
+    c->iq_freq_mode = UHSDR_IQ_CONV_M12KHZ;
+    c->audio_source = UHSDR_TX_AUDIO_MIC;
+    c->mic_gain_mult = 15;                       /* MIC_GAIN_DEFAULT, hardware/uhsdr_board.h:142 */
+    c->mic_boost = 0;
+    c->comp_level = 2;                           /* TX_AUDIO_COMPRESSION_DEFAULT, audio_driver.h:467 */
+    c->alc_decay = 10;                           /* ALC_DECAY_DEFAULT, audio_driver.h:410 */
+    c->alc_postfilt_gain = 1;                    /* ALC_POSTFILT_GAIN_DEFAULT, audio_driver.h:415 */
+    c->tx_filter = 0;
+    c->bass_gain = 4;
+    c->treble_gain = 4;
+    c->filter_disable = 0;
+    c->power_factor = 0.5f;
+    c->gain_i = 1.0f;
+    c->gain_q = 1.0f;
+    c->phase_balance = 0.0f;
+}
+
+/* AudioManagement_CalcTxCompLevel preset table, audio_management.c:250-265 */
+static const uint8_t alc_params[13][2] = { { 1, 15 }, { 2, 12 }, { 4, 10 }, { 6, 9 }, { 7, 8 }, { 8, 7 }, { 10, 6 },
+                                           { 12, 5 }, { 15, 4 }, { 17, 3 }, { 20, 2 }, { 25, 1 }, { 25, 0 } };
+
+/* TxProcessor_Init / TxProcessor_Set / AudioFilter_SetTxHilbertFIR / AudioManagement_CalcTxCompLevel
+   (tx_processor.c:72-144, audio_filter.c:1231-1256, audio_management.c:15-19,267-290) and the
+   constant parts of TxProcessor_AudioBufferFill / _VoiceCompressor / _IqFinalProcessing */
+uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
+{
+    if (!cfg || !p) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
+    if (cfg->dmod_mode != UHSDR_DEMOD_USB && cfg->dmod_mode != UHSDR_DEMOD_LSB)
+    {
+        uhsdr_set_error("transmit mode %d: only SSB (USB/LSB) voice is implemented", cfg->dmod_mode);
+        return UHSDR_UNSUPPORTED;
+    }
+    if (cfg->audio_source < UHSDR_TX_AUDIO_MIC || cfg->audio_source > UHSDR_TX_AUDIO_LINEIN_R)
+    {
+        uhsdr_set_error("transmit audio source %d: codec sources (mic, line in) only", cfg->audio_source);
+        return UHSDR_UNSUPPORTED;
+    }
+    memset(p, 0, sizeof *p);
+    p->dmod_mode = cfg->dmod_mode;
+    p->lsb = cfg->dmod_mode == UHSDR_DEMOD_LSB;
+    p->audio_source = cfg->audio_source;
+
+    /* TxProcessor_AudioBufferFill gain (tx_processor.c:354-381) */
+    float gain_calc;
+    if (cfg->audio_source == UHSDR_TX_AUDIO_MIC)
+    {
+        gain_calc = (uint32_t)cfg->mic_gain_mult;
+        gain_calc /= 2;                                      /* MIC_GAIN_RESCALE, audio_driver.h:399 */
+        if (cfg->mic_boost > 0) gain_calc += 25.1;
+    }
+    else
+    {
+        gain_calc = 20;                                      /* LINE_IN_GAIN_RESCALE, audio_driver.h:398 */
+    }
+    gain_calc *= 0.0000152587890625;                         /* AUDIO_BIT_SCALE_DOWN, audio_driver.h:605 */
+    p->in_gain = gain_calc;
+    p->apply_in_gain = gain_calc != 1.0;
+
+    /* TxProcessor_FilterAudio: lattice band-pass unless disabled, biquads for codec sources */
+    p->run_lattice = !cfg->filter_disable;
+    p->run_biquad = 1;
+    const int sel = cfg->tx_filter == 2 ? 1 : cfg->tx_filter == 3 ? 2 : 0;   /* TENOR, BASS, default SOPRANO */
+    const uhsdr_lattice_desc* l = &uhsdr_tx_lattices[sel];
+    p->lat_stages = l->stages;
+    copy_bits(p->lat_k, l->k, l->stages);
+    copy_bits(p->lat_v, l->v, l->stages + 1);
+    float c[5];
+    calc_highshelf(c, 1700, 0.9, cfg->treble_gain, AUDIO_SAMPLE_RATE);
+    memcpy(p->biquad + 0, c, sizeof c);
+    calc_lowshelf(c, 300, 0.7, cfg->bass_gain, AUDIO_SAMPLE_RATE);
+    memcpy(p->biquad + 5, c, sizeof c);
+    memcpy(p->biquad + 10, biquad_passthrough, sizeof c);
+
+    /* voice compressor */
+    p->comp_on = cfg->comp_level > -1;
+    uint32_t postfilt, decay_var;
+    if (-1 < cfg->comp_level && cfg->comp_level < 13) { postfilt = alc_params[cfg->comp_level][0]; decay_var = alc_params[cfg->comp_level][1]; }
+    else if (cfg->comp_level == 13) { postfilt = cfg->alc_postfilt_gain; decay_var = cfg->alc_decay; }
+    else { postfilt = 4; decay_var = 10; }
+    p->postfilt_gain = ((float)postfilt) / 2.0 + 0.5;
+    p->alc_decay = exp10f(-((((float)decay_var) + 35.0) / 10.0));
+    p->alc_gain_scaling = 1.00;                              /* SSB_ALC_GAIN_CORRECTION, audio_driver.h:417 */
+
+    /* TX Hilbert pair, swapped for LSB (tx_processor.c:477-478) */
+    const int T = uhsdr_tx_hilbert_taps;
+    copy_bits(p->hilbert_i, p->lsb ? uhsdr_tx_hilbert_q : uhsdr_tx_hilbert_i, T);
+    copy_bits(p->hilbert_q, p->lsb ? uhsdr_tx_hilbert_i : uhsdr_tx_hilbert_q, T);
+
+    /* FreqShift by AudioDriver_GetTranslateFreq (tx_processor.c:484-487) */
+    switch (cfg->iq_freq_mode)
+    {
+    case UHSDR_IQ_CONV_P6KHZ: p->freq_shift_hz = 6000; break;
+    case UHSDR_IQ_CONV_M6KHZ: p->freq_shift_hz = -6000; break;
+    case UHSDR_IQ_CONV_P12KHZ: p->freq_shift_hz = 12000; break;
+    case UHSDR_IQ_CONV_M12KHZ: p->freq_shift_hz = -12000; break;
+    default: p->freq_shift_hz = 0; break;
+    }
+    if (p->freq_shift_hz != 0)
+    {
+        const int32_t conv = p->freq_shift_hz < 0 ? -p->freq_shift_hz : p->freq_shift_hz;
+        const float rate = conv / (float)IQ_SAMPLE_RATE;
+        p->shift_kind = (rate == 0.25) ? 1 : 2;
+        const double r = (2 * M_PI * conv) / (float)IQ_SAMPLE_RATE;
+        p->osc_cos = cos(r);
+        p->osc_sin = sin(r);
+        p->shift_up = !(p->freq_shift_hz > 0);
+    }
+
+    /* TxProcessor_IqFinalProcessing (tx_processor.c:282-330) with iq_gain_comp = SSB_GAIN_COMP */
+    float scaling = 1.133;                                   /* SSB_GAIN_COMP, audio_driver.h:419 */
+    scaling *= (1 << 16);                                    /* IQ_BIT_SCALE_UP */
+    p->final_i_gain = cfg->power_factor * cfg->gain_i * scaling;
+    p->final_q_gain = cfg->power_factor * cfg->gain_q * scaling;
+    p->phase_balance = cfg->phase_balance;
+    return UHSDR_OK;
+}
+
+int32_t uhsdr_sizeof_tx_config(void) { return (int32_t)sizeof(uhsdr_tx_config); }
+int32_t uhsdr_sizeof_tx_plan(void) { return (int32_t)sizeof(uhsdr_tx_plan); }

@@ -1,0 +1,403 @@
+// MI355X (gfx950) SSB transmit chain of the UHSDR firmware, batched over channels.
+//
+// One uhsdr_tx_process() call == N/32 consecutive TX-mode AudioDriver_I2SCallback invocations
+// (drivers/audio/audio_driver.c:3010-3036 -> TxProcessor_Run, drivers/audio/tx_processor.c:891-1078)
+// on each of C independent channels.  Two kernels:
+//
+//  tx_voice  (sequential per channel: lane == channel)
+//      codec frame -> f32, mic gain                     tx_processor.c:339-405
+//      TX band-pass lattice, bass/treble biquads        :416-429
+//      ALC compressor + 9-call look-ahead delay         :173-242
+//    -> compressed audio txa[C][N] (= adb.a_buffer[0]) in HBM; delay ring [10][32][C] in HBM
+//
+//  tx_iq     (time-parallel within a channel, the rx_front scheme)
+//      201-tap Hilbert pair (one LDS window, two FIR blocks)   :467-483
+//      FreqShift (Fs/4 exchange or recursive oscillator)       :484-487, freq_shift.c:219-334
+//      I/Q gain + phase, float -> int32 DAC frames             :282-330
+//
+// Arithmetic: the reference's binary32 operation sequence (-ffp-contract=off): outputs are
+// bit-identical to the firmware built for x86 (tests/test_gpu_tx.py).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
+#include <math.h>
+#include "uhsdr_internal.h"
+#include "uhsdr_dsp.h"
+
+#define TX_DELAY_SLOTS (UHSDR_TX_DELAY / BLK)   // 10 blocks of 32
+#define TX_T UHSDR_TX_HILBERT_TAPS
+
+struct TxVoiceArgs
+{
+    const uhsdr_tx_plan* plan;
+    const int2* audio;      // [C][N] codec frames {l, r}
+    float* txa;             // [C][N] compressed audio out
+    float* a0;              // optional copy of txa for the caller (adb.a_buffer[0])
+    float* lat;             // [10][C]
+    float* bq;              // [12][C]
+    float* alc;             // [C]
+    float* delay;           // [10][32][C]
+    int C, N;
+    int delay_phase;        // alc_delay_inbuf / 32 before this launch
+};
+
+// TxProcessor_AudioBufferFill + _FilterAudio + _VoiceCompressor, one lane per channel
+template <int S>
+__global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
+{
+    const uhsdr_tx_plan* __restrict__ P = a.plan;
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    const bool live = c < a.C;
+    const int cl = live ? c : a.C - 1;
+    const int C = a.C;
+    float lk[S], lv[S + 1], g[S], bc[15], bq[12];
+#pragma unroll
+    for (int i = 0; i < S; ++i) lk[i] = P->lat_k[i];
+#pragma unroll
+    for (int i = 0; i <= S; ++i) lv[i] = P->lat_v[i];
+#pragma unroll
+    for (int i = 0; i < 15; ++i) bc[i] = P->biquad[i];
+#pragma unroll
+    for (int i = 0; i < S; ++i) g[i] = a.lat[i * C + cl];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) bq[i] = a.bq[i * C + cl];
+    float alc_val = a.alc[cl];
+    const bool right = P->audio_source == UHSDR_TX_AUDIO_LINEIN_R;
+    const bool apply_gain = P->apply_in_gain, run_lat = P->run_lattice, run_bq = P->run_biquad, comp = P->comp_on;
+    const float in_gain = P->in_gain, post = P->postfilt_gain, decay = P->alc_decay, gscale = P->alc_gain_scaling;
+    const int calls = a.N / BLK;
+    for (int k = 0; k < calls; ++k)
+    {
+        float x[BLK];
+        const int4* src = (const int4*)(a.audio + (size_t)cl * a.N + k * BLK);
+#pragma unroll
+        for (int j = 0; j < BLK / 2; ++j)
+        {
+            const int4 v = src[j];
+            x[2 * j] = (float)(right ? v.y : v.x);
+            x[2 * j + 1] = (float)(right ? v.w : v.z);
+        }
+        const int slot_in = (a.delay_phase + k + 1) % TX_DELAY_SLOTS;   // alc_delay_inbuf after += 32
+        const int slot_out = (a.delay_phase + k + 2) % TX_DELAY_SLOTS;  // alc_delay_outbuf
+        float dly[BLK];
+        if (comp)
+        {
+            const float* dr = a.delay + ((size_t)slot_out * BLK) * C + cl;
+#pragma unroll
+            for (int m = 0; m < BLK; ++m) dly[m] = dr[(size_t)m * C];
+        }
+#pragma unroll
+        for (int m = 0; m < BLK; ++m)
+        {
+            float v = x[m];
+            if (apply_gain) v = v * in_gain;
+            if (run_lat) v = lattice_step<S>(v, g, lk, lv);
+            if (run_bq)
+            {
+#pragma unroll
+                for (int st = 0; st < 3; ++st)
+                    v = biquad_step(v, bq[4 * st], bq[4 * st + 1], bq[4 * st + 2], bq[4 * st + 3], bc + 5 * st);
+            }
+            x[m] = v;
+        }
+        if (comp)
+        {
+            float* dw = a.delay + ((size_t)slot_in * BLK) * C + c;
+#pragma unroll
+            for (int m = 0; m < BLK; ++m)
+            {
+                const float v = x[m] * post;
+                // ALC (tx_processor.c:197-221)
+                const float alc_var = (float)((double)(fabsf(v * alc_val) / 30000) - 1.0);
+                if (alc_var < 0)
+                {
+                    alc_val -= alc_val * decay * alc_var;
+                }
+                else
+                {
+                    alc_val = (float)((double)alc_val - (double)alc_val * 0.1 * (double)alc_var);
+                    if ((double)alc_val < 0.001) alc_val = 0.001f;
+                }
+                if (alc_val > 1) alc_val = 1;
+                if (live) dw[(size_t)m * C] = v;                        // into the delay buffer
+                x[m] = dly[m] * (alc_val * gscale);                     // delayed audio x ALC gain
+            }
+        }
+        if (live)
+        {
+            float* dst = a.txa + (size_t)c * a.N + k * BLK;
+            float* d0 = a.a0 ? a.a0 + (size_t)c * a.N + k * BLK : nullptr;
+#pragma unroll
+            for (int m = 0; m < BLK; m += 4)
+            {
+                const float4 v = make_float4(x[m], x[m + 1], x[m + 2], x[m + 3]);
+                *(float4*)(dst + m) = v;
+                if (d0) *(float4*)(d0 + m) = v;
+            }
+        }
+    }
+    if (live)
+    {
+#pragma unroll
+        for (int i = 0; i < S; ++i) a.lat[i * C + c] = g[i];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) a.bq[i * C + c] = bq[i];
+        a.alc[c] = alc_val;
+    }
+}
+
+struct TxIqArgs
+{
+    const uhsdr_tx_plan* plan;
+    const float* txa;        // [C][ld] compressed audio, frame 0 of this launch
+    float* hist;             // [C][200] Hilbert history (shared by the I and Q filters: same input)
+    const float* osc_in;     // [2] oscillator {I, Q} at launch start
+    float* osc_out;          // [2]
+    int2* iq;                // [C][ld] DAC frames, frame 0 of this launch
+    int C, N, ld, lw;
+};
+
+__device__ __forceinline__ int tx_to_int32(float f)
+{
+    return (f > -2147483904.0f && f < 2147483648.0f) ? (int)f : INT32_MIN;
+}
+
+template <int R>
+__global__ void __launch_bounds__(64) tx_iq(TxIqArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const uhsdr_tx_plan* __restrict__ P = a.plan;
+    const int N = a.N, C = a.C;
+    const int lane = threadIdx.x;
+    const int nb = N / R;
+    const int CPW = 64 / nb;
+    int g, b;
+    front_lane(lane, nb, R, g, b);
+    const int c = blockIdx.x * CPW + g;
+    const bool act = g < CPW;
+    const bool live = act && c < C;
+    const int gs = act ? g : 0;
+    const int cl = c < C ? c : C - 1;
+    constexpr int HQ = hist_q(TX_T);
+    float* W = smem + gs * a.lw;
+    float* osc = smem + CPW * a.lw;                 // [2N] oscillator trajectory (shift kind 2)
+
+    float xv[R];
+    {
+        const float4* src = (const float4*)(a.txa + (size_t)cl * a.ld + b * R);
+#pragma unroll
+        for (int j = 0; j < R / 4; ++j)
+        {
+            const float4 v = src[j];
+            xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
+        }
+    }
+    vf4 hA[HQ];
+    front_load_row<TX_T>(a.hist, cl, b, nb, hA);
+    const int shift = P->freq_shift_hz != 0 ? P->shift_kind : 0;
+    if (shift == 2 && lane == 0)
+    {
+        const float oc = P->osc_cos, os = P->osc_sin;
+        float vi = a.osc_in[0], vq = a.osc_in[1];
+        for (int n = 0; n < N; ++n)
+        {
+            const float oq = (vq * oc) - (vi * os);
+            const float oi = (vi * oc) + (vq * os);
+            osc[2 * n] = oq;
+            osc[2 * n + 1] = oi;
+            vq = oq; vi = oi;
+            if ((n & (BLK - 1)) == BLK - 1)
+            {
+                const float gn = (3 - ((vq * vq) + (vi * vi))) / 2;
+                vq = gn * vq; vi = gn * vi;
+            }
+        }
+        if (blockIdx.x == 0) { a.osc_out[0] = vi; a.osc_out[1] = vq; }
+    }
+    front_fill<TX_T>(W, a.hist, c, act, live, b, nb, hA, xv, R);
+    float hi[R], hq[R];
+    fir_block<TX_T, R, 1>(W + b * R, as_taps(P->hilbert_i), hi);
+    fir_block<TX_T, R, 1>(W + b * R, as_taps(P->hilbert_q), hq);
+    const bool up = P->shift_up;
+    const float gi = P->final_i_gain, gq = P->final_q_gain, ph = P->phase_balance;
+    int out[2 * R];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+    {
+        const int n = b * R + r;
+        float I = hi[r], Q = hq[r];
+        if (shift)
+        {
+            float ib = up ? I : Q, qb = up ? Q : I;
+            if (shift == 1)
+            {
+                const float iv = ib, qv = qb;
+                switch (n & 3)
+                {
+                case 0: break;
+                case 1: ib = qv; qb = -iv; break;
+                case 2: ib = -iv; qb = -qv; break;
+                default: ib = -qv; qb = iv; break;
+                }
+            }
+            else
+            {
+                const float oq = osc[2 * n], oi = osc[2 * n + 1];
+                const float qt = qb, it = ib;
+                qb = (qt * oq) - (it * oi);
+                ib = (it * oq) + (qt * oi);
+            }
+            I = up ? ib : qb;
+            Q = up ? qb : ib;
+        }
+        I = I * gi;
+        Q = Q * gq;
+        if (ph < 0) { const float e = I * ph; Q = Q + e; }
+        else if (ph > 0) { const float e = Q * ph; I = I + e; }
+        out[2 * r] = tx_to_int32(I);
+        out[2 * r + 1] = tx_to_int32(Q);
+    }
+    if (live)
+    {
+        int4* dst = (int4*)(a.iq + (size_t)c * a.ld + b * R);
+#pragma unroll
+        for (int j = 0; j < R / 2; ++j) dst[j] = make_int4(out[4 * j], out[4 * j + 1], out[4 * j + 2], out[4 * j + 3]);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// host runtime
+
+struct uhsdr_tx_s
+{
+    uhsdr_tx_plan plan;
+    uhsdr_tx_plan* d_plan;
+    int C, N, Nf, R, lw;
+    hipStream_t stream;
+    float *lat, *bq, *alc, *delay, *hist, *osc, *txa;
+    void* arena;
+    size_t arena_bytes;
+    long long calls_done, iq_launches;
+};
+
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { uhsdr_set_error("%s: %s", #x, hipGetErrorString(e_)); return UHSDR_DEVICE_ERROR; } } while (0)
+
+static int tx_pitch(int Nf, int R)
+{
+    const int nb = Nf / R, cpw = 64 / nb;
+    const int need = (TX_T - 1 + Nf + FRONT_TAIL + 3) & ~3;
+    int best = need, best_cost = 1 << 30;
+    for (int lw = need; lw < need + 64; lw += 4)
+    {
+        const int cost = window_conflicts(lw, nb, cpw, R, R, 4);
+        if (cost < best_cost) { best_cost = cost; best = lw; }
+    }
+    return best;
+}
+
+extern "C" uhsdr_status uhsdr_tx_reset(uhsdr_tx_handle h)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    HIPCHK(hipMemsetAsync(h->arena, 0, h->arena_bytes, h->stream));
+    // ads.alc_val = 1 (TxProcessor_Init, tx_processor.c:137); oscillator {I=0, Q=1} (freq_shift.c:48-49)
+    float* ones = (float*)malloc(sizeof(float) * h->C);
+    for (int i = 0; i < h->C; ++i) ones[i] = 1.0f;
+    HIPCHK(hipMemcpyAsync(h->alc, ones, sizeof(float) * h->C, hipMemcpyHostToDevice, h->stream));
+    const float osc0[4] = { 0.0f, 1.0f, 0.0f, 1.0f };
+    HIPCHK(hipMemcpyAsync(h->osc, osc0, sizeof osc0, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    free(ones);
+    h->calls_done = 0;
+    h->iq_launches = 0;
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_tx_create(const uhsdr_tx_config* cfg, int32_t C, int32_t N, void* stream,
+                                        uhsdr_tx_handle* out)
+{
+    if (!cfg || !out || C <= 0 || N <= 0) { uhsdr_set_error("bad argument"); return UHSDR_ARGUMENT_ERROR; }
+    if (N % BLK) { uhsdr_set_error("frames_per_call %d not a multiple of %d", N, BLK); return UHSDR_LENGTH_ERROR; }
+    *out = nullptr;
+    uhsdr_tx_s* h = (uhsdr_tx_s*)calloc(1, sizeof(uhsdr_tx_s));
+    uhsdr_status st = uhsdr_tx_plan_build(cfg, &h->plan);
+    if (st != UHSDR_OK) { free(h); return st; }
+    if (h->plan.lat_stages != 10) { free(h); uhsdr_set_error("TX lattice with %d stages", h->plan.lat_stages); return UHSDR_UNSUPPORTED; }
+    h->C = C; h->N = N;
+    h->stream = (hipStream_t)stream;
+    h->R = 8;
+    h->Nf = N < 64 * h->R ? N : 64 * h->R;
+    if (h->Nf / h->R < 4) { h->R = 8; }
+    if (N % h->Nf || h->Nf % h->R || h->Nf / h->R < 4)
+    { free(h); uhsdr_set_error("frames_per_call %d: need a multiple of 32 of at least 32", N); return UHSDR_LENGTH_ERROR; }
+    h->lw = tx_pitch(h->Nf, h->R);
+    size_t fl = 0;
+    auto take = [&](size_t n) { size_t o = fl; fl += (n + 63) & ~(size_t)63; return o; };
+    const size_t o_lat = take((size_t)10 * C), o_bq = take((size_t)12 * C), o_alc = take((size_t)C);
+    const size_t o_dly = take((size_t)UHSDR_TX_DELAY * C), o_hist = take((size_t)hist_stride(TX_T) * C);
+    const size_t o_osc = take(4), o_txa = take((size_t)C * N);
+    h->arena_bytes = fl * sizeof(float);
+    if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess || hipMalloc((void**)&h->d_plan, sizeof(uhsdr_tx_plan)) != hipSuccess)
+    {
+        uhsdr_set_error("hipMalloc failed (%zu bytes state)", h->arena_bytes);
+        if (h->arena) (void)hipFree(h->arena);
+        free(h);
+        return UHSDR_DEVICE_ERROR;
+    }
+    float* A = (float*)h->arena;
+    h->lat = A + o_lat; h->bq = A + o_bq; h->alc = A + o_alc; h->delay = A + o_dly;
+    h->hist = A + o_hist; h->osc = A + o_osc; h->txa = A + o_txa;
+    if (hipMemcpy(h->d_plan, &h->plan, sizeof(uhsdr_tx_plan), hipMemcpyHostToDevice) != hipSuccess)
+    {
+        uhsdr_set_error("plan upload failed");
+        return UHSDR_DEVICE_ERROR;
+    }
+    *out = h;
+    return uhsdr_tx_reset(h);
+}
+
+extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio, int32_t* iq, float* a0)
+{
+    if (!h || !audio || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
+    TxVoiceArgs va;
+    va.plan = h->d_plan; va.audio = (const int2*)audio; va.txa = h->txa; va.a0 = a0;
+    va.lat = h->lat; va.bq = h->bq; va.alc = h->alc; va.delay = h->delay;
+    va.C = h->C; va.N = h->N;
+    va.delay_phase = (int)(h->calls_done % TX_DELAY_SLOTS);
+    hipLaunchKernelGGL(tx_voice<10>, dim3((h->C + 63) / 64), dim3(64), 0, h->stream, va);
+    HIPCHK(hipGetLastError());
+    const int cpw = 64 / (h->Nf / h->R);
+    const size_t lds = sizeof(float) * ((size_t)cpw * h->lw + (h->plan.shift_kind == 2 ? 2 * h->Nf : 0));
+    for (int f0 = 0; f0 < h->N; f0 += h->Nf)
+    {
+        TxIqArgs ia;
+        ia.plan = h->d_plan; ia.txa = h->txa + f0; ia.hist = h->hist;
+        ia.osc_in = h->osc + 2 * (h->iq_launches & 1);
+        ia.osc_out = h->osc + 2 * ((h->iq_launches + 1) & 1);
+        ia.iq = (int2*)iq + f0;
+        ia.C = h->C; ia.N = h->Nf; ia.ld = h->N; ia.lw = h->lw;
+        hipLaunchKernelGGL(tx_iq<8>, dim3((h->C + cpw - 1) / cpw), dim3(64), lds, h->stream, ia);
+        HIPCHK(hipGetLastError());
+        h->iq_launches += 1;
+    }
+    h->calls_done += h->N / BLK;
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_tx_get_plan(uhsdr_tx_handle h, uhsdr_tx_plan* plan)
+{
+    if (!h || !plan) return UHSDR_ARGUMENT_ERROR;
+    memcpy(plan, &h->plan, sizeof *plan);
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_tx_destroy(uhsdr_tx_handle h)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipFree(h->arena);
+    (void)hipFree(h->d_plan);
+    free(h);
+    return UHSDR_OK;
+}

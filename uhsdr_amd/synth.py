@@ -143,6 +143,19 @@ def fm_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier
     return _frames(i_sig, q_sig)
 
 
+def tx_audio(channels, start: int, nframes: int, kind: str = "ssb2tone", noise_sigma: float = 10.0):
+    """C4 SSB-TX input: the codec's microphone frames (AudioSample_t {int32 l, r}, the sample in
+    both channels as (int16) value << 16) carrying a per-channel two-tone audio signal."""
+    channels = np.asarray(channels, dtype=np.int64)
+    f1, f2, a1, a2, p1, p2 = channel_params(channels, kind)
+    n = np.arange(start, start + nframes, dtype=np.float64)[None, :]
+    s = (a1[:, None] * np.cos(2.0 * np.pi * f1[:, None] / FS * n + p1[:, None])
+         + a2[:, None] * np.cos(2.0 * np.pi * f2[:, None] / FS * n + p2[:, None]))
+    if noise_sigma > 0:
+        s = s + _noise(channels, start, nframes, noise_sigma)[0]
+    return _frames(s, s)
+
+
 def ssb_iq_torch(c0: int, nch: int, start: int, nframes: int, device, noise_sigma: float = 30.0):
     """Same signal model as ``ssb_iq`` (kind "ssb2tone"), generated on the GPU for large
     benchmark batches: channels c0 .. c0+nch-1.  Tone parameters and noise come from the

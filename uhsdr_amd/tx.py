@@ -1,0 +1,51 @@
+"""Host-side mirror of the reference SSB transmit interface for the batched device chain.
+
+    chain = TxChain(config, channels=C, frames=N)   # TxProcessor_Init + TxProcessor_Set
+    chain.process(audio_dev, iq_dev, a0_dev)         # N/32 x TX-mode AudioDriver_I2SCallback
+
+``audio`` is [C][N][2] int32 AudioSample_t codec frames, ``iq`` [C][N][2] int32 IqSample_t DAC
+frames, ``a0`` optional [C][N] f32 compressed audio (adb.a_buffer[0]).  All arithmetic runs in
+libuhsdr_amd.so (uhsdr_tx.hip); torch tensors only provide device memory.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import _abi
+
+
+class TxChain:
+    def __init__(self, config: _abi.TxConfig | None = None, channels: int = 1, frames: int = 32,
+                 stream: int | None = None, **overrides):
+        self.lib = _abi.load()
+        self.config = config if config is not None else _abi.default_tx_config(**overrides)
+        self.channels, self.frames = int(channels), int(frames)
+        h = C.c_void_p()
+        _abi.check(self.lib.uhsdr_tx_create(C.byref(self.config), self.channels, self.frames,
+                                            C.c_void_p(stream or 0), C.byref(h)), "uhsdr_tx_create")
+        self.handle = h
+        self.plan = _abi.TxPlan()
+        _abi.check(self.lib.uhsdr_tx_get_plan(h, C.byref(self.plan)), "uhsdr_tx_get_plan")
+
+    def reset(self) -> None:
+        _abi.check(self.lib.uhsdr_tx_reset(self.handle), "uhsdr_tx_reset")
+
+    def process(self, audio, iq, a0=None) -> None:
+        want = (self.channels, self.frames, 2)
+        if tuple(audio.shape) != want or tuple(iq.shape) != want:
+            raise ValueError(f"audio / iq must be {want}")
+        if a0 is not None and tuple(a0.shape) != want[:2]:
+            raise ValueError(f"a0 must be {want[:2]}")
+        _abi.check(self.lib.uhsdr_tx_process(self.handle, C.c_void_p(audio.data_ptr()), C.c_void_p(iq.data_ptr()),
+                                             C.c_void_p(a0.data_ptr() if a0 is not None else 0)), "uhsdr_tx_process")
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.uhsdr_tx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

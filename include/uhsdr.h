@@ -280,6 +280,67 @@ uhsdr_status uhsdr_tx_destroy(uhsdr_tx_handle h);
 int32_t      uhsdr_sizeof_tx_config(void);
 int32_t      uhsdr_sizeof_tx_plan(void);
 
+/* ---- spectrum display ----
+ * Replaces the no-zoom producer AudioDriver_SpectrumNoZoomProcessSamples (audio_driver.c:
+ * 1811-1851: I/Q-corrected samples into an interleaved [Q, I] ring) and the consumer
+ * UiSpectrum_RedrawSpectrum states 0-3 (drivers/ui/lcd/ui_spectrum.c:1350-1446): Hann window,
+ * arm_cfft_f32 (CMSIS TransformFunctions/arm_cfft_f32.c:574-632), arm_cmplx_mag_f32 and the IIR
+ * average clamped at 1.  Batched semantics: every fft_len consecutive input samples of a channel
+ * (counted from reset) form one display frame; the firmware's main loop snapshots the ring at
+ * arbitrary times, the batch takes it exactly when fft_len new samples have arrived.
+ * The I/Q correction runs on the handle's own copy of the auto-correction state (it depends only
+ * on the input), so a spectrum handle beside an RX handle sees what the firmware's ring sees.
+ */
+#define UHSDR_SPECTRUM_MAX_LEN 1024
+#define UHSDR_SPECTRUM_MAX_BITREV 1800   /* ARMBITREVINDEXTABLE1024_TABLE_LENGTH, arm_common_tables.h:96 */
+
+typedef struct uhsdr_spectrum_config
+{
+    int32_t fft_len;              /* 256 (320x240), 512 (480x320 / 800x480: ui_spectrum.c:966-984) or 1024 */
+    int32_t spectrum_filter;      /* ts.spectrum_filter 1..20, default 4 (ui_spectrum.h:143-145) */
+    int32_t iq_auto_correction;   /* ts.iq_auto_correction, as uhsdr_rx_config */
+    float   iq_gain_i, iq_gain_q; /* ts.rx_adj_gain_var.i / .q */
+    float   iq_phase_balance;     /* ads.iq_phase_balance_rx */
+    int32_t reserved[10];
+} uhsdr_spectrum_config;
+
+typedef struct uhsdr_spectrum_plan
+{
+    int32_t fft_len;
+    int32_t window_formula;       /* 0: x *= window[i] (von_Hann_512/1024 tables, USE_PREDEFINED_WINDOW_DATA);
+                                     1: x = 0.5 * ((window[i]) * x) with window = 1 - arm_cos_f32(2 pi i / (2L - 1))
+                                        (ui_spectrum.c:403-406; no 2048-float table exists) */
+    int32_t iq_auto_correction;
+    float   iq_gain_i, iq_gain_q, iq_phase_balance;
+    float   filt_factor;          /* 1 / (float)spectrum_filter (ui_spectrum.c:1434) */
+    int32_t bitrev_len;           /* S->bitRevLength */
+    float   window[2 * UHSDR_SPECTRUM_MAX_LEN];    /* per float of the interleaved [Q, I] frame */
+    float   twiddle[2 * UHSDR_SPECTRUM_MAX_LEN];   /* twiddleCoef_<L> (arm_common_tables.c) */
+    uint16_t bitrev[UHSDR_SPECTRUM_MAX_BITREV];    /* armBitRevIndexTable<L>: byte-offset swap pairs */
+    uint16_t perm[UHSDR_SPECTRUM_MAX_LEN];         /* bin k of the output = butterfly result perm[k] */
+    int32_t reserved[16];
+} uhsdr_spectrum_plan;
+
+typedef struct uhsdr_spectrum_s* uhsdr_spectrum_handle;
+
+void         uhsdr_spectrum_config_default(uhsdr_spectrum_config* cfg);
+uhsdr_status uhsdr_spectrum_plan_build(const uhsdr_spectrum_config* cfg, uhsdr_spectrum_plan* plan);
+/* frames_per_call N: a multiple of 32 and either a multiple of fft_len (N/L display frames per
+   call) or a divisor of it (one frame every L/N calls); otherwise UHSDR_LENGTH_ERROR. */
+uhsdr_status uhsdr_spectrum_create(const uhsdr_spectrum_config* cfg, int32_t num_channels, int32_t frames_per_call,
+                                   void* stream, uhsdr_spectrum_handle* out);
+uhsdr_status uhsdr_spectrum_reset(uhsdr_spectrum_handle h);
+/* iq: device IqSample_t [C][N][2] int32 (the RX input).  mag / avg: optional device f32
+   [C][F][L], F = max(1, N/L): per completed frame sd.FFT_MagData and sd.FFT_AVGData (natural
+   FFT bin order, as arm_cfft_f32 leaves them).  *frames (optional) = frames completed by this
+   call (0 .. F); nothing is written to mag / avg when it is 0. */
+uhsdr_status uhsdr_spectrum_process(uhsdr_spectrum_handle h, const int32_t* iq, float* mag, float* avg,
+                                    int32_t* frames);
+uhsdr_status uhsdr_spectrum_get_plan(uhsdr_spectrum_handle h, uhsdr_spectrum_plan* plan);
+uhsdr_status uhsdr_spectrum_destroy(uhsdr_spectrum_handle h);
+int32_t      uhsdr_sizeof_spectrum_config(void);
+int32_t      uhsdr_sizeof_spectrum_plan(void);
+
 /* ---- diagnostics ---- */
 const char*  uhsdr_version(void);
 /* sizeof(uhsdr_rx_config), sizeof(uhsdr_rx_plan): lets FFI bindings check their layouts */

@@ -33,6 +33,11 @@ def load():
         lib.uo_tx_state_init.argtypes = [C.c_void_p, C.c_void_p]
         lib.uo_tx_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                             C.c_void_p, C.c_void_p, C.c_int]
+        lib.uo_spec_state_size.restype = C.c_size_t
+        lib.uo_spec_state_init.argtypes = [C.c_void_p, C.c_void_p]
+        lib.uo_cfft.argtypes = [C.c_void_p, C.c_void_p]
+        lib.uo_spec_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                              C.c_void_p, C.c_void_p, C.c_int]
         _lib = lib
     return _lib
 
@@ -86,3 +91,37 @@ class OracleTx:
         if st != 0:
             raise RuntimeError(f"uo_tx_process_batch status {st}")
         return iq, a0
+
+
+class OracleSpectrum:
+    """C channels of the spectrum display path (producer ring + UiSpectrum states 0-3) on the CPU."""
+
+    def __init__(self, plan, channels: int):
+        self.lib = load()
+        self.plan = plan
+        self.channels = channels
+        self.ssize = self.lib.uo_spec_state_size()
+        self.states = (C.c_char * (self.ssize * channels))()
+        for c in range(channels):
+            self.lib.uo_spec_state_init(C.byref(plan), C.byref(self.states, c * self.ssize))
+
+    def process(self, iq: np.ndarray, threads: int = 1):
+        """-> (mag, avg) [C][F][L] for the F frames this call completed"""
+        iq = np.ascontiguousarray(iq, dtype=np.int32)
+        Cn, n, _ = iq.shape
+        assert Cn == self.channels
+        L = self.plan.fft_len
+        fmax = max(1, n // L)
+        mag = np.zeros((Cn, fmax, L), np.float32)
+        avg = np.zeros((Cn, fmax, L), np.float32)
+        f = self.lib.uo_spec_process_batch(C.byref(self.plan), self.states, Cn, iq.ctypes.data_as(C.c_void_p), n,
+                                           mag.ctypes.data_as(C.c_void_p), avg.ctypes.data_as(C.c_void_p), threads)
+        if f < 0:
+            raise RuntimeError(f"uo_spec_process_batch: {f}")
+        return mag[:, :f], avg[:, :f]
+
+    def cfft(self, x: np.ndarray) -> np.ndarray:
+        """arm_cfft_f32(S, x, 0, 1) restated, on one interleaved frame"""
+        x = np.ascontiguousarray(x, dtype=np.float32).copy()
+        self.lib.uo_cfft(C.byref(self.plan), x.ctypes.data_as(C.c_void_p))
+        return x

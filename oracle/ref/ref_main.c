@@ -51,6 +51,11 @@ extern arm_fir_instance_f32 Fir_Tx_Hilbert_I, Fir_Tx_Hilbert_Q;
 void oracle_ref_agc_dump(void);
 unsigned long oracle_harness_layout(void);
 unsigned long oracle_driver_layout(void);
+int ref_spec_ring_len(int L);
+void ref_spec_setup(int L);
+void ref_spec_snapshot(float* out);
+void ref_spec_frame(int L, int spectrum_filter, const float* ring, float* mag, float* avg);
+void ref_spec_dump(void);
 extern arm_fir_instance_f32 Fir_Rx_Hilbert_I, Fir_Rx_Hilbert_Q;
 extern arm_fir_decimate_instance_f32 DECIMATE_RX_I, DECIMATE_RX_Q;
 
@@ -161,6 +166,7 @@ int main(int argc, char** argv)
     }
     const char* dump = arg(argc, argv, "dump", "");
     if (strcmp(dump, "paths") == 0) { dump_paths(); return 0; }
+    if (strcmp(dump, "spectrum") == 0) { ref_spec_dump(); return 0; }
 
     const int mode = (int)iarg(argc, argv, "mode", DEMOD_USB);
     const int path = (int)iarg(argc, argv, "path", 0);
@@ -204,7 +210,9 @@ int main(int argc, char** argv)
     agc_wdsp_conf.tau_decay[3] = 250;
     agc_wdsp_conf.tau_decay[4] = 50;
     agc_wdsp_conf.tau_hang_decay = 500;
-    sd.fft_iq_len = 0;          /* spectrum tap off for the audio oracle */
+    sd.fft_iq_len = 0;          /* spectrum tap off unless spec=L (ref_spectrum.c) */
+    const int spec = (int)iarg(argc, argv, "spec", 0);
+    const int spec_filter = (int)iarg(argc, argv, "specfilt", 4);   /* SPECTRUM_FILTER_DEFAULT */
     /* transmit settings (hardware/uhsdr_board.h:301-460, defaults ui_configuration.c) */
     const int tx = (int)iarg(argc, argv, "tx", 0);
     ts.tx_mic_gain_mult = iarg(argc, argv, "micmult", 15);
@@ -242,6 +250,15 @@ int main(int argc, char** argv)
     fclose(f);
 
     IqSample_t blk[IQ_BLOCK_SIZE];
+    float* stream = NULL;
+    int ring = 0;
+    if (spec)
+    {
+        if ((spec != 256 && spec != 512 && spec != 1024) || n % spec) { fprintf(stderr, "spec=256|512|1024 dividing n\n"); return 2; }
+        ring = ref_spec_ring_len(spec);
+        ref_spec_setup(spec);
+        stream = calloc(2 * n, sizeof(float));
+    }
     if (tx)
     {
         /* TX: the codec's audio frames in, IQ frames out (AudioDriver_I2SCallback TX branch,
@@ -263,6 +280,24 @@ int main(int argc, char** argv)
         memcpy(blk, iq + off, sizeof(IqSample_t) * block);   /* the ISR's DMA half-buffer */
         AudioDriver_I2SCallback(dst + off, blk, NULL, block);
         memcpy(a1 + off, adb.a_buffer[1], sizeof(float) * block);
+        if (spec && (off + block) % (ring / 2) == 0)       /* the ring holds ring/2 new samples */
+            ref_spec_snapshot(stream + 2 * (off + block - ring / 2));
+    }
+    if (spec)
+    {
+        const char* out_mag = arg(argc, argv, "out_mag", NULL);
+        const char* out_avg = arg(argc, argv, "out_avg", NULL);
+        float* mag = calloc(n, sizeof(float));
+        float* avgs = calloc(n, sizeof(float));
+        float avg[1024] = { 0 };                /* sd.FFT_AVGData starts zeroed (global) */
+        for (long fr = 0; fr < n / spec; ++fr)
+        {
+            ref_spec_frame(spec, spec_filter, stream + 2 * fr * spec, mag + fr * spec, avg);
+            memcpy(avgs + fr * spec, avg, sizeof(float) * spec);
+        }
+        if (out_mag) { f = fopen(out_mag, "wb"); fwrite(mag, sizeof(float), n, f); fclose(f); }
+        if (out_avg) { f = fopen(out_avg, "wb"); fwrite(avgs, sizeof(float), n, f); fclose(f); }
+        free(mag); free(avgs); free(stream);
     }
     if (out_a) { f = fopen(out_a, "wb"); fwrite(a1, sizeof(float), n, f); fclose(f); }
     if (out_dst) { f = fopen(out_dst, "wb"); fwrite(dst, sizeof(AudioSample_t), n, f); fclose(f); }

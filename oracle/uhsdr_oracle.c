@@ -756,3 +756,335 @@ int uo_tx_process_batch(const uhsdr_tx_plan* p, uo_tx_state* states, int C, cons
         for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
     return UHSDR_OK;
 }
+
+/* ============================= spectrum display ============================= */
+
+size_t uo_spec_state_size(void) { return sizeof(uo_spec_state); }
+
+void uo_spec_state_init(const uhsdr_spectrum_plan* p, uo_spec_state* s)
+{
+    (void)p;
+    memset(s, 0, sizeof *s);
+}
+
+/* 8-point DFT core of arm_radix8_butterfly_f32 (CMSIS TransformFunctions/arm_cfft_radix8_f32.c:
+   130-383) on the complex values at x[2*(base + k*stride)], k = 0..7.  Both of the reference's
+   loops (the twiddle-free first group :149-221 and the twiddled groups :228-372) form the same
+   eight intermediate values X_k with the same operation sequence; the twiddled groups then
+   rotate X_k (k >= 1) by twiddle[k * tstep] as (c*re + s*im, c*im - s*re).  tstep 0: no rotation. */
+static void cfft_radix8(float* x, int base, int stride, const float* tw, int tstep)
+{
+    const float C81 = 0.70710678118f;
+    float re[8], im[8];
+    for (int k = 0; k < 8; k++)
+    {
+        re[k] = x[2 * (base + k * stride)];
+        im[k] = x[2 * (base + k * stride) + 1];
+    }
+    float sr[4], dr[4], si[4], di[4];
+    for (int k = 0; k < 4; k++)
+    {
+        sr[k] = re[k] + re[k + 4];
+        dr[k] = re[k] - re[k + 4];
+        si[k] = im[k] + im[k + 4];
+        di[k] = im[k] - im[k + 4];
+    }
+    float Xr[8], Xi[8];
+    /* even outputs */
+    const float a = sr[0] - sr[2], b = sr[0] + sr[2], cc = sr[1] - sr[3], d = sr[1] + sr[3];
+    const float ai = si[0] - si[2], bi = si[0] + si[2], ci = si[1] - si[3], dd = si[1] + si[3];
+    Xr[0] = b + d;   Xi[0] = bi + dd;
+    Xr[4] = b - d;   Xi[4] = bi - dd;
+    Xr[2] = a + ci;  Xi[2] = ai - cc;
+    Xr[6] = a - ci;  Xi[6] = ai + cc;
+    /* odd outputs */
+    const float u = (dr[1] - dr[3]) * C81, v = (dr[1] + dr[3]) * C81;
+    const float ui = (di[1] - di[3]) * C81, vi = (di[1] + di[3]) * C81;
+    const float e0 = dr[0] - u, e1 = dr[0] + u, f0 = dr[2] - v, f1 = dr[2] + v;
+    const float g0 = di[0] - ui, g1 = di[0] + ui, h0 = di[2] - vi, h1 = di[2] + vi;
+    Xr[1] = e1 + h1; Xi[1] = g1 - f1;
+    Xr[7] = e1 - h1; Xi[7] = g1 + f1;
+    Xr[5] = e0 + h0; Xi[5] = g0 - f0;
+    Xr[3] = e0 - h0; Xi[3] = g0 + f0;
+    for (int k = 0; k < 8; k++)
+    {
+        float yr = Xr[k], yi = Xi[k];
+        if (tstep && k)
+        {
+            const float c = tw[2 * k * tstep], s = tw[2 * k * tstep + 1];
+            const float p1 = c * Xr[k], p2 = s * Xi[k], p3 = c * Xi[k], p4 = s * Xr[k];
+            yr = p1 + p2;
+            yi = p3 - p4;
+        }
+        x[2 * (base + k * stride)] = yr;
+        x[2 * (base + k * stride) + 1] = yi;
+    }
+}
+
+/* arm_radix8_butterfly_f32 stage loop on n points at x (complex), twiddle modifier tm */
+static void cfft_radix8_stages(float* x, int n, const float* tw, int tm)
+{
+    for (int span = n; span >= 8; span >>= 3, tm <<= 3)
+    {
+        const int stride = span >> 3;
+        for (int j = 0; j < stride; j++)
+            for (int g = j; g < n; g += span)
+                cfft_radix8(x, g, stride, tw, j * tm);
+    }
+}
+
+/* complex rotation forms of the first stages */
+static void rot_fwd(float* y, float xr, float xi, float c, float s)   /* (m0 + m1, m2 - m3) */
+{
+    const float m0 = xr * c, m1 = xi * s, m2 = xi * c, m3 = xr * s;
+    y[0] = m0 + m1;
+    y[1] = m2 - m3;
+}
+
+/* arm_cfft_radix8by2_f32 (arm_cfft_f32.c:207-317): radix-2 split of n = 2H points */
+static void cfft_by2(float* x, int n, const float* tw)
+{
+    const int H = n / 2, Q = n / 4;
+    for (int a = 0; a < Q; a++)
+    {
+        float* p1 = x + 2 * a;
+        float* p3 = x + 2 * (a + Q);
+        float* p2 = x + 2 * (a + H);
+        float* p4 = x + 2 * (a + H + Q);
+        const float t2r = p1[0] - p2[0], t2i = p1[1] - p2[1];
+        const float t4r = p4[0] - p3[0], t4i = p4[1] - p3[1];
+        p1[0] = p1[0] + p2[0];
+        p1[1] = p1[1] + p2[1];
+        p3[0] = p3[0] + p4[0];
+        p3[1] = p3[1] + p4[1];
+        const float c = tw[2 * a], s = tw[2 * a + 1];
+        rot_fwd(p2, t2r, t2i, c, s);
+        /* the mirrored column (:283-290): (t4r*s - t4i*c, t4i*s + t4r*c) */
+        const float m0 = t4r * s, m1 = t4i * c, m2 = t4i * s, m3 = t4r * c;
+        p4[0] = m0 - m1;
+        p4[1] = m2 + m3;
+    }
+    cfft_radix8_stages(x, H, tw, 2);
+    cfft_radix8_stages(x + 2 * H, H, tw, 2);
+}
+
+/* arm_cfft_radix8by4_f32 (arm_cfft_f32.c:319-557): radix-4 split of n = 4Q points */
+static void cfft_by4(float* x, int n, const float* tw)
+{
+    const int Q = n / 4;
+    float* c1 = x;
+    float* c2 = x + 2 * Q;
+    float* c3 = x + 4 * Q;
+    float* c4 = x + 6 * Q;
+    /* top half (t = 0 .. Q/2; t = 0 untwiddled, t = Q/2 is the reference's MIDDLE block) */
+    for (int t = 0; t <= Q / 2; t++)
+    {
+        float* p1 = c1 + 2 * t;
+        float* p2 = c2 + 2 * t;
+        float* p3 = c3 + 2 * t;
+        float* p4 = c4 + 2 * t;
+        const float s13r = p1[0] + p3[0], d13r = p1[0] - p3[0];
+        const float s13i = p1[1] + p3[1], d13i = p1[1] - p3[1];
+        const float t2r = d13r + p2[1] - p4[1], t2i = d13i - p2[0] + p4[0];
+        const float t3r = s13r - p2[0] - p4[0], t3i = s13i - p2[1] - p4[1];
+        const float t4r = d13r - p2[1] + p4[1], t4i = d13i + p2[0] - p4[0];
+        p1[0] = s13r + p2[0] + p4[0];
+        p1[1] = s13i + p2[1] + p4[1];
+        if (t == 0)
+        {
+            p2[0] = t2r; p2[1] = t2i;
+            p3[0] = t3r; p3[1] = t3i;
+            p4[0] = t4r; p4[1] = t4i;
+            continue;
+        }
+        rot_fwd(p2, t2r, t2i, tw[2 * t], tw[2 * t + 1]);
+        rot_fwd(p3, t3r, t3i, tw[4 * t], tw[4 * t + 1]);
+        rot_fwd(p4, t4r, t4i, tw[6 * t], tw[6 * t + 1]);
+    }
+    /* bottom half (b = Q - t, t = 1 .. Q/2 - 1) with the mirrored twiddles of t */
+    for (int t = 1; t < Q / 2; t++)
+    {
+        const int b = Q - t;
+        float* p1 = c1 + 2 * b;
+        float* p2 = c2 + 2 * b;
+        float* p3 = c3 + 2 * b;
+        float* p4 = c4 + 2 * b;
+        const float s13r = p1[0] + p3[0], d13r = p1[0] - p3[0];
+        const float s13i = p1[1] + p3[1], d13i = p1[1] - p3[1];
+        const float u2r = p2[1] - p4[1] + d13r;
+        const float u2i = p1[1] - p3[1] - p2[0] + p4[0];
+        const float u3r = s13r - p2[0] - p4[0];
+        const float u3i = s13i - p2[1] - p4[1];
+        const float u4r = p2[1] - p4[1] - d13r;
+        const float u4i = p4[0] - p2[0] - d13i;
+        p1[1] = s13i + p2[1] + p4[1];
+        p1[0] = s13r + p2[0] + p4[0];
+        {
+            const float c = tw[2 * t], s = tw[2 * t + 1];
+            const float m0 = u2i * s, m1 = u2r * c, m2 = u2r * s, m3 = u2i * c;
+            p2[1] = m0 - m1;
+            p2[0] = m2 + m3;
+        }
+        {
+            const float c = tw[4 * t], s = tw[4 * t + 1];
+            const float m0 = -u3i * c, m1 = u3r * s, m2 = u3r * c, m3 = u3i * s;
+            p3[1] = m0 - m1;
+            p3[0] = m3 - m2;
+        }
+        {
+            const float c = tw[6 * t], s = tw[6 * t + 1];
+            const float m0 = u4i * s, m1 = u4r * c, m2 = u4r * s, m3 = u4i * c;
+            p4[1] = m0 - m1;
+            p4[0] = m2 + m3;
+        }
+    }
+    for (int k = 0; k < 4; k++) cfft_radix8_stages(x + 2 * k * Q, Q, tw, 4);
+}
+
+void uo_cfft(const uhsdr_spectrum_plan* p, float* x)
+{
+    const int n = p->fft_len;
+    switch (n)             /* arm_cfft_f32.c:594-611 */
+    {
+    case 1024: cfft_by2(x, n, p->twiddle); break;
+    case 256: cfft_by4(x, n, p->twiddle); break;
+    case 512: cfft_radix8_stages(x, n, p->twiddle, 1); break;
+    default: return;
+    }
+    /* arm_bitreversal_32 (arm_bitreversal2.S:136-180): swap the complex values at the byte
+       offsets of each table pair */
+    uint32_t* w = (uint32_t*)x;
+    for (int k = 0; k + 1 < p->bitrev_len; k += 2)
+    {
+        const int a = p->bitrev[k] >> 2, b = p->bitrev[k + 1] >> 2;
+        uint32_t t = w[a]; w[a] = w[b]; w[b] = t;
+        t = w[a + 1]; w[a + 1] = w[b + 1]; w[b + 1] = t;
+    }
+}
+
+/* one display frame from the full ring (ui_spectrum.c:1362-1446) */
+static void spec_frame(const uhsdr_spectrum_plan* p, uo_spec_state* s, float* mag, float* avg)
+{
+    const int L = p->fft_len;
+    float x[2 * UHSDR_SPECTRUM_MAX_LEN];
+    for (int i = 0; i < 2 * L; i++)
+        x[i] = p->window_formula ? 0.5f * (p->window[i] * s->frame[i]) : s->frame[i] * p->window[i];
+    uo_cfft(p, x);
+    const float f = p->filt_factor;
+    for (int k = 0; k < L; k++)
+    {
+        const float re = x[2 * k], im = x[2 * k + 1];
+        const float m = sqrtf((re * re) + (im * im));             /* arm_cmplx_mag_f32 */
+        float a = s->avg[k];
+        const float old = a * f;                                  /* arm_scale_f32 */
+        a = a - old;                                              /* arm_sub_f32 */
+        const float add = m * f;
+        a = add + a;                                              /* arm_add_f32 */
+        if (a < 1) a = 1;
+        s->avg[k] = a;
+        mag[k] = m;
+        avg[k] = a;
+    }
+}
+
+/* producer: convert + I/Q correction per 32-frame call (as rx_call), then into the ring
+   (AudioDriver_SpectrumCopyIqBuffers, audio_driver.c:1811-1826: Q first, then I) */
+static int spec_channel(const uhsdr_spectrum_plan* p, uo_spec_state* s, const int32_t* iq, int n,
+                        float* mag, float* avg)
+{
+    const int L = p->fft_len;
+    int frames = 0;
+    for (int off = 0; off < n; off += BLK)
+    {
+        float ib[BLK], qb[BLK];
+        for (int i = 0; i < BLK; i++) { ib[i] = iq[2 * (off + i)]; qb[i] = iq[2 * (off + i) + 1]; }
+        for (int i = 0; i < BLK; i++) ib[i] = ib[i] * IQ_BIT_SCALE_DOWN;
+        for (int i = 0; i < BLK; i++) qb[i] = qb[i] * IQ_BIT_SCALE_DOWN;
+        if (!p->iq_auto_correction)
+        {
+            for (int i = 0; i < BLK; i++) ib[i] = ib[i] * p->iq_gain_i;
+            for (int i = 0; i < BLK; i++) qb[i] = qb[i] * p->iq_gain_q;
+            const float ph = p->iq_phase_balance;
+            if (ph < 0)
+                for (int i = 0; i < BLK; i++) { const float e = ib[i] * ph; qb[i] = qb[i] + e; }
+            else if (ph > 0)
+                for (int i = 0; i < BLK; i++) { const float e = qb[i] * ph; ib[i] = ib[i] + e; }
+        }
+        else
+        {
+            float t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
+            for (int i = 0; i < BLK; i++)
+            {
+                t1 += sign_new(ib[i]) * qb[i];
+                t2 += sign_new(ib[i]) * ib[i];
+                t3 += sign_new(qb[i]) * qb[i];
+            }
+            t1 = -0.003 * (t1 / BLK) + 0.997 * s->teta1_old;
+            t2 = 0.003 * (t2 / BLK) + 0.997 * s->teta2_old;
+            t3 = 0.003 * (t3 / BLK) + 0.997 * s->teta3_old;
+            const float M_c1 = (t2 != 0.0) ? t1 / t2 : 0.0;
+            float help = (t2 * t2);
+            if (help > 0.0) help = (t3 * t3 - t1 * t1) / help;
+            const float M_c2 = (help > 0.0) ? sqrtf(help) : 1.0;
+            s->teta1_old = t1;
+            s->teta2_old = t2;
+            s->teta3_old = t3;
+            for (int i = 0; i < BLK; i++) qb[i] += M_c1 * ib[i];
+            for (int i = 0; i < BLK; i++) ib[i] = ib[i] * M_c2;
+        }
+        for (int i = 0; i < BLK; i++)
+        {
+            s->frame[2 * s->fill] = qb[i];
+            s->frame[2 * s->fill + 1] = ib[i];
+            if (++s->fill == L)
+            {
+                spec_frame(p, s, mag + (size_t)frames * L, avg + (size_t)frames * L);
+                frames++;
+                s->fill = 0;
+            }
+        }
+    }
+    return frames;
+}
+
+typedef struct
+{
+    const uhsdr_spectrum_plan* p;
+    uo_spec_state* states;
+    const int32_t* iq;
+    float *mag, *avg;
+    int c0, c1, n, fmax, frames;
+} uo_spec_job;
+
+static void* uo_spec_worker(void* arg)
+{
+    uo_spec_job* j = (uo_spec_job*)arg;
+    const size_t L = j->p->fft_len;
+    for (int c = j->c0; c < j->c1; c++)
+        j->frames = spec_channel(j->p, &j->states[c], j->iq + (size_t)c * j->n * 2, j->n,
+                                 j->mag + (size_t)c * j->fmax * L, j->avg + (size_t)c * j->fmax * L);
+    return NULL;
+}
+
+int uo_spec_process_batch(const uhsdr_spectrum_plan* p, uo_spec_state* states, int C, const int32_t* iq, int n,
+                          float* mag, float* avg, int threads)
+{
+    const int L = p->fft_len;
+    if (n <= 0 || n % BLK || !(L == 256 || L == 512 || L == 1024) || (n % L && L % n)) return UHSDR_LENGTH_ERROR;
+    const int fmax = n >= L ? n / L : 1;
+    if (threads < 1) threads = 1;
+    if (threads > C) threads = C;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    uo_spec_job jobs[256];
+    for (int t = 0; t < threads; t++)
+    {
+        jobs[t] = (uo_spec_job){ p, states, iq, mag, avg, (int)((long)C * t / threads),
+                                 (int)((long)C * (t + 1) / threads), n, fmax, 0 };
+        if (threads == 1) uo_spec_worker(&jobs[t]);
+        else pthread_create(&tid[t], NULL, uo_spec_worker, &jobs[t]);
+    }
+    if (threads > 1)
+        for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+    return jobs[0].frames;
+}

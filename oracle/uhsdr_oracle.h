@@ -77,6 +77,25 @@ void uo_tx_state_init(const uhsdr_tx_plan* p, uo_tx_state* s);
 int uo_tx_process_batch(const uhsdr_tx_plan* p, uo_tx_state* states, int C, const int32_t* audio, int n,
                         int32_t* iq, float* a0, int threads);
 
+/* spectrum display: producer ring + UiSpectrum_RedrawSpectrum states 0-3
+   (audio_driver.c:1811-1851, ui_spectrum.c:1350-1446) */
+typedef struct uo_spec_state
+{
+    float teta1_old, teta2_old, teta3_old;          /* the I/Q correction the ring sees */
+    float frame[2 * UHSDR_SPECTRUM_MAX_LEN];        /* the [Q, I] ring, oldest first */
+    float avg[UHSDR_SPECTRUM_MAX_LEN];              /* sd.FFT_AVGData */
+    int32_t fill;                                   /* samples in frame[] */
+} uo_spec_state;
+
+size_t uo_spec_state_size(void);
+void uo_spec_state_init(const uhsdr_spectrum_plan* p, uo_spec_state* s);
+/* arm_cfft_f32(S, x, 0, 1) restated: forward CFFT in place, natural order out */
+void uo_cfft(const uhsdr_spectrum_plan* p, float* x);
+/* n samples of C channels; mag / avg [C][F][L] with F = frames completed (same for every
+   channel); returns F, or a negative status */
+int uo_spec_process_batch(const uhsdr_spectrum_plan* p, uo_spec_state* states, int C, const int32_t* iq, int n,
+                          float* mag, float* avg, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -118,6 +118,51 @@ def tx_tables():
         json.dump(out, fo, separators=(",", ":"))
 
 
+# spectrum display (a19): name -> (uhsdr_ref args incl. spec=L, signal kwargs).  The firmware's
+# producer (audio_driver.c:1838-1851) fills the ring while the RX chain runs in `mode`/`path`.
+SPEC_CONFIGS = {
+    "p70_sam_1024": ({"mode": 4, "path": 70, "spec": 1024}, {"am": True}),          # C3
+    "p48_usb_512": ({"mode": 0, "path": 48, "spec": 512}, {}),                      # 480x320 display
+    "p48_usb_256": ({"mode": 0, "path": 48, "spec": 256, "specfilt": 1}, {}),       # 320x240 display
+    "p48_iqauto_256": ({"mode": 0, "path": 48, "spec": 256, "iq_auto": 1}, {}),
+    "p48_iqman_1024": ({"mode": 0, "path": 48, "spec": 1024, "gain_i": 1.03125, "gain_q": 0.96875,
+                        "phase": -0.0125, "specfilt": 20}, {}),
+    "p48_iqman2_512": ({"mode": 0, "path": 48, "spec": 512, "gain_i": 0.98, "gain_q": 1.01, "phase": 0.02,
+                        "specfilt": 7}, {}),
+}
+SPEC_FRAMES = 4096
+
+
+def make_spec(name: str):
+    args, sig = SPEC_CONFIGS[name]
+    if sig.get("am"):
+        iq = synth.am_iq(np.arange(NCH), 0, SPEC_FRAMES)
+    else:
+        iq = synth.ssb_iq(np.arange(NCH), 0, SPEC_FRAMES)
+    L = args["spec"]
+    mag = np.empty((NCH, SPEC_FRAMES // L, L), np.float32)
+    avg = np.empty_like(mag)
+    for c in range(NCH):
+        with tempfile.TemporaryDirectory() as td:
+            fin, fm, fa = (os.path.join(td, x) for x in ("in.bin", "m.bin", "a.bin"))
+            iq[c].astype(np.int32).tofile(fin)
+            cmd = [REF, f"in={fin}", f"n={SPEC_FRAMES}", f"out_mag={fm}", f"out_avg={fa}"]
+            subprocess.run(cmd + [f"{k}={v}" for k, v in args.items()], check=True)
+            mag[c] = np.fromfile(fm, dtype=np.float32).reshape(-1, L)
+            avg[c] = np.fromfile(fa, dtype=np.float32).reshape(-1, L)
+    np.savez_compressed(os.path.join(HERE, f"spec_{name}.npz"), iq=iq, mag=mag, avg=avg, args=json.dumps(args))
+    print(f"spec_{name:14s} peak mag={float(mag.max()):10.2f}  min avg={float(avg.min()):6.2f}")
+
+
+def spectrum_tables():
+    """CMSIS twiddle / bit-reversal tables of arm_cfft_sR_f32_len256/512/1024
+    (arm_const_structs.c:63-73, arm_common_tables.c) and the Hann windows of
+    ui_spectrum.c:359-406, as raw bits from the compiled reference."""
+    d = ref_json({"mode": 0, "path": 48}, "spectrum")
+    with open(os.path.join(HERE, "spectrum_tables.json"), "w") as fo:
+        json.dump(d, fo, separators=(",", ":"))
+
+
 def run_ref(args: dict, iq: np.ndarray):
     n = iq.shape[0]
     with tempfile.TemporaryDirectory() as td:
@@ -168,6 +213,11 @@ def main():
     with open(os.path.join(HERE, "filter_paths.json"), "w") as f:
         json.dump(json.loads(paths), f, separators=(",", ":"))
     tx_tables()
+    spectrum_tables()
+    for name in SPEC_CONFIGS:
+        if a.only and name != a.only:
+            continue
+        make_spec(name)
     for name in CONFIGS:
         if a.only and name != a.only:
             continue

@@ -1,0 +1,120 @@
+"""Spectrum display path on the CPU: the oracle's restatement
+(oracle/uhsdr_oracle.c, uo_spec_*) against the reference firmware's own outputs
+(tests/golden/spec_*.npz, made by tests/golden/make_golden.py from the x86 build of
+audio_driver.c's producer + CMSIS arm_cfft_f32 stages / arm_cmplx_mag_f32 + the consumer glue of
+ui_spectrum.c), and the product's setup (uhsdr_spectrum_plan_build) against the dumped tables.
+
+Pinning: the butterfly arithmetic, magnitude and averaging are the reference's compiled code; the
+final bit reversal (ARM assembly only, arm_bitreversal2.S) is restated from its listing and
+checked here against a float64 DFT, which fixes the output order independently."""
+import ctypes as C
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import uhsdr_amd as U
+from golden_util import GOLDEN, assert_bitexact
+
+
+def spec_files():
+    return sorted(glob.glob(os.path.join(GOLDEN, "spec_*.npz")))
+
+
+def load_spec(path):
+    d = np.load(path)
+    return {"iq": d["iq"], "mag": d["mag"], "avg": d["avg"], "args": json.loads(str(d["args"]))}
+
+
+def tables():
+    return json.load(open(os.path.join(GOLDEN, "spectrum_tables.json")))
+
+
+@pytest.mark.parametrize("path", spec_files(), ids=lambda p: os.path.basename(p)[5:-4])
+def test_oracle_matches_reference_spectrum(path):
+    g = load_spec(path)
+    plan = U.build_spectrum_plan(U.spectrum_config_from_ref_args(g["args"]))
+    mag, avg = oracle.OracleSpectrum(plan, g["iq"].shape[0]).process(g["iq"])
+    assert_bitexact(mag, g["mag"], "FFT_MagData")
+    assert_bitexact(avg, g["avg"], "FFT_AVGData")
+
+
+@pytest.mark.parametrize("path", spec_files()[:3], ids=lambda p: os.path.basename(p)[5:-4])
+@pytest.mark.parametrize("calls", [1, 2, 8, 128])
+def test_oracle_call_granularity(path, calls):
+    """the ring carries across calls: any split of the input gives the same frames"""
+    g = load_spec(path)
+    plan = U.build_spectrum_plan(U.spectrum_config_from_ref_args(g["args"]))
+    L = plan.fft_len
+    n = g["iq"].shape[1]
+    step = n // calls if n // calls >= L else L // (L // (n // calls))
+    o = oracle.OracleSpectrum(plan, g["iq"].shape[0])
+    mags, avgs = [], []
+    for off in range(0, n, step):
+        m, a = o.process(g["iq"][:, off:off + step])
+        mags.append(m)
+        avgs.append(a)
+    assert_bitexact(np.concatenate(mags, axis=1), g["mag"], "mag")
+    assert_bitexact(np.concatenate(avgs, axis=1), g["avg"], "avg")
+
+
+@pytest.mark.parametrize("L", [256, 512, 1024])
+def test_plan_tables_match_reference_dump(L):
+    t = tables()
+    p = U.build_spectrum_plan(U.default_spectrum_config(fft_len=L))
+    assert p.fft_len == L and p.bitrev_len == len(t[f"bitrev_{L}"])
+    tw = np.frombuffer(bytes(p.twiddle), np.uint32)[:2 * L]
+    np.testing.assert_array_equal(tw, np.array(t[f"twiddle_{L}"], np.uint32))
+    win = np.frombuffer(bytes(p.window), np.uint32)[:2 * L]
+    key = {256: "hann_512", 512: "hann_1024", 1024: "hann_formula_2048"}[L]
+    np.testing.assert_array_equal(win, np.array(t[key], np.uint32))
+    assert p.window_formula == (L == 1024)
+    br = np.frombuffer(bytes(p.bitrev), np.uint16)[:p.bitrev_len]
+    np.testing.assert_array_equal(br, np.array(t[f"bitrev_{L}"], np.uint16))
+    perm = np.frombuffer(bytes(p.perm), np.uint16)[:L]
+    assert sorted(perm.tolist()) == list(range(L)), "bit reversal is a permutation"
+
+
+@pytest.mark.parametrize("L", [256, 512, 1024])
+def test_cfft_order_pinned_by_float64_dft(L):
+    """natural-order output: within binary32 rounding of numpy's float64 FFT"""
+    rng = np.random.default_rng(L)
+    p = U.build_spectrum_plan(U.default_spectrum_config(fft_len=L))
+    o = oracle.OracleSpectrum(p, 1)
+    for _ in range(4):
+        z = (rng.standard_normal(L) + 1j * rng.standard_normal(L)) * 1000
+        x = np.empty(2 * L, np.float32)
+        x[0::2], x[1::2] = z.real, z.imag
+        y = o.cfft(x)
+        ref = np.fft.fft(x[0::2].astype(np.float64) + 1j * x[1::2].astype(np.float64))
+        err = np.abs((y[0::2] + 1j * y[1::2]) - ref).max() / np.abs(ref).max()
+        assert err < 2e-6, err
+
+
+def test_plan_window_is_hann():
+    """the three windows are Hann windows over 2L floats (formula (1 - cos) for 1024 points)"""
+    for L in (256, 512, 1024):
+        p = U.build_spectrum_plan(U.default_spectrum_config(fft_len=L))
+        w = np.frombuffer(bytes(p.window), np.float32)[:2 * L].astype(np.float64)
+        if p.window_formula:
+            w = 0.5 * w
+        n = np.arange(2 * L)
+        ref = 0.5 * (1 - np.cos(2 * np.pi * n / (2 * L - 1)))
+        assert np.abs(w - ref).max() < 1e-5, L
+
+
+def test_plan_rejects_bad_config():
+    lib = U.load()
+    plan = U.SpectrumPlan()
+    for over in [dict(fft_len=128), dict(fft_len=2048), dict(spectrum_filter=0), dict(spectrum_filter=21)]:
+        cfg = U.default_spectrum_config(**over)
+        assert lib.uhsdr_spectrum_plan_build(C.byref(cfg), C.byref(plan)) == -1, over
+    h = C.c_void_p()
+    cfg = U.default_spectrum_config(fft_len=1024)
+    assert lib.uhsdr_spectrum_create(C.byref(cfg), 4, 96, None, C.byref(h)) == -2     # neither divides
+    assert lib.uhsdr_spectrum_create(C.byref(cfg), 4, 1000, None, C.byref(h)) == -2   # N % 32
+    assert lib.uhsdr_spectrum_create(C.byref(cfg), 0, 1024, None, C.byref(h)) == -1
+    assert lib.uhsdr_spectrum_process(None, None, None, None, None) == -1

@@ -106,6 +106,29 @@ class TxPlan(C.Structure):
     ]
 
 
+SPECTRUM_MAX_LEN = 1024
+SPECTRUM_MAX_BITREV = 1800
+
+
+class SpectrumConfig(C.Structure):
+    _fields_ = [
+        ("fft_len", C.c_int32), ("spectrum_filter", C.c_int32), ("iq_auto_correction", C.c_int32),
+        ("iq_gain_i", C.c_float), ("iq_gain_q", C.c_float), ("iq_phase_balance", C.c_float),
+        ("reserved", C.c_int32 * 10),
+    ]
+
+
+class SpectrumPlan(C.Structure):
+    _fields_ = [
+        ("fft_len", C.c_int32), ("window_formula", C.c_int32), ("iq_auto_correction", C.c_int32),
+        ("iq_gain_i", C.c_float), ("iq_gain_q", C.c_float), ("iq_phase_balance", C.c_float),
+        ("filt_factor", C.c_float), ("bitrev_len", C.c_int32),
+        ("window", C.c_float * (2 * SPECTRUM_MAX_LEN)), ("twiddle", C.c_float * (2 * SPECTRUM_MAX_LEN)),
+        ("bitrev", C.c_uint16 * SPECTRUM_MAX_BITREV), ("perm", C.c_uint16 * SPECTRUM_MAX_LEN),
+        ("reserved", C.c_int32 * 16),
+    ]
+
+
 # every exported entry point of include/uhsdr.h: name -> (restype, argtypes)
 SIGNATURES = {
     "uhsdr_rx_config_default": (None, [C.POINTER(RxConfig)]),
@@ -140,6 +163,16 @@ SIGNATURES = {
     "uhsdr_tx_destroy": (C.c_int, [C.c_void_p]),
     "uhsdr_sizeof_tx_config": (C.c_int32, []),
     "uhsdr_sizeof_tx_plan": (C.c_int32, []),
+    "uhsdr_spectrum_config_default": (None, [C.POINTER(SpectrumConfig)]),
+    "uhsdr_spectrum_plan_build": (C.c_int, [C.POINTER(SpectrumConfig), C.POINTER(SpectrumPlan)]),
+    "uhsdr_spectrum_create": (C.c_int, [C.POINTER(SpectrumConfig), C.c_int32, C.c_int32, C.c_void_p,
+                                        C.POINTER(C.c_void_p)]),
+    "uhsdr_spectrum_reset": (C.c_int, [C.c_void_p]),
+    "uhsdr_spectrum_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)]),
+    "uhsdr_spectrum_get_plan": (C.c_int, [C.c_void_p, C.POINTER(SpectrumPlan)]),
+    "uhsdr_spectrum_destroy": (C.c_int, [C.c_void_p]),
+    "uhsdr_sizeof_spectrum_config": (C.c_int32, []),
+    "uhsdr_sizeof_spectrum_plan": (C.c_int32, []),
 }
 
 _lib = None
@@ -162,6 +195,9 @@ def load(path: str | None = None) -> C.CDLL:
         raise RuntimeError("ctypes layout of uhsdr_rx_config / uhsdr_rx_plan does not match include/uhsdr.h")
     if lib.uhsdr_sizeof_tx_config() != C.sizeof(TxConfig) or lib.uhsdr_sizeof_tx_plan() != C.sizeof(TxPlan):
         raise RuntimeError("ctypes layout of uhsdr_tx_config / uhsdr_tx_plan does not match include/uhsdr.h")
+    if (lib.uhsdr_sizeof_spectrum_config() != C.sizeof(SpectrumConfig)
+            or lib.uhsdr_sizeof_spectrum_plan() != C.sizeof(SpectrumPlan)):
+        raise RuntimeError("ctypes layout of uhsdr_spectrum_config / _plan does not match include/uhsdr.h")
     if path is None:
         _lib = lib
     return lib
@@ -229,4 +265,29 @@ def tx_config_from_ref_args(args: dict) -> TxConfig:
 def build_tx_plan(cfg: TxConfig) -> TxPlan:
     plan = TxPlan()
     check(load().uhsdr_tx_plan_build(C.byref(cfg), C.byref(plan)), "uhsdr_tx_plan_build")
+    return plan
+
+
+# uhsdr_ref spectrum key=value names (tests/golden/spec_*.npz) -> SpectrumConfig fields
+SPEC_ARG_MAP = {
+    "spec": "fft_len", "specfilt": "spectrum_filter", "iq_auto": "iq_auto_correction",
+    "gain_i": "iq_gain_i", "gain_q": "iq_gain_q", "phase": "iq_phase_balance",
+}
+
+
+def default_spectrum_config(**overrides) -> SpectrumConfig:
+    cfg = SpectrumConfig()
+    load().uhsdr_spectrum_config_default(C.byref(cfg))
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def spectrum_config_from_ref_args(args: dict) -> SpectrumConfig:
+    return default_spectrum_config(**{SPEC_ARG_MAP[k]: v for k, v in args.items() if k in SPEC_ARG_MAP})
+
+
+def build_spectrum_plan(cfg: SpectrumConfig) -> SpectrumPlan:
+    plan = SpectrumPlan()
+    check(load().uhsdr_spectrum_plan_build(C.byref(cfg), C.byref(plan)), "uhsdr_spectrum_plan_build")
     return plan

@@ -46,6 +46,17 @@ extern const uint32_t* const uhsdr_tx_hilbert_i;
 extern const uint32_t* const uhsdr_tx_hilbert_q;
 extern const int uhsdr_tx_hilbert_taps;
 
+/* spectrum display tables (tools/gen_filter_tables.py from tests/golden/spectrum_tables.json) */
+typedef struct
+{
+    int fft_len, window_formula;
+    const uint32_t* twiddle;      /* 2L floats */
+    const uint32_t* window;       /* 2L floats */
+    const uint16_t* bitrev;
+    int bitrev_len;
+} uhsdr_spectrum_desc;
+extern const uhsdr_spectrum_desc uhsdr_spectrum_tables[3];
+
 int uhsdr_rx_mode_supported(const uhsdr_rx_plan* p);
 
 /* thread-local last error text for uhsdr_last_error() */

@@ -549,3 +549,57 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
 
 int32_t uhsdr_sizeof_tx_config(void) { return (int32_t)sizeof(uhsdr_tx_config); }
 int32_t uhsdr_sizeof_tx_plan(void) { return (int32_t)sizeof(uhsdr_tx_plan); }
+
+/* ---- spectrum display (UiSpectrum_InitSpectrumDisplayData, ui_spectrum.c:955-990; window and
+   averaging of UiSpectrum_RedrawSpectrum, :1350-1446) ---- */
+void uhsdr_spectrum_config_default(uhsdr_spectrum_config* cfg)
+{
+    if (!cfg) return;
+    memset(cfg, 0, sizeof *cfg);
+    cfg->fft_len = 1024;                  /* C3; the firmware's displays use 256 / 512 */
+    cfg->spectrum_filter = 4;             /* SPECTRUM_FILTER_DEFAULT */
+    cfg->iq_auto_correction = 0;
+    cfg->iq_gain_i = 1.0f;
+    cfg->iq_gain_q = 1.0f;
+    cfg->iq_phase_balance = 0.0f;
+}
+
+uhsdr_status uhsdr_spectrum_plan_build(const uhsdr_spectrum_config* cfg, uhsdr_spectrum_plan* p)
+{
+    if (!cfg || !p) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
+    const uhsdr_spectrum_desc* d = NULL;
+    for (int i = 0; i < 3; ++i)
+        if (uhsdr_spectrum_tables[i].fft_len == cfg->fft_len) d = &uhsdr_spectrum_tables[i];
+    if (!d) { uhsdr_set_error("fft_len %d: need 256, 512 or 1024", cfg->fft_len); return UHSDR_ARGUMENT_ERROR; }
+    if (cfg->spectrum_filter < 1 || cfg->spectrum_filter > 20)
+    { uhsdr_set_error("spectrum_filter %d outside 1..20", cfg->spectrum_filter); return UHSDR_ARGUMENT_ERROR; }
+    memset(p, 0, sizeof *p);
+    const int L = d->fft_len;
+    p->fft_len = L;
+    p->window_formula = d->window_formula;
+    p->iq_auto_correction = cfg->iq_auto_correction != 0;
+    p->iq_gain_i = cfg->iq_gain_i;
+    p->iq_gain_q = cfg->iq_gain_q;
+    p->iq_phase_balance = cfg->iq_phase_balance;
+    p->filt_factor = 1 / (float)cfg->spectrum_filter;
+    p->bitrev_len = d->bitrev_len;
+    memcpy(p->window, d->window, sizeof(float) * 2 * L);
+    memcpy(p->twiddle, d->twiddle, sizeof(float) * 2 * L);
+    memcpy(p->bitrev, d->bitrev, sizeof(uint16_t) * d->bitrev_len);
+    /* arm_bitreversal_32 (arm_bitreversal2.S:136-180) swaps the complex values at byte offsets
+       bitrev[2k], bitrev[2k+1]; applied to the identity it gives where each output bin comes from */
+    for (int k = 0; k < L; ++k) p->perm[k] = (uint16_t)k;
+    for (int it = 0; it < ((d->bitrev_len + 1) >> 2); ++it)
+        for (int s = 0; s < 2; ++s)
+        {
+            const int a = d->bitrev[4 * it + 2 * s] >> 3, b = d->bitrev[4 * it + 2 * s + 1] >> 3;
+            if (a >= L || b >= L) { uhsdr_set_error("bit-reversal table entry out of range"); return UHSDR_ARGUMENT_ERROR; }
+            const uint16_t t = p->perm[a];
+            p->perm[a] = p->perm[b];
+            p->perm[b] = t;
+        }
+    return UHSDR_OK;
+}
+
+int32_t uhsdr_sizeof_spectrum_config(void) { return (int32_t)sizeof(uhsdr_spectrum_config); }
+int32_t uhsdr_sizeof_spectrum_plan(void) { return (int32_t)sizeof(uhsdr_spectrum_plan); }

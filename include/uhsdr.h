@@ -318,6 +318,7 @@ typedef struct uhsdr_spectrum_plan
     float   twiddle[2 * UHSDR_SPECTRUM_MAX_LEN];   /* twiddleCoef_<L> (arm_common_tables.c) */
     uint16_t bitrev[UHSDR_SPECTRUM_MAX_BITREV];    /* armBitRevIndexTable<L>: byte-offset swap pairs */
     uint16_t perm[UHSDR_SPECTRUM_MAX_LEN];         /* bin k of the output = butterfly result perm[k] */
+    uint16_t iperm[UHSDR_SPECTRUM_MAX_LEN];        /* butterfly result p lands in bin iperm[p] */
     int32_t reserved[16];
 } uhsdr_spectrum_plan;
 

@@ -598,6 +598,7 @@ uhsdr_status uhsdr_spectrum_plan_build(const uhsdr_spectrum_config* cfg, uhsdr_s
             p->perm[a] = p->perm[b];
             p->perm[b] = t;
         }
+    for (int k = 0; k < L; ++k) p->iperm[p->perm[k]] = (uint16_t)k;
     return UHSDR_OK;
 }
 

@@ -35,6 +35,7 @@ struct SpecArgs
     float* teta;             // [3][C] auto I/Q correction low-pass state
     float* avg_state;        // [C][L] sd.FFT_AVGData
     float* carry;            // [C][2L] windowed ring of an incomplete frame (positions < fill)
+                             // avg_state is kept in butterfly-output order (bins via plan->iperm)
     float* mag;              // optional [C][F][L]
     float* avg;              // optional [C][F][L]
     int C, N, ld, F, fill0, lds_pitch;
@@ -42,146 +43,97 @@ struct SpecArgs
 
 __device__ __forceinline__ float sign_new(float x) { return (x < 0) ? -1.0f : ((x > 0) ? 1.0f : 0.0f); }
 
-// arm_radix8_butterfly_f32 butterfly on the 8 complex values x[base + k*stride] (LDS): the
-// reference's two loop bodies share one sequence of adds for the eight outputs X_k; the twiddled
-// groups then rotate X_k, k >= 1, by twiddle[k * tstep] as (c*re + s*im, c*im - s*re).
-__device__ __forceinline__ void bfly8(float* __restrict__ x, int base, int stride, const float* __restrict__ tw, int tstep)
+// complex index with one pad slot per 8: the strided butterfly reads of every stage hit
+// distinct LDS banks (at most the two passes a 64-lane ds_read_b64 needs anyway)
+__device__ __forceinline__ int padp(int p) { return p + (p >> 3); }
+
+// arm_radix8_butterfly_f32 butterfly (CMSIS arm_cfft_radix8_f32.c:130-383) on eight complex
+// values in registers.  The reference's two loop bodies (twiddle-free first group :149-221,
+// twiddled groups :228-372) form the same eight values X_k with the same sequence of adds; the
+// twiddled groups then rotate X_k, k >= 1, by twiddle[k * tstep] as (c*re + s*im, c*im - s*re).
+__device__ __forceinline__ void dft8(float2* z, const float* __restrict__ tw, int tstep)
 {
     const float C81 = 0.70710678118f;
-    float re[8], im[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-    {
-        const float2 v = *(const float2*)(x + 2 * (base + k * stride));
-        re[k] = v.x;
-        im[k] = v.y;
-    }
     float sr[4], dr[4], si[4], di[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
     {
-        sr[k] = re[k] + re[k + 4];
-        dr[k] = re[k] - re[k + 4];
-        si[k] = im[k] + im[k + 4];
-        di[k] = im[k] - im[k + 4];
+        sr[k] = z[k].x + z[k + 4].x;
+        dr[k] = z[k].x - z[k + 4].x;
+        si[k] = z[k].y + z[k + 4].y;
+        di[k] = z[k].y - z[k + 4].y;
     }
-    float Xr[8], Xi[8];
     const float a = sr[0] - sr[2], b = sr[0] + sr[2], cc = sr[1] - sr[3], d = sr[1] + sr[3];
     const float ai = si[0] - si[2], bi = si[0] + si[2], ci = si[1] - si[3], dd = si[1] + si[3];
-    Xr[0] = b + d;   Xi[0] = bi + dd;
-    Xr[4] = b - d;   Xi[4] = bi - dd;
-    Xr[2] = a + ci;  Xi[2] = ai - cc;
-    Xr[6] = a - ci;  Xi[6] = ai + cc;
+    z[0] = make_float2(b + d, bi + dd);
+    z[4] = make_float2(b - d, bi - dd);
+    z[2] = make_float2(a + ci, ai - cc);
+    z[6] = make_float2(a - ci, ai + cc);
     const float u = (dr[1] - dr[3]) * C81, v = (dr[1] + dr[3]) * C81;
     const float ui = (di[1] - di[3]) * C81, vi = (di[1] + di[3]) * C81;
     const float e0 = dr[0] - u, e1 = dr[0] + u, f0 = dr[2] - v, f1 = dr[2] + v;
     const float g0 = di[0] - ui, g1 = di[0] + ui, h0 = di[2] - vi, h1 = di[2] + vi;
-    Xr[1] = e1 + h1; Xi[1] = g1 - f1;
-    Xr[7] = e1 - h1; Xi[7] = g1 + f1;
-    Xr[5] = e0 + h0; Xi[5] = g0 - f0;
-    Xr[3] = e0 - h0; Xi[3] = g0 + f0;
+    z[1] = make_float2(e1 + h1, g1 - f1);
+    z[7] = make_float2(e1 - h1, g1 + f1);
+    z[5] = make_float2(e0 + h0, g0 - f0);
+    z[3] = make_float2(e0 - h0, g0 + f0);
     if (tstep)
     {
 #pragma unroll
         for (int k = 1; k < 8; ++k)
         {
             const float2 t = *(const float2*)(tw + 2 * k * tstep);
-            const float p1 = t.x * Xr[k], p2 = t.y * Xi[k], p3 = t.x * Xi[k], p4 = t.y * Xr[k];
-            Xr[k] = p1 + p2;
-            Xi[k] = p3 - p4;
+            const float p1 = t.x * z[k].x, p2 = t.y * z[k].y, p3 = t.x * z[k].y, p4 = t.y * z[k].x;
+            z[k] = make_float2(p1 + p2, p3 - p4);
         }
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) *(float2*)(x + 2 * (base + k * stride)) = make_float2(Xr[k], Xi[k]);
-}
-
-// arm_radix8_butterfly_f32 stages on NSUB sub-arrays of n points each (contiguous), twiddle
-// modifier TM0; butterflies of a stage are independent, spread over the wave's lanes
-template <int n, int NSUB, int TM0>
-__device__ __forceinline__ void radix8_stages(float* x, const float* tw, int lane)
-{
-#pragma unroll
-    for (int span = n, tm = TM0; span >= 8; span >>= 3, tm <<= 3)
-    {
-        const int stride = span >> 3;
-        constexpr int per_sub = n / 8;
-        for (int q = lane; q < NSUB * per_sub; q += 64)
-        {
-            const int sub = q / per_sub, r = q % per_sub;
-            const int j = r % stride, g = j + span * (r / stride);
-            bfly8(x + 2 * n * sub, g, stride, tw, j * tm);
-        }
-        wave_sync();
     }
 }
 
-__device__ __forceinline__ float2 rot_fwd(float xr, float xi, float c, float s)
+__device__ __forceinline__ float2 rot_fwd(float2 x, float2 t)
 {
-    const float m0 = xr * c, m1 = xi * s, m2 = xi * c, m3 = xr * s;
+    const float m0 = x.x * t.x, m1 = x.y * t.y, m2 = x.y * t.x, m3 = x.x * t.y;
     return make_float2(m0 + m1, m2 - m3);
 }
 
-// arm_cfft_radix8by2_f32 (arm_cfft_f32.c:207-317) radix-2 split, n = 1024
-template <int n>
-__device__ __forceinline__ void split_by2(float* x, const float* tw, int lane)
+// arm_cfft_radix8by2_f32 split (arm_cfft_f32.c:207-317), n = 1024, on the lane's 16 values
+// z[k] = x[lane + 64k]: column a = lane + 64m pairs x[a], x[a+256] with x[a+512], x[a+768]
+__device__ __forceinline__ void split_by2_regs(float2 (&z)[16], const float* __restrict__ tw, int lane)
 {
-    constexpr int H = n / 2, Q = n / 4;
-    for (int a = lane; a < Q; a += 64)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
     {
-        float2* p1 = (float2*)x + a;
-        float2* p3 = (float2*)x + a + Q;
-        float2* p2 = (float2*)x + a + H;
-        float2* p4 = (float2*)x + a + H + Q;
-        const float2 x1 = *p1, x2 = *p2, x3 = *p3, x4 = *p4;
-        const float t2r = x1.x - x2.x, t2i = x1.y - x2.y;
-        const float t4r = x4.x - x3.x, t4i = x4.y - x3.y;
-        *p1 = make_float2(x1.x + x2.x, x1.y + x2.y);
-        *p3 = make_float2(x3.x + x4.x, x3.y + x4.y);
-        const float2 t = *(const float2*)(tw + 2 * a);
-        *p2 = rot_fwd(t2r, t2i, t.x, t.y);
-        const float m0 = t4r * t.y, m1 = t4i * t.x, m2 = t4i * t.y, m3 = t4r * t.x;
-        *p4 = make_float2(m0 - m1, m2 + m3);
+        const float2 x1 = z[m], x3 = z[m + 4], x2 = z[m + 8], x4 = z[m + 12];
+        const float2 t2 = make_float2(x1.x - x2.x, x1.y - x2.y);
+        const float2 t4 = make_float2(x4.x - x3.x, x4.y - x3.y);
+        z[m] = make_float2(x1.x + x2.x, x1.y + x2.y);
+        z[m + 4] = make_float2(x3.x + x4.x, x3.y + x4.y);
+        const float2 t = *(const float2*)(tw + 2 * (lane + 64 * m));
+        z[m + 8] = rot_fwd(t2, t);
+        const float m0 = t4.x * t.y, m1 = t4.y * t.x, m2 = t4.y * t.y, m3 = t4.x * t.x;
+        z[m + 12] = make_float2(m0 - m1, m2 + m3);
     }
-    wave_sync();
 }
 
-// arm_cfft_radix8by4_f32 (arm_cfft_f32.c:319-557) radix-4 split, n = 256: lanes 0..Q/2 take
-// the top rows t (t = 0 untwiddled, t = Q/2 the reference's MIDDLE block), lanes Q/2+1.. the
-// bottom rows Q - t with the mirrored twiddles of t
-template <int n>
-__device__ __forceinline__ void split_by4(float* x, const float* tw, int lane)
+// arm_cfft_radix8by4_f32 split (arm_cfft_f32.c:319-557), n = 256, row r = lane of the four
+// quarters (z[k] = x[r + 64k]): rows 0..32 are the reference's TOP rows t = r (t = 0
+// untwiddled, t = 32 its MIDDLE block), rows 33..63 its BOTTOM rows 64 - t with the twiddles of t
+__device__ __forceinline__ void split_by4_regs(float2 (&z)[4], const float* __restrict__ tw, int lane)
 {
-    constexpr int Q = n / 4;
-    static_assert(Q == 64, "one row per lane");
+    constexpr int Q = 64;
     const bool top = lane <= Q / 2;
-    const int t = top ? lane : lane - Q / 2;
-    const int row = top ? t : Q - t;
-    float2* p1 = (float2*)x + row;
-    float2* p2 = p1 + Q;
-    float2* p3 = p1 + 2 * Q;
-    float2* p4 = p1 + 3 * Q;
-    const float2 x1 = *p1, x2 = *p2, x3 = *p3, x4 = *p4;
+    const int t = top ? lane : Q - lane;
+    const float2 x1 = z[0], x2 = z[1], x3 = z[2], x4 = z[3];
     const float s13r = x1.x + x3.x, d13r = x1.x - x3.x;
     const float s13i = x1.y + x3.y, d13i = x1.y - x3.y;
     const float2 w2 = *(const float2*)(tw + 2 * t), w3 = *(const float2*)(tw + 4 * t), w4 = *(const float2*)(tw + 6 * t);
+    z[0] = make_float2(s13r + x2.x + x4.x, s13i + x2.y + x4.y);
     if (top)
     {
-        const float t2r = d13r + x2.y - x4.y, t2i = d13i - x2.x + x4.x;
-        const float t3r = s13r - x2.x - x4.x, t3i = s13i - x2.y - x4.y;
-        const float t4r = d13r - x2.y + x4.y, t4i = d13i + x2.x - x4.x;
-        *p1 = make_float2(s13r + x2.x + x4.x, s13i + x2.y + x4.y);
-        if (t == 0)
-        {
-            *p2 = make_float2(t2r, t2i);
-            *p3 = make_float2(t3r, t3i);
-            *p4 = make_float2(t4r, t4i);
-        }
-        else
-        {
-            *p2 = rot_fwd(t2r, t2i, w2.x, w2.y);
-            *p3 = rot_fwd(t3r, t3i, w3.x, w3.y);
-            *p4 = rot_fwd(t4r, t4i, w4.x, w4.y);
-        }
+        const float2 t2 = make_float2(d13r + x2.y - x4.y, d13i - x2.x + x4.x);
+        const float2 t3 = make_float2(s13r - x2.x - x4.x, s13i - x2.y - x4.y);
+        const float2 t4 = make_float2(d13r - x2.y + x4.y, d13i + x2.x - x4.x);
+        if (t == 0) { z[1] = t2; z[2] = t3; z[3] = t4; }
+        else { z[1] = rot_fwd(t2, w2); z[2] = rot_fwd(t3, w3); z[3] = rot_fwd(t4, w4); }
     }
     else
     {
@@ -191,176 +143,331 @@ __device__ __forceinline__ void split_by4(float* x, const float* tw, int lane)
         const float u3i = s13i - x2.y - x4.y;
         const float u4r = x2.y - x4.y - d13r;
         const float u4i = x4.x - x2.x - d13i;
-        *p1 = make_float2(s13r + x2.x + x4.x, s13i + x2.y + x4.y);
         {
             const float m0 = u2i * w2.y, m1 = u2r * w2.x, m2 = u2r * w2.y, m3 = u2i * w2.x;
-            *p2 = make_float2(m2 + m3, m0 - m1);
+            z[1] = make_float2(m2 + m3, m0 - m1);
         }
         {
             const float m0 = -u3i * w3.x, m1 = u3r * w3.y, m2 = u3r * w3.x, m3 = u3i * w3.y;
-            *p3 = make_float2(m3 - m2, m0 - m1);
+            z[2] = make_float2(m3 - m2, m0 - m1);
         }
         {
             const float m0 = u4i * w4.y, m1 = u4r * w4.x, m2 = u4r * w4.y, m3 = u4i * w4.x;
-            *p4 = make_float2(m2 + m3, m0 - m1);
+            z[3] = make_float2(m2 + m3, m0 - m1);
         }
     }
-    wave_sync();
+}
+
+// Frame layout per wave (LDS): the frame as padded complex; before the frame is written there,
+// the same words hold the auto-I/Q products of this segment ([3][L], swizzled per call so the
+// sequential per-call sums read conflict-free), then T = [5][NCALL] sums / factors.
+template <int L>
+struct SpecGeom
+{
+    static constexpr int K = L / 64;                       // positions per lane before the LDS stages
+    static constexpr int NCALL = L / BLK;
+    static constexpr int NBF = L / 8;                      // butterflies per radix-8 stage
+    static constexpr int R3 = (NBF + 63) / 64;             // final-stage butterflies per lane
+    static constexpr int SUBN = L == 256 ? 64 : 512;       // sub-array of the middle radix-8 stage
+    static constexpr int TMID = L == 1024 ? 16 : (L == 512 ? 8 : 4);   // its twiddle modifier
+    static constexpr int FRAME = 2 * (L + L / 8);          // floats, padded complex
+    static constexpr int SCRATCH = 3 * L;
+    static constexpr int REGION = FRAME > SCRATCH ? FRAME : SCRATCH;
+    static constexpr int PITCH = REGION + 5 * NCALL + 4;   // floats per wave
+};
+
+struct SpecParams
+{
+    const float* win;
+    float gi, gq, ph;
+    bool formula, iq_auto;
+};
+
+// Producer side for the lane's positions p = lane + 64k of one segment [fill, end) of a frame:
+// convert (audio_driver.c:2660-2685), I/Q correction (:2254-2316; the auto variant's per-call
+// statistics summed in sample order through LDS), window (ui_spectrum.c:402-414).  PART: the
+// segment does not start at 0 (positions below fill hold the carried, already windowed values)
+// or does not reach L.  Positions outside [fill, end) are left alone.
+template <int L, bool PART>
+__device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2* __restrict__ src, int fill, int end,
+                                        const SpecParams& sp, float* S, float* T, float& o1, float& o2, float& o3,
+                                        int lane)
+{
+    using G = SpecGeom<L>;
+    constexpr int K = G::K, NCALL = G::NCALL;
+    auto in_seg = [&](int p) { return !PART || (p >= fill && p < end); };
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+    {
+        const int p = lane + 64 * k;
+        if (in_seg(p))
+        {
+            const int2 v = src[p - fill];
+            float I = (float)v.x, Q = (float)v.y;
+            I = I * IQ_BIT_SCALE_DOWN;
+            Q = Q * IQ_BIT_SCALE_DOWN;
+            z[k] = make_float2(Q, I);
+        }
+    }
+    if (sp.iq_auto)
+    {
+        // per-call sums of sgn(I)Q, sgn(I)I, sgn(Q)Q in sample order (audio_driver.c:2274-2285):
+        // the products are exact, so they are formed here and summed sequentially per call
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+        {
+            const int p = lane + 64 * k;
+            if (in_seg(p))
+            {
+                const int j = p >> 5, i = p & 31;
+                const int at = j * 32 + (i ^ j);
+                const float Q = z[k].x, I = z[k].y;
+                S[at] = sign_new(I) * Q;
+                S[L + at] = sign_new(I) * I;
+                S[2 * L + at] = sign_new(Q) * Q;
+            }
+        }
+        wave_sync();
+        const int j = (fill >> 5) + lane;
+        if (j < (end >> 5))
+        {
+            float t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
+            for (int i = 0; i < BLK; ++i)
+            {
+                const int at = j * 32 + (i ^ j);
+                t1 += S[at];
+                t2 += S[L + at];
+                t3 += S[2 * L + at];
+            }
+            T[j] = t1; T[NCALL + j] = t2; T[2 * NCALL + j] = t3;
+        }
+        wave_sync();
+        for (int jj = fill >> 5; jj < (end >> 5); ++jj)        // the low-pass recursion, uniform
+        {
+            float t1 = T[jj], t2 = T[NCALL + jj], t3 = T[2 * NCALL + jj];
+            t1 = (float)(-0.003 * (double)(t1 / (float)BLK) + 0.997 * (double)o1);
+            t2 = (float)(0.003 * (double)(t2 / (float)BLK) + 0.997 * (double)o2);
+            t3 = (float)(0.003 * (double)(t3 / (float)BLK) + 0.997 * (double)o3);
+            const float M_c1 = (t2 != 0.0f) ? t1 / t2 : 0.0f;
+            float help = (t2 * t2);
+            if (help > 0.0f) help = (t3 * t3 - t1 * t1) / help;
+            const float M_c2 = (help > 0.0f) ? sqrtf(help) : 1.0f;
+            o1 = t1; o2 = t2; o3 = t3;
+            if (lane == 0) { T[3 * NCALL + jj] = M_c1; T[4 * NCALL + jj] = M_c2; }
+        }
+        wave_sync();
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+    {
+        const int p = lane + 64 * k;
+        if (in_seg(p))
+        {
+            float Q = z[k].x, I = z[k].y;
+            if (!sp.iq_auto)
+            {
+                I = I * sp.gi;
+                Q = Q * sp.gq;
+                if (sp.ph < 0) { const float e3 = I * sp.ph; Q = Q + e3; }
+                else if (sp.ph > 0) { const float e3 = Q * sp.ph; I = I + e3; }
+            }
+            else
+            {
+                Q += T[3 * NCALL + (p >> 5)] * I;
+                I = I * T[4 * NCALL + (p >> 5)];
+            }
+            const float2 wv = *(const float2*)(sp.win + 2 * p);
+            if (sp.formula) z[k] = make_float2(0.5f * (wv.x * Q), 0.5f * (wv.y * I));
+            else z[k] = make_float2(Q * wv.x, I * wv.y);
+        }
+    }
 }
 
 template <int L>
-__device__ __forceinline__ void cfft(float* x, const float* tw, int lane)
+__device__ __forceinline__ SpecParams spec_params(const uhsdr_spectrum_plan* __restrict__ P)
 {
+    SpecParams sp;
+    sp.win = P->window;
+    sp.gi = P->iq_gain_i; sp.gq = P->iq_gain_q; sp.ph = P->iq_phase_balance;
+    sp.formula = P->window_formula;
+    sp.iq_auto = P->iq_auto_correction;
+    return sp;
+}
+
+// One display frame from the produced positions z[k] = x[lane + 64k]: arm_cfft_f32's first
+// stages in registers, the middle radix-8 stage through LDS, the last stage into registers,
+// the bit reversal as the output bin of each butterfly result, then magnitude and average
+// (ui_spectrum.c:1405, 1432-1446).
+template <int L>
+__device__ __forceinline__ void spectrum_frame(float2 (&z)[SpecGeom<L>::K], float2* X, const float* __restrict__ tw,
+                                               float (&av)[SpecGeom<L>::R3][8], float f, const SpecArgs& a, int c,
+                                               int frame, int lane)
+{
+    using G = SpecGeom<L>;
+    constexpr int K = G::K, NBF = G::NBF, R3 = G::R3;
+    const uhsdr_spectrum_plan* __restrict__ P = a.plan;
     if constexpr (L == 1024)
     {
-        split_by2<L>(x, tw, lane);
-        radix8_stages<L / 2, 2, 2>(x, tw, lane);
+        split_by2_regs(z, tw, lane);
+        dft8(z, tw, lane * 2);                   // radix-8 stage span 512 of each half (j = lane)
+        dft8(z + 8, tw, lane * 2);
     }
     else if constexpr (L == 512)
     {
-        radix8_stages<L, 1, 1>(x, tw, lane);
+        dft8(z, tw, lane);
     }
     else
     {
-        split_by4<L>(x, tw, lane);
-        radix8_stages<L / 4, 4, 4>(x, tw, lane);
+        split_by4_regs(z, tw, lane);
+    }
+    wave_sync();                                 // earlier LDS readers (scratch / last frame) done
+#pragma unroll
+    for (int k = 0; k < K; ++k) X[padp(lane + 64 * k)] = z[k];
+    wave_sync();
+    for (int q = lane; q < NBF; q += 64)
+    {
+        constexpr int PER = G::SUBN / 8;
+        const int sub = q / PER, rr = q % PER;
+        const int j = rr & 7;
+        const int base = sub * G::SUBN + j + 64 * (rr >> 3);
+        float2 y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y[k] = X[padp(base + 8 * k)];
+        dft8(y, tw, j * G::TMID);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) X[padp(base + 8 * k)] = y[k];
+    }
+    wave_sync();
+    float* __restrict__ mo = a.mag ? a.mag + ((size_t)c * a.F + frame) * L : nullptr;
+    float* __restrict__ ao = a.avg ? a.avg + ((size_t)c * a.F + frame) * L : nullptr;
+#pragma unroll
+    for (int r = 0; r < R3; ++r)
+    {
+        const int q = lane + 64 * r;
+        if (q < NBF)
+        {
+            float2 y[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) y[k] = X[padp(8 * q + k)];
+            dft8(y, tw, 0);
+            const uint4 bins = *(const uint4*)(P->iperm + 8 * q);   // 8 x u16
+            const uint32_t bw[4] = { bins.x, bins.y, bins.z, bins.w };
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+            {
+                const float mg = sqrtf((y[k].x * y[k].x) + (y[k].y * y[k].y));
+                float s = av[r][k];
+                const float old = s * f;
+                s = s - old;
+                const float add = mg * f;
+                s = add + s;
+                if (s < 1) s = 1;
+                av[r][k] = s;
+                const int bin = (bw[k >> 1] >> (16 * (k & 1))) & 0xffff;
+                if (mo) mo[bin] = mg;
+                if (ao) ao[bin] = s;
+            }
+        }
     }
 }
 
+// A call that completes no frame (frames_per_call < fft_len): produce into the carried ring.
+template <int L>
+__global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_accumulate(SpecArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    using G = SpecGeom<L>;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * SPEC_WAVES + w;
+    if (c >= a.C) return;
+    float* S = smem + w * G::PITCH;
+    const SpecParams sp = spec_params<L>(a.plan);
+    float o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
+    if (sp.iq_auto) { o1 = a.teta[c]; o2 = a.teta[a.C + c]; o3 = a.teta[2 * a.C + c]; }
+    const int fill = a.fill0, end = a.fill0 + a.N;
+    float2 z[G::K];
+    produce<L, true>(z, a.iq + (size_t)c * a.ld, fill, end, sp, S, S + G::REGION, o1, o2, o3, lane);
+    float2* __restrict__ carry = (float2*)a.carry + (size_t)c * L;
+#pragma unroll
+    for (int k = 0; k < G::K; ++k)
+    {
+        const int p = lane + 64 * k;
+        if (p >= fill && p < end) carry[p] = z[k];
+    }
+    if (sp.iq_auto && lane == 0) { a.teta[c] = o1; a.teta[a.C + c] = o2; a.teta[2 * a.C + c] = o3; }
+}
+
+// Calls that complete frames: every segment ends a frame; the first may start from the carry.
 template <int L>
 __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int NB = L / 64;                   // bins per lane
-    constexpr int NCALL = L / BLK;               // 32-frame calls per display frame
+    using G = SpecGeom<L>;
+    constexpr int K = G::K, NBF = G::NBF, R3 = G::R3;
     const uhsdr_spectrum_plan* __restrict__ P = a.plan;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * SPEC_WAVES + w;
     if (c >= a.C) return;                        // whole wave; no workgroup barrier below
-    float* X = smem + w * a.lds_pitch;           // the frame, [re = Q, im = I] interleaved
-    float* T = X + 2 * L;                        // auto I/Q: per-call sums, then factors [3][NCALL]
+    float* S = smem + w * G::PITCH;              // auto-I/Q products, then the frame
+    float2* X = (float2*)S;
+    float* T = S + G::REGION;
     const float* __restrict__ tw = P->twiddle;
-    const float* __restrict__ win = P->window;
-    const bool formula = P->window_formula;
-    const bool iq_auto = P->iq_auto_correction;
-    const float gi = P->iq_gain_i, gq = P->iq_gain_q, ph = P->iq_phase_balance, f = P->filt_factor;
+    const SpecParams sp = spec_params<L>(P);
+    const float f = P->filt_factor;
     const int C = a.C, N = a.N;
+    const size_t row = (size_t)c * L;
 
-    int fill = a.fill0;
-    for (int i = lane; i < 2 * fill; i += 64) X[i] = a.carry[(size_t)c * 2 * L + i];
-    float av[NB];
+    // the final-stage outputs this lane owns: positions 8q + k, q = lane + 64r; their running
+    // averages stay in registers (state kept in position order, bins via plan->iperm)
+    float av[R3][8];
 #pragma unroll
-    for (int m = 0; m < NB; ++m) av[m] = a.avg_state[(size_t)c * L + lane + 64 * m];
-    float o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
-    if (iq_auto) { o1 = a.teta[c]; o2 = a.teta[C + c]; o3 = a.teta[2 * C + c]; }
-    const int2* __restrict__ src = a.iq + (size_t)c * a.ld;
-    int frame = 0;
-    for (int n0 = 0; n0 < N;)
+    for (int r = 0; r < R3; ++r)
     {
-        const int seg = min(L - fill, N - n0);   // multiple of 32
-        // ---- convert into the ring ----
-        for (int i = lane; i < seg; i += 64)
-        {
-            const int2 v = src[n0 + i];
-            float I = (float)v.x, Q = (float)v.y;
-            I = I * IQ_BIT_SCALE_DOWN;
-            Q = Q * IQ_BIT_SCALE_DOWN;
-            *(float2*)(X + 2 * (fill + i)) = make_float2(Q, I);
-        }
-        wave_sync();
-        // ---- auto I/Q correction factors per 32-frame call (audio_driver.c:2274-2313) ----
-        if (iq_auto)
-        {
-            const int ncall = seg / BLK;
-            if (lane < ncall)
-            {
-                float t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
-                const float* s = X + 2 * (fill + lane * BLK);
-                for (int i = 0; i < BLK; ++i)
-                {
-                    const float Q = s[2 * i], I = s[2 * i + 1];
-                    t1 += sign_new(I) * Q;
-                    t2 += sign_new(I) * I;
-                    t3 += sign_new(Q) * Q;
-                }
-                T[lane] = t1; T[NCALL + lane] = t2; T[2 * NCALL + lane] = t3;
-            }
-            wave_sync();
-            float m1v = 0.0f, m2v = 0.0f;
-            for (int j = 0; j < ncall; ++j)           // the low-pass recursion, uniform in all lanes
-            {
-                float t1 = T[j], t2 = T[NCALL + j], t3 = T[2 * NCALL + j];
-                t1 = (float)(-0.003 * (double)(t1 / (float)BLK) + 0.997 * (double)o1);
-                t2 = (float)(0.003 * (double)(t2 / (float)BLK) + 0.997 * (double)o2);
-                t3 = (float)(0.003 * (double)(t3 / (float)BLK) + 0.997 * (double)o3);
-                const float M_c1 = (t2 != 0.0f) ? t1 / t2 : 0.0f;
-                float help = (t2 * t2);
-                if (help > 0.0f) help = (t3 * t3 - t1 * t1) / help;
-                const float M_c2 = (help > 0.0f) ? sqrtf(help) : 1.0f;
-                o1 = t1; o2 = t2; o3 = t3;
-                if (j == lane) { m1v = M_c1; m2v = M_c2; }
-            }
-            wave_sync();
-            if (lane < ncall) { T[lane] = m1v; T[NCALL + lane] = m2v; }
-            wave_sync();
-        }
-        // ---- correction + window, in place ----
-        for (int i = lane; i < seg; i += 64)
-        {
-            const int p = fill + i;
-            const float2 v = *(const float2*)(X + 2 * p);
-            float Q = v.x, I = v.y;
-            if (!iq_auto)
-            {
-                I = I * gi;
-                Q = Q * gq;
-                if (ph < 0) { const float e3 = I * ph; Q = Q + e3; }
-                else if (ph > 0) { const float e3 = Q * ph; I = I + e3; }
-            }
-            else
-            {
-                const int j = i / BLK;
-                Q += T[j] * I;
-                I = I * T[NCALL + j];
-            }
-            const float2 wv = *(const float2*)(win + 2 * p);
-            float wq, wi;
-            if (formula) { wq = 0.5f * (wv.x * Q); wi = 0.5f * (wv.y * I); }
-            else { wq = Q * wv.x; wi = I * wv.y; }
-            *(float2*)(X + 2 * p) = make_float2(wq, wi);
-        }
-        wave_sync();
-        fill += seg;
-        n0 += seg;
-        if (fill < L) break;                     // frame continues in the next call
-        // ---- one display frame ----
-        cfft<L>(X, tw, lane);
-        float* mo = a.mag ? a.mag + ((size_t)c * a.F + frame) * L : nullptr;
-        float* ao = a.avg ? a.avg + ((size_t)c * a.F + frame) * L : nullptr;
+        const int q = lane + 64 * r;
 #pragma unroll
-        for (int m = 0; m < NB; ++m)
-        {
-            const int k = lane + 64 * m;
-            const float2 v = *(const float2*)(X + 2 * (int)P->perm[k]);
-            const float mg = sqrtf((v.x * v.x) + (v.y * v.y));
-            float s = av[m];
-            const float old = s * f;
-            s = s - old;
-            const float add = mg * f;
-            s = add + s;
-            if (s < 1) s = 1;
-            av[m] = s;
-            if (mo) mo[k] = mg;
-            if (ao) ao[k] = s;
-        }
-        wave_sync();
-        ++frame;
-        fill = 0;
+        for (int k = 0; k < 8; ++k) av[r][k] = q < NBF ? a.avg_state[row + 8 * q + k] : 0.0f;
     }
-    for (int i = lane; i < 2 * fill; i += 64) a.carry[(size_t)c * 2 * L + i] = X[i];
+    float o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
+    if (sp.iq_auto) { o1 = a.teta[c]; o2 = a.teta[C + c]; o3 = a.teta[2 * C + c]; }
+    const int2* __restrict__ src = a.iq + (size_t)c * a.ld;
+
+    int n0 = 0, frame = 0;
+    if (a.fill0)
+    {
+        // ---- the frame begun in earlier calls ----
+        const float2* __restrict__ carry = (const float2*)a.carry + (size_t)c * L;
+        float2 z[K];
 #pragma unroll
-    for (int m = 0; m < NB; ++m) a.avg_state[(size_t)c * L + lane + 64 * m] = av[m];
-    if (iq_auto && lane == 0) { a.teta[c] = o1; a.teta[C + c] = o2; a.teta[2 * C + c] = o3; }
+        for (int k = 0; k < K; ++k)
+        {
+            const int p = lane + 64 * k;
+            z[k] = carry[p < a.fill0 ? p : 0];
+        }
+        produce<L, true>(z, src, a.fill0, L, sp, S, T, o1, o2, o3, lane);
+        spectrum_frame<L>(z, X, tw, av, f, a, c, frame, lane);
+        n0 = L - a.fill0;
+        ++frame;
+    }
+    for (; n0 < N; n0 += L, ++frame)
+    {
+        // per-frame reloads (L1-resident) instead of loop-invariant registers: keeps the window
+        // and the twiddles from being hoisted out of the frame loop into VGPRs
+        SpecParams spf = sp;
+        const float* __restrict__ twf = tw;
+        asm volatile("" : "+s"(spf.win), "+s"(twf));
+        float2 z[K];
+        produce<L, false>(z, src + n0, 0, L, spf, S, T, o1, o2, o3, lane);
+        spectrum_frame<L>(z, X, twf, av, f, a, c, frame, lane);
+    }
+#pragma unroll
+    for (int r = 0; r < R3; ++r)
+    {
+        const int q = lane + 64 * r;
+        if (q < NBF)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a.avg_state[row + 8 * q + k] = av[r][k];
+    }
+    if (sp.iq_auto && lane == 0) { a.teta[c] = o1; a.teta[C + c] = o2; a.teta[2 * C + c] = o3; }
 }
 
 } // namespace
@@ -378,7 +485,10 @@ struct uhsdr_spectrum_s
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { uhsdr_set_error("%s: %s", #x, hipGetErrorString(e_)); return UHSDR_DEVICE_ERROR; } } while (0)
 
-static int spec_pitch(int L) { return 2 * L + 3 * (L / BLK) + 4; }
+static int spec_pitch(int L)
+{
+    return L == 256 ? SpecGeom<256>::PITCH : (L == 512 ? SpecGeom<512>::PITCH : SpecGeom<1024>::PITCH);
+}
 
 extern "C" uhsdr_status uhsdr_spectrum_reset(uhsdr_spectrum_handle h)
 {
@@ -442,12 +552,16 @@ extern "C" uhsdr_status uhsdr_spectrum_process(uhsdr_spectrum_handle h, const in
     sa.lds_pitch = spec_pitch(h->L);
     const size_t lds = sizeof(float) * (size_t)SPEC_WAVES * sa.lds_pitch;
     const dim3 grid((h->C + SPEC_WAVES - 1) / SPEC_WAVES), block(64 * SPEC_WAVES);
+    const bool completes = h->fill + h->N >= h->L;
+#define SPEC_LAUNCH(LEN) do { if (completes) hipLaunchKernelGGL(spectrum_frames<LEN>, grid, block, lds, h->stream, sa); \
+                              else hipLaunchKernelGGL(spectrum_accumulate<LEN>, grid, block, lds, h->stream, sa); } while (0)
     switch (h->L)
     {
-    case 256: hipLaunchKernelGGL(spectrum_frames<256>, grid, block, lds, h->stream, sa); break;
-    case 512: hipLaunchKernelGGL(spectrum_frames<512>, grid, block, lds, h->stream, sa); break;
-    default: hipLaunchKernelGGL(spectrum_frames<1024>, grid, block, lds, h->stream, sa); break;
+    case 256: SPEC_LAUNCH(256); break;
+    case 512: SPEC_LAUNCH(512); break;
+    default: SPEC_LAUNCH(1024); break;
     }
+#undef SPEC_LAUNCH
     HIPCHK(hipGetLastError());
     const int done = (h->fill + h->N) / h->L;
     h->fill = (h->fill + h->N) % h->L;

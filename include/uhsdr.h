@@ -319,6 +319,8 @@ typedef struct uhsdr_spectrum_plan
     uint16_t bitrev[UHSDR_SPECTRUM_MAX_BITREV];    /* armBitRevIndexTable<L>: byte-offset swap pairs */
     uint16_t perm[UHSDR_SPECTRUM_MAX_LEN];         /* bin k of the output = butterfly result perm[k] */
     uint16_t iperm[UHSDR_SPECTRUM_MAX_LEN];        /* butterfly result p lands in bin iperm[p] */
+    float   tw_lane[8][64][2];    /* the first-stage twiddles each of 64 lanes uses, laid out per lane
+                                     (same values as twiddle[]; device read coalescing only) */
     int32_t reserved[16];
 } uhsdr_spectrum_plan;
 

@@ -17,10 +17,9 @@ meta = {}
 for f in sorted(glob.glob(os.path.join(base, "p*", "pmc_counter_collection.csv"))):
     for row in csv.DictReader(open(f)):
         name = row["Kernel_Name"]
-        if "rx_front" in name:
-            k = "rx_front"
-        elif "rx_back" in name:
-            k = "rx_back"
+        for k in ("rx_front", "rx_back", "rx_fm", "tx_voice", "tx_iq", "spectrum_frames", "spectrum_accumulate"):
+            if k in name:
+                break
         else:
             continue
         key = (row["Dispatch_Id"], f)

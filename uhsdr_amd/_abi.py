@@ -125,7 +125,7 @@ class SpectrumPlan(C.Structure):
         ("filt_factor", C.c_float), ("bitrev_len", C.c_int32),
         ("window", C.c_float * (2 * SPECTRUM_MAX_LEN)), ("twiddle", C.c_float * (2 * SPECTRUM_MAX_LEN)),
         ("bitrev", C.c_uint16 * SPECTRUM_MAX_BITREV), ("perm", C.c_uint16 * SPECTRUM_MAX_LEN),
-        ("iperm", C.c_uint16 * SPECTRUM_MAX_LEN),
+        ("iperm", C.c_uint16 * SPECTRUM_MAX_LEN), ("tw_lane", C.c_float * (8 * 64 * 2)),
         ("reserved", C.c_int32 * 16),
     ]
 

@@ -599,6 +599,18 @@ uhsdr_status uhsdr_spectrum_plan_build(const uhsdr_spectrum_config* cfg, uhsdr_s
             p->perm[b] = t;
         }
     for (int k = 0; k < L; ++k) p->iperm[p->perm[k]] = (uint16_t)k;
+    /* per-lane copies of the first-stage twiddles (uhsdr_spectrum.hip): radix-8 stage of span
+       L (512 / 1024: twiddle k * lane * tm, tm = 1024 / L) or the radix-4 rows of the 256-point
+       split (twiddles t, 2t, 3t of row t = lane <= 32 ? lane : 64 - lane) */
+    for (int lane = 0; lane < 64; ++lane)
+        for (int k = 0; k < 8; ++k)
+        {
+            int idx = 0;
+            if (L == 256) idx = k >= 1 && k <= 3 ? k * (lane <= 32 ? lane : 64 - lane) : 0;
+            else idx = k * lane * (L == 1024 ? 2 : 1);
+            p->tw_lane[k][lane][0] = p->twiddle[2 * idx];
+            p->tw_lane[k][lane][1] = p->twiddle[2 * idx + 1];
+        }
     return UHSDR_OK;
 }
 

@@ -89,6 +89,23 @@ __device__ __forceinline__ void dft8(float2* z, const float* __restrict__ tw, in
     }
 }
 
+// the same butterfly with per-lane twiddles (plan->tw_lane[k][lane], coalesced); lane 0 of a
+// first stage is the reference's twiddle-free group j = 0
+__device__ __forceinline__ void dft8_lane(float2* z, const float* __restrict__ twl, int lane)
+{
+    dft8(z, nullptr, 0);
+    if (lane)
+    {
+#pragma unroll
+        for (int k = 1; k < 8; ++k)
+        {
+            const float2 t = *(const float2*)(twl + k * 128 + 2 * lane);
+            const float p1 = t.x * z[k].x, p2 = t.y * z[k].y, p3 = t.x * z[k].y, p4 = t.y * z[k].x;
+            z[k] = make_float2(p1 + p2, p3 - p4);
+        }
+    }
+}
+
 __device__ __forceinline__ float2 rot_fwd(float2 x, float2 t)
 {
     const float m0 = x.x * t.x, m1 = x.y * t.y, m2 = x.y * t.x, m3 = x.x * t.y;
@@ -117,7 +134,7 @@ __device__ __forceinline__ void split_by2_regs(float2 (&z)[16], const float* __r
 // arm_cfft_radix8by4_f32 split (arm_cfft_f32.c:319-557), n = 256, row r = lane of the four
 // quarters (z[k] = x[r + 64k]): rows 0..32 are the reference's TOP rows t = r (t = 0
 // untwiddled, t = 32 its MIDDLE block), rows 33..63 its BOTTOM rows 64 - t with the twiddles of t
-__device__ __forceinline__ void split_by4_regs(float2 (&z)[4], const float* __restrict__ tw, int lane)
+__device__ __forceinline__ void split_by4_regs(float2 (&z)[4], const float* __restrict__ twl, int lane)
 {
     constexpr int Q = 64;
     const bool top = lane <= Q / 2;
@@ -125,7 +142,9 @@ __device__ __forceinline__ void split_by4_regs(float2 (&z)[4], const float* __re
     const float2 x1 = z[0], x2 = z[1], x3 = z[2], x4 = z[3];
     const float s13r = x1.x + x3.x, d13r = x1.x - x3.x;
     const float s13i = x1.y + x3.y, d13i = x1.y - x3.y;
-    const float2 w2 = *(const float2*)(tw + 2 * t), w3 = *(const float2*)(tw + 4 * t), w4 = *(const float2*)(tw + 6 * t);
+    // twiddles t, 2t, 3t of the row (plan->tw_lane[1..3][lane])
+    const float2 w2 = *(const float2*)(twl + 128 + 2 * lane), w3 = *(const float2*)(twl + 256 + 2 * lane),
+                 w4 = *(const float2*)(twl + 384 + 2 * lane);
     z[0] = make_float2(s13r + x2.x + x4.x, s13i + x2.y + x4.y);
     if (top)
     {
@@ -180,7 +199,6 @@ struct SpecParams
 {
     const float* win;
     float gi, gq, ph;
-    bool formula, iq_auto;
 };
 
 // Producer side for the lane's positions p = lane + 64k of one segment [fill, end) of a frame:
@@ -188,13 +206,14 @@ struct SpecParams
 // statistics summed in sample order through LDS), window (ui_spectrum.c:402-414).  PART: the
 // segment does not start at 0 (positions below fill hold the carried, already windowed values)
 // or does not reach L.  Positions outside [fill, end) are left alone.
-template <int L, bool PART>
+template <int L, bool PART, bool AUTO>
 __device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2* __restrict__ src, int fill, int end,
                                         const SpecParams& sp, float* S, float* T, float& o1, float& o2, float& o3,
                                         int lane)
 {
     using G = SpecGeom<L>;
     constexpr int K = G::K, NCALL = G::NCALL;
+    constexpr bool FORMULA = L == 1024;          // plan->window_formula (checked on the host)
     auto in_seg = [&](int p) { return !PART || (p >= fill && p < end); };
 #pragma unroll
     for (int k = 0; k < K; ++k)
@@ -209,7 +228,7 @@ __device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2*
             z[k] = make_float2(Q, I);
         }
     }
-    if (sp.iq_auto)
+    if constexpr (AUTO)
     {
         // per-call sums of sgn(I)Q, sgn(I)I, sgn(Q)Q in sample order (audio_driver.c:2274-2285):
         // the products are exact, so they are formed here and summed sequentially per call
@@ -264,12 +283,14 @@ __device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2*
         if (in_seg(p))
         {
             float Q = z[k].x, I = z[k].y;
-            if (!sp.iq_auto)
+            if constexpr (!AUTO)
             {
                 I = I * sp.gi;
                 Q = Q * sp.gq;
-                if (sp.ph < 0) { const float e3 = I * sp.ph; Q = Q + e3; }
-                else if (sp.ph > 0) { const float e3 = Q * sp.ph; I = I + e3; }
+                // AudioDriver_IQPhaseAdjust (:1776-1801) as selects on the uniform sign of ph
+                const float qa = Q + I * sp.ph, ia = I + Q * sp.ph;
+                Q = sp.ph < 0 ? qa : Q;
+                I = sp.ph > 0 ? ia : I;
             }
             else
             {
@@ -277,7 +298,7 @@ __device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2*
                 I = I * T[4 * NCALL + (p >> 5)];
             }
             const float2 wv = *(const float2*)(sp.win + 2 * p);
-            if (sp.formula) z[k] = make_float2(0.5f * (wv.x * Q), 0.5f * (wv.y * I));
+            if constexpr (FORMULA) z[k] = make_float2(0.5f * (wv.x * Q), 0.5f * (wv.y * I));
             else z[k] = make_float2(Q * wv.x, I * wv.y);
         }
     }
@@ -289,8 +310,6 @@ __device__ __forceinline__ SpecParams spec_params(const uhsdr_spectrum_plan* __r
     SpecParams sp;
     sp.win = P->window;
     sp.gi = P->iq_gain_i; sp.gq = P->iq_gain_q; sp.ph = P->iq_phase_balance;
-    sp.formula = P->window_formula;
-    sp.iq_auto = P->iq_auto_correction;
     return sp;
 }
 
@@ -306,19 +325,20 @@ __device__ __forceinline__ void spectrum_frame(float2 (&z)[SpecGeom<L>::K], floa
     using G = SpecGeom<L>;
     constexpr int K = G::K, NBF = G::NBF, R3 = G::R3;
     const uhsdr_spectrum_plan* __restrict__ P = a.plan;
+    const float* __restrict__ twl = &P->tw_lane[0][0][0];
     if constexpr (L == 1024)
     {
         split_by2_regs(z, tw, lane);
-        dft8(z, tw, lane * 2);                   // radix-8 stage span 512 of each half (j = lane)
-        dft8(z + 8, tw, lane * 2);
+        dft8_lane(z, twl, lane);                 // radix-8 stage span 512 of each half (j = lane)
+        dft8_lane(z + 8, twl, lane);
     }
     else if constexpr (L == 512)
     {
-        dft8(z, tw, lane);
+        dft8_lane(z, twl, lane);
     }
     else
     {
-        split_by4_regs(z, tw, lane);
+        split_by4_regs(z, twl, lane);
     }
     wave_sync();                                 // earlier LDS readers (scratch / last frame) done
 #pragma unroll
@@ -338,24 +358,32 @@ __device__ __forceinline__ void spectrum_frame(float2 (&z)[SpecGeom<L>::K], floa
         for (int k = 0; k < 8; ++k) X[padp(base + 8 * k)] = y[k];
     }
     wave_sync();
-    float* __restrict__ mo = a.mag ? a.mag + ((size_t)c * a.F + frame) * L : nullptr;
-    float* __restrict__ ao = a.avg ? a.avg + ((size_t)c * a.F + frame) * L : nullptr;
+    float2 y[R3][8];
 #pragma unroll
     for (int r = 0; r < R3; ++r)
     {
         const int q = lane + 64 * r;
         if (q < NBF)
         {
-            float2 y[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) y[k] = X[padp(8 * q + k)];
-            dft8(y, tw, 0);
+            for (int k = 0; k < 8; ++k) y[r][k] = X[padp(8 * q + k)];
+            dft8(y[r], tw, 0);
+        }
+    }
+    wave_sync();                                 // the frame is consumed: its LDS now stages the outputs
+    float* O = (float*)X;                        // [2][L] in bin order
+#pragma unroll
+    for (int r = 0; r < R3; ++r)
+    {
+        const int q = lane + 64 * r;
+        if (q < NBF)
+        {
             const uint4 bins = *(const uint4*)(P->iperm + 8 * q);   // 8 x u16
             const uint32_t bw[4] = { bins.x, bins.y, bins.z, bins.w };
 #pragma unroll
             for (int k = 0; k < 8; ++k)
             {
-                const float mg = sqrtf((y[k].x * y[k].x) + (y[k].y * y[k].y));
+                const float mg = sqrtf((y[r][k].x * y[r][k].x) + (y[r][k].y * y[r][k].y));
                 float s = av[r][k];
                 const float old = s * f;
                 s = s - old;
@@ -364,15 +392,26 @@ __device__ __forceinline__ void spectrum_frame(float2 (&z)[SpecGeom<L>::K], floa
                 if (s < 1) s = 1;
                 av[r][k] = s;
                 const int bin = (bw[k >> 1] >> (16 * (k & 1))) & 0xffff;
-                if (mo) mo[bin] = mg;
-                if (ao) ao[bin] = s;
+                O[bin] = mg;
+                O[L + bin] = s;
             }
         }
     }
+    wave_sync();
+    float* __restrict__ mo = a.mag ? a.mag + ((size_t)c * a.F + frame) * L : nullptr;
+    float* __restrict__ ao = a.avg ? a.avg + ((size_t)c * a.F + frame) * L : nullptr;
+#pragma unroll
+    for (int m = 0; m < L / 256; ++m)
+    {
+        const int i = 4 * (lane + 64 * m);
+        if (mo) *(float4*)(mo + i) = *(const float4*)(O + i);
+        if (ao) *(float4*)(ao + i) = *(const float4*)(O + L + i);
+    }
+    wave_sync();                                 // staged outputs read before the next frame lands
 }
 
 // A call that completes no frame (frames_per_call < fft_len): produce into the carried ring.
-template <int L>
+template <int L, bool AUTO>
 __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_accumulate(SpecArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -380,13 +419,13 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_accumulate(SpecArgs 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * SPEC_WAVES + w;
     if (c >= a.C) return;
-    float* S = smem + w * G::PITCH;
+    float* S = smem + w * a.lds_pitch;
     const SpecParams sp = spec_params<L>(a.plan);
     float o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
-    if (sp.iq_auto) { o1 = a.teta[c]; o2 = a.teta[a.C + c]; o3 = a.teta[2 * a.C + c]; }
+    if (AUTO) { o1 = a.teta[c]; o2 = a.teta[a.C + c]; o3 = a.teta[2 * a.C + c]; }
     const int fill = a.fill0, end = a.fill0 + a.N;
     float2 z[G::K];
-    produce<L, true>(z, a.iq + (size_t)c * a.ld, fill, end, sp, S, S + G::REGION, o1, o2, o3, lane);
+    produce<L, true, AUTO>(z, a.iq + (size_t)c * a.ld, fill, end, sp, S, S + G::REGION, o1, o2, o3, lane);
     float2* __restrict__ carry = (float2*)a.carry + (size_t)c * L;
 #pragma unroll
     for (int k = 0; k < G::K; ++k)
@@ -394,11 +433,11 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_accumulate(SpecArgs 
         const int p = lane + 64 * k;
         if (p >= fill && p < end) carry[p] = z[k];
     }
-    if (sp.iq_auto && lane == 0) { a.teta[c] = o1; a.teta[a.C + c] = o2; a.teta[2 * a.C + c] = o3; }
+    if (AUTO && lane == 0) { a.teta[c] = o1; a.teta[a.C + c] = o2; a.teta[2 * a.C + c] = o3; }
 }
 
 // Calls that complete frames: every segment ends a frame; the first may start from the carry.
-template <int L>
+template <int L, bool AUTO>
 __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -408,9 +447,9 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * SPEC_WAVES + w;
     if (c >= a.C) return;                        // whole wave; no workgroup barrier below
-    float* S = smem + w * G::PITCH;              // auto-I/Q products, then the frame
+    float* S = smem + w * a.lds_pitch;           // auto-I/Q products, then the frame
     float2* X = (float2*)S;
-    float* T = S + G::REGION;
+    float* T = S + G::REGION;                    // used only with auto I/Q correction
     const float* __restrict__ tw = P->twiddle;
     const SpecParams sp = spec_params<L>(P);
     const float f = P->filt_factor;
@@ -428,7 +467,7 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
         for (int k = 0; k < 8; ++k) av[r][k] = q < NBF ? a.avg_state[row + 8 * q + k] : 0.0f;
     }
     float o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
-    if (sp.iq_auto) { o1 = a.teta[c]; o2 = a.teta[C + c]; o3 = a.teta[2 * C + c]; }
+    if (AUTO) { o1 = a.teta[c]; o2 = a.teta[C + c]; o3 = a.teta[2 * C + c]; }
     const int2* __restrict__ src = a.iq + (size_t)c * a.ld;
 
     int n0 = 0, frame = 0;
@@ -443,7 +482,7 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
             const int p = lane + 64 * k;
             z[k] = carry[p < a.fill0 ? p : 0];
         }
-        produce<L, true>(z, src, a.fill0, L, sp, S, T, o1, o2, o3, lane);
+        produce<L, true, AUTO>(z, src, a.fill0, L, sp, S, T, o1, o2, o3, lane);
         spectrum_frame<L>(z, X, tw, av, f, a, c, frame, lane);
         n0 = L - a.fill0;
         ++frame;
@@ -456,7 +495,7 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
         const float* __restrict__ twf = tw;
         asm volatile("" : "+s"(spf.win), "+s"(twf));
         float2 z[K];
-        produce<L, false>(z, src + n0, 0, L, spf, S, T, o1, o2, o3, lane);
+        produce<L, false, AUTO>(z, src + n0, 0, L, spf, S, T, o1, o2, o3, lane);
         spectrum_frame<L>(z, X, twf, av, f, a, c, frame, lane);
     }
 #pragma unroll
@@ -467,7 +506,7 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
 #pragma unroll
             for (int k = 0; k < 8; ++k) a.avg_state[row + 8 * q + k] = av[r][k];
     }
-    if (sp.iq_auto && lane == 0) { a.teta[c] = o1; a.teta[C + c] = o2; a.teta[2 * C + c] = o3; }
+    if (AUTO && lane == 0) { a.teta[c] = o1; a.teta[C + c] = o2; a.teta[2 * C + c] = o3; }
 }
 
 } // namespace
@@ -485,9 +524,13 @@ struct uhsdr_spectrum_s
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { uhsdr_set_error("%s: %s", #x, hipGetErrorString(e_)); return UHSDR_DEVICE_ERROR; } } while (0)
 
-static int spec_pitch(int L)
+// LDS floats per wave: the padded frame; with auto I/Q correction also the product scratch and
+// the per-call sums / factors behind it
+template <int L>
+static int spec_pitch_t(bool iq_auto) { return iq_auto ? SpecGeom<L>::PITCH : SpecGeom<L>::FRAME + 4; }
+static int spec_pitch(int L, bool iq_auto)
 {
-    return L == 256 ? SpecGeom<256>::PITCH : (L == 512 ? SpecGeom<512>::PITCH : SpecGeom<1024>::PITCH);
+    return L == 256 ? spec_pitch_t<256>(iq_auto) : (L == 512 ? spec_pitch_t<512>(iq_auto) : spec_pitch_t<1024>(iq_auto));
 }
 
 extern "C" uhsdr_status uhsdr_spectrum_reset(uhsdr_spectrum_handle h)
@@ -508,6 +551,12 @@ extern "C" uhsdr_status uhsdr_spectrum_create(const uhsdr_spectrum_config* cfg, 
     uhsdr_status st = uhsdr_spectrum_plan_build(cfg, &h->plan);
     if (st != UHSDR_OK) { free(h); return st; }
     const int L = h->plan.fft_len;
+    if ((L == 1024) != (h->plan.window_formula != 0))
+    {
+        free(h);
+        uhsdr_set_error("window kind does not match fft_len %d", L);
+        return UHSDR_UNSUPPORTED;
+    }
     if (N % BLK || (N % L && L % N))
     {
         free(h);
@@ -549,12 +598,14 @@ extern "C" uhsdr_status uhsdr_spectrum_process(uhsdr_spectrum_handle h, const in
     sa.teta = h->teta; sa.avg_state = h->avg; sa.carry = h->carry;
     sa.mag = mag; sa.avg = avg;
     sa.C = h->C; sa.N = h->N; sa.ld = h->N; sa.F = h->F; sa.fill0 = h->fill;
-    sa.lds_pitch = spec_pitch(h->L);
+    sa.lds_pitch = spec_pitch(h->L, h->plan.iq_auto_correction != 0);
     const size_t lds = sizeof(float) * (size_t)SPEC_WAVES * sa.lds_pitch;
     const dim3 grid((h->C + SPEC_WAVES - 1) / SPEC_WAVES), block(64 * SPEC_WAVES);
     const bool completes = h->fill + h->N >= h->L;
-#define SPEC_LAUNCH(LEN) do { if (completes) hipLaunchKernelGGL(spectrum_frames<LEN>, grid, block, lds, h->stream, sa); \
-                              else hipLaunchKernelGGL(spectrum_accumulate<LEN>, grid, block, lds, h->stream, sa); } while (0)
+    const bool au = h->plan.iq_auto_correction != 0;
+#define SPEC_LAUNCH2(LEN, AU) do { if (completes) hipLaunchKernelGGL((spectrum_frames<LEN, AU>), grid, block, lds, h->stream, sa); \
+                                   else hipLaunchKernelGGL((spectrum_accumulate<LEN, AU>), grid, block, lds, h->stream, sa); } while (0)
+#define SPEC_LAUNCH(LEN) do { if (au) SPEC_LAUNCH2(LEN, true); else SPEC_LAUNCH2(LEN, false); } while (0)
     switch (h->L)
     {
     case 256: SPEC_LAUNCH(256); break;
@@ -562,6 +613,7 @@ extern "C" uhsdr_status uhsdr_spectrum_process(uhsdr_spectrum_handle h, const in
     default: SPEC_LAUNCH(1024); break;
     }
 #undef SPEC_LAUNCH
+#undef SPEC_LAUNCH2
     HIPCHK(hipGetLastError());
     const int done = (h->fill + h->N) / h->L;
     h->fill = (h->fill + h->N) % h->L;

@@ -178,8 +178,9 @@ __device__ __forceinline__ void split_by4_regs(float2 (&z)[4], const float* __re
 }
 
 // Frame layout per wave (LDS): the frame as padded complex; before the frame is written there,
-// the same words hold the auto-I/Q products of this segment ([3][L], swizzled per call so the
-// sequential per-call sums read conflict-free), then T = [5][NCALL] sums / factors.
+// the same words hold the auto-I/Q products of this segment ([3][32][33]: sample-in-call major,
+// so the per-call sequential sums of 32 lanes read consecutive words), then T = [5][NCALL]
+// sums / factors.
 template <int L>
 struct SpecGeom
 {
@@ -190,7 +191,8 @@ struct SpecGeom
     static constexpr int SUBN = L == 256 ? 64 : 512;       // sub-array of the middle radix-8 stage
     static constexpr int TMID = L == 1024 ? 16 : (L == 512 ? 8 : 4);   // its twiddle modifier
     static constexpr int FRAME = 2 * (L + L / 8);          // floats, padded complex
-    static constexpr int SCRATCH = 3 * L;
+    static constexpr int PROD = 32 * 33;                   // one product array, [i][call], padded
+    static constexpr int SCRATCH = 3 * PROD;
     static constexpr int REGION = FRAME > SCRATCH ? FRAME : SCRATCH;
     static constexpr int PITCH = REGION + 5 * NCALL + 4;   // floats per wave
 };
@@ -238,12 +240,11 @@ __device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2*
             const int p = lane + 64 * k;
             if (in_seg(p))
             {
-                const int j = p >> 5, i = p & 31;
-                const int at = j * 32 + (i ^ j);
+                const int at = (p & 31) * 33 + (p >> 5);      // transposed, padded: [i][33]
                 const float Q = z[k].x, I = z[k].y;
                 S[at] = sign_new(I) * Q;
-                S[L + at] = sign_new(I) * I;
-                S[2 * L + at] = sign_new(Q) * Q;
+                S[G::PROD + at] = sign_new(I) * I;
+                S[2 * G::PROD + at] = sign_new(Q) * Q;
             }
         }
         wave_sync();
@@ -251,30 +252,40 @@ __device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2*
         if (j < (end >> 5))
         {
             float t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
+#pragma unroll 4
             for (int i = 0; i < BLK; ++i)
             {
-                const int at = j * 32 + (i ^ j);
+                const int at = i * 33 + j;
                 t1 += S[at];
-                t2 += S[L + at];
-                t3 += S[2 * L + at];
+                t2 += S[G::PROD + at];
+                t3 += S[2 * G::PROD + at];
             }
             T[j] = t1; T[NCALL + j] = t2; T[2 * NCALL + j] = t3;
         }
         wave_sync();
-        for (int jj = fill >> 5; jj < (end >> 5); ++jj)        // the low-pass recursion, uniform
+        // the low-pass recursion (:2288-2290) is the only serial part: uniform in all lanes, each
+        // lane keeping the state after its own call; the factors (:2292-2303) then in parallel
+        float m1 = 0.0f, m2 = 0.0f, m3 = 0.0f;
+#pragma unroll 1
+        for (int jj = fill >> 5; jj < (end >> 5); ++jj)
         {
-            float t1 = T[jj], t2 = T[NCALL + jj], t3 = T[2 * NCALL + jj];
-            t1 = (float)(-0.003 * (double)(t1 / (float)BLK) + 0.997 * (double)o1);
-            t2 = (float)(0.003 * (double)(t2 / (float)BLK) + 0.997 * (double)o2);
-            t3 = (float)(0.003 * (double)(t3 / (float)BLK) + 0.997 * (double)o3);
+            o1 = (float)(-0.003 * (double)(T[jj] / (float)BLK) + 0.997 * (double)o1);
+            o2 = (float)(0.003 * (double)(T[NCALL + jj] / (float)BLK) + 0.997 * (double)o2);
+            o3 = (float)(0.003 * (double)(T[2 * NCALL + jj] / (float)BLK) + 0.997 * (double)o3);
+            if (jj == j) { m1 = o1; m2 = o2; m3 = o3; }
+        }
+        if (j < (end >> 5))
+        {
+            const float t1 = m1, t2 = m2, t3 = m3;
             const float M_c1 = (t2 != 0.0f) ? t1 / t2 : 0.0f;
             float help = (t2 * t2);
             if (help > 0.0f) help = (t3 * t3 - t1 * t1) / help;
             const float M_c2 = (help > 0.0f) ? sqrtf(help) : 1.0f;
-            o1 = t1; o2 = t2; o3 = t3;
-            if (lane == 0) { T[3 * NCALL + jj] = M_c1; T[4 * NCALL + jj] = M_c2; }
+            T[3 * NCALL + j] = M_c1;
+            T[4 * NCALL + j] = M_c2;
         }
         wave_sync();
+        __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k)
@@ -301,6 +312,8 @@ __device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2*
             if constexpr (FORMULA) z[k] = make_float2(0.5f * (wv.x * Q), 0.5f * (wv.y * I));
             else z[k] = make_float2(Q * wv.x, I * wv.y);
         }
+        if constexpr (AUTO)
+            if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight
     }
 }
 

@@ -108,7 +108,11 @@ typedef struct uhsdr_rx_config
     int32_t fade_leveler;         /* ads.fade_leveler (1) */
     int32_t fm_sql_threshold;     /* ts.fm_sql_threshold (FM_SQUELCH_DEFAULT 12, audio_driver.h:449) */
     int32_t fm_deviation_5k;      /* FLAGS2_FM_MODE_DEVIATION_5KHZ (RadioManagement_FmDevIs5khz) */
-    int32_t reserved[9];
+    int32_t cw_sidetone_freq;     /* ts.cw_sidetone_freq (750): the CW decoder's Goertzel frequency */
+    int32_t cw_decoder_blocksize; /* cw_decoder_config.blocksize (88, 8..128, cw_decoder.h:12-13) */
+    int32_t cw_decoder_thresh;    /* cw_decoder_config.thresh (32000, cw_decoder.h:15-17) */
+    int32_t cw_decoder_noisecancel; /* cw_decoder_config.noisecancel_enable (1) */
+    int32_t reserved[5];
 } uhsdr_rx_config;
 
 /* AudioAgc_SetupAgcWdsp() results (audio_agc.c:126-339) */
@@ -175,7 +179,12 @@ typedef struct uhsdr_rx_plan
     int32_t sq_stages;            /* IIR_Squelch_HPF = IIR_15k_hpf (audio_driver.c:481-484) */
     float   sq_k[UHSDR_MAX_LATTICE];
     float   sq_v[UHSDR_MAX_LATTICE + 1];
-    int32_t reserved[64];
+    /* CW decoder front end (CwDecode_RxProcessor, cw_decoder.c:383-397, 182-316): Goertzel per
+       block on a_buffer[0] after biquad_1, in CW / AM / SAM at 12 ksps (audio_driver.c:2550-2557) */
+    int32_t cw_enabled, cw_blocksize, cw_noisecancel;
+    float   cw_thresh;
+    float   cw_r, cw_cos, cw_sin;     /* AudioFilter_CalcGoertzel (audio_filter.c:1281-1288) */
+    int32_t reserved[57];
 } uhsdr_rx_plan;
 
 typedef struct uhsdr_rx_s* uhsdr_rx_handle;
@@ -343,6 +352,14 @@ uhsdr_status uhsdr_spectrum_get_plan(uhsdr_spectrum_handle h, uhsdr_spectrum_pla
 uhsdr_status uhsdr_spectrum_destroy(uhsdr_spectrum_handle h);
 int32_t      uhsdr_sizeof_spectrum_config(void);
 int32_t      uhsdr_sizeof_spectrum_plan(void);
+
+/* CW decoder front end outputs of the following uhsdr_rx_process calls (device pointers, either
+   may be NULL): signal = ads.CW_signal after every 32-frame call, uint8 [C][N/32];
+   energy = the Goertzel energy of every CW block completed, f32 [C][uhsdr_rx_cw_blocks_max(h)],
+   the first uhsdr_rx_cw_blocks_last(h) of them valid after a call. */
+uhsdr_status uhsdr_rx_set_cw_outputs(uhsdr_rx_handle h, uint8_t* signal, float* energy);
+int32_t      uhsdr_rx_cw_blocks_max(uhsdr_rx_handle h);
+int32_t      uhsdr_rx_cw_blocks_last(uhsdr_rx_handle h);
 
 /* ---- diagnostics ---- */
 const char*  uhsdr_version(void);

@@ -29,6 +29,8 @@ def load():
         lib.uo_rx_process.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         lib.uo_rx_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                             C.c_void_p, C.c_void_p, C.c_int]
+        lib.uo_rx_process_batch_cw.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         lib.uo_tx_state_size.restype = C.c_size_t
         lib.uo_tx_state_init.argtypes = [C.c_void_p, C.c_void_p]
         lib.uo_tx_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
@@ -91,6 +93,22 @@ class OracleTx:
         if st != 0:
             raise RuntimeError(f"uo_tx_process_batch status {st}")
         return iq, a0
+
+
+def rx_process_cw(orx, iq: np.ndarray, bmax: int, threads: int = 1):
+    """OracleRx.process plus the CW decoder front end: -> (a1, dst, signal [C][n/32], energy [C][bmax])"""
+    iq = np.ascontiguousarray(iq, dtype=np.int32)
+    Cn, n, _ = iq.shape
+    a1 = np.empty((Cn, n), np.float32)
+    dst = np.empty((Cn, n, 2), np.int32)
+    sig = np.zeros((Cn, n // 32), np.uint8)
+    en = np.zeros((Cn, max(bmax, 1)), np.float32)
+    st = orx.lib.uo_rx_process_batch_cw(C.byref(orx.plan), orx.states, Cn, iq.ctypes.data_as(C.c_void_p), n,
+                                        a1.ctypes.data_as(C.c_void_p), dst.ctypes.data_as(C.c_void_p),
+                                        sig.ctypes.data_as(C.c_void_p), en.ctypes.data_as(C.c_void_p), bmax, threads)
+    if st != 0:
+        raise RuntimeError(f"uo_rx_process_batch_cw: {st}")
+    return a1, dst, sig, en[:, :bmax]
 
 
 class OracleSpectrum:

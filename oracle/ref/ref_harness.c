@@ -85,10 +85,8 @@ bool RadioManagement_UsesTxSidetone(void) { return ts.dmod_mode == DEMOD_CW; }
 
 /* ---- control-plane hooks (features disabled in every oracle configuration) ---- */
 void Board_GreenLed(ledstate_t s) { (void)s; }
-void CwDecode_Filter_Set(void) {}
-void CwDecode_RxProcessor(float32_t* const src, int16_t blockSize) { (void)src; (void)blockSize; }
-void CwGen_Init(void) {}
-bool CwGen_Process(float32_t* i_buffer, float32_t* q_buffer, uint32_t size) { (void)i_buffer; (void)q_buffer; (void)size; return false; }
+
+
 int32_t FreeDV_Iq_Get_FrameLen(void) { return 0; }
 void NR_Init(void) {}
 bool NR_in_buffer_add(void* c) { (void)c; return false; }
@@ -98,10 +96,23 @@ bool NR_out_has_data(void) { return false; }
 void Psk_Modem_Init(uint32_t output_sample_rate) { (void)output_sample_rate; }
 void Psk_Demodulator_ProcessSample(float32_t sample) { (void)sample; }
 int16_t Psk_Modulator_GenSample(void) { return 0; }
-void Rtty_Modem_Init(uint32_t output_sample_rate) { (void)output_sample_rate; }
-void Rtty_Demodulator_ProcessSample(float32_t sample) { (void)sample; }
-float32_t Rtty_Modulator_GenSample(void) { return 0.0f; }
 void UhsdrHwI2s_Codec_ClearTxDmaBuffer(void) {}
 void UiDriver_Callback_AudioISR(void) {}
 void UsbdAudio_FillTxBuffer(AudioSample_t* buffer, uint32_t len) { (void)buffer; (void)len; }
 void UsbdAudio_PutSample(int16_t sample) { (void)sample; }
+
+/* hardware / CAT / UI / digital-mode hooks of the CW keyer and decoder (cw_gen.c, cw_decoder.c):
+   no key lines pressed, no CAT, no text output, empty digital-mode TX buffer */
+#include "uhsdr_digi_buffer.h"
+bool Board_DitLinePressed(void) { return false; }
+bool Board_PttDahLinePressed(void) { return false; }
+void Board_RedLed(ledstate_t state) { (void)state; }
+bool CatDriver_CWKeyPressed(void) { return false; }
+bool CatDriver_CatPttActive(void) { return false; }
+uint8_t DigiModes_TxBufferHasDataFor(digi_buff_consumer_t consumer) { (void)consumer; return 0; }
+bool DigiModes_TxBufferRemove(uint8_t* c_ptr, digi_buff_consumer_t consumer) { (void)c_ptr; (void)consumer; return false; }
+int32_t DigiModes_TxBufferPutChar(uint8_t c, digi_buff_consumer_t source) { (void)c; (void)source; return 0; }
+void DigiModes_TxBufferPutSign(const char* s, digi_buff_consumer_t source) { (void)s; (void)source; }
+void RadioManagement_Request_TxOn(void) {}
+void RadioManagement_Request_TxOff(void) {}
+void UiDriver_TextMsgPutChar(char ch) { (void)ch; }

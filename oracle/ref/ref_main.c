@@ -30,6 +30,7 @@
 #include "audio_agc.h"
 #include "ui_spectrum.h"
 #include "filters.h"
+#include "cw_decoder.h"
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -56,6 +57,9 @@ void ref_spec_setup(int L);
 void ref_spec_snapshot(float* out);
 void ref_spec_frame(int L, int spectrum_filter, const float* ring, float* mag, float* avg);
 void ref_spec_dump(void);
+extern float oracle_cw_energy_log[4096];
+extern int oracle_cw_energy_count;
+const Goertzel* oracle_ref_cw_goertzel(void);
 extern arm_fir_instance_f32 Fir_Rx_Hilbert_I, Fir_Rx_Hilbert_Q;
 extern arm_fir_decimate_instance_f32 DECIMATE_RX_I, DECIMATE_RX_Q;
 
@@ -149,7 +153,12 @@ static void dump_setup(void)
     print_fvec("tx_hilbert_q", Fir_Tx_Hilbert_Q.pCoeffs, Fir_Tx_Hilbert_Q.numTaps, 0);
     {
         const float alc[2] = { ads.alc_decay, (float)ts.alc_tx_postfilt_gain_var };
-        print_fvec("tx_alc", alc, 2, 1);
+        print_fvec("tx_alc", alc, 2, 0);
+    }
+    {   /* CW decoder Goertzel (CwDecode_Filter_Set via SetProcessingChain, audio_driver.c:1158) */
+        const Goertzel* g = oracle_ref_cw_goertzel();
+        const float cw[3] = { g->r, g->cos, g->sin };
+        print_fvec("cw_goertzel", cw, 3, 1);
     }
     printf("}\n");
 }
@@ -192,6 +201,12 @@ int main(int argc, char** argv)
     ts.dsp.bass_gain = iarg(argc, argv, "bass", 2);
     ts.dsp.treble_gain = iarg(argc, argv, "treble", 0);
     ts.stereo_enable = false;
+    ts.cw_sidetone_freq = iarg(argc, argv, "sidetone", CW_SIDETONE_FREQ_DEFAULT);   /* CW decoder Goertzel */
+    ts.cw_keyer_speed = 20;                        /* CW_KEYER_SPEED_DEFAULT (ui_configuration.h:59) */
+    ts.cw_keyer_weight = CW_KEYER_WEIGHT_DEFAULT;
+    cw_decoder_config.blocksize = iarg(argc, argv, "cwblock", CW_DECODER_BLOCKSIZE_DEFAULT);
+    cw_decoder_config.thresh = iarg(argc, argv, "cwthresh", CW_DECODER_THRESH_DEFAULT);
+    cw_decoder_config.noisecancel_enable = iarg(argc, argv, "cwnc", 1);
     ts.cw_keyer_mode = CW_KEYER_MODE_STRAIGHT;
     ts.fm_sql_threshold = iarg(argc, argv, "sql", FM_SQUELCH_DEFAULT);
     if (iarg(argc, argv, "fm5k", 0)) ts.flags2 |= FLAGS2_FM_MODE_DEVIATION_5KHZ;
@@ -250,6 +265,9 @@ int main(int argc, char** argv)
     fclose(f);
 
     IqSample_t blk[IQ_BLOCK_SIZE];
+    const char* out_cw = arg(argc, argv, "out_cw", NULL);        /* Goertzel energy per CW block */
+    const char* out_cws = arg(argc, argv, "out_cws", NULL);      /* ads.CW_signal after each call */
+    uint8_t* cw_signal = out_cws ? calloc(n / block, 1) : NULL;
     float* stream = NULL;
     int ring = 0;
     if (spec)
@@ -280,6 +298,7 @@ int main(int argc, char** argv)
         memcpy(blk, iq + off, sizeof(IqSample_t) * block);   /* the ISR's DMA half-buffer */
         AudioDriver_I2SCallback(dst + off, blk, NULL, block);
         memcpy(a1 + off, adb.a_buffer[1], sizeof(float) * block);
+        if (cw_signal) cw_signal[off / block] = ads.CW_signal;
         if (spec && (off + block) % (ring / 2) == 0)       /* the ring holds ring/2 new samples */
             ref_spec_snapshot(stream + 2 * (off + block - ring / 2));
     }
@@ -300,6 +319,12 @@ int main(int argc, char** argv)
         free(mag); free(avgs); free(stream);
     }
     if (out_a) { f = fopen(out_a, "wb"); fwrite(a1, sizeof(float), n, f); fclose(f); }
+    if (out_cw)
+    {
+        const int cnt = oracle_cw_energy_count < 4096 ? oracle_cw_energy_count : 4096;
+        f = fopen(out_cw, "wb"); fwrite(oracle_cw_energy_log, sizeof(float), cnt, f); fclose(f);
+    }
+    if (out_cws) { f = fopen(out_cws, "wb"); fwrite(cw_signal, 1, n / block, f); fclose(f); free(cw_signal); }
     if (out_dst) { f = fopen(out_dst, "wb"); fwrite(dst, sizeof(AudioSample_t), n, f); fclose(f); }
     free(iq); free(dst); free(a1);
     return 0;

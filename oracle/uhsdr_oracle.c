@@ -28,6 +28,47 @@ void uo_rx_state_init(const uhsdr_rx_plan* p, uo_rx_state* s)
     s->out_index = p->agc.out_index0;
     s->in_index = p->agc.in_index0;
     s->fm_squelched = 1;       /* AudioDriver_FM_Rx_Init: "we start squelched" (audio_driver.c:475) */
+    s->cw_old = 0.001f;        /* static float32_t old_siglevel = 0.001 (cw_decoder.c:189) */
+}
+
+/* CwDecode_RxProcessor (cw_decoder.c:383-397) and CW_Decode_exe steps 1-5 (:182-316) with the
+   default configuration (one Goertzel, cw_decoder.h:19): Goertzel over the first blocksize
+   samples of each block (AudioFilter_GoertzelInput / _Energy, audio_filter.c:1290-1305),
+   exponential smoothing, threshold, two-sample noise cancel -> ads.CW_signal */
+static void cw_front(const uhsdr_rx_plan* p, uo_rx_state* s, const float* x, int n)
+{
+    s->cw_blocks_out = 0;
+    for (int i = 0; i < n; i++)
+    {
+        if (s->cw_count < p->cw_blocksize)
+        {
+            const float g0 = p->cw_r * s->cw_g1 - s->cw_g2 + x[i];
+            s->cw_g2 = s->cw_g1;
+            s->cw_g1 = g0;
+        }
+        s->cw_count++;
+    }
+    if (s->cw_count >= p->cw_blocksize)
+    {
+        const float a = (s->cw_g1 - (s->cw_g2 * p->cw_cos));
+        const float b = (s->cw_g2 * p->cw_sin);
+        s->cw_g1 = s->cw_g2 = 0.0f;
+        const float magnitude = sqrtf(a * a + b * b);
+        float siglevel = magnitude;
+        siglevel = siglevel * 0.1 + (1.0 - 0.1) * s->cw_old;       /* SIGNAL_TAU = 0.1 */
+        s->cw_old = magnitude;
+        const int newstate = (siglevel >= p->cw_thresh);
+        if (p->cw_noisecancel)
+        {
+            if (s->cw_change) { s->cw_state = newstate; s->cw_change = 0; }
+            else if (newstate != s->cw_state) s->cw_change = 1;
+        }
+        else s->cw_state = newstate;
+        s->cw_energy_out = magnitude;
+        s->cw_blocks_out = 1;
+        s->cw_count = 0;
+    }
+    s->cw_signal_out = s->cw_state;
 }
 
 /* ---- CMSIS-DSP f32 kernels, restated (generic code paths; the CM7 unrolled versions
@@ -548,6 +589,7 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
     agc_run(&p->agc, s, a0, nd);
     for (int i = 0; i < nd; i++) a0[i] = a0[i] * p->post_agc_scale;
     biquad_df1(p->biquad1, 4, s->bq1, a0, nd);
+    if (p->cw_enabled) cw_front(p, s, a0, nd);         /* audio_driver.c:2550-2557 */
     if (p->interp_phase > 0) fir_interpolate(p->interp, p->interp_L, p->interp_phase, s->interp, a0, a1, nd);
     if (p->aa_stages > 0) iir_lattice(p->aa_k, p->aa_v, p->aa_stages, s->aa, a1, a1, n);
 
@@ -586,6 +628,58 @@ static void* uo_worker(void* arg)
         uo_rx_process(j->p, &j->states[c], j->iq + (size_t)c * j->n * 2, j->n, j->a1 + (size_t)c * j->n,
                       j->dst ? j->dst + (size_t)c * j->n * 2 : NULL);
     return NULL;
+}
+
+typedef struct
+{
+    const uhsdr_rx_plan* p;
+    uo_rx_state* states;
+    const int32_t* iq;
+    float* a1;
+    int32_t* dst;
+    uint8_t* sig;
+    float* en;
+    int c0, c1, n, bmax;
+} uo_cw_job;
+
+static void* uo_cw_worker(void* arg)
+{
+    uo_cw_job* j = (uo_cw_job*)arg;
+    for (int c = j->c0; c < j->c1; c++)
+    {
+        uo_rx_state* s = &j->states[c];
+        int nb = 0;
+        for (int off = 0; off < j->n; off += BLK)
+        {
+            rx_call(j->p, s, j->iq + ((size_t)c * j->n + off) * 2, j->a1 + (size_t)c * j->n + off,
+                    j->dst ? j->dst + ((size_t)c * j->n + off) * 2 : NULL);
+            if (j->sig) j->sig[(size_t)c * (j->n / BLK) + off / BLK] = (uint8_t)s->cw_signal_out;
+            if (j->p->cw_enabled && s->cw_blocks_out && j->en && nb < j->bmax) j->en[(size_t)c * j->bmax + nb] = s->cw_energy_out;
+            if (j->p->cw_enabled && s->cw_blocks_out) nb++;
+        }
+    }
+    return NULL;
+}
+
+int uo_rx_process_batch_cw(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
+                           float* a1, int32_t* dst, uint8_t* cw_signal, float* cw_energy, int bmax, int threads)
+{
+    if (n % BLK) return UHSDR_LENGTH_ERROR;
+    if (threads < 1) threads = 1;
+    if (threads > C) threads = C;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    uo_cw_job jobs[256];
+    for (int t = 0; t < threads; t++)
+    {
+        jobs[t] = (uo_cw_job){ p, states, iq, a1, dst, cw_signal, cw_energy, (int)((long)C * t / threads),
+                               (int)((long)C * (t + 1) / threads), n, bmax };
+        if (threads == 1) uo_cw_worker(&jobs[t]);
+        else pthread_create(&tid[t], NULL, uo_cw_worker, &jobs[t]);
+    }
+    if (threads > 1)
+        for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+    return UHSDR_OK;
 }
 
 int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,

@@ -50,6 +50,13 @@ typedef struct uo_rx_state
     float fm_i_prev, fm_q_prev, fm_lpf_prev, fm_hpf_prev_a, fm_hpf_prev_b, fm_sql_avg;
     float fm_sq[UHSDR_MAX_LATTICE + 1];
     int32_t fm_squelched, fm_count;
+    /* CW decoder front end: cw_goertzel.buf[1..2], CW_Decode_exe's statics old_siglevel /
+       prevstate-free cw_state / change, CwDecode_RxProcessor's sample_counter (cw_decoder.c) */
+    float cw_g1, cw_g2, cw_old;
+    int32_t cw_state, cw_change, cw_count;
+    /* outputs of the current call: energies of blocks completed, ads.CW_signal */
+    float cw_energy_out;
+    int32_t cw_blocks_out, cw_signal_out;
 } uo_rx_state;
 
 size_t uo_rx_state_size(void);
@@ -59,6 +66,10 @@ int uo_rx_process(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, int
 /* C channels, channel-major buffers, `threads` POSIX threads (0 = 1) */
 int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
                         float* a1, int32_t* dst, int threads);
+/* the same, also recording the CW decoder front end: cw_signal [C][n/32] (ads.CW_signal after
+   each call), cw_energy [C][bmax] (Goertzel energy of each block completed, in order) */
+int uo_rx_process_batch_cw(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
+                           float* a1, int32_t* dst, uint8_t* cw_signal, float* cw_energy, int bmax, int threads);
 
 /* transmit: TxProcessor_Run SSB voice path (drivers/audio/tx_processor.c:891-1078) */
 typedef struct uo_tx_state

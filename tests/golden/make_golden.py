@@ -132,6 +132,45 @@ SPEC_CONFIGS = {
 }
 SPEC_FRAMES = 4096
 
+# CW decoder front end (a20): name -> (uhsdr_ref args, signal kwargs).  Keyed CW at the sidetone
+# pitch; thresholds low enough that the signal state toggles.
+CW_CONFIGS = {
+    "p4_cw": ({"mode": 2, "path": 4, "cwthresh": 1000}, {"cw": True}),
+    "p4_cw_nonc": ({"mode": 2, "path": 4, "cwthresh": 1500, "cwnc": 0}, {"cw": True}),
+    "p10_cw_b60": ({"mode": 2, "path": 10, "cwthresh": 1000, "cwblock": 60, "sidetone": 700}, {"cw": True, "tone": 700.0}),
+    "p4_cw_b90": ({"mode": 2, "path": 4, "cwthresh": 800, "cwblock": 90}, {"cw": True}),
+    "p70_sam_cw": ({"mode": 4, "path": 70, "cwthresh": 20000}, {"am": True}),
+    "p4_cw_default": ({"mode": 2, "path": 4}, {"cw": True}),
+}
+CW_FRAMES = 8192
+
+
+def make_cw(name: str):
+    args, sig = CW_CONFIGS[name]
+    sig = dict(sig)
+    if sig.pop("am", False):
+        iq = synth.am_iq(np.arange(NCH), 0, CW_FRAMES)
+    else:
+        sig.pop("cw")
+        iq = synth.cw_iq(np.arange(NCH), 0, CW_FRAMES, **sig)
+    calls = CW_FRAMES // 32
+    a1 = np.empty((NCH, CW_FRAMES), np.float32)
+    sg = np.empty((NCH, calls), np.uint8)
+    en = []
+    for c in range(NCH):
+        with tempfile.TemporaryDirectory() as td:
+            fin, fa, fcw, fs = (os.path.join(td, x) for x in ("in.bin", "a.bin", "cw.bin", "s.bin"))
+            iq[c].astype(np.int32).tofile(fin)
+            cmd = [REF, f"in={fin}", f"n={CW_FRAMES}", f"out_a={fa}", f"out_cw={fcw}", f"out_cws={fs}"]
+            subprocess.run(cmd + [f"{k}={v}" for k, v in args.items()], check=True)
+            a1[c] = np.fromfile(fa, dtype=np.float32)
+            sg[c] = np.fromfile(fs, dtype=np.uint8)
+            en.append(np.fromfile(fcw, dtype=np.float32))
+    en = np.stack(en)
+    np.savez_compressed(os.path.join(HERE, f"cw_{name}.npz"), iq=iq, signal=sg, energy=en,
+                        setup=json.dumps(ref_json(args, "setup")), args=json.dumps(args))
+    print(f"cw_{name:14s} blocks={en.shape[1]:4d} on-fraction={float(sg.mean()):.3f} peak energy={float(en.max()):.1f}")
+
 
 def make_spec(name: str):
     args, sig = SPEC_CONFIGS[name]
@@ -214,6 +253,10 @@ def main():
         json.dump(json.loads(paths), f, separators=(",", ":"))
     tx_tables()
     spectrum_tables()
+    for name in CW_CONFIGS:
+        if a.only and name != a.only:
+            continue
+        make_cw(name)
     for name in SPEC_CONFIGS:
         if a.only and name != a.only:
             continue

@@ -39,7 +39,8 @@ class RxConfig(C.Structure):
         ("agc_hang_thresh", C.c_int32), ("agc_tau_decay", C.c_int32 * 6), ("agc_tau_hang_decay", C.c_int32),
         ("sam_sideband", C.c_int32), ("sam_pll_fmax", C.c_int32), ("sam_zeta", C.c_int32), ("sam_omega_n", C.c_int32),
         ("fade_leveler", C.c_int32), ("fm_sql_threshold", C.c_int32), ("fm_deviation_5k", C.c_int32),
-        ("reserved", C.c_int32 * 9),
+        ("cw_sidetone_freq", C.c_int32), ("cw_decoder_blocksize", C.c_int32), ("cw_decoder_thresh", C.c_int32),
+        ("cw_decoder_noisecancel", C.c_int32), ("reserved", C.c_int32 * 5),
     ]
 
 
@@ -75,7 +76,10 @@ class RxPlan(C.Structure):
         ("fade_mtauR", C.c_float), ("fade_onem_mtauR", C.c_float), ("fade_mtauI", C.c_float),
         ("fade_onem_mtauI", C.c_float),
         ("fm_scale", C.c_float), ("fm_sql_threshold", C.c_int32), ("sq_stages", C.c_int32),
-        ("sq_k", C.c_float * MAX_LATTICE), ("sq_v", C.c_float * (MAX_LATTICE + 1)), ("reserved", C.c_int32 * 64),
+        ("sq_k", C.c_float * MAX_LATTICE), ("sq_v", C.c_float * (MAX_LATTICE + 1)),
+        ("cw_enabled", C.c_int32), ("cw_blocksize", C.c_int32), ("cw_noisecancel", C.c_int32),
+        ("cw_thresh", C.c_float), ("cw_r", C.c_float), ("cw_cos", C.c_float), ("cw_sin", C.c_float),
+        ("reserved", C.c_int32 * 57),
     ]
 
 
@@ -151,6 +155,9 @@ SIGNATURES = {
     "uhsdr_rx_kernel_times": (C.c_int32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int32), C.c_int32]),
     "uhsdr_rx_kernel_name": (C.c_char_p, [C.c_int32]),
     "uhsdr_rx_synchronize": (C.c_int, [C.c_void_p]),
+    "uhsdr_rx_set_cw_outputs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "uhsdr_rx_cw_blocks_max": (C.c_int32, [C.c_void_p]),
+    "uhsdr_rx_cw_blocks_last": (C.c_int32, [C.c_void_p]),
     "uhsdr_device_alloc": (C.c_void_p, [C.c_uint64]),
     "uhsdr_device_free": (None, [C.c_void_p]),
     "uhsdr_copy_to_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
@@ -236,6 +243,8 @@ REF_ARG_MAP = {
     "agc_mode": "agc_mode", "agc_thresh": "agc_thresh", "agc_slope": "agc_slope", "agc_hang": "agc_hang_enable",
     "sam_sb": "sam_sideband", "pll_fmax": "sam_pll_fmax", "zeta": "sam_zeta", "omegan": "sam_omega_n",
     "fade": "fade_leveler", "sql": "fm_sql_threshold", "fm5k": "fm_deviation_5k",
+    "sidetone": "cw_sidetone_freq", "cwblock": "cw_decoder_blocksize", "cwthresh": "cw_decoder_thresh",
+    "cwnc": "cw_decoder_noisecancel",
 }
 
 

@@ -342,6 +342,7 @@ struct BackState
     float* agc;      // [6 + AGC_Q][C]  spare volts save_volts fast_bavg hang_bavg wold | call maxima[Q-1], leaving sample
     int* agci;       // [3][C]   hang_counter decay_type state
     float* sam;      // AM / SAM: [7 + 96][C] phs omega2 fil_out dsI dsQ dc27 dc_insert | allpass a,b,c,d[24]
+    float* cw;       // CW decoder front end: [5][C] goertzel buf[1] buf[2], old_siglevel, cw_state, change
 };
 
 struct BackArgs
@@ -354,6 +355,10 @@ struct BackArgs
     BackState s;
     int C, N, Nd;
     int ring_phase;      // (32-frame calls processed so far) mod AGC_Q
+    uint8_t* cw_signal;  // optional [C][N/32]: ads.CW_signal after each call
+    float* cw_energy;    // optional [C][cw_bmax]: Goertzel energy per completed CW block
+    int cw_count0;       // CwDecode_RxProcessor's sample_counter at launch start (same for all channels)
+    int cw_bmax;
 };
 
 // Math_log10f_fast, misc/uhsdr_math.c:26-39
@@ -628,6 +633,18 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
     for (int i = 0; i < 16; ++i) bq1[i] = a.s.bq1[i * C + cl];
 #pragma unroll
     for (int i = 0; i < PH - 1; ++i) ip[i] = a.s.interp[i * C + cl];
+    // CW decoder front end (CwDecode_RxProcessor + CW_Decode_exe steps 1-5, cw_decoder.c:182-316,
+    // 383-397) on a_buffer[0] after biquad_1; 12 ksps paths only (L == 4)
+    const bool cw = L == 4 && P->cw_enabled;
+    float g1 = 0.0f, g2 = 0.0f, cw_old = 0.0f;
+    bool cw_state = false, cw_change = false;
+    int cw_count = a.cw_count0, cw_block = 0;
+    const int cw_bs = P->cw_blocksize;
+    if (cw)
+    {
+        g1 = a.s.cw[cl]; g2 = a.s.cw[C + cl]; cw_old = a.s.cw[2 * C + cl];
+        cw_state = a.s.cw[3 * C + cl] != 0.0f; cw_change = a.s.cw[4 * C + cl] != 0.0f;
+    }
     for (int it = 0; it < calls + ROLES - 1; ++it)
     {
         const int call = it - ST;
@@ -643,6 +660,17 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
 #pragma unroll
                 for (int st = 0; st < 4; ++st)
                     x = biquad_step(x, bq1[4 * st], bq1[4 * st + 1], bq1[4 * st + 2], bq1[4 * st + 3], b1 + 5 * st);
+                if (cw)
+                {
+                    // raw_signal_buffer[sample_counter++] = x; samples past blocksize are dropped
+                    if (cw_count < cw_bs)
+                    {
+                        const float g0 = P->cw_r * g1 - g2 + x;    // AudioFilter_GoertzelInput (audio_filter.c:1290-1295)
+                        g2 = g1;
+                        g1 = g0;
+                    }
+                    ++cw_count;
+                }
                 // polyphase interpolator: output j uses phase L-1-j (arm_fir_interpolate_f32.c:482-575)
                 float win[PH];
 #pragma unroll
@@ -659,6 +687,31 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
 #pragma unroll
                 for (int t = 0; t + 1 < PH; ++t) ip[t] = win[t + 1];
             }
+            if (cw)
+            {
+                if (cw_count >= cw_bs)
+                {
+                    // AudioFilter_GoertzelEnergy (audio_filter.c:1296-1305), then the signal state:
+                    // exponential smoothing, threshold, noise cancel (cw_decoder.c:288-316)
+                    const float ga = (g1 - (g2 * P->cw_cos));
+                    const float gb = (g2 * P->cw_sin);
+                    const float e = sqrtf(ga * ga + gb * gb);
+                    g1 = 0.0f; g2 = 0.0f;
+                    const float siglevel = (float)((double)e * 0.1 + (1.0 - 0.1) * (double)cw_old);
+                    cw_old = e;
+                    const bool newstate = siglevel >= P->cw_thresh;
+                    if (P->cw_noisecancel)
+                    {
+                        if (cw_change) { cw_state = newstate; cw_change = false; }
+                        else if (newstate != cw_state) cw_change = true;
+                    }
+                    else cw_state = newstate;
+                    if (a.cw_energy && live) a.cw_energy[(size_t)c * a.cw_bmax + cw_block] = e;
+                    ++cw_block;
+                    cw_count = 0;
+                }
+                if (a.cw_signal && live) a.cw_signal[(size_t)c * calls + call] = cw_state;
+            }
         }
         __syncthreads();
     }
@@ -668,6 +721,11 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
         for (int i = 0; i < 16; ++i) a.s.bq1[i * C + c] = bq1[i];
 #pragma unroll
         for (int i = 0; i < PH - 1; ++i) a.s.interp[i * C + c] = ip[i];
+        if (cw)
+        {
+            a.s.cw[c] = g1; a.s.cw[C + c] = g2; a.s.cw[2 * C + c] = cw_old;
+            a.s.cw[3 * C + c] = cw_state ? 1.0f : 0.0f; a.s.cw[4 * C + c] = cw_change ? 1.0f : 0.0f;
+        }
     }
 }
 
@@ -1171,6 +1229,10 @@ struct uhsdr_rx_s
     void* arena;
     size_t arena_bytes;
     long long dec_samples;   // decimated samples processed (AGC ring phase)
+    int cw_count;            // CW decoder sample_counter (uniform over channels)
+    int cw_bmax, cw_blocks_last;
+    uint8_t* cw_signal;      // user outputs (uhsdr_rx_set_cw_outputs)
+    float* cw_energy;
     long long calls_done;
     long long front_launches; // oscillator ping-pong parity
     // per-kernel timing (uhsdr_rx_enable_timing)
@@ -1260,10 +1322,21 @@ extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
     // oscillator starts at {I=0, Q=1} (freq_shift.c:48-49); both ping-pong copies
     const float osc0[4] = { 0.0f, 1.0f, 0.0f, 1.0f };
     HIPCHK(hipMemcpyAsync(h->osc, osc0, sizeof osc0, hipMemcpyHostToDevice, h->stream));
+    if (h->bs.cw)
+    {
+        // old_siglevel starts at 0.001 (function static, cw_decoder.c:189)
+        float* v = (float*)malloc(sizeof(float) * h->C);
+        for (int i = 0; i < h->C; ++i) v[i] = 0.001f;
+        HIPCHK(hipMemcpyAsync(h->bs.cw + 2 * (size_t)h->C, v, sizeof(float) * h->C, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        free(v);
+    }
     HIPCHK(hipStreamSynchronize(h->stream));
     h->dec_samples = 0;
     h->calls_done = 0;
     h->front_launches = 0;
+    h->cw_count = 0;
+    h->cw_blocks_last = 0;
     return UHSDR_OK;
 }
 
@@ -1306,6 +1379,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const size_t o_agc = take((size_t)(6 + AGC_Q) * C), o_agci = take((size_t)3 * C);
     const bool am = h->bv->dm != DM_NONE;
     const size_t o_sam = take(am ? (size_t)(7 + 96) * C : 0), o_adq = take(am ? (size_t)C * h->Nd : 0);
+    const bool cw = p.cw_enabled && p.decimation_rate == 4;
+    const size_t o_cw = take(cw ? (size_t)5 * C : 0);
     h->arena_bytes = fl * sizeof(float);
     if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess ||
         hipMalloc((void**)&h->adec, sizeof(float) * (size_t)C * h->Nd) != hipSuccess ||
@@ -1323,6 +1398,12 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->bs.pre = A + o_pre; h->bs.aa = A + o_aa; h->bs.bq1 = A + o_bq1; h->bs.bq2 = A + o_bq2;
     h->bs.interp = A + o_ip; h->bs.ring = A + o_ring; h->bs.agc = A + o_agc; h->bs.agci = (int*)(A + o_agci);
     h->bs.sam = am ? A + o_sam : nullptr;
+    h->bs.cw = cw ? A + o_cw : nullptr;
+    {
+        // blocks per call: one completes at the end of every ceil(blocksize / NDC)-th call
+        const int ndc = BLK / p.decimation_rate, cpb = (p.cw_blocksize + ndc - 1) / ndc;
+        h->cw_bmax = cw ? (N / BLK + cpb - 1) / cpb : 0;
+    }
     h->adec_q = am ? A + o_adq : nullptr;
     if (hipMemcpy(h->d_plan, &h->plan, sizeof(uhsdr_rx_plan), hipMemcpyHostToDevice) != hipSuccess)
     {
@@ -1332,6 +1413,17 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     *out = h;
     return uhsdr_rx_reset(h);
 }
+
+extern "C" uhsdr_status uhsdr_rx_set_cw_outputs(uhsdr_rx_handle h, uint8_t* signal, float* energy)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    h->cw_signal = signal;
+    h->cw_energy = energy;
+    return UHSDR_OK;
+}
+
+extern "C" int32_t uhsdr_rx_cw_blocks_max(uhsdr_rx_handle h) { return h ? h->cw_bmax : 0; }
+extern "C" int32_t uhsdr_rx_cw_blocks_last(uhsdr_rx_handle h) { return h ? h->cw_blocks_last : 0; }
 
 extern "C" uhsdr_status uhsdr_rx_set_stream(uhsdr_rx_handle h, void* stream)
 {
@@ -1375,6 +1467,21 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
     ba.s = h->bs;
     ba.C = h->C; ba.N = h->N; ba.Nd = h->Nd;
     ba.ring_phase = (int)(h->calls_done % (h->bv->dm == DM_FM ? 200 : AGC_Q));   // FM: fm_data.count phase
+    ba.cw_signal = h->bs.cw ? h->cw_signal : nullptr;
+    ba.cw_energy = h->bs.cw ? h->cw_energy : nullptr;
+    ba.cw_count0 = h->cw_count;
+    ba.cw_bmax = h->cw_bmax;
+    if (h->bs.cw)
+    {
+        const int ndc = BLK / h->plan.decimation_rate;
+        int blocks = 0;
+        for (int k = 0; k < h->N / BLK; ++k)
+        {
+            h->cw_count += ndc;
+            if (h->cw_count >= h->plan.cw_blocksize) { h->cw_count = 0; ++blocks; }
+        }
+        h->cw_blocks_last = blocks;
+    }
     time_mark(h, 1, 0);
     hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH), back_lds(h), h->stream, ba);
     HIPCHK(hipGetLastError());

@@ -83,6 +83,10 @@ void uhsdr_rx_config_default(uhsdr_rx_config* c)
     c->fade_leveler = 1;
     c->fm_sql_threshold = 12;                    /* FM_SQUELCH_DEFAULT, audio_driver.h:449 */
     c->fm_deviation_5k = 0;
+    c->cw_sidetone_freq = 750;                   /* CW_SIDETONE_FREQ_DEFAULT, uhsdr_board.h:396 */
+    c->cw_decoder_blocksize = 88;                /* CW_DECODER_BLOCKSIZE_DEFAULT, cw_decoder.h:13 */
+    c->cw_decoder_thresh = 32000;                /* CW_DECODER_THRESH_DEFAULT, cw_decoder.h:17 */
+    c->cw_decoder_noisecancel = 1;               /* CW_DECODER_FLAGS_DEFAULT bit 0, cw_decoder.h:19 */
 }
 
 /* IIR_15k_hpf (drivers/audio/filters/iir_15k_hpf_fm_squelch.c): 6-stage lattice high-pass of
@@ -406,6 +410,28 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
     p->sq_stages = 6;
     copy_bits(p->sq_k, squelch_k_bits, 6);
     copy_bits(p->sq_v, squelch_v_bits, 7);
+    /* CW decoder front end: CwDecode_RxProcessor runs on a_buffer[0] in CW, AM and SAM when the
+       decimated rate is 12 ksps (audio_driver.c:2536-2557); CwDecode_Filter_Set (cw_decoder.c:
+       69-74, called from SetProcessingChain :1158) -> AudioFilter_CalcGoertzel (audio_filter.c:
+       1281-1288) with coefficient 1.0 and cw_decoder_config.sampling_freq = 12000.0 */
+    if (cfg->cw_decoder_blocksize < 1 || cfg->cw_decoder_blocksize > 128)
+    { uhsdr_set_error("cw_decoder_blocksize %d outside 1..128", cfg->cw_decoder_blocksize); return UHSDR_ARGUMENT_ERROR; }
+    p->cw_enabled = (p->dmod_mode == UHSDR_DEMOD_CW || p->dmod_mode == UHSDR_DEMOD_AM || p->dmod_mode == UHSDR_DEMOD_SAM)
+                    && p->decimated_freq == 12000;
+    p->cw_blocksize = cfg->cw_decoder_blocksize;
+    p->cw_noisecancel = cfg->cw_decoder_noisecancel != 0;
+    p->cw_thresh = (float)(uint32_t)cfg->cw_decoder_thresh;
+    {
+        const float freq = (float)(uint32_t)cfg->cw_sidetone_freq;
+        const float goertzel_coeff = 1.0f;
+        const uint32_t size = (uint32_t)cfg->cw_decoder_blocksize;
+        const float samplerate = 12000.0f;
+        const int ga = (0.5 + (freq * goertzel_coeff) * size / samplerate);
+        const float gb = (2 * CMSIS_PI * ga) / size;
+        p->cw_sin = sinf(gb);
+        p->cw_cos = cosf(gb);
+        p->cw_r = 2 * p->cw_cos;
+    }
     return UHSDR_OK;
 }
 

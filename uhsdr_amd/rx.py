@@ -70,6 +70,26 @@ class RxChain:
             dst.ctypes.data_as(C.c_void_p)), "uhsdr_rx_process_host")
         return audio, dst
 
+    def set_cw_outputs(self, signal=None, energy=None) -> None:
+        """CW decoder front end outputs of the following calls: signal uint8 [C][N/32] (ads.CW_signal
+        after each call), energy f32 [C][cw_blocks_max] (Goertzel energy per completed block)"""
+        if signal is not None and tuple(signal.shape) != (self.channels, self.frames // 32):
+            raise ValueError("signal must be [C][N/32]")
+        if energy is not None and tuple(energy.shape) != (self.channels, max(self.cw_blocks_max, 1)):
+            raise ValueError("energy must be [C][cw_blocks_max]")
+        self._cw = (signal, energy)   # keep the tensors alive
+        _abi.check(self.lib.uhsdr_rx_set_cw_outputs(self.handle, C.c_void_p(signal.data_ptr() if signal is not None else 0),
+                                                    C.c_void_p(energy.data_ptr() if energy is not None else 0)),
+                   "uhsdr_rx_set_cw_outputs")
+
+    @property
+    def cw_blocks_max(self) -> int:
+        return self.lib.uhsdr_rx_cw_blocks_max(self.handle)
+
+    @property
+    def cw_blocks_last(self) -> int:
+        return self.lib.uhsdr_rx_cw_blocks_last(self.handle)
+
     def enable_timing(self, enable: bool = True) -> None:
         _abi.check(self.lib.uhsdr_rx_enable_timing(self.handle, int(enable)), "uhsdr_rx_enable_timing")
 

@@ -124,6 +124,27 @@ def am_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier
     return _frames(i_sig, q_sig)
 
 
+def cw_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier: float = 12000.0,
+          tone: float = 750.0, amplitude: float = 1500.0, element: int = 2400):
+    """C5 CW: an on/off keyed carrier at `carrier` + `tone` +- 40 Hz per
+    channel (the receiver's sidetone pitch), keyed in elements of `element` frames (50 ms =
+    24 wpm at 48 ksps) with a per-channel pseudo-random pattern, plus noise."""
+    channels = np.asarray(channels, dtype=np.int64)
+    ch = channels.astype(np.uint64)
+    base = (np.uint64(SEED_BASE) + ch) << np.uint64(20)
+    off = 40.0 * (2.0 * _uniform(base + np.uint64(11)) - 1.0)
+    ph_c = 2.0 * np.pi * _uniform(base + np.uint64(12))
+    n = np.arange(start, start + nframes, dtype=np.float64)[None, :]
+    el = (np.arange(start, start + nframes) // element).astype(np.uint64)[None, :]
+    key = _uniform((base[:, None] + np.uint64(1 << 19)) + el) < 0.55
+    ph = 2.0 * np.pi * (carrier + tone + off[:, None]) / FS * n + ph_c[:, None]
+    i_sig, q_sig = amplitude * key * np.cos(ph), amplitude * key * np.sin(ph)
+    if noise_sigma > 0:
+        ni, nq = _noise(channels, start, nframes, noise_sigma)
+        i_sig, q_sig = i_sig + ni, q_sig + nq
+    return _frames(i_sig, q_sig)
+
+
 def fm_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier: float = 12000.0,
           deviation: float = 2500.0, tone: float = 1000.0, amplitude: float = 3000.0):
     """C4 FM-RX: carrier at `carrier` Hz, a `tone` Hz audio tone at

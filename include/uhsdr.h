@@ -228,7 +228,8 @@ uhsdr_status uhsdr_copy_to_host(void* dst, const void* src, uint64_t bytes);
 #define UHSDR_TX_HILBERT_TAPS 201    /* iq_tx_wide, drivers/audio/filters/iq_tx_filter.h:22 */
 #define UHSDR_TX_DELAY 320           /* AUDIO_DELAY_BUFSIZE, audio_driver.h:516 */
 
-/* TX_AUDIO_*, hardware/uhsdr_board.h:128-131 */
+/* TX_AUDIO_*, hardware/uhsdr_board.h:128-131.  Modes: UHSDR_DEMOD_USB / LSB (SSB voice) and
+   UHSDR_DEMOD_FM (FM voice, needs iq_freq_mode != OFF like the reference, tx_processor.c:1009) */
 enum { UHSDR_TX_AUDIO_MIC = 0, UHSDR_TX_AUDIO_LINEIN_L = 1, UHSDR_TX_AUDIO_LINEIN_R = 2, UHSDR_TX_AUDIO_DIG = 3 };
 
 typedef struct uhsdr_tx_config
@@ -248,7 +249,9 @@ typedef struct uhsdr_tx_config
     float   power_factor;         /* ts.tx_power_factor */
     float   gain_i, gain_q;       /* ts.tx_adj_gain_var[trans].i / .q */
     float   phase_balance;        /* ads.iq_phase_balance_tx[trans] */
-    int32_t reserved[16];
+    int32_t fm_deviation_5k;      /* FLAGS2_FM_MODE_DEVIATION_5KHZ: FM transmit deviation 5 kHz (else 2.5) */
+    int32_t fm_subaudible_tone;   /* ts.fm_subaudible_tone_gen_select: index into fm_subaudible_tone_table, 0 = off */
+    int32_t reserved[14];
 } uhsdr_tx_config;
 
 typedef struct uhsdr_tx_plan
@@ -271,6 +274,16 @@ typedef struct uhsdr_tx_plan
     float   osc_cos, osc_sin;
     float   final_i_gain, final_q_gain;   /* tx_power_factor * tx_adj_gain_var * SSB_GAIN_COMP * 2^16 */
     float   phase_balance;
+    /* FM transmit (TxProcessor_FM, tx_processor.c:534-588): pre-emphasis, optional sub-audible
+       tone from a softdds NCO, 16-bit accumulator NCO over the softdds sine table */
+    int32_t fm;
+    float   fm_mod_mult;          /* 2 with 5 kHz deviation, else 1 */
+    uint32_t fm_word;             /* (65536 * |translate_freq|) / 48000 */
+    int32_t fm_swap;              /* translate_freq < 0: I and Q buffers exchanged */
+    int32_t fm_sub_on;
+    uint32_t fm_sub_step;         /* softdds_stepForSampleRate(tone, 48000) (softdds.c:26-32) */
+    float   fm_sub_scale;         /* FM_SUBAUDIBLE_TONE_AMPLITUDE_SCALING * fm_mod_mult */
+    int16_t dds_table[1024];      /* DDS_TABLE, softdds/dds_table.c */
     int32_t reserved[32];
 } uhsdr_tx_plan;
 

@@ -31,6 +31,7 @@
 #include "ui_spectrum.h"
 #include "filters.h"
 #include "cw_decoder.h"
+#include "dds_table.h"
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -60,6 +61,22 @@ void ref_spec_dump(void);
 extern float oracle_cw_energy_log[4096];
 extern int oracle_cw_energy_count;
 const Goertzel* oracle_ref_cw_goertzel(void);
+const float* oracle_ref_subaudible_table(int* n);
+extern const int16_t DDS_TABLE[];
+
+static void print_fvec(const char* name, const float* p, int n, int last);
+
+/* dump=txextra: softdds sine table (softdds/dds_table.c) and the FM sub-audible tone table */
+static void dump_txextra(void)
+{
+    int n = 0;
+    const float* t = oracle_ref_subaudible_table(&n);
+    printf("{\"dds_table\": [");
+    for (int i = 0; i < DDS_TBL_SIZE; ++i) printf("%s%d", i ? "," : "", DDS_TABLE[i]);
+    printf("], ");
+    print_fvec("subaudible", t, n, 1);
+    printf("}\n");
+}
 extern arm_fir_instance_f32 Fir_Rx_Hilbert_I, Fir_Rx_Hilbert_Q;
 extern arm_fir_decimate_instance_f32 DECIMATE_RX_I, DECIMATE_RX_Q;
 
@@ -176,6 +193,7 @@ int main(int argc, char** argv)
     const char* dump = arg(argc, argv, "dump", "");
     if (strcmp(dump, "paths") == 0) { dump_paths(); return 0; }
     if (strcmp(dump, "spectrum") == 0) { ref_spec_dump(); return 0; }
+    if (strcmp(dump, "txextra") == 0) { dump_txextra(); return 0; }
 
     const int mode = (int)iarg(argc, argv, "mode", DEMOD_USB);
     const int path = (int)iarg(argc, argv, "path", 0);
@@ -236,6 +254,7 @@ int main(int argc, char** argv)
     ts.alc_decay = ALC_DECAY_DEFAULT;
     ts.alc_tx_postfilt_gain = ALC_POSTFILT_GAIN_DEFAULT;
     ts.tx_filter = iarg(argc, argv, "txfilter", 0);
+    ts.fm_subaudible_tone_gen_select = iarg(argc, argv, "subtone", 0);   /* FM_SUBAUDIBLE_TONE_OFF */
     ts.dsp.tx_bass_gain = iarg(argc, argv, "txbass", 4);
     ts.dsp.tx_treble_gain = iarg(argc, argv, "txtreble", 4);
     ts.tx_power_factor = farg(argc, argv, "txpwr", 0.5f);

@@ -9,3 +9,10 @@
 
 const arm_iir_lattice_instance_f32* oracle_ref_tx_lattice(void) { return &IIR_TXFilter; }
 const arm_biquad_casd_df1_inst_f32* oracle_ref_tx_biquad(void) { return &IIR_TX_biquad; }
+
+/* fm_subaudible_tone_table (drivers/audio/fm_subaudible_tone_table.h, included by tx_processor.c) */
+const float* oracle_ref_subaudible_table(int* n)
+{
+    *n = (int)(sizeof fm_subaudible_tone_table / sizeof fm_subaudible_tone_table[0]);
+    return fm_subaudible_tone_table;
+}

@@ -760,6 +760,39 @@ static void tx_call(const uhsdr_tx_plan* p, uo_tx_state* s, const int32_t* audio
         for (int i = 0; i < n; i++) a[i] = a[i] * valbuf[i];
     }
     if (a0) memcpy(a0, a, sizeof(float) * n);
+    if (p->fm)
+    {
+        /* TxProcessor_FM (:534-588): differentiating pre-emphasis, sub-audible tone, NCO */
+        float a1[BLK];
+        for (int i = 0; i < n; i++)
+        {
+            const float x = a[i];
+            s->fm_hpf_b = 0.05 * (s->fm_hpf_b + x - s->fm_hpf_a);         /* FM_TX_HPF_ALPHA */
+            s->fm_hpf_a = x;
+            a1[i] = s->fm_hpf_b;
+        }
+        if (p->fm_sub_on)                                                  /* softdds_addSingleTone */
+            for (int i = 0; i < n; i++)
+            {
+                const uint32_t k = (s->fm_sub_acc >> 22) % 1024;
+                s->fm_sub_acc += p->fm_sub_step;
+                a1[i] += (float)p->dds_table[k] * p->fm_sub_scale;
+            }
+        float* ip = p->fm_swap ? qb : ib;
+        float* qp = p->fm_swap ? ib : qb;
+        for (int i = 0; i < n; i++)
+        {
+            /* uint32 += float: the sum in float, back through a 64-bit truncation as x86 does */
+            const float sum = (float)s->fm_accum + (p->fm_word + (a1[i] * 16 * p->fm_mod_mult));
+            s->fm_accum = (uint32_t)(int64_t)sum;
+            s->fm_accum %= 65536;
+            const uint32_t idx = s->fm_accum >> 6;
+            ip[i] = p->dds_table[idx];
+            qp[i] = p->dds_table[(idx + 768) % 1024];
+        }
+    }
+    else
+    {
     /* TxProcessor_SSB (:467-490): Hilbert pair, then FreqShift */
     fir(p->hilbert_i, UHSDR_TX_HILBERT_TAPS, s->hil_i, a, ib, n);
     fir(p->hilbert_q, UHSDR_TX_HILBERT_TAPS, s->hil_q, a, qb, n);
@@ -795,6 +828,7 @@ static void tx_call(const uhsdr_tx_plan* p, uo_tx_state* s, const int32_t* audio
             s->osc_vq = g * s->osc_vq;
             s->osc_vi = g * s->osc_vi;
         }
+    }
     }
     /* TxProcessor_IqFinalProcessing (:282-330) */
     for (int i = 0; i < n; i++) ib[i] = ib[i] * p->final_i_gain;

@@ -81,6 +81,9 @@ typedef struct uo_tx_state
     int32_t delay_in;                         /* alc_delay_inbuf (function static) */
     float hil_i[UHSDR_TX_HILBERT_TAPS], hil_q[UHSDR_TX_HILBERT_TAPS];
     float osc_vi, osc_vq;
+    /* TxProcessor_FM statics (tx_processor.c:536-537) and the sub-audible tone softdds */
+    float fm_hpf_a, fm_hpf_b;
+    uint32_t fm_accum, fm_sub_acc;
 } uo_tx_state;
 
 size_t uo_tx_state_size(void);

@@ -91,6 +91,12 @@ TX_CONFIGS = {
     "usb_iqadj": {"mode": 0, "path": 48, "txgi": 0.97, "txgq": 1.02, "txphase": -0.015, "txpwr": 0.8},
     "usb_m6k": {"mode": 0, "path": 48, "iqmode": 2},
     "usb_off": {"mode": 0, "path": 48, "iqmode": 0, "txphase": 0.01},
+    # FM transmit (TxProcessor_FM, tx_processor.c:534-588): pre-emphasis + 16-bit softdds NCO
+    "fm": {"mode": 5, "path": 1, "iqmode": 4},
+    "fm_p12k_5k": {"mode": 5, "path": 1, "iqmode": 3, "fm5k": 1},
+    "fm_subtone": {"mode": 5, "path": 1, "iqmode": 4, "subtone": 10},
+    "fm_m6k_subtone": {"mode": 5, "path": 1, "iqmode": 2, "subtone": 33, "fm5k": 1, "comp": 3},
+    "fm_p6k_iqadj": {"mode": 5, "path": 1, "iqmode": 1, "txgi": 0.97, "txgq": 1.02, "txphase": 0.02},
 }
 
 
@@ -114,6 +120,10 @@ def tx_tables():
         d = ref_json({"mode": 0, "path": 48, "tx": 1, "txfilter": f}, "setup")
         out["lattice"][str(f)] = {"k": d["tx_k"], "v": d["tx_v"]}
         out["hilbert_i"], out["hilbert_q"] = d["tx_hilbert_i"], d["tx_hilbert_q"]
+    d = ref_json({"mode": 5, "path": 1, "tx": 1}, "setup")      # IIR_TX_2k7_FM (tx_processor.c:104-107)
+    out["lattice"]["fm"] = {"k": d["tx_k"], "v": d["tx_v"]}
+    x = ref_json({"mode": 0, "path": 48}, "txextra")              # softdds DDS_TABLE, sub-audible tones
+    out["dds_table"], out["subaudible"] = x["dds_table"], x["subaudible"]
     with open(os.path.join(HERE, "tx_tables.json"), "w") as fo:
         json.dump(out, fo, separators=(",", ":"))
 

@@ -1,4 +1,4 @@
-"""Device SSB transmit (uhsdr_tx.hip through the C ABI) against the reference firmware's own
+"""Device SSB and FM transmit (uhsdr_tx.hip through the C ABI) against the reference firmware's own
 TX fixtures (tests/golden/tx_*.npz) and against the CPU oracle on ragged batches: bit for bit
 (IQ DAC frames and the compressed audio)."""
 import numpy as np
@@ -39,15 +39,17 @@ def test_device_tx_matches_reference_firmware(cuda, path):
 
 
 @pytest.mark.parametrize("frames", [32, 64, 512, 2048])
-def test_device_tx_call_granularity(cuda, frames):
-    g = load_tx(tx_files()[0])
+@pytest.mark.parametrize("name", ["tx_usb", "tx_fm_m6k_subtone"])
+def test_device_tx_call_granularity(cuda, frames, name):
+    g = load_tx([p for p in tx_files() if p.endswith(name + ".npz")][0])
     iq, _ = run_tx(U.tx_config_from_ref_args(g["args"]), g["audio"], frames)
     np.testing.assert_array_equal(iq, g["iq"])
 
 
-@pytest.mark.parametrize("mode,iqmode,channels", [(0, 4, 333), (1, 2, 130), (0, 0, 65)])
+@pytest.mark.parametrize("mode,iqmode,channels", [(0, 4, 333), (1, 2, 130), (0, 0, 65), (5, 3, 200), (5, 1, 70)])
 def test_device_tx_matches_oracle_ragged(cuda, mode, iqmode, channels):
-    cfg = U.default_tx_config(dmod_mode=mode, iq_freq_mode=iqmode)
+    cfg = U.default_tx_config(dmod_mode=mode, iq_freq_mode=iqmode, fm_subaudible_tone=7 if mode == 5 else 0,
+                              fm_deviation_5k=int(iqmode == 1))
     audio = synth.tx_audio(np.arange(channels), 0, 1024)
     iq, a0 = run_tx(cfg, audio, 256)
     ref_iq, ref_a0 = oracle.OracleTx(U.build_tx_plan(cfg), channels).process(audio, threads=8)

@@ -1,4 +1,4 @@
-"""SSB transmit (TxProcessor_Run, drivers/audio/tx_processor.c:891-1078): the product's TX setup
+"""SSB and FM transmit (TxProcessor_Run, drivers/audio/tx_processor.c:891-1078): the product's TX setup
 layer (uhsdr_tx_plan_build) and the CPU oracle's TX chain against the reference firmware's own
 fixtures (tests/golden/tx_*.npz: codec mic frames in, IQ DAC frames out), bit for bit."""
 import glob

@@ -93,7 +93,8 @@ class TxConfig(C.Structure):
         ("mic_gain_mult", C.c_int32), ("mic_boost", C.c_int32), ("comp_level", C.c_int32), ("alc_decay", C.c_int32),
         ("alc_postfilt_gain", C.c_int32), ("tx_filter", C.c_int32), ("bass_gain", C.c_int32),
         ("treble_gain", C.c_int32), ("filter_disable", C.c_int32), ("power_factor", C.c_float),
-        ("gain_i", C.c_float), ("gain_q", C.c_float), ("phase_balance", C.c_float), ("reserved", C.c_int32 * 16),
+        ("gain_i", C.c_float), ("gain_q", C.c_float), ("phase_balance", C.c_float),
+        ("fm_deviation_5k", C.c_int32), ("fm_subaudible_tone", C.c_int32), ("reserved", C.c_int32 * 14),
     ]
 
 
@@ -106,7 +107,10 @@ class TxPlan(C.Structure):
         ("alc_gain_scaling", C.c_float), ("hilbert_i", C.c_float * (TX_HILBERT_TAPS + 7)),
         ("hilbert_q", C.c_float * (TX_HILBERT_TAPS + 7)), ("freq_shift_hz", C.c_int32), ("shift_kind", C.c_int32),
         ("shift_up", C.c_int32), ("osc_cos", C.c_float), ("osc_sin", C.c_float), ("final_i_gain", C.c_float),
-        ("final_q_gain", C.c_float), ("phase_balance", C.c_float), ("reserved", C.c_int32 * 32),
+        ("final_q_gain", C.c_float), ("phase_balance", C.c_float),
+        ("fm", C.c_int32), ("fm_mod_mult", C.c_float), ("fm_word", C.c_uint32), ("fm_swap", C.c_int32),
+        ("fm_sub_on", C.c_int32), ("fm_sub_step", C.c_uint32), ("fm_sub_scale", C.c_float),
+        ("dds_table", C.c_int16 * 1024), ("reserved", C.c_int32 * 32),
     ]
 
 
@@ -257,6 +261,7 @@ TX_ARG_MAP = {
     "mode": "dmod_mode", "iqmode": "iq_freq_mode", "micmult": "mic_gain_mult", "boost": "mic_boost",
     "comp": "comp_level", "txfilter": "tx_filter", "txbass": "bass_gain", "txtreble": "treble_gain",
     "txpwr": "power_factor", "txgi": "gain_i", "txgq": "gain_q", "txphase": "phase_balance",
+    "fm5k": "fm_deviation_5k", "subtone": "fm_subaudible_tone",
 }
 
 

@@ -41,7 +41,10 @@ typedef struct
     const uint32_t* v;
 } uhsdr_lattice_desc;
 
-extern const uhsdr_lattice_desc uhsdr_tx_lattices[3];
+extern const uhsdr_lattice_desc uhsdr_tx_lattices[4];
+extern const int16_t uhsdr_dds_table[1024];
+extern const uint32_t* const uhsdr_fm_subaudible;
+extern const int uhsdr_fm_subaudible_count;
 extern const uint32_t* const uhsdr_tx_hilbert_i;
 extern const uint32_t* const uhsdr_tx_hilbert_q;
 extern const int uhsdr_tx_hilbert_taps;

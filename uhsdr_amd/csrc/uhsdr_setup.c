@@ -483,10 +483,22 @@ static const uint8_t alc_params[13][2] = { { 1, 15 }, { 2, 12 }, { 4, 10 }, { 6,
 uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
 {
     if (!cfg || !p) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
-    if (cfg->dmod_mode != UHSDR_DEMOD_USB && cfg->dmod_mode != UHSDR_DEMOD_LSB)
+    const int fm = cfg->dmod_mode == UHSDR_DEMOD_FM;
+    if (cfg->dmod_mode != UHSDR_DEMOD_USB && cfg->dmod_mode != UHSDR_DEMOD_LSB && !fm)
     {
-        uhsdr_set_error("transmit mode %d: only SSB (USB/LSB) voice is implemented", cfg->dmod_mode);
+        uhsdr_set_error("transmit mode %d: SSB (USB/LSB) and FM voice are implemented", cfg->dmod_mode);
         return UHSDR_UNSUPPORTED;
+    }
+    if (fm && cfg->iq_freq_mode == UHSDR_IQ_CONV_OFF)
+    {
+        /* "No FM possible unless in frequency translate mode" (tx_processor.c:1009-1011) */
+        uhsdr_set_error("FM transmit needs the I/Q frequency translation");
+        return UHSDR_UNSUPPORTED;
+    }
+    if (fm && (cfg->fm_subaudible_tone < 0 || cfg->fm_subaudible_tone >= uhsdr_fm_subaudible_count))
+    {
+        uhsdr_set_error("fm_subaudible_tone %d outside 0..%d", cfg->fm_subaudible_tone, uhsdr_fm_subaudible_count - 1);
+        return UHSDR_ARGUMENT_ERROR;
     }
     if (cfg->audio_source < UHSDR_TX_AUDIO_MIC || cfg->audio_source > UHSDR_TX_AUDIO_LINEIN_R)
     {
@@ -514,10 +526,11 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
     p->in_gain = gain_calc;
     p->apply_in_gain = gain_calc != 1.0;
 
-    /* TxProcessor_FilterAudio: lattice band-pass unless disabled, biquads for codec sources */
-    p->run_lattice = !cfg->filter_disable;
+    /* TxProcessor_FilterAudio: lattice band-pass unless disabled (FM always filters,
+       tx_processor.c:1012), biquads for codec sources; FM uses IIR_TX_2k7_FM (:104-107) */
+    p->run_lattice = fm || !cfg->filter_disable;
     p->run_biquad = 1;
-    const int sel = cfg->tx_filter == 2 ? 1 : cfg->tx_filter == 3 ? 2 : 0;   /* TENOR, BASS, default SOPRANO */
+    const int sel = fm ? 3 : cfg->tx_filter == 2 ? 1 : cfg->tx_filter == 3 ? 2 : 0;   /* TENOR, BASS, default SOPRANO */
     const uhsdr_lattice_desc* l = &uhsdr_tx_lattices[sel];
     p->lat_stages = l->stages;
     copy_bits(p->lat_k, l->k, l->stages);
@@ -537,7 +550,8 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
     else { postfilt = 4; decay_var = 10; }
     p->postfilt_gain = ((float)postfilt) / 2.0 + 0.5;
     p->alc_decay = exp10f(-((((float)decay_var) + 35.0) / 10.0));
-    p->alc_gain_scaling = 1.00;                              /* SSB_ALC_GAIN_CORRECTION, audio_driver.h:417 */
+    p->alc_gain_scaling = fm ? 0.95 : 1.00;                  /* FM_ALC_GAIN_CORRECTION (tx_processor.c:521) /
+                                                                SSB_ALC_GAIN_CORRECTION (audio_driver.h:417) */
 
     /* TX Hilbert pair, swapped for LSB (tx_processor.c:477-478) */
     const int T = uhsdr_tx_hilbert_taps;
@@ -564,12 +578,33 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
         p->shift_up = !(p->freq_shift_hz > 0);
     }
 
-    /* TxProcessor_IqFinalProcessing (tx_processor.c:282-330) with iq_gain_comp = SSB_GAIN_COMP */
-    float scaling = 1.133;                                   /* SSB_GAIN_COMP, audio_driver.h:419 */
+    /* TxProcessor_IqFinalProcessing (tx_processor.c:282-330) with iq_gain_comp = SSB_GAIN_COMP
+       or FM_MOD_AMPLITUDE_SCALING (:500, :1014) */
+    float scaling = fm ? 0.875 : 1.133;                      /* SSB_GAIN_COMP, audio_driver.h:419 */
     scaling *= (1 << 16);                                    /* IQ_BIT_SCALE_UP */
     p->final_i_gain = cfg->power_factor * cfg->gain_i * scaling;
     p->final_q_gain = cfg->power_factor * cfg->gain_q * scaling;
     p->phase_balance = cfg->phase_balance;
+
+    /* FM modulator (TxProcessor_FM, tx_processor.c:534-588) and its softdds tables */
+    memcpy(p->dds_table, uhsdr_dds_table, sizeof p->dds_table);
+    if (fm)
+    {
+        p->fm = 1;
+        p->fm_mod_mult = cfg->fm_deviation_5k ? 2 : 1;
+        const int32_t tf = p->freq_shift_hz;
+        p->fm_word = (uint32_t)(((1 << 16) * (tf < 0 ? -tf : tf)) / IQ_SAMPLE_RATE);   /* FM_MOD_ACC_MAX_VALUE */
+        p->fm_swap = tf < 0;
+        float tone;
+        memcpy(&tone, &uhsdr_fm_subaudible[cfg->fm_subaudible_tone], 4);
+        /* AudioManagement_CalcSubaudibleGenFreq -> softdds_setFreqDDS (softdds.c:26-47) */
+        p->fm_sub_on = tone > 0;
+        uint64_t freq64_shifted = tone * 1024;                /* DDS_TBL_SIZE */
+        freq64_shifted <<= 22;                                /* SOFTDDS_ACC_SHIFT */
+        p->fm_sub_step = (uint32_t)(freq64_shifted / IQ_SAMPLE_RATE);
+        const float fm_mod_mult = p->fm_mod_mult;
+        p->fm_sub_scale = 0.00045 * fm_mod_mult;              /* FM_SUBAUDIBLE_TONE_AMPLITUDE_SCALING */
+    }
     return UHSDR_OK;
 }
 

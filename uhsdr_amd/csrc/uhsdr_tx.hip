@@ -39,12 +39,20 @@ struct TxVoiceArgs
     float* bq;              // [12][C]
     float* alc;             // [C]
     float* delay;           // [10][32][C]
+    uint32_t* fm;           // FM: [4][C] hpf_prev_a, hpf_prev_b (f32 bits), fm_mod_accum, sub-audible dds acc
+    int2* iq;               // FM: DAC frames [C][N] written here (no tx_iq)
     int C, N;
     int delay_phase;        // alc_delay_inbuf / 32 before this launch
 };
 
-// TxProcessor_AudioBufferFill + _FilterAudio + _VoiceCompressor, one lane per channel
-template <int S>
+__device__ __forceinline__ int tx_to_int32(float f)
+{
+    return (f > -2147483904.0f && f < 2147483648.0f) ? (int)f : INT32_MIN;
+}
+
+// TxProcessor_AudioBufferFill + _FilterAudio + _VoiceCompressor, one lane per channel; with FM
+// also TxProcessor_FM (tx_processor.c:534-588) and TxProcessor_IqFinalProcessing (:282-330)
+template <int S, bool FM>
 __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
 {
     const uhsdr_tx_plan* __restrict__ P = a.plan;
@@ -68,6 +76,13 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
     const bool apply_gain = P->apply_in_gain, run_lat = P->run_lattice, run_bq = P->run_biquad, comp = P->comp_on;
     const float in_gain = P->in_gain, post = P->postfilt_gain, decay = P->alc_decay, gscale = P->alc_gain_scaling;
     const int calls = a.N / BLK;
+    float hpf_a = 0.0f, hpf_b = 0.0f;
+    uint32_t fm_acc = 0, sub_acc = 0;
+    if constexpr (FM)
+    {
+        hpf_a = __uint_as_float(a.fm[cl]); hpf_b = __uint_as_float(a.fm[C + cl]);
+        fm_acc = a.fm[2 * C + cl]; sub_acc = a.fm[3 * C + cl];
+    }
     for (int k = 0; k < calls; ++k)
     {
         float x[BLK];
@@ -127,16 +142,66 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
         }
         if (live)
         {
-            float* dst = a.txa + (size_t)c * a.N + k * BLK;
             float* d0 = a.a0 ? a.a0 + (size_t)c * a.N + k * BLK : nullptr;
+            float* dst = FM ? nullptr : a.txa + (size_t)c * a.N + k * BLK;
 #pragma unroll
             for (int m = 0; m < BLK; m += 4)
             {
                 const float4 v = make_float4(x[m], x[m + 1], x[m + 2], x[m + 3]);
-                *(float4*)(dst + m) = v;
+                if (!FM) *(float4*)(dst + m) = v;
                 if (d0) *(float4*)(d0 + m) = v;
             }
         }
+        if constexpr (FM)
+        {
+            const int16_t* __restrict__ dds = P->dds_table;
+            const bool sub = P->fm_sub_on, swap = P->fm_swap;
+            const float mult = P->fm_mod_mult, sub_scale = P->fm_sub_scale;
+            const uint32_t word = P->fm_word, step = P->fm_sub_step;
+            const float gi = P->final_i_gain, gq = P->final_q_gain, ph = P->phase_balance;
+            int out[2 * BLK];
+#pragma unroll
+            for (int m = 0; m < BLK; ++m)
+            {
+                const float av = x[m];
+                hpf_b = (float)(0.05 * (double)(hpf_b + av - hpf_a));    // FM_TX_HPF_ALPHA pre-emphasis
+                hpf_a = av;
+                float a1 = hpf_b;
+                if (sub)
+                {
+                    // softdds_addSingleTone (softdds.c:113-119): index (acc >> 22) % 1024, then acc += step
+                    const uint32_t idx = (sub_acc >> 22) % 1024u;
+                    sub_acc += step;
+                    a1 += (float)dds[idx] * sub_scale;
+                }
+                // fm_mod_accum += word + a1 * FM_MOD_SCALING * mult; as on x86, the float sum is
+                // truncated through a 64-bit integer (cvttss2si) into the uint32 accumulator
+                const float t = word + (a1 * 16 * mult);
+                const float sum = (float)fm_acc + t;
+                fm_acc = (uint32_t)(long long)sum;
+                fm_acc %= 65536u;
+                const uint32_t idx = fm_acc >> 6;                            // FM_MOD_DDS_ACC_SHIFT
+                const float vi = dds[idx], vq = dds[(idx + 768u) % 1024u];
+                float I = swap ? vq : vi, Q = swap ? vi : vq;
+                I = I * gi;
+                Q = Q * gq;
+                if (ph < 0) { const float e = I * ph; Q = Q + e; }
+                else if (ph > 0) { const float e = Q * ph; I = I + e; }
+                out[2 * m] = tx_to_int32(I);
+                out[2 * m + 1] = tx_to_int32(Q);
+            }
+            if (live)
+            {
+                int4* dq = (int4*)(a.iq + (size_t)c * a.N + k * BLK);
+#pragma unroll
+                for (int j = 0; j < BLK / 2; ++j) dq[j] = make_int4(out[4 * j], out[4 * j + 1], out[4 * j + 2], out[4 * j + 3]);
+            }
+        }
+    }
+    if (FM && live)
+    {
+        a.fm[c] = __float_as_uint(hpf_a); a.fm[C + c] = __float_as_uint(hpf_b);
+        a.fm[2 * C + c] = fm_acc; a.fm[3 * C + c] = sub_acc;
     }
     if (live)
     {
@@ -158,11 +223,6 @@ struct TxIqArgs
     int2* iq;                // [C][ld] DAC frames, frame 0 of this launch
     int C, N, ld, lw;
 };
-
-__device__ __forceinline__ int tx_to_int32(float f)
-{
-    return (f > -2147483904.0f && f < 2147483648.0f) ? (int)f : INT32_MIN;
-}
 
 template <int R>
 __global__ void __launch_bounds__(64) tx_iq(TxIqArgs a)
@@ -277,6 +337,7 @@ struct uhsdr_tx_s
     int C, N, Nf, R, lw;
     hipStream_t stream;
     float *lat, *bq, *alc, *delay, *hist, *osc, *txa;
+    uint32_t* fm;            // FM modulator state [4][C] (null for SSB)
     void* arena;
     size_t arena_bytes;
     long long calls_done, iq_launches;
@@ -336,7 +397,8 @@ extern "C" uhsdr_status uhsdr_tx_create(const uhsdr_tx_config* cfg, int32_t C, i
     auto take = [&](size_t n) { size_t o = fl; fl += (n + 63) & ~(size_t)63; return o; };
     const size_t o_lat = take((size_t)10 * C), o_bq = take((size_t)12 * C), o_alc = take((size_t)C);
     const size_t o_dly = take((size_t)UHSDR_TX_DELAY * C), o_hist = take((size_t)hist_stride(TX_T) * C);
-    const size_t o_osc = take(4), o_txa = take((size_t)C * N);
+    const size_t o_osc = take(4), o_txa = take(h->plan.fm ? 0 : (size_t)C * N);
+    const size_t o_fm = take(h->plan.fm ? (size_t)4 * C : 0);
     h->arena_bytes = fl * sizeof(float);
     if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess || hipMalloc((void**)&h->d_plan, sizeof(uhsdr_tx_plan)) != hipSuccess)
     {
@@ -348,6 +410,7 @@ extern "C" uhsdr_status uhsdr_tx_create(const uhsdr_tx_config* cfg, int32_t C, i
     float* A = (float*)h->arena;
     h->lat = A + o_lat; h->bq = A + o_bq; h->alc = A + o_alc; h->delay = A + o_dly;
     h->hist = A + o_hist; h->osc = A + o_osc; h->txa = A + o_txa;
+    h->fm = h->plan.fm ? (uint32_t*)(A + o_fm) : nullptr;
     if (hipMemcpy(h->d_plan, &h->plan, sizeof(uhsdr_tx_plan), hipMemcpyHostToDevice) != hipSuccess)
     {
         uhsdr_set_error("plan upload failed");
@@ -363,9 +426,18 @@ extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio
     TxVoiceArgs va;
     va.plan = h->d_plan; va.audio = (const int2*)audio; va.txa = h->txa; va.a0 = a0;
     va.lat = h->lat; va.bq = h->bq; va.alc = h->alc; va.delay = h->delay;
+    va.fm = h->fm; va.iq = (int2*)iq;
     va.C = h->C; va.N = h->N;
     va.delay_phase = (int)(h->calls_done % TX_DELAY_SLOTS);
-    hipLaunchKernelGGL(tx_voice<10>, dim3((h->C + 63) / 64), dim3(64), 0, h->stream, va);
+    if (h->plan.fm)
+    {
+        // FM: the modulator is sequential per channel and finishes in tx_voice
+        hipLaunchKernelGGL((tx_voice<10, true>), dim3((h->C + 63) / 64), dim3(64), 0, h->stream, va);
+        HIPCHK(hipGetLastError());
+        h->calls_done += h->N / BLK;
+        return UHSDR_OK;
+    }
+    hipLaunchKernelGGL((tx_voice<10, false>), dim3((h->C + 63) / 64), dim3(64), 0, h->stream, va);
     HIPCHK(hipGetLastError());
     const int cpw = 64 / (h->Nf / h->R);
     const size_t lds = sizeof(float) * ((size_t)cpw * h->lw + (h->plan.shift_kind == 2 ? 2 * h->Nf : 0));

@@ -15,15 +15,19 @@
 #define BLK UHSDR_IQ_BLOCK_SIZE
 #define IQ_BIT_SCALE_DOWN 0.0000152587890625f
 
+// native 4-float vector: arrays of HIP's float4 (a struct with a union) loaded from global
+// memory defeat SROA and end up in scratch
+typedef float vf4 __attribute__((ext_vector_type(4)));
+
 // acc[r] = sum_{k<T} c[k] * win[r*M + k], r < R; tap order k = 0..T-1 from +0.0f exactly as
 // arm_fir_f32 / arm_fir_decimate_f32 (CMSIS .../arm_fir_f32.c:482-560).  `win` is the lane's
 // first window sample in LDS (16-byte aligned); `c` the tap table in the plan (global, read
-// with scalar loads: the index is wave-uniform), zero beyond T up to a multiple of 8 (a +-0
-// product never changes a finite accumulator that started at +0, so the padding is exact).
-// The chunk loop over 8 taps is deliberately not unrolled: the register window (WA samples,
-// a multiple of 8) slides by 8 samples per chunk and the next 8 samples (two ds_read_b128)
-// and the next 8 taps are fetched before the current MACs, so the live set stays at R
-// accumulators + one window.  Reads run up to 22 samples past the last one used (zeroed).
+// with scalar loads: the index is wave-uniform).  Taps run in chunks of 8 and a final chunk
+// of T % 8: the register window (WA samples, a multiple of 8) slides by 8 samples per chunk and
+// the next 8 samples (two ds_read_b128) and taps are fetched before the current MACs, so the
+// live set stays at R accumulators + one window; the chunk loop is unrolled by the window's
+// rotation period, which turns the slide into register renaming.  Reads run up to 22 samples
+// past the last one used (zeroed).
 // LDS load of V (4 or 2) consecutive floats into w[j..j+V)
 template <int V, int N>
 __device__ __forceinline__ void lds_vec(const float* p, float (&w)[N], int j)
@@ -50,13 +54,14 @@ template <int T, int R, int M, int V = 4>
 __device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&acc)[R])
 {
     constexpr int WA = (M * (R - 1) + 8 + 7) & ~7;
-    constexpr int NCH = (T + 7) / 8;
+    constexpr int NCH = T / 8, TR = T % 8;           // full 8-tap chunks, then TR taps
+    constexpr int ROT = WA / 8 + 1;
     float w[WA];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.0f;
 #pragma unroll
     for (int j = 0; j < WA; j += V) lds_vec<V>(win + j, w, j);
-#pragma unroll 1
+#pragma unroll ROT
     for (int ch = 0; ch < NCH; ++ch)
     {
         float cc[8];
@@ -75,6 +80,73 @@ __device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&
         for (int j = 0; j < WA - 8; ++j) w[j] = w[j + 8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) w[WA - 8 + q] = nw[q];
+    }
+#pragma unroll
+    for (int kk = 0; kk < TR; ++kk)
+    {
+        const float ck = c[8 * NCH + kk];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * ck;
+    }
+}
+
+// Two filters in one pass over an interleaved window {x0[n], x1[n]} -- the I and Q branches
+// of a pair (Hilbert I / Q, or the I and Q decimators): acc[r] = { sum_k c0[k] * x0[rM+k],
+// sum_k c1[k] * x1[rM+k] } with taps c[k] = {c0[k], c1[k]}.  Per element this is exactly the
+// binary32 sequence of fir_block (tap order k = 0..T-1 from +0.0f, separate multiply and add),
+// but each v_pk_mul_f32 / v_pk_add_f32 does two of them in one issue slot: packed f32 issues
+// at the scalar VALU rate on gfx950 (tools/micro/pk_rate.hip: 4.3 vs 4.1 cycles per wave
+// instruction), so a FIR pair costs half the VALU time of two fir_block calls.
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(4))) v2f ctaps2_t;
+__device__ __forceinline__ ctaps2_t* as_taps2(const float* p) { return (ctaps2_t*)p; }
+
+template <int T, int R, int M>
+__device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&acc)[R])
+{
+    constexpr int WA = (M * (R - 1) + 8 + 7) & ~7;   // window pairs in registers
+    constexpr int NCH = T / 8, TR = T % 8;           // full 8-tap chunks, then TR taps
+    constexpr int ROT = WA / 8 + 1;                  // chunks until the window registers repeat
+    v2f w[WA];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = v2f{ 0.0f, 0.0f };
+#pragma unroll
+    for (int j = 0; j < WA; j += 2)
+    {
+        const vf4 v = *(const vf4*)(win + 2 * j);
+        w[j] = v.xy; w[j + 1] = v.zw;
+    }
+    // unrolled by the rotation period, the window slide is pure register renaming
+#pragma unroll ROT
+    for (int ch = 0; ch < NCH; ++ch)
+    {
+        v2f cc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cc[q] = c[8 * ch + q];
+        v2f nw[8];
+#pragma unroll
+        for (int q = 0; q < 8; q += 2)
+        {
+            const vf4 v = *(const vf4*)(win + 2 * (8 * ch + WA + q));
+            nw[q] = v.xy; nw[q + 1] = v.zw;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+        {
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * cc[kk];
+        }
+#pragma unroll
+        for (int j = 0; j < WA - 8; ++j) w[j] = w[j + 8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) w[WA - 8 + q] = nw[q];
+    }
+#pragma unroll
+    for (int kk = 0; kk < TR; ++kk)
+    {
+        const v2f ck = c[8 * NCH + kk];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * ck;
     }
 }
 
@@ -98,9 +170,6 @@ __host__ __device__ constexpr int hist_stride(int T) { return (T - 1 + 3) & ~3; 
 // with fewer lanes the rest is loaded when the window is filled)
 __host__ __device__ constexpr int hist_q(int T) { return (hist_stride(T) / 4 + 7) / 8; }
 
-// native 4-float vector: arrays of HIP's float4 (a struct with a union) loaded from global
-// memory defeat SROA and end up in scratch
-typedef float vf4 __attribute__((ext_vector_type(4)));
 
 // history row of a T-tap filter for channel cl: lane b of nb loads float4s b, b+nb, ... (HQ per lane)
 template <int T, int HQM>
@@ -149,6 +218,63 @@ __device__ __forceinline__ void front_fill(float* W, float* row, int c, bool act
     {
         const float4 v = *(const float4*)(W + nnew + 4 * q);
         if (live) *(float4*)(ho + 4 * q) = v;
+    }
+}
+
+// front_fill for a FIR pair: the window holds interleaved pairs {x0[n], x1[n]} (8 bytes per
+// sample) built from the two history rows (row0 / row1, prefetched as buf0 / buf1) and NV new
+// pairs per lane; the next call's history rows are de-interleaved back to HBM.
+template <int T, int HQM>
+__device__ __forceinline__ void front_fill2(float* W, float* row0, float* row1, int c, bool act, bool live, int b,
+                                            int nb, const vf4 (&buf0)[HQM], const vf4 (&buf1)[HQM],
+                                            const v2f* vals, int NV)
+{
+    constexpr int hs4 = hist_stride(T) / 4, HQ = hist_q(T);
+    static_assert(((T - 1) & 1) == 0, "pair windows store new samples two pairs at a time");
+    const int nnew = nb * NV;
+    if (act)
+    {
+        // pad samples (T-1 .. HS-1) land where the new samples go and are overwritten below
+#pragma unroll
+        for (int i = 0; i < HQ; ++i)
+        {
+            const int q = b + nb * i;
+            if (q < hs4)
+            {
+                const vf4 x = buf0[i], y = buf1[i];
+                *(vf4*)(W + 8 * q) = vf4{ x.x, y.x, x.y, y.y };
+                *(vf4*)(W + 8 * q + 4) = vf4{ x.z, y.z, x.w, y.w };
+            }
+        }
+        const size_t ro = (size_t)(live ? c : 0) * (hs4 * 4);
+        const vf4* h0 = (const vf4*)(row0 + ro);
+        const vf4* h1 = (const vf4*)(row1 + ro);
+        for (int q = b + nb * HQ; q < hs4; q += nb)
+        {
+            const vf4 x = h0[q], y = h1[q];
+            *(vf4*)(W + 8 * q) = vf4{ x.x, y.x, x.y, y.y };
+            *(vf4*)(W + 8 * q + 4) = vf4{ x.z, y.z, x.w, y.w };
+        }
+    }
+    wave_sync();
+    if (act)
+    {
+        float* d = W + 2 * (T - 1 + b * NV);
+        for (int j = 0; j < NV; j += 2)
+            *(vf4*)(d + 2 * j) = vf4{ vals[j].x, vals[j].y, vals[j + 1].x, vals[j + 1].y };
+        for (int t = b; t < FRONT_TAIL; t += nb) *(v2f*)(W + 2 * (T - 1 + nnew + t)) = v2f{ 0.0f, 0.0f };
+    }
+    wave_sync();
+    const size_t ro = (size_t)c * (hs4 * 4);
+    for (int q = b; q < hs4; q += nb)
+    {
+        const vf4 p0 = *(const vf4*)(W + 2 * (nnew + 4 * q));
+        const vf4 p1 = *(const vf4*)(W + 2 * (nnew + 4 * q) + 4);
+        if (live)
+        {
+            *(vf4*)(row0 + ro + 4 * q) = vf4{ p0.x, p0.z, p1.x, p1.z };
+            *(vf4*)(row1 + ro + 4 * q) = vf4{ p0.y, p0.w, p1.y, p1.w };
+        }
     }
 }
 

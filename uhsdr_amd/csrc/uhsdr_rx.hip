@@ -49,6 +49,8 @@ struct FrontArgs
     float* osc_out;          // [2] written by workgroup 0
     float* adec;             // decimated output of this launch; row stride ldd
     float* adec_q;           // AM / SAM: decimated Q (adec holds I)
+    const float* taps2a;     // first FIR pair, interleaved {c_i[k], c_q[k]} (zero-padded to 8k taps)
+    const float* taps2b;     // decimate-first paths: the Hilbert pair on the decimated I/Q
     int C, N, ld, ldd;
     int lw;                  // LDS window pitch per channel (floats, multiple of 4; host picks it
                              // for conflict-free ds_read_b128, front_window_pitch)
@@ -61,50 +63,85 @@ struct InputStage
     int iq_auto, shift, shift_up;
 };
 
-__device__ __forceinline__ void convert_frame(const int2 v, const InputStage& s, int n, const float* m1, const float* m2,
-                                              const float* osc, float& I, float& Q)
+// FreqShift on one lane's R frames, in place on (ib, qb) = (I, Q) for FREQ_SHIFT_UP and (Q, I)
+// otherwise (freq_shift.c:324).  Fs/4 exchange (freq_shift.c:219-262): frame n of a group of 4
+// gets {x0, -j x1, -x2, j x3}; the lane's first frame is a multiple of 4, so n & 3 == j & 3 and
+// the exchange is register renaming.  Recursive oscillator (FreqShift_Approx,
+// freq_shift.c:57-101): the shared trajectory osc[2n] / osc[2n+1] from LDS.
+template <int R>
+__device__ __forceinline__ void freq_shift_block(float (&ib)[R], float (&qb)[R], int kind, const float* osc, int n0)
 {
-    I = (float)v.x;
-    Q = (float)v.y;
-    I = I * IQ_BIT_SCALE_DOWN;
-    Q = Q * IQ_BIT_SCALE_DOWN;
-    if (!s.iq_auto)
+    if (kind == 1)
     {
-        I = I * s.gi;
-        Q = Q * s.gq;
-        if (s.ph < 0) { const float e3 = I * s.ph; Q = Q + e3; }
-        else if (s.ph > 0) { const float e3 = Q * s.ph; I = I + e3; }
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+        {
+            const float iv = ib[j], qv = qb[j];
+            switch (j & 3)
+            {
+            case 0: break;
+            case 1: ib[j] = qv; qb[j] = -iv; break;
+            case 2: ib[j] = -iv; qb[j] = -qv; break;
+            default: ib[j] = -qv; qb[j] = iv; break;
+            }
+        }
     }
     else
     {
-        const int b = n / BLK;
-        Q += m1[b] * I;
-        I = I * m2[b];
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+        {
+            const float oq = osc[2 * (n0 + j)], oi = osc[2 * (n0 + j) + 1];
+            const float qt = qb[j], it = ib[j];
+            qb[j] = (qt * oq) - (it * oi);
+            ib[j] = (it * oq) + (qt * oi);
+        }
+    }
+}
+
+// R consecutive frames n0.. of one channel: int32 -> f32 x 2^-16 (audio_driver.c:2660-2685),
+// I/Q correction (manual :2294-2313 via AudioDriver_IQPhaseAdjust :1776-1801, or auto with
+// this call's factors m1 / m2, :2274-2293), FreqShift (:2700-2705).  Every branch is
+// wave-uniform and hoisted out of the per-frame loops, so each case is straight-line code.
+template <int R>
+__device__ __forceinline__ void convert_block(const int4 (&raw)[R / 2], const InputStage& s, int n0, const float* m1,
+                                              const float* m2, const float* osc, float (&xi)[R], float (&xq)[R])
+{
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+    {
+        const int vi = (j & 1) ? raw[j / 2].z : raw[j / 2].x;
+        const int vq = (j & 1) ? raw[j / 2].w : raw[j / 2].y;
+        xi[j] = ((float)vi) * IQ_BIT_SCALE_DOWN;
+        xq[j] = ((float)vq) * IQ_BIT_SCALE_DOWN;
+    }
+    if (!s.iq_auto)
+    {
+#pragma unroll
+        for (int j = 0; j < R; ++j) { xi[j] = xi[j] * s.gi; xq[j] = xq[j] * s.gq; }
+        if (s.ph < 0)
+        {
+#pragma unroll
+            for (int j = 0; j < R; ++j) { const float e3 = xi[j] * s.ph; xq[j] = xq[j] + e3; }
+        }
+        else if (s.ph > 0)
+        {
+#pragma unroll
+            for (int j = 0; j < R; ++j) { const float e3 = xq[j] * s.ph; xi[j] = xi[j] + e3; }
+        }
+    }
+    else
+    {
+        // R <= 16 frames never straddle a 32-frame call: one factor pair per lane
+        const int bb = n0 / BLK;
+        const float f1 = m1[bb], f2 = m2[bb];
+#pragma unroll
+        for (int j = 0; j < R; ++j) { xq[j] += f1 * xi[j]; xi[j] = xi[j] * f2; }
     }
     if (s.shift)
     {
-        float ib = s.shift_up ? I : Q;
-        float qb = s.shift_up ? Q : I;
-        if (s.shift == 1)
-        {
-            const float iv = ib, qv = qb;
-            switch (n & 3)
-            {
-            case 0: break;
-            case 1: ib = qv; qb = -iv; break;
-            case 2: ib = -iv; qb = -qv; break;
-            default: ib = -qv; qb = iv; break;
-            }
-        }
-        else
-        {
-            const float oq = osc[2 * n], oi = osc[2 * n + 1];
-            const float qt = qb, it = ib;
-            qb = (qt * oq) - (it * oi);
-            ib = (it * oq) + (qt * oi);
-        }
-        I = s.shift_up ? ib : qb;
-        Q = s.shift_up ? qb : ib;
+        if (s.shift_up) freq_shift_block<R>(xi, xq, s.shift, osc, n0);
+        else freq_shift_block<R>(xq, xi, s.shift, osc, n0);
     }
 }
 
@@ -128,18 +165,14 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
     const int N = a.N, C = a.C;
     const int lane = threadIdx.x;
     const int nb = N / R;                            // lanes per channel (>= 4)
-    const int CPW = FRONT_WAVE / nb;                 // channels per wave
+    const int CPW = FRONT_WAVE / nb;                 // channels per wave (one channel group)
     int g, b;
-    front_lane(lane, nb, R, g, b);
-    const int c = blockIdx.x * CPW + g;
+    front_lane(lane, nb, 2 * R, g, b);               // lane map for the pair window (2R floats per lane)
     const bool act = g < CPW;
-    const bool live = act && c < C;
     const int gs = act ? g : 0;
-    const int cl = c < C ? c : C - 1;                // loads clamped: no exec-masked load branches
     const int nblk32 = N / BLK;
     constexpr int RD = R / M;                        // decimated samples per lane
-    constexpr int HQ1 = hist_q(T1), HQ2 = hist_q(T2);
-    constexpr int HQM = HQ1 > HQ2 ? HQ1 : HQ2;
+    constexpr int HQ1 = hist_q(T1), HQ2 = hist_q(T2 > 0 ? T2 : 1);
     const int LW = a.lw;
     float* W = smem + gs * LW;                       // this channel's window
     float* aux = smem + CPW * LW;                    // auto-IQ factors [2][CPW][nblk32], osc [2N]
@@ -147,70 +180,28 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
     float* m2 = aux + CPW * nblk32;
     float* osc = aux + (P->iq_auto_correction ? 2 * CPW * nblk32 : 0);
 
-    // ---- entry: issue the I/Q frames and the history rows of passes 0 and 1 ----
-    int4 raw[R / 2];
-    {
-        const int4* src = (const int4*)(a.iq + (size_t)cl * a.ld + b * R);
-#pragma unroll
-        for (int j = 0; j < R / 2; ++j) raw[j] = src[j];
-    }
-    vf4 hA[HQM], hB[HQM];
-    front_load_row<T1>(a.hist1_i, cl, b, nb, hA);
-    front_load_row<T1>(a.hist1_q, cl, b, nb, hB);
-
     InputStage in;
     in.gi = P->iq_gain_i; in.gq = P->iq_gain_q; in.ph = P->iq_phase_balance;
     in.iq_auto = P->iq_auto_correction;
     in.shift = P->freq_shift_hz != 0 ? P->shift_kind : 0;
     in.shift_up = P->shift_up;
+    ctaps2_t* tA = as_taps2(a.taps2a);
+    const bool lsb = P->lsb;
 
-    // ---- pre-pass: auto I/Q statistics per 32-frame call; oscillator trajectory ----
-    if (in.iq_auto)
+    // One wave per channel group.  The I/Q frames and the stage-1 history rows are issued at
+    // entry; the stage-2 rows are issued before the stage-1 FIR, so their latency hides behind it.
+    const int grp = blockIdx.x;
+    int4 raw[R / 2];
+    vf4 hA[HQ1], hB[HQ1];
+    const int c = grp * CPW + g;
+    const bool live = act && c < C;
+    const int cl = c < C ? c : C - 1;                // loads clamped: no exec-masked load branches
     {
-        for (int e = lane; e < CPW * nblk32; e += FRONT_WAVE)
-        {
-            const int gg = e / nblk32, bb = e % nblk32;
-            const int cc = blockIdx.x * CPW + gg;
-            float t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
-            if (cc < C)
-                for (int i = 0; i < BLK; ++i)
-                {
-                    const int2 v = a.iq[(size_t)cc * a.ld + bb * BLK + i];
-                    const float I = ((float)v.x) * IQ_BIT_SCALE_DOWN;
-                    const float Q = ((float)v.y) * IQ_BIT_SCALE_DOWN;
-                    const float sI = (I < 0) ? -1.0f : ((I > 0) ? 1.0f : 0.0f);
-                    const float sQ = (Q < 0) ? -1.0f : ((Q > 0) ? 1.0f : 0.0f);
-                    t1 += sI * Q;
-                    t2 += sI * I;
-                    t3 += sQ * Q;
-                }
-            m1[e] = t1;
-            m2[e] = t2;
-            smem[e] = t3;                            // scratch; the windows are filled later
-        }
-        wave_sync();
-        for (int gg = lane; gg < CPW; gg += FRONT_WAVE)
-        {
-            const int cc = blockIdx.x * CPW + gg;
-            if (cc >= C) continue;
-            float o1 = a.teta[cc], o2 = a.teta[C + cc], o3 = a.teta[2 * C + cc];
-            for (int bb = 0; bb < nblk32; ++bb)
-            {
-                const int e = gg * nblk32 + bb;
-                float t1 = m1[e], t2 = m2[e], t3 = smem[e];
-                t1 = (float)(-0.003 * (double)(t1 / (float)BLK) + 0.997 * (double)o1);
-                t2 = (float)(0.003 * (double)(t2 / (float)BLK) + 0.997 * (double)o2);
-                t3 = (float)(0.003 * (double)(t3 / (float)BLK) + 0.997 * (double)o3);
-                const float M_c1 = (t2 != 0.0f) ? t1 / t2 : 0.0f;
-                float help = (t2 * t2);
-                if (help > 0.0f) help = (t3 * t3 - t1 * t1) / help;
-                const float M_c2 = (help > 0.0f) ? sqrtf(help) : 1.0f;
-                m1[e] = M_c1;
-                m2[e] = M_c2;
-                o1 = t1; o2 = t2; o3 = t3;
-            }
-            a.teta[cc] = o1; a.teta[C + cc] = o2; a.teta[2 * C + cc] = o3;
-        }
+        const int4* src = (const int4*)(a.iq + (size_t)cl * a.ld + b * R);
+#pragma unroll
+        for (int j = 0; j < R / 2; ++j) raw[j] = src[j];
+        front_load_row<T1>(a.hist1_i, cl, b, nb, hA);
+        front_load_row<T1>(a.hist1_q, cl, b, nb, hB);
     }
     if (in.shift == 2 && lane == 0)
     {
@@ -233,86 +224,127 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
         }
         if (blockIdx.x == 0) { a.osc_out[0] = vi; a.osc_out[1] = vq; }
     }
-    wave_sync();
 
-    // ---- this lane's R frames, converted; I and Q kept in registers ----
-    float xi[R], xq[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j)
     {
-        const int2 v = (j & 1) ? make_int2(raw[j / 2].z, raw[j / 2].w) : make_int2(raw[j / 2].x, raw[j / 2].y);
-        convert_frame(v, in, b * R + j, m1 + gs * nblk32, m2 + gs * nblk32, osc, xi[j], xq[j]);
-    }
-
-    const bool lsb = P->lsb;
-    float o[RD];
-    if constexpr (T2 == 0)
-    {
-        // AM / SAM: decimate I and Q with the path's own tables (DECIMATE_RX_I / _Q,
-        // audio_filter.c:1167-1176, audio_driver.c:2742-2746), no Hilbert (:2748);
-        // FM: the Hilbert / low-pass pair at 48 ksps (:2748-2753), no decimation.
-        // The demodulator in rx_back / rx_fm takes both I and Q.
-        float dq[RD];
-        front_fill<T1>(W, a.hist1_i, c, act, live, b, nb, hA, xi, R);
-        fir_block<T1, RD, M>(W + b * R, as_taps(DECIM_FIRST ? P->dec : P->hilbert_i), o);
-        wave_sync();
-        front_fill<T1>(W, a.hist1_q, c, act, live, b, nb, hB, xq, R);
-        fir_block<T1, RD, M>(W + b * R, as_taps(DECIM_FIRST ? P->dec_q : P->hilbert_q), dq);
-        if (live)
+        // ---- auto I/Q statistics per 32-frame call of this group (audio_driver.c:2274-2293) ----
+        if (in.iq_auto)
         {
-            float* dst = a.adec_q + (size_t)c * a.ldd + b * RD;
-#pragma unroll
-            for (int r = 0; r < RD; ++r) dst[r] = dq[r];
+            for (int e = lane; e < CPW * nblk32; e += FRONT_WAVE)
+            {
+                const int gg = e / nblk32, bb = e % nblk32;
+                const int cc = grp * CPW + gg;
+                float t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
+                if (cc < C)
+                    for (int i = 0; i < BLK; ++i)
+                    {
+                        const int2 v = a.iq[(size_t)cc * a.ld + bb * BLK + i];
+                        const float I = ((float)v.x) * IQ_BIT_SCALE_DOWN;
+                        const float Q = ((float)v.y) * IQ_BIT_SCALE_DOWN;
+                        const float sI = (I < 0) ? -1.0f : ((I > 0) ? 1.0f : 0.0f);
+                        const float sQ = (Q < 0) ? -1.0f : ((Q > 0) ? 1.0f : 0.0f);
+                        t1 += sI * Q;
+                        t2 += sI * I;
+                        t3 += sQ * Q;
+                    }
+                m1[e] = t1;
+                m2[e] = t2;
+                smem[e] = t3;                        // scratch; the windows are filled later
+            }
+            wave_sync();
+            for (int gg = lane; gg < CPW; gg += FRONT_WAVE)
+            {
+                const int cc = grp * CPW + gg;
+                if (cc >= C) continue;
+                float o1 = a.teta[cc], o2 = a.teta[C + cc], o3 = a.teta[2 * C + cc];
+                for (int bb = 0; bb < nblk32; ++bb)
+                {
+                    const int e = gg * nblk32 + bb;
+                    float t1 = m1[e], t2 = m2[e], t3 = smem[e];
+                    t1 = (float)(-0.003 * (double)(t1 / (float)BLK) + 0.997 * (double)o1);
+                    t2 = (float)(0.003 * (double)(t2 / (float)BLK) + 0.997 * (double)o2);
+                    t3 = (float)(0.003 * (double)(t3 / (float)BLK) + 0.997 * (double)o3);
+                    const float M_c1 = (t2 != 0.0f) ? t1 / t2 : 0.0f;
+                    float help = (t2 * t2);
+                    if (help > 0.0f) help = (t3 * t3 - t1 * t1) / help;
+                    const float M_c2 = (help > 0.0f) ? sqrtf(help) : 1.0f;
+                    m1[e] = M_c1;
+                    m2[e] = M_c2;
+                    o1 = t1; o2 = t2; o3 = t3;
+                }
+                a.teta[cc] = o1; a.teta[C + cc] = o2; a.teta[2 * C + cc] = o3;
+            }
         }
-    }
-    else if (!DECIM_FIRST)
-    {
-        float hi[R], hq[R];
-        front_fill<T1>(W, a.hist1_i, c, act, live, b, nb, hA, xi, R);
-        front_load_row<T2>(a.hist2_i, cl, b, nb, hA);
-        fir_block<T1, R, 1>(W + b * R, as_taps(P->hilbert_i), hi);
         wave_sync();
-        front_fill<T1>(W, a.hist1_q, c, act, live, b, nb, hB, xq, R);
-        fir_block<T1, R, 1>(W + b * R, as_taps(P->hilbert_q), hq);
-        // a = I + Q (USB) or I - Q (LSB), audio_driver.c:2781-2790
-#pragma unroll
-        for (int r = 0; r < R; ++r) hi[r] = lsb ? (hi[r] - hq[r]) : (hi[r] + hq[r]);
-        wave_sync();
-        front_fill<T2>(W, a.hist2_i, c, act, live, b, nb, hA, hi, R);
-        fir_block<T2, RD, M>(W + b * R, as_taps(P->dec), o);
-    }
-    else
-    {
-        constexpr int V2 = RD % 4 == 0 ? 4 : 2;
-        float di[RD], dq[RD], hi[RD], hq[RD];
-        front_fill<T1>(W, a.hist1_i, c, act, live, b, nb, hA, xi, R);
-        front_load_row<T2>(a.hist2_i, cl, b, nb, hA);
-        fir_block<T1, RD, M>(W + b * R, as_taps(P->dec), di);
-        wave_sync();
-        front_fill<T1>(W, a.hist1_q, c, act, live, b, nb, hB, xq, R);
-        front_load_row<T2>(a.hist2_q, cl, b, nb, hB);
-        fir_block<T1, RD, M>(W + b * R, as_taps(P->dec), dq);
-        wave_sync();
-        front_fill<T2>(W, a.hist2_i, c, act, live, b, nb, hA, di, RD);
-        fir_block<T2, RD, 1, V2>(W + b * RD, as_taps(P->hilbert_i), hi);
-        wave_sync();
-        front_fill<T2>(W, a.hist2_q, c, act, live, b, nb, hB, dq, RD);
-        fir_block<T2, RD, 1, V2>(W + b * RD, as_taps(P->hilbert_q), hq);
-#pragma unroll
-        for (int r = 0; r < RD; ++r) o[r] = lsb ? (hi[r] - hq[r]) : (hi[r] + hq[r]);
-    }
-    if (live)
-    {
-        float* dst = a.adec + (size_t)c * a.ldd + b * RD;
-        if (RD % 4 == 0)
+
+        // ---- this lane's R frames, converted; the I/Q branches run as FIR pairs (fir_block2)
+        //      over the window {I[n], Q[n]} ----
+        v2f x2[R];
         {
+            float xi[R], xq[R];
+            convert_block<R>(raw, in, b * R, m1 + gs * nblk32, m2 + gs * nblk32, osc, xi, xq);
 #pragma unroll
-            for (int r = 0; r < RD; r += 4) *(float4*)(dst + r) = make_float4(o[r], o[r + 1], o[r + 2], o[r + 3]);
+            for (int j = 0; j < R; ++j) x2[j] = v2f{ xi[j], xq[j] };
+        }
+        front_fill2<T1>(W, a.hist1_i, a.hist1_q, c, act, live, b, nb, hA, hB, x2, R);
+
+        float o[RD];
+        if constexpr (T2 == 0)
+        {
+            // AM / SAM: decimate I and Q with the path's own tables (DECIMATE_RX_I / _Q,
+            // audio_filter.c:1167-1176, audio_driver.c:2742-2746), no Hilbert (:2748);
+            // FM: the Hilbert / low-pass pair at 48 ksps (:2748-2753), no decimation.
+            // The demodulator in rx_back / rx_fm takes both I and Q.
+                v2f d2[RD];
+            fir_block2<T1, RD, M>(W + 2 * b * R, tA, d2);
+#pragma unroll
+            for (int r = 0; r < RD; ++r) o[r] = d2[r].x;
+            if (live)
+            {
+                float* dst = a.adec_q + (size_t)c * a.ldd + b * RD;
+#pragma unroll
+                for (int r = 0; r < RD; ++r) dst[r] = d2[r].y;
+            }
+        }
+        else if constexpr (!DECIM_FIRST)
+        {
+            vf4 hC[HQ2];
+            front_load_row<T2>(a.hist2_i, cl, b, nb, hC);
+                v2f h2[R];
+            float hs[R];
+            fir_block2<T1, R, 1>(W + 2 * b * R, tA, h2);
+            // a = I + Q (USB) or I - Q (LSB), audio_driver.c:2781-2790
+#pragma unroll
+            for (int r = 0; r < R; ++r) hs[r] = lsb ? (h2[r].x - h2[r].y) : (h2[r].x + h2[r].y);
+            wave_sync();
+            front_fill<T2>(W, a.hist2_i, c, act, live, b, nb, hC, hs, R);
+            fir_block<T2, RD, M>(W + b * R, as_taps(P->dec), o);
         }
         else
         {
+            vf4 hC[HQ2], hD[HQ2];
+            front_load_row<T2>(a.hist2_i, cl, b, nb, hC);
+            front_load_row<T2>(a.hist2_q, cl, b, nb, hD);
+                v2f d2[RD], h2[RD];
+            fir_block2<T1, RD, M>(W + 2 * b * R, tA, d2);
+            wave_sync();
+            front_fill2<T2>(W, a.hist2_i, a.hist2_q, c, act, live, b, nb, hC, hD, d2, RD);
+            fir_block2<T2, RD, 1>(W + 2 * b * RD, as_taps2(a.taps2b), h2);
 #pragma unroll
-            for (int r = 0; r < RD; ++r) dst[r] = o[r];
+            for (int r = 0; r < RD; ++r) o[r] = lsb ? (h2[r].x - h2[r].y) : (h2[r].x + h2[r].y);
+        }
+        if (live)
+        {
+            float* dst = a.adec + (size_t)c * a.ldd + b * RD;
+            if (RD % 4 == 0)
+            {
+#pragma unroll
+                for (int r = 0; r < RD; r += 4) *(float4*)(dst + r) = make_float4(o[r], o[r + 1], o[r + 2], o[r + 3]);
+            }
+            else
+            {
+#pragma unroll
+                for (int r = 0; r < RD; ++r) dst[r] = o[r];
+            }
         }
     }
 }
@@ -1212,6 +1244,8 @@ static const BackVariant* find_back(const uhsdr_rx_plan& p)
 // ------------------------------------------------------------------------------------
 // host runtime
 
+constexpr int TAPS2_MAX = (UHSDR_MAX_FIR_TAPS + 7) & ~7;   // taps per pair table
+
 struct uhsdr_rx_s
 {
     uhsdr_rx_plan plan;
@@ -1224,6 +1258,7 @@ struct uhsdr_rx_s
     hipStream_t stream;
     // front state
     float *hist1_i, *hist1_q, *hist2_i, *hist2_q, *teta, *osc, *adec, *adec_q;
+    float* d_taps2;          // FIR pair tables: [2][2 * TAPS2_MAX] (pass 1, pass 2)
     // back state
     BackState bs;
     void* arena;
@@ -1273,24 +1308,37 @@ static void time_harvest(uhsdr_rx_s* h)
 
 // LDS window pitch per channel: room for every pass (T-1 history + new samples + tail),
 // a multiple of 4 floats, chosen among 16 candidates for the fewest ds_read bank conflicts
+// Pass 1 is always a FIR pair over an interleaved window (2 floats per sample); pass 2 is the
+// scalar audio decimator (Hilbert-first paths) or the Hilbert pair (decimate-first paths).
 static int front_window_pitch(const uhsdr_rx_s* h)
 {
     const int N = h->Nf, R = h->fv->R, M = h->plan.decimation_rate;
     const bool df = h->plan.use_decimated_iq;
     const int nb = N / R, cpw = FRONT_WAVE / nb;
     const int n2 = df ? N / M : N;
-    int need = h->T1 - 1 + N + FRONT_TAIL;
-    const int need2 = h->T2 - 1 + n2 + FRONT_TAIL;
+    int need = 2 * (h->T1 - 1 + N + FRONT_TAIL);
+    const int need2 = h->T2 ? (df ? 2 : 1) * (h->T2 - 1 + n2 + FRONT_TAIL) : 0;
     need = ((need > need2 ? need : need2) + 3) & ~3;
     const int rd = R / M;
     int best = need, best_cost = 1 << 30;
     for (int lw = need; lw < need + 64; lw += 4)
     {
-        int cost = window_conflicts(lw, nb, cpw, R, R, 4);
-        if (df) cost += window_conflicts(lw, nb, cpw, R, rd, rd % 4 == 0 ? 4 : 2);
+        int cost = window_conflicts(lw, nb, cpw, 2 * R, 2 * R, 4);
+        if (h->T2) cost += window_conflicts(lw, nb, cpw, 2 * R, df ? 2 * rd : R, 4);
         if (cost < best_cost) { best_cost = cost; best = lw; }
     }
     return best;
+}
+
+// interleaved tap pairs {c0[k], c1[k]} for fir_block2, zero-padded to a multiple of 8 taps
+static void pair_taps(float* dst, const float* c0, const float* c1, int T)
+{
+    const int n = (T + 7) & ~7;
+    for (int k = 0; k < n; ++k)
+    {
+        dst[2 * k] = k < T ? c0[k] : 0.0f;
+        dst[2 * k + 1] = k < T ? c1[k] : 0.0f;
+    }
 }
 
 // LDS of one front workgroup (one wave): must match the carve-up in rx_front
@@ -1384,7 +1432,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->arena_bytes = fl * sizeof(float);
     if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess ||
         hipMalloc((void**)&h->adec, sizeof(float) * (size_t)C * h->Nd) != hipSuccess ||
-        hipMalloc((void**)&h->d_plan, sizeof(uhsdr_rx_plan)) != hipSuccess)
+        hipMalloc((void**)&h->d_plan, sizeof(uhsdr_rx_plan)) != hipSuccess ||
+        hipMalloc((void**)&h->d_taps2, sizeof(float) * 4 * TAPS2_MAX) != hipSuccess)
     {
         uhsdr_set_error("hipMalloc failed (%zu bytes state)", h->arena_bytes);
         if (h->arena) (void)hipFree(h->arena);
@@ -1405,6 +1454,26 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         h->cw_bmax = cw ? (N / BLK + cpb - 1) / cpb : 0;
     }
     h->adec_q = am ? A + o_adq : nullptr;
+    {
+        // pass 1: the Hilbert / low-pass pair (Hilbert-first and FM), or the I and Q decimators
+        // (DECIMATE_RX_I / _Q: the same table for SSB, the path's I and Q tables for AM / SAM);
+        // pass 2 (decimate-first SSB): the Hilbert pair at the decimated rate
+        float t2[4 * TAPS2_MAX];
+        memset(t2, 0, sizeof t2);
+        if (p.use_decimated_iq)
+        {
+            const bool amq = h->bv->dm != DM_NONE;
+            pair_taps(t2, p.dec, amq ? p.dec_q : p.dec, p.dec_taps);
+            if (h->T2) pair_taps(t2 + 2 * TAPS2_MAX, p.hilbert_i, p.hilbert_q, p.hilbert_taps);
+        }
+        else
+            pair_taps(t2, p.hilbert_i, p.hilbert_q, p.hilbert_taps);
+        if (hipMemcpy(h->d_taps2, t2, sizeof t2, hipMemcpyHostToDevice) != hipSuccess)
+        {
+            uhsdr_set_error("tap upload failed");
+            return UHSDR_DEVICE_ERROR;
+        }
+    }
     if (hipMemcpy(h->d_plan, &h->plan, sizeof(uhsdr_rx_plan), hipMemcpyHostToDevice) != hipSuccess)
     {
         uhsdr_set_error("plan upload failed");
@@ -1452,6 +1521,8 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
         fa.adec_q = h->adec_q ? h->adec_q + f0 / h->plan.decimation_rate : nullptr;
         fa.C = h->C; fa.N = h->Nf; fa.ld = h->N; fa.ldd = h->Nd;
         fa.lw = h->lw;
+        fa.taps2a = h->d_taps2;
+        fa.taps2b = h->d_taps2 + 2 * TAPS2_MAX;
         hipLaunchKernelGGL(h->fv->fn, dim3((h->C + cpw - 1) / cpw), dim3(FRONT_WAVE), lds, h->stream, fa);
         HIPCHK(hipGetLastError());
         h->front_launches += 1;
@@ -1597,6 +1668,7 @@ extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
     (void)hipFree(h->arena);
     (void)hipFree(h->adec);
     (void)hipFree(h->d_plan);
+    (void)hipFree(h->d_taps2);
     free(h);
     return UHSDR_OK;
 }

@@ -27,3 +27,11 @@ def cuda():
         # -m gpu runs only on the MI355X box: a missing GPU there is a failure, not a skip
         pytest.fail("GPU test requested but torch.cuda.is_available() is False")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(params=["pipe", "fused"])
+def back(request, monkeypatch):
+    """Both back-end kernels: the wave pipeline (rx_back, small batches) and the fused
+    one-wave-per-64-channels kernel (rx_back_fused, large batches), forced per handle."""
+    monkeypatch.setenv("UHSDR_BACK_FUSED", "1" if request.param == "fused" else "0")
+    return request.param

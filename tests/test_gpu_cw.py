@@ -35,7 +35,7 @@ def run_cw(cfg, iq, frames):
 
 
 @pytest.mark.parametrize("path", cw_files(), ids=lambda p: p.split("cw_")[-1][:-4])
-def test_device_cw_matches_reference_firmware(cuda, path):
+def test_device_cw_matches_reference_firmware(cuda, back, path):
     g = load_cw(path)
     sig, en, _ = run_cw(U.config_from_ref_args(g["args"]), g["iq"], 256)
     assert_bitexact(en, g["energy"], "Goertzel energy")
@@ -52,7 +52,7 @@ def test_device_cw_call_granularity(cuda, frames):
 
 
 @pytest.mark.parametrize("mode,path,channels", [(U.DEMOD_CW, 4, 333), (U.DEMOD_CW, 12, 130), (U.DEMOD_SAM, 70, 65)])
-def test_device_cw_matches_oracle_ragged(cuda, mode, path, channels):
+def test_device_cw_matches_oracle_ragged(cuda, back, mode, path, channels):
     cfg = U.default_config(dmod_mode=mode, filter_path=path, cw_decoder_thresh=1200, cw_decoder_blocksize=72)
     n = 4096
     iq = synth.cw_iq(np.arange(channels), 3, n) if mode == U.DEMOD_CW else synth.am_iq(np.arange(channels), 3, n)

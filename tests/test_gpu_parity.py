@@ -39,7 +39,7 @@ def run_device(cfg, iq, frames_per_call, want_dst=True):
 
 
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("rx_")[-1][:-4])
-def test_device_matches_reference_firmware(cuda, path):
+def test_device_matches_reference_firmware(cuda, back, path):
     g = load(path)
     cfg = U.config_from_ref_args(g["args"])
     a1, dst = run_device(cfg, g["iq"], 256)
@@ -48,7 +48,7 @@ def test_device_matches_reference_firmware(cuda, path):
 
 
 @pytest.mark.parametrize("frames", [32, 64, 128, 1024, 2048])
-def test_device_call_granularity(cuda, frames):
+def test_device_call_granularity(cuda, back, frames):
     g = load(golden_file("p48_usb"))
     cfg = U.config_from_ref_args(g["args"])
     a1, _ = run_device(cfg, g["iq"], frames, want_dst=False)
@@ -56,7 +56,7 @@ def test_device_call_granularity(cuda, frames):
 
 
 @pytest.mark.parametrize("path,channels", [(48, 1000), (35, 333), (55, 130), (4, 65)])
-def test_device_matches_oracle_ragged_batches(cuda, path, channels):
+def test_device_matches_oracle_ragged_batches(cuda, back, path, channels):
     mode = U.DEMOD_CW if path == 4 else U.DEMOD_USB
     cfg = U.default_config(filter_path=path, dmod_mode=mode)
     iq = synth.ssb_iq(np.arange(channels), 0, 1024)
@@ -99,7 +99,7 @@ def test_device_north_star_batch_sampled_channels(cuda, path):
     assert_bitexact(got, ref, "north-star sampled")
 
 
-def test_device_reset_restarts_stream(cuda):
+def test_device_reset_restarts_stream(cuda, back):
     import torch
     g = load(golden_file("p48_usb"))
     cfg = U.config_from_ref_args(g["args"])
@@ -143,7 +143,7 @@ def test_plain_c_host_matches_reference_firmware(cuda, tmp_path):
 @pytest.mark.parametrize("path,mode,sb,channels", [(70, U.DEMOD_AM, 0, 300), (70, U.DEMOD_SAM, 0, 257),
                                                    (86, U.DEMOD_SAM, 0, 129), (75, U.DEMOD_SAM, 2, 65),
                                                    (83, U.DEMOD_AM, 0, 100)])
-def test_device_am_sam_matches_oracle(cuda, path, mode, sb, channels):
+def test_device_am_sam_matches_oracle(cuda, back, path, mode, sb, channels):
     cfg = U.default_config(filter_path=path, dmod_mode=mode, sam_sideband=sb)
     iq = synth.am_iq(np.arange(channels), 0, 1024)
     a1, dst = run_device(cfg, iq, 256)

@@ -450,56 +450,77 @@ __device__ __forceinline__ BackLds back_lds_carve(float* smem)
     return l;
 }
 
-#define BACK_PROLOGUE                                                                          \
-    const uhsdr_rx_plan* __restrict__ P = a.plan;                                              \
-    const int lane = threadIdx.x & (BACK_CH - 1);                                              \
-    const int c = blockIdx.x * BACK_CH + lane;                                                 \
-    const bool live = c < a.C;                                                                 \
-    const int cl = live ? c : a.C - 1; /* loads clamped: no exec-masked load branches */       \
-    const int C = a.C;                                                                         \
-    constexpr int NDC = BLK / L;       /* decimated samples per 32-frame call */               \
-    const int calls = a.N / BLK;                                                               \
-    (void)P; (void)live;
-
-// ---- agc role: IIR lattice pre-filter (audio_driver.c:2473-2482) + AudioAgc_RunAgcWdsp ----
-// input: adec from HBM (SSB: rx_front summed I +- Q), or the demod role's LDS output
-template <int PRE, int L, int W, int DM>
-__device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
+// Lane == channel.  c: this lane's channel; cl: clamped for loads (no exec-masked load branches).
+struct BackLane
 {
-    BACK_PROLOGUE
-    constexpr int ROLES = back_roles(DM), ST = DM ? 1 : 0;
-    static_assert(W == AGC_Q * NDC + 1, "AGC window must be AGC_Q calls + 1 sample");
-    // plan values copied to registers once (uniform -> SGPRs); reading them through P
-    // inside the loop would reload them every sample (the state stores may alias)
-    const uhsdr_agc_plan A = P->agc;
-    float pk[PRE > 0 ? PRE : 1], pv[PRE + 1];
-#pragma unroll
-    for (int i = 0; i < PRE; ++i) pk[i] = P->pre_k[i];
-#pragma unroll
-    for (int i = 0; i <= PRE; ++i) pv[i] = P->pre_v[i];
-    float pre[PRE > 0 ? PRE : 1];
-#pragma unroll
-    for (int i = 0; i < PRE; ++i) pre[i] = a.s.pre[i * C + cl];
-    const bool agc_on = A.mode != 5;
-    float volts = a.s.agc[1 * C + cl];
-    float save_volts = a.s.agc[2 * C + cl];
-    float fast_bavg = a.s.agc[3 * C + cl];
-    float hang_bavg = a.s.agc[4 * C + cl];
-    float wold = a.s.agc[5 * C + cl];
-    float cmax[AGC_Q - 1];                               // maxima of calls k-Q+1 .. k-1 (oldest first)
-#pragma unroll
-    for (int i = 0; i < AGC_Q - 1; ++i) cmax[i] = a.s.agc[(6 + i) * C + cl];
-    float leave_last = a.s.agc[(5 + AGC_Q) * C + cl];   // last sample of call k-Q-1
-    int hang_counter = a.s.agci[0 * C + cl];
-    int decay_type = a.s.agci[1 * C + cl];
-    int state = a.s.agci[2 * C + cl];
+    int lane, c, cl, C, calls;
+    bool live;
+    __device__ __forceinline__ explicit BackLane(const BackArgs& a)
+    {
+        lane = threadIdx.x & (BACK_CH - 1);
+        c = blockIdx.x * BACK_CH + lane;
+        live = c < a.C;
+        cl = live ? c : a.C - 1;
+        C = a.C;
+        calls = a.N / BLK;
+    }
+};
 
-    // the decimated input and the ring slot of call `it` are fetched one call ahead
-    float xnext[NDC], rnext[NDC];
-    auto fetch = [&](int call) {
+// The back-end stages below hold one channel's state in registers for a launch: load() reads
+// it ([field][C], lane-coalesced), the per-call / per-sample steps run the reference's
+// arithmetic, store() writes it back.  The pipelined kernel (rx_back) runs each stage in its own
+// wave; the fused kernel (rx_back_fused) runs all of them per sample in one wave.
+
+// ---- agc stage: IIR lattice pre-filter (audio_driver.c:2473-2482) + AudioAgc_RunAgcWdsp ----
+// input: adec from HBM (SSB: rx_front summed I +- Q), or the demod stage's output
+template <int PRE, int L, int W, int DM>
+struct AgcStage
+{
+    static constexpr int NDC = BLK / L;
+    static_assert(W == AGC_Q * NDC + 1, "AGC window must be AGC_Q calls + 1 sample");
+    // The AGC plan values live in the caller's local copy of P->agc, passed to step() (uniform
+    // -> SGPRs; reading them through P inside the loop would reload them every sample since the
+    // state stores may alias, and a struct member copy of it defeats SROA and lands in scratch).
+    float pk[PRE > 0 ? PRE : 1], pv[PRE + 1], pre[PRE > 0 ? PRE : 1];
+    bool agc_on;
+    float volts, save_volts, fast_bavg, hang_bavg, wold;
+    float cmax[AGC_Q - 1];                               // maxima of calls k-Q+1 .. k-1 (oldest first)
+    float leave_last;                                    // last sample of call k-Q-1
+    int hang_counter, decay_type, state;
+    float xnext[NDC], rnext[NDC];                        // input and ring slot of the next call
+    float old[NDC], sfx[NDC], wmax, pmax;                // this call's ring slot, suffix maxima
+    float* ring_out;
+
+    __device__ __forceinline__ void load(const BackArgs& a, const BackLane& l, const uhsdr_agc_plan& A)
+    {
+        const uhsdr_rx_plan* __restrict__ P = a.plan;
+        const int C = l.C, cl = l.cl;
+#pragma unroll
+        for (int i = 0; i < PRE; ++i) pk[i] = P->pre_k[i];
+#pragma unroll
+        for (int i = 0; i <= PRE; ++i) pv[i] = P->pre_v[i];
+#pragma unroll
+        for (int i = 0; i < PRE; ++i) pre[i] = a.s.pre[i * C + cl];
+        agc_on = A.mode != 5;
+        volts = a.s.agc[1 * C + cl];
+        save_volts = a.s.agc[2 * C + cl];
+        fast_bavg = a.s.agc[3 * C + cl];
+        hang_bavg = a.s.agc[4 * C + cl];
+        wold = a.s.agc[5 * C + cl];
+#pragma unroll
+        for (int i = 0; i < AGC_Q - 1; ++i) cmax[i] = a.s.agc[(6 + i) * C + cl];
+        leave_last = a.s.agc[(5 + AGC_Q) * C + cl];
+        hang_counter = a.s.agci[0 * C + cl];
+        decay_type = a.s.agci[1 * C + cl];
+        state = a.s.agci[2 * C + cl];
+    }
+
+    // the decimated input and the ring slot of a call are fetched one call ahead
+    __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
+    {
         if (!DM)
         {
-            const float* src = a.adec + (size_t)cl * a.Nd + call * NDC;
+            const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
 #pragma unroll
             for (int m = 0; m < NDC; m += 4)
             {
@@ -510,128 +531,127 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
         if (agc_on)
         {
             const int slot = (a.ring_phase + call) % AGC_Q;
-            const float* rs = a.s.ring + (size_t)slot * NDC * C + cl;
+            const float* rs = a.s.ring + (size_t)slot * NDC * l.C + l.cl;
 #pragma unroll
-            for (int m = 0; m < NDC; ++m) rnext[m] = rs[(size_t)m * C];
+            for (int m = 0; m < NDC; ++m) rnext[m] = rs[(size_t)m * l.C];
         }
-    };
-    fetch(0);
-    for (int it = 0; it < calls + ROLES - 1; ++it)
-    {
-        const int call = it - ST;
-        if (call >= 0 && call < calls)
-        {
-            float xin[NDC], old[NDC];
-#pragma unroll
-            for (int m = 0; m < NDC; ++m) { xin[m] = xnext[m]; old[m] = rnext[m]; }
-            if (DM)
-            {
-                const float* di = lds.dem + (call & 1) * NDC * BACK_CH + lane;
-#pragma unroll
-                for (int m = 0; m < NDC; ++m) xin[m] = di[m * BACK_CH];
-            }
-            if (call + 1 < calls) fetch(call + 1);
-            // suffix maxima of call k-Q; maximum of the whole calls k-Q+1 .. k-1
-            float sfx[NDC];
-            sfx[NDC - 1] = fabsf(old[NDC - 1]);
-#pragma unroll
-            for (int m = NDC - 2; m >= 0; --m) sfx[m] = fmaxf(sfx[m + 1], fabsf(old[m]));
-            float wmax = cmax[0];
-#pragma unroll
-            for (int i = 1; i < AGC_Q - 1; ++i) wmax = fmaxf(wmax, cmax[i]);
-            float pmax = 0.0f;
-            float* ring_out = a.s.ring + (size_t)((a.ring_phase + call) % AGC_Q) * NDC * C + c;
-            float* ao = lds.agc + (call & 1) * NDC * BACK_CH + lane;
-#pragma unroll
-            for (int m = 0; m < NDC; ++m)
-            {
-                float x = xin[m];
-                if (PRE > 0) x = lattice_step<PRE>(x, pre, pk, pv);
-                // ---- AudioAgc_RunAgcWdsp, audio_agc.c:349-595 ----
-                if (!agc_on)
-                {
-                    x = x * A.fixed_gain;
-                }
-                else
-                {
-                    const float out_sample = m ? old[m - 1] : leave_last;
-                    const float abs_out = fabsf(out_sample);
-                    if (live) ring_out[(size_t)m * C] = x;
-                    fast_bavg = A.fast_backmult * abs_out + A.onemfast_backmult * fast_bavg;
-                    hang_bavg = A.hang_backmult * abs_out + A.onemhang_backmult * hang_bavg;
-                    pmax = fmaxf(pmax, fabsf(x));
-                    const float ring_max = fmaxf(fmaxf(pmax, wmax), sfx[m]);
-                    if (hang_counter > 0) --hang_counter;
-                    // the 5-state attack / decay / hang machine (audio_agc.c:436-551), as
-                    // selects: mu = the multiplier the taken branch applies
-                    const float rv = ring_max - volts;
-                    const bool atk = ring_max >= volts;
-                    float mu = 0.0f;
-                    bool upd = false, save = false;
-                    int ns = state;
-                    if (state == 0)
-                    {
-                        const bool fast = volts > A.pop_ratio * fast_bavg;
-                        const bool hang = A.hang_enable && (hang_bavg > A.hang_level);
-                        ns = atk ? 0 : fast ? 1 : hang ? 2 : 3;
-                        upd = atk || fast || !hang;
-                        mu = atk ? A.attack_mult : fast ? A.fast_decay_mult : A.decay_mult;
-                        if (!atk && !fast)
-                        {
-                            hang_counter = hang ? A.hang_counter_init : hang_counter;
-                            decay_type = hang ? 1 : 0;
-                        }
-                    }
-                    else if (state == 1)
-                    {
-                        const bool fd = volts > save_volts;
-                        const bool hc = hang_counter > 0;
-                        ns = atk ? 0 : fd ? 1 : hc ? 2 : (decay_type == 0) ? 3 : 4;
-                        upd = atk || fd || !hc;
-                        mu = atk ? A.attack_mult : fd ? A.fast_decay_mult
-                                                       : (decay_type == 0) ? A.decay_mult : A.hang_decay_mult;
-                    }
-                    else if (state == 2)
-                    {
-                        const bool hz = hang_counter == 0;
-                        ns = atk ? 0 : hz ? 4 : 2;
-                        upd = atk || hz;
-                        save = atk;
-                        mu = atk ? A.attack_mult : A.hang_decay_mult;
-                    }
-                    else
-                    {
-                        ns = atk ? 0 : state;
-                        upd = true;
-                        save = atk;
-                        mu = atk ? A.attack_mult : (state == 3) ? A.decay_mult : A.hang_decay_mult;
-                    }
-                    state = ns;
-                    if (save) save_volts = volts;
-                    if (upd) volts += rv * mu;
-                    if (volts < A.min_volts) volts = A.min_volts;
-                    float vo = log10f_fast(A.inv_max_input * volts);
-                    if (vo > 0.0f) vo = 0.0f;
-                    const float mult = (A.out_target - A.slope_constant * vo) / volts;
-                    x = out_sample * mult;
-                }
-                if (agc_on && A.remove_dc)                      // mode 5 returns first (audio_agc.c:354-365)
-                {
-                    const float w = (float)((double)x + (double)wold * 0.9999);
-                    x = w - wold;
-                    wold = w;
-                }
-                ao[m * BACK_CH] = x;
-            }
-            leave_last = old[NDC - 1];
-#pragma unroll
-            for (int i = 0; i + 1 < AGC_Q - 1; ++i) cmax[i] = cmax[i + 1];
-            cmax[AGC_Q - 2] = pmax;
-        }
-        __syncthreads();
     }
-    if (live)
+
+    // start of call `call`: take the fetched data (xin: SSB input; AM/SAM get theirs from the
+    // demod stage), issue the next call's fetch, suffix maxima of call k-Q, maximum of the
+    // whole calls k-Q+1 .. k-1
+    __device__ __forceinline__ void begin(const BackArgs& a, const BackLane& l, int call, float (&xin)[NDC])
     {
+#pragma unroll
+        for (int m = 0; m < NDC; ++m) { if (!DM) xin[m] = xnext[m]; old[m] = rnext[m]; }
+        if (call + 1 < l.calls) fetch(a, l, call + 1);
+        sfx[NDC - 1] = fabsf(old[NDC - 1]);
+#pragma unroll
+        for (int m = NDC - 2; m >= 0; --m) sfx[m] = fmaxf(sfx[m + 1], fabsf(old[m]));
+        wmax = cmax[0];
+#pragma unroll
+        for (int i = 1; i < AGC_Q - 1; ++i) wmax = fmaxf(wmax, cmax[i]);
+        pmax = 0.0f;
+        ring_out = a.s.ring + (size_t)((a.ring_phase + call) % AGC_Q) * NDC * l.C + l.c;
+    }
+
+    // sample m of the call
+    __device__ __forceinline__ float step(int m, float x, const BackLane& l, const uhsdr_agc_plan& A)
+    {
+        if (PRE > 0) x = lattice_step<PRE>(x, pre, pk, pv);
+        // ---- AudioAgc_RunAgcWdsp, audio_agc.c:349-595 ----
+        if (!agc_on)
+        {
+            x = x * A.fixed_gain;
+        }
+        else
+        {
+            const float out_sample = m ? old[m - 1] : leave_last;
+            const float abs_out = fabsf(out_sample);
+            if (l.live) ring_out[(size_t)m * l.C] = x;
+            fast_bavg = A.fast_backmult * abs_out + A.onemfast_backmult * fast_bavg;
+            hang_bavg = A.hang_backmult * abs_out + A.onemhang_backmult * hang_bavg;
+            pmax = fmaxf(pmax, fabsf(x));
+            const float ring_max = fmaxf(fmaxf(pmax, wmax), sfx[m]);
+            if (hang_counter > 0) --hang_counter;
+            // the 5-state attack / decay / hang machine (audio_agc.c:436-551), as
+            // selects: mu = the multiplier the taken branch applies (selects between values,
+            // not between fields of A, which would pin A in scratch memory)
+            const float attack_mult = A.attack_mult, decay_mult = A.decay_mult;
+            const float fast_decay_mult = A.fast_decay_mult, hang_decay_mult = A.hang_decay_mult;
+            const int hang_counter_init = A.hang_counter_init;
+            const float rv = ring_max - volts;
+            const bool atk = ring_max >= volts;
+            float mu = 0.0f;
+            bool upd = false, save = false;
+            int ns = state;
+            if (state == 0)
+            {
+                const bool fast = volts > A.pop_ratio * fast_bavg;
+                const bool hang = A.hang_enable && (hang_bavg > A.hang_level);
+                ns = atk ? 0 : fast ? 1 : hang ? 2 : 3;
+                upd = atk || fast || !hang;
+                mu = atk ? attack_mult : fast ? fast_decay_mult : decay_mult;
+                if (!atk && !fast)
+                {
+                    hang_counter = hang ? hang_counter_init : hang_counter;
+                    decay_type = hang ? 1 : 0;
+                }
+            }
+            else if (state == 1)
+            {
+                const bool fd = volts > save_volts;
+                const bool hc = hang_counter > 0;
+                ns = atk ? 0 : fd ? 1 : hc ? 2 : (decay_type == 0) ? 3 : 4;
+                upd = atk || fd || !hc;
+                mu = atk ? attack_mult : fd ? fast_decay_mult
+                                               : (decay_type == 0) ? decay_mult : hang_decay_mult;
+            }
+            else if (state == 2)
+            {
+                const bool hz = hang_counter == 0;
+                ns = atk ? 0 : hz ? 4 : 2;
+                upd = atk || hz;
+                save = atk;
+                mu = atk ? attack_mult : hang_decay_mult;
+            }
+            else
+            {
+                ns = atk ? 0 : state;
+                upd = true;
+                save = atk;
+                mu = atk ? attack_mult : (state == 3) ? decay_mult : hang_decay_mult;
+            }
+            state = ns;
+            if (save) save_volts = volts;
+            if (upd) volts += rv * mu;
+            if (volts < A.min_volts) volts = A.min_volts;
+            float vo = log10f_fast(A.inv_max_input * volts);
+            if (vo > 0.0f) vo = 0.0f;
+            const float mult = (A.out_target - A.slope_constant * vo) / volts;
+            x = out_sample * mult;
+        }
+        if (agc_on && A.remove_dc)                      // mode 5 returns first (audio_agc.c:354-365)
+        {
+            const float w = (float)((double)x + (double)wold * 0.9999);
+            x = w - wold;
+            wold = w;
+        }
+        return x;
+    }
+
+    __device__ __forceinline__ void end()
+    {
+        leave_last = old[NDC - 1];
+#pragma unroll
+        for (int i = 0; i + 1 < AGC_Q - 1; ++i) cmax[i] = cmax[i + 1];
+        cmax[AGC_Q - 2] = pmax;
+    }
+
+    __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l)
+    {
+        if (!l.live) return;
+        const int C = l.C, c = l.c;
 #pragma unroll
         for (int i = 0; i < PRE; ++i) a.s.pre[i * C + c] = pre[i];
         a.s.agc[1 * C + c] = volts;
@@ -646,109 +666,115 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
         a.s.agci[1 * C + c] = decay_type;
         a.s.agci[2 * C + c] = state;
     }
-}
+};
 
-// ---- audio role: post-AGC scale (audio_driver.c:2513-2524), biquad_1 (:2527), interpolator (:2560-2577)
+// ---- audio stage: post-AGC scale (audio_driver.c:2513-2524), biquad_1 (:2527), CW decoder
+//      front end (:2550-2557), interpolator (:2560-2577) ----
 template <int L, int PH, int DM>
-__device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
+struct AudioStage
 {
-    BACK_PROLOGUE
-    constexpr int ROLES = back_roles(DM), ST = DM ? 2 : 1;
-    float b1[20], ic[L * PH];
-#pragma unroll
-    for (int i = 0; i < 20; ++i) b1[i] = P->biquad1[i];
-#pragma unroll
-    for (int i = 0; i < L * PH; ++i) ic[i] = P->interp[i];
-    const float scale = P->post_agc_scale;
+    float b1[20], ic[L * PH], scale;
     float bq1[16], ip[PH > 1 ? PH - 1 : 1];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) bq1[i] = a.s.bq1[i * C + cl];
-#pragma unroll
-    for (int i = 0; i < PH - 1; ++i) ip[i] = a.s.interp[i * C + cl];
     // CW decoder front end (CwDecode_RxProcessor + CW_Decode_exe steps 1-5, cw_decoder.c:182-316,
     // 383-397) on a_buffer[0] after biquad_1; 12 ksps paths only (L == 4)
-    const bool cw = L == 4 && P->cw_enabled;
-    float g1 = 0.0f, g2 = 0.0f, cw_old = 0.0f;
-    bool cw_state = false, cw_change = false;
-    int cw_count = a.cw_count0, cw_block = 0;
-    const int cw_bs = P->cw_blocksize;
-    if (cw)
+    bool cw;
+    float g1, g2, cw_old, cw_r;
+    bool cw_state, cw_change;
+    int cw_count, cw_block, cw_bs;
+
+    __device__ __forceinline__ void load(const BackArgs& a, const BackLane& l)
     {
-        g1 = a.s.cw[cl]; g2 = a.s.cw[C + cl]; cw_old = a.s.cw[2 * C + cl];
-        cw_state = a.s.cw[3 * C + cl] != 0.0f; cw_change = a.s.cw[4 * C + cl] != 0.0f;
-    }
-    for (int it = 0; it < calls + ROLES - 1; ++it)
-    {
-        const int call = it - ST;
-        if (call >= 0 && call < calls)
+        const uhsdr_rx_plan* __restrict__ P = a.plan;
+        const int C = l.C, cl = l.cl;
+#pragma unroll
+        for (int i = 0; i < 20; ++i) b1[i] = P->biquad1[i];
+#pragma unroll
+        for (int i = 0; i < L * PH; ++i) ic[i] = P->interp[i];
+        scale = P->post_agc_scale;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) bq1[i] = a.s.bq1[i * C + cl];
+#pragma unroll
+        for (int i = 0; i < PH - 1; ++i) ip[i] = a.s.interp[i * C + cl];
+        cw = L == 4 && P->cw_enabled;
+        g1 = 0.0f; g2 = 0.0f; cw_old = 0.0f;
+        cw_state = false; cw_change = false;
+        cw_count = a.cw_count0; cw_block = 0;
+        cw_bs = P->cw_blocksize;
+        cw_r = P->cw_r;
+        if (cw)
         {
-            const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + lane;
-            float* mo = lds.mid + (call & 1) * BLK * BACK_CH + lane;
-#pragma unroll
-            for (int m = 0; m < NDC; ++m)
-            {
-                float x = ai[m * BACK_CH];
-                x = x * scale;
-#pragma unroll
-                for (int st = 0; st < 4; ++st)
-                    x = biquad_step(x, bq1[4 * st], bq1[4 * st + 1], bq1[4 * st + 2], bq1[4 * st + 3], b1 + 5 * st);
-                if (cw)
-                {
-                    // raw_signal_buffer[sample_counter++] = x; samples past blocksize are dropped
-                    if (cw_count < cw_bs)
-                    {
-                        const float g0 = P->cw_r * g1 - g2 + x;    // AudioFilter_GoertzelInput (audio_filter.c:1290-1295)
-                        g2 = g1;
-                        g1 = g0;
-                    }
-                    ++cw_count;
-                }
-                // polyphase interpolator: output j uses phase L-1-j (arm_fir_interpolate_f32.c:482-575)
-                float win[PH];
-#pragma unroll
-                for (int t = 0; t < PH - 1; ++t) win[t] = ip[t];
-                win[PH - 1] = x;
-#pragma unroll
-                for (int i = L; i > 0; --i)
-                {
-                    float sum = 0.0f;
-#pragma unroll
-                    for (int t = 0; t < PH; ++t) sum += win[t] * ic[(i - 1) + t * L];
-                    mo[(m * L + (L - i)) * BACK_CH] = sum;
-                }
-#pragma unroll
-                for (int t = 0; t + 1 < PH; ++t) ip[t] = win[t + 1];
-            }
-            if (cw)
-            {
-                if (cw_count >= cw_bs)
-                {
-                    // AudioFilter_GoertzelEnergy (audio_filter.c:1296-1305), then the signal state:
-                    // exponential smoothing, threshold, noise cancel (cw_decoder.c:288-316)
-                    const float ga = (g1 - (g2 * P->cw_cos));
-                    const float gb = (g2 * P->cw_sin);
-                    const float e = sqrtf(ga * ga + gb * gb);
-                    g1 = 0.0f; g2 = 0.0f;
-                    const float siglevel = (float)((double)e * 0.1 + (1.0 - 0.1) * (double)cw_old);
-                    cw_old = e;
-                    const bool newstate = siglevel >= P->cw_thresh;
-                    if (P->cw_noisecancel)
-                    {
-                        if (cw_change) { cw_state = newstate; cw_change = false; }
-                        else if (newstate != cw_state) cw_change = true;
-                    }
-                    else cw_state = newstate;
-                    if (a.cw_energy && live) a.cw_energy[(size_t)c * a.cw_bmax + cw_block] = e;
-                    ++cw_block;
-                    cw_count = 0;
-                }
-                if (a.cw_signal && live) a.cw_signal[(size_t)c * calls + call] = cw_state;
-            }
+            g1 = a.s.cw[cl]; g2 = a.s.cw[C + cl]; cw_old = a.s.cw[2 * C + cl];
+            cw_state = a.s.cw[3 * C + cl] != 0.0f; cw_change = a.s.cw[4 * C + cl] != 0.0f;
         }
-        __syncthreads();
     }
-    if (live)
+
+    // one decimated sample in, L samples at 48 ksps out (out[j], j = 0..L-1)
+    __device__ __forceinline__ void step(float x, float (&out)[L])
     {
+        x = x * scale;
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+            x = biquad_step(x, bq1[4 * st], bq1[4 * st + 1], bq1[4 * st + 2], bq1[4 * st + 3], b1 + 5 * st);
+        if (cw)
+        {
+            // raw_signal_buffer[sample_counter++] = x; samples past blocksize are dropped
+            if (cw_count < cw_bs)
+            {
+                const float g0 = cw_r * g1 - g2 + x;    // AudioFilter_GoertzelInput (audio_filter.c:1290-1295)
+                g2 = g1;
+                g1 = g0;
+            }
+            ++cw_count;
+        }
+        // polyphase interpolator: output j uses phase L-1-j (arm_fir_interpolate_f32.c:482-575)
+        float win[PH];
+#pragma unroll
+        for (int t = 0; t < PH - 1; ++t) win[t] = ip[t];
+        win[PH - 1] = x;
+#pragma unroll
+        for (int i = L; i > 0; --i)
+        {
+            float sum = 0.0f;
+#pragma unroll
+            for (int t = 0; t < PH; ++t) sum += win[t] * ic[(i - 1) + t * L];
+            out[L - i] = sum;
+        }
+#pragma unroll
+        for (int t = 0; t + 1 < PH; ++t) ip[t] = win[t + 1];
+    }
+
+    // end of a call: a completed CW block (AudioFilter_GoertzelEnergy, audio_filter.c:1296-1305,
+    // then the signal state: exponential smoothing, threshold, noise cancel, cw_decoder.c:288-316)
+    __device__ __forceinline__ void end(const BackArgs& a, const BackLane& l, int call)
+    {
+        if (!cw) return;
+        const uhsdr_rx_plan* __restrict__ P = a.plan;
+        if (cw_count >= cw_bs)
+        {
+            const float ga = (g1 - (g2 * P->cw_cos));
+            const float gb = (g2 * P->cw_sin);
+            const float e = sqrtf(ga * ga + gb * gb);
+            g1 = 0.0f; g2 = 0.0f;
+            const float siglevel = (float)((double)e * 0.1 + (1.0 - 0.1) * (double)cw_old);
+            cw_old = e;
+            const bool newstate = siglevel >= P->cw_thresh;
+            if (P->cw_noisecancel)
+            {
+                if (cw_change) { cw_state = newstate; cw_change = false; }
+                else if (newstate != cw_state) cw_change = true;
+            }
+            else cw_state = newstate;
+            if (a.cw_energy && l.live) a.cw_energy[(size_t)l.c * a.cw_bmax + cw_block] = e;
+            ++cw_block;
+            cw_count = 0;
+        }
+        if (a.cw_signal && l.live) a.cw_signal[(size_t)l.c * l.calls + call] = cw_state;
+    }
+
+    __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l)
+    {
+        if (!l.live) return;
+        const int C = l.C, c = l.c;
 #pragma unroll
         for (int i = 0; i < 16; ++i) a.s.bq1[i * C + c] = bq1[i];
 #pragma unroll
@@ -759,112 +785,104 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
             a.s.cw[3 * C + c] = cw_state ? 1.0f : 0.0f; a.s.cw[4 * C + c] = cw_change ? 1.0f : 0.0f;
         }
     }
-}
+};
 
-// ---- output role: anti-alias lattice (audio_driver.c:2581-2590), biquad_2 (:2832), line-out
-//      scale (:2860), f32 audio and int32 codec frames (:2911-2923) ----
-template <int AA, int L, int DM>
-__device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
+// ---- output stage: anti-alias lattice (audio_driver.c:2581-2590), biquad_2 (:2832), line-out
+//      scale (:2860); f32 audio and int32 codec frames (:2911-2923) by the caller ----
+template <int AA>
+struct OutputStage
 {
-    BACK_PROLOGUE
-    constexpr int ROLES = back_roles(DM), ST = DM ? 3 : 2;
     float aa[AA > 0 ? AA : 1], bq2[4];
-    float ak[AA > 0 ? AA : 1], av[AA + 1], b2[5];
-#pragma unroll
-    for (int i = 0; i < AA; ++i) ak[i] = P->aa_k[i];
-#pragma unroll
-    for (int i = 0; i <= AA; ++i) av[i] = P->aa_v[i];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) b2[i] = P->biquad2[i];
-#pragma unroll
-    for (int i = 0; i < AA; ++i) aa[i] = a.s.aa[i * C + cl];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bq2[i] = a.s.bq2[i * C + cl];
-    const float lo = P->line_out_scale;
-    for (int it = 0; it < calls + ROLES - 1; ++it)
+    float ak[AA > 0 ? AA : 1], av[AA + 1], b2[5], lo;
+
+    __device__ __forceinline__ void load(const BackArgs& a, const BackLane& l)
     {
-        const int call = it - ST;
-        if (call >= 0)
-        {
-            const float* mi = lds.mid + (call & 1) * BLK * BACK_CH + lane;
-            float* ao = a.audio ? a.audio + (size_t)c * a.N + call * BLK : nullptr;
-            int2* dd = a.dst ? a.dst + (size_t)c * a.N + call * BLK : nullptr;
-#pragma unroll 2
-            for (int n0 = 0; n0 < BLK; n0 += 4)
-            {
-                float y[4];
+        const uhsdr_rx_plan* __restrict__ P = a.plan;
+        const int C = l.C, cl = l.cl;
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                {
-                    float v = mi[(n0 + j) * BACK_CH];
-                    if (AA > 0) v = lattice_step<AA>(v, aa, ak, av);
-                    v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
-                    y[j] = v * lo;
-                }
-                if (live)
-                {
-                    if (ao) *(float4*)(ao + n0) = make_float4(y[0], y[1], y[2], y[3]);
-                    if (dd)
-                    {
-                        const int d0 = to_dma(y[0]), d1 = to_dma(y[1]), d2 = to_dma(y[2]), d3 = to_dma(y[3]);
-                        *(int4*)(dd + n0) = make_int4(d0, d0, d1, d1);
-                        *(int4*)(dd + n0 + 2) = make_int4(d2, d2, d3, d3);
-                    }
-                }
-            }
-        }
-        __syncthreads();
+        for (int i = 0; i < AA; ++i) ak[i] = P->aa_k[i];
+#pragma unroll
+        for (int i = 0; i <= AA; ++i) av[i] = P->aa_v[i];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) b2[i] = P->biquad2[i];
+#pragma unroll
+        for (int i = 0; i < AA; ++i) aa[i] = a.s.aa[i * C + cl];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bq2[i] = a.s.bq2[i * C + cl];
+        lo = P->line_out_scale;
     }
-    if (live)
+
+    __device__ __forceinline__ float step(float v)
     {
+        if (AA > 0) v = lattice_step<AA>(v, aa, ak, av);
+        v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
+        return v * lo;
+    }
+
+    __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l)
+    {
+        if (!l.live) return;
 #pragma unroll
-        for (int i = 0; i < AA; ++i) a.s.aa[i * C + c] = aa[i];
+        for (int i = 0; i < AA; ++i) a.s.aa[i * l.C + l.c] = aa[i];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a.s.bq2[i * C + c] = bq2[i];
+        for (int i = 0; i < 4; ++i) a.s.bq2[i * l.C + l.c] = bq2[i];
+    }
+};
+
+// four consecutive output frames n0..n0+3 of a call: f32 audio and int32 codec frames
+__device__ __forceinline__ void back_store4(const BackArgs& a, const BackLane& l, int call, int n0, const float (&y)[4])
+{
+    if (!l.live) return;
+    if (a.audio) *(float4*)(a.audio + (size_t)l.c * a.N + call * BLK + n0) = make_float4(y[0], y[1], y[2], y[3]);
+    if (a.dst)
+    {
+        int2* dd = a.dst + (size_t)l.c * a.N + call * BLK;
+        const int d0 = to_dma(y[0]), d1 = to_dma(y[1]), d2 = to_dma(y[2]), d3 = to_dma(y[3]);
+        *(int4*)(dd + n0) = make_int4(d0, d0, d1, d1);
+        *(int4*)(dd + n0 + 2) = make_int4(d2, d2, d3, d3);
     }
 }
 
-// ---- demod role: AudioDriver_DemodSAM (audio_driver.c:1990-2166): AM envelope
+// ---- demod stage: AudioDriver_DemodSAM (audio_driver.c:1990-2166): AM envelope
 //      (:2008-2020) or the SAM PLL (:2021-2147), fade leveler (:1911-1923) ----
 template <int L, int DM>
-__device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
+struct DemodStage
 {
-    BACK_PROLOGUE
-    constexpr int ROLES = back_roles(DM);
-    const bool fade = P->fade_leveler;
-    const float mtauR = P->fade_mtauR, onem_mtauR = P->fade_onem_mtauR;
-    const float mtauI = P->fade_mtauI, onem_mtauI = P->fade_onem_mtauI;
-    const float g1 = P->sam_g1, g2 = P->sam_g2, omega_min = P->sam_omega_min, omega_max = P->sam_omega_max;
-    const bool lsb_sb = P->sam_sideband == UHSDR_SAM_SIDEBAND_LSB;
-    float phs = a.s.sam[0 * C + cl], omega2 = a.s.sam[1 * C + cl], fil_out = a.s.sam[2 * C + cl];
-    float dsI = a.s.sam[3 * C + cl], dsQ = a.s.sam[4 * C + cl];
-    float dc27 = a.s.sam[5 * C + cl], dc_insert = a.s.sam[6 * C + cl];
-    constexpr int NA = DM == DM_SAM_SB ? 24 : 1;         // allpass delay lines (sam_data.a..d)
+    static constexpr int NDC = BLK / L;
+    static constexpr int NA = DM == DM_SAM_SB ? 24 : 1;   // allpass delay lines (sam_data.a..d)
+    bool fade, lsb_sb;
+    float mtauR, onem_mtauR, mtauI, onem_mtauI;
+    float g1, g2, omega_min, omega_max;
+    float phs, omega2, fil_out, dsI, dsQ, dc27, dc_insert;
     float ap[4][NA];
-    if (DM == DM_SAM_SB)
-    {
-#pragma unroll
-        for (int f = 0; f < 4; ++f)
-#pragma unroll
-            for (int j = 0; j < NA; ++j) ap[f][j] = a.s.sam[(7 + f * 24 + j) * C + cl];
-    }
-    // demod_sam_const (audio_driver.c:1931-1953), binary32 as the firmware stores them
-    const float sc0[7] = { -0.328201924180698f, -0.744171491539427f, -0.923022915444215f, -0.978490468768238f,
-                           -0.994128272402075f, -0.998458978159551f, -0.999790306259206f };
-    const float sc1[7] = { -0.0991227952747244f, -0.565619728761389f, -0.857467122550052f, -0.959123933111275f,
-                           -0.988739372718090f, -0.996959189310611f, -0.999282492800792f };
-    const double two_pi = 2.0 * (double)3.14159265358979f;   // 2.0 * PI (CMSIS/Include/arm_math.h:334)
-
-    auto fade_leveler = [&](float audio, float corr) {
-        dc27 = mtauR * dc27 + onem_mtauR * audio;
-        dc_insert = mtauI * dc_insert + onem_mtauI * corr;
-        return audio + dc_insert - dc27;
-    };
-
     float inext[NDC], qnext[NDC];
-    auto fetch = [&](int call) {
-        const float* si = a.adec + (size_t)cl * a.Nd + call * NDC;
-        const float* sq = a.adec_q + (size_t)cl * a.Nd + call * NDC;
+    float xi[NDC], xq[NDC];
+
+    __device__ __forceinline__ void load(const BackArgs& a, const BackLane& l)
+    {
+        const uhsdr_rx_plan* __restrict__ P = a.plan;
+        const int C = l.C, cl = l.cl;
+        fade = P->fade_leveler;
+        mtauR = P->fade_mtauR; onem_mtauR = P->fade_onem_mtauR;
+        mtauI = P->fade_mtauI; onem_mtauI = P->fade_onem_mtauI;
+        g1 = P->sam_g1; g2 = P->sam_g2; omega_min = P->sam_omega_min; omega_max = P->sam_omega_max;
+        lsb_sb = P->sam_sideband == UHSDR_SAM_SIDEBAND_LSB;
+        phs = a.s.sam[0 * C + cl]; omega2 = a.s.sam[1 * C + cl]; fil_out = a.s.sam[2 * C + cl];
+        dsI = a.s.sam[3 * C + cl]; dsQ = a.s.sam[4 * C + cl];
+        dc27 = a.s.sam[5 * C + cl]; dc_insert = a.s.sam[6 * C + cl];
+        if (DM == DM_SAM_SB)
+        {
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int j = 0; j < NA; ++j) ap[f][j] = a.s.sam[(7 + f * 24 + j) * C + cl];
+        }
+    }
+
+    __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
+    {
+        const float* si = a.adec + (size_t)l.cl * a.Nd + call * NDC;
+        const float* sq = a.adec_q + (size_t)l.cl * a.Nd + call * NDC;
 #pragma unroll
         for (int m = 0; m < NDC; m += 4)
         {
@@ -873,82 +891,92 @@ __device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
             inext[m] = v.x; inext[m + 1] = v.y; inext[m + 2] = v.z; inext[m + 3] = v.w;
             qnext[m] = w.x; qnext[m + 1] = w.y; qnext[m + 2] = w.z; qnext[m + 3] = w.w;
         }
-    };
-    fetch(0);
-    for (int it = 0; it < calls + ROLES - 1; ++it)
-    {
-        if (it < calls)
-        {
-            float xi[NDC], xq[NDC];
-#pragma unroll
-            for (int m = 0; m < NDC; ++m) { xi[m] = inext[m]; xq[m] = qnext[m]; }
-            if (it + 1 < calls) fetch(it + 1);
-            float* dout = lds.dem + (it & 1) * NDC * BACK_CH + lane;
-#pragma unroll
-            for (int m = 0; m < NDC; ++m)
-            {
-                float audio;
-                if (DM == DM_AM)
-                {
-                    const float in = xi[m] * xi[m] + xq[m] * xq[m];
-                    audio = (in >= 0.0f) ? sqrtf(in) : 0.0f;      // arm_sqrt_f32, arm_math.h:5745-5771
-                    if (fade) audio = fade_leveler(audio, 0.0f);
-                }
-                else
-                {
-                    float Sin, Cos;
-                    ul_sincosf(phs, &Sin, &Cos);                   // glibc-exact (uhsdr_libm.h)
-                    const float ai = Cos * xi[m];
-                    const float bi = Sin * xi[m];
-                    const float aq = Cos * xq[m];
-                    const float bq = Sin * xq[m];
-                    const float corr0 = ai + bq, corr1 = -bi + aq;
-                    if (DM == DM_SAM_SB)
-                    {
-                        // 7-stage allpass pair per path (audio_driver.c:2059-2097)
-                        ap[0][0] = dsI; ap[1][0] = bi; ap[2][0] = dsQ; ap[3][0] = aq;
-                        dsI = ai; dsQ = bq;
-#pragma unroll
-                        for (int j = 0; j < 7; ++j)
-                        {
-                            const int k = 3 * j;
-#pragma unroll
-                            for (int f = 0; f < 4; ++f)
-                            {
-                                const float cc = (f & 1) ? sc1[j] : sc0[j];
-                                ap[f][k + 3] = cc * (ap[f][k] - ap[f][k + 5]) + ap[f][k + 2];
-                            }
-                        }
-                        const float ai_ps = ap[0][21], bi_ps = ap[1][21], bq_ps = ap[2][21], aq_ps = ap[3][21];
-#pragma unroll
-                        for (int j = NA - 1; j > 0; --j)
-#pragma unroll
-                            for (int f = 0; f < 4; ++f) ap[f][j] = ap[f][j - 1];
-                        audio = lsb_sb ? (ai_ps + bi_ps) - (aq_ps - bq_ps) : (ai_ps - bi_ps) + (aq_ps + bq_ps);
-                    }
-                    else
-                    {
-                        audio = corr0;
-                    }
-                    if (fade) audio = fade_leveler(audio, corr0);
-                    // PLL (audio_driver.c:2128-2147)
-                    const float phzerror = ul_atan2f(corr1, corr0);
-                    const float del_out = fil_out;
-                    omega2 = omega2 + g2 * phzerror;
-                    if (omega2 < omega_min) omega2 = omega_min;
-                    else if (omega2 > omega_max) omega2 = omega_max;
-                    fil_out = g1 * phzerror + omega2;
-                    phs = phs + del_out;
-                    while ((double)phs >= two_pi) phs = (float)((double)phs - two_pi);
-                    while ((double)phs < 0.0) phs = (float)((double)phs + two_pi);
-                }
-                dout[m * BACK_CH] = audio;
-            }
-        }
-        __syncthreads();
     }
-    if (live)
+
+    __device__ __forceinline__ void begin(const BackArgs& a, const BackLane& l, int call)
     {
+#pragma unroll
+        for (int m = 0; m < NDC; ++m) { xi[m] = inext[m]; xq[m] = qnext[m]; }
+        if (call + 1 < l.calls) fetch(a, l, call + 1);
+    }
+
+    __device__ __forceinline__ float fade_leveler(float audio, float corr)
+    {
+        dc27 = mtauR * dc27 + onem_mtauR * audio;
+        dc_insert = mtauI * dc_insert + onem_mtauI * corr;
+        return audio + dc_insert - dc27;
+    }
+
+    __device__ __forceinline__ float step(int m)
+    {
+        // demod_sam_const (audio_driver.c:1931-1953), binary32 as the firmware stores them
+        const float sc0[7] = { -0.328201924180698f, -0.744171491539427f, -0.923022915444215f, -0.978490468768238f,
+                               -0.994128272402075f, -0.998458978159551f, -0.999790306259206f };
+        const float sc1[7] = { -0.0991227952747244f, -0.565619728761389f, -0.857467122550052f, -0.959123933111275f,
+                               -0.988739372718090f, -0.996959189310611f, -0.999282492800792f };
+        const double two_pi = 2.0 * (double)3.14159265358979f;   // 2.0 * PI (CMSIS/Include/arm_math.h:334)
+        float audio;
+        if (DM == DM_AM)
+        {
+            const float in = xi[m] * xi[m] + xq[m] * xq[m];
+            audio = (in >= 0.0f) ? sqrtf(in) : 0.0f;      // arm_sqrt_f32, arm_math.h:5745-5771
+            if (fade) audio = fade_leveler(audio, 0.0f);
+        }
+        else
+        {
+            float Sin, Cos;
+            ul_sincosf(phs, &Sin, &Cos);                   // glibc-exact (uhsdr_libm.h)
+            const float ai = Cos * xi[m];
+            const float bi = Sin * xi[m];
+            const float aq = Cos * xq[m];
+            const float bq = Sin * xq[m];
+            const float corr0 = ai + bq, corr1 = -bi + aq;
+            if (DM == DM_SAM_SB)
+            {
+                // 7-stage allpass pair per path (audio_driver.c:2059-2097)
+                ap[0][0] = dsI; ap[1][0] = bi; ap[2][0] = dsQ; ap[3][0] = aq;
+                dsI = ai; dsQ = bq;
+#pragma unroll
+                for (int j = 0; j < 7; ++j)
+                {
+                    const int k = 3 * j;
+#pragma unroll
+                    for (int f = 0; f < 4; ++f)
+                    {
+                        const float cc = (f & 1) ? sc1[j] : sc0[j];
+                        ap[f][k + 3] = cc * (ap[f][k] - ap[f][k + 5]) + ap[f][k + 2];
+                    }
+                }
+                const float ai_ps = ap[0][21], bi_ps = ap[1][21], bq_ps = ap[2][21], aq_ps = ap[3][21];
+#pragma unroll
+                for (int j = NA - 1; j > 0; --j)
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) ap[f][j] = ap[f][j - 1];
+                audio = lsb_sb ? (ai_ps + bi_ps) - (aq_ps - bq_ps) : (ai_ps - bi_ps) + (aq_ps + bq_ps);
+            }
+            else
+            {
+                audio = corr0;
+            }
+            if (fade) audio = fade_leveler(audio, corr0);
+            // PLL (audio_driver.c:2128-2147)
+            const float phzerror = ul_atan2f(corr1, corr0);
+            const float del_out = fil_out;
+            omega2 = omega2 + g2 * phzerror;
+            if (omega2 < omega_min) omega2 = omega_min;
+            else if (omega2 > omega_max) omega2 = omega_max;
+            fil_out = g1 * phzerror + omega2;
+            phs = phs + del_out;
+            while ((double)phs >= two_pi) phs = (float)((double)phs - two_pi);
+            while ((double)phs < 0.0) phs = (float)((double)phs + two_pi);
+        }
+        return audio;
+    }
+
+    __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l)
+    {
+        if (!l.live) return;
+        const int C = l.C, c = l.c;
         a.s.sam[0 * C + c] = phs; a.s.sam[1 * C + c] = omega2; a.s.sam[2 * C + c] = fil_out;
         a.s.sam[3 * C + c] = dsI; a.s.sam[4 * C + c] = dsQ;
         a.s.sam[5 * C + c] = dc27; a.s.sam[6 * C + c] = dc_insert;
@@ -960,6 +988,119 @@ __device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
                 for (int j = 0; j < NA; ++j) a.s.sam[(7 + f * 24 + j) * C + c] = ap[f][j];
         }
     }
+};
+
+// ---- pipelined roles (rx_back): stage s of the wave pipeline works on call it - s in
+//      iteration it; hand-offs through double-buffered LDS, one barrier per iteration ----
+template <int PRE, int L, int W, int DM>
+__device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
+{
+    const BackLane l(a);
+    constexpr int NDC = BLK / L, ROLES = back_roles(DM), ST = DM ? 1 : 0;
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    const uhsdr_agc_plan A = P->agc;
+    AgcStage<PRE, L, W, DM> s;
+    s.load(a, l, A);
+    s.fetch(a, l, 0);
+    for (int it = 0; it < l.calls + ROLES - 1; ++it)
+    {
+        const int call = it - ST;
+        if (call >= 0 && call < l.calls)
+        {
+            float xin[NDC];
+            if (DM)
+            {
+                const float* di = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
+#pragma unroll
+                for (int m = 0; m < NDC; ++m) xin[m] = di[m * BACK_CH];
+            }
+            s.begin(a, l, call, xin);
+            float* ao = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) ao[m * BACK_CH] = s.step(m, xin[m], l, A);
+            s.end();
+        }
+        __syncthreads();
+    }
+    s.store(a, l);
+}
+
+template <int L, int PH, int DM>
+__device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
+{
+    const BackLane l(a);
+    constexpr int NDC = BLK / L, ROLES = back_roles(DM), ST = DM ? 2 : 1;
+    AudioStage<L, PH, DM> s;
+    s.load(a, l);
+    for (int it = 0; it < l.calls + ROLES - 1; ++it)
+    {
+        const int call = it - ST;
+        if (call >= 0 && call < l.calls)
+        {
+            const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
+            float* mo = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m)
+            {
+                float u[L];
+                s.step(ai[m * BACK_CH], u);
+#pragma unroll
+                for (int j = 0; j < L; ++j) mo[(m * L + j) * BACK_CH] = u[j];
+            }
+            s.end(a, l, call);
+        }
+        __syncthreads();
+    }
+    s.store(a, l);
+}
+
+template <int AA, int L, int DM>
+__device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
+{
+    const BackLane l(a);
+    constexpr int ROLES = back_roles(DM), ST = DM ? 3 : 2;
+    OutputStage<AA> s;
+    s.load(a, l);
+    for (int it = 0; it < l.calls + ROLES - 1; ++it)
+    {
+        const int call = it - ST;
+        if (call >= 0)
+        {
+            const float* mi = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
+#pragma unroll 2
+            for (int n0 = 0; n0 < BLK; n0 += 4)
+            {
+                float y[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = s.step(mi[(n0 + j) * BACK_CH]);
+                back_store4(a, l, call, n0, y);
+            }
+        }
+        __syncthreads();
+    }
+    s.store(a, l);
+}
+
+template <int L, int DM>
+__device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
+{
+    const BackLane l(a);
+    constexpr int NDC = BLK / L, ROLES = back_roles(DM);
+    DemodStage<L, DM> s;
+    s.load(a, l);
+    s.fetch(a, l, 0);
+    for (int it = 0; it < l.calls + ROLES - 1; ++it)
+    {
+        if (it < l.calls)
+        {
+            s.begin(a, l, it);
+            float* dout = lds.dem + (it & 1) * NDC * BACK_CH + l.lane;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) dout[m * BACK_CH] = s.step(m);
+        }
+        __syncthreads();
+    }
+    s.store(a, l);
 }
 
 // PRE / AA lattice stages, L interpolation factor, PH polyphase length, W AGC window,
@@ -979,6 +1120,64 @@ __global__ void __launch_bounds__(4 * BACK_CH) rx_back(BackArgs a)
         rx_back_audio<L, PH, DM>(a, lds);
     else
         rx_back_output<AA, L, DM>(a, lds);
+}
+
+// Fused back end for large batches: one wave per 64 channels runs every stage per sample with
+// all state in registers -- no LDS, no barriers, no pipeline fill / drain.  With enough
+// channels to keep every SIMD busy this beats the wave pipeline, whose only purpose is to
+// shorten the per-call critical path when channels are few.
+template <int PRE, int AA, int L, int PH, int W, int DM>
+__global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
+{
+    const BackLane l(a);
+    constexpr int NDC = BLK / L;
+    static_assert(L == 2 || L == 4, "4 output frames per 1 or 2 decimated samples");
+    DemodStage<L, DM> dm;
+    AgcStage<PRE, L, W, DM> ag;
+    AudioStage<L, PH, DM> au;
+    OutputStage<AA> ou;
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    const uhsdr_agc_plan A = P->agc;
+    if (DM) { dm.load(a, l); dm.fetch(a, l, 0); }
+    ag.load(a, l, A);
+    ag.fetch(a, l, 0);
+    au.load(a, l);
+    ou.load(a, l);
+    for (int call = 0; call < l.calls; ++call)
+    {
+        float xin[NDC];
+        if (DM)
+        {
+            dm.begin(a, l, call);
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) xin[m] = dm.step(m);
+        }
+        ag.begin(a, l, call, xin);
+        // the call's 32 output frames are stored in one burst at its end: interleaved with the
+        // chain's arithmetic, the partial-line stores of 64 rows get evicted from L2 before
+        // their lines fill, doubling the HBM write bytes
+        float y[BLK];
+#pragma unroll
+        for (int m = 0; m < NDC; ++m)
+        {
+            float u[L];
+            au.step(ag.step(m, xin[m], l, A), u);
+#pragma unroll
+            for (int j = 0; j < L; ++j) y[m * L + j] = ou.step(u[j]);
+        }
+#pragma unroll
+        for (int n0 = 0; n0 < BLK; n0 += 4)
+        {
+            const float y4[4] = { y[n0], y[n0 + 1], y[n0 + 2], y[n0 + 3] };
+            back_store4(a, l, call, n0, y4);
+        }
+        ag.end();
+        au.end(a, l, call);
+    }
+    if (DM) dm.store(a, l);
+    ag.store(a, l);
+    au.store(a, l);
+    ou.store(a, l);
 }
 
 
@@ -1163,7 +1362,7 @@ typedef void (*front_fn)(FrontArgs);
 typedef void (*back_fn)(BackArgs);
 
 struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; };
-struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; };
+struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; };
 
 // R = FIR outputs per lane: 16 for large batches (more MACs per window load), 8 for small
 // batches (twice the waves in flight)
@@ -1182,7 +1381,7 @@ static const FrontVariant kFront[] = {
     { 89, 0, 1, 0, rx_front<89, 0, 1, false, 8>, 8 },
 };
 
-#define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm> }
+#define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm> }
 static const BackVariant kBack[] = {
     // SSB / CW / DIGI
     BACK_V(10, 6, 4, 1, 49, DM_NONE), BACK_V(10, 0, 4, 4, 49, DM_NONE), BACK_V(0, 0, 2, 8, 97, DM_NONE),
@@ -1197,7 +1396,7 @@ static const BackVariant kBack[] = {
     BACK_V(8, 0, 2, 8, 97, DM_SAM_SB), BACK_V(8, 6, 2, 2, 97, DM_SAM_SB),
 };
 // FM: its own kernel (squelch lattice stages)
-static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6> };
+static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6>, nullptr };
 #undef BACK_V
 
 static int plan_dm(const uhsdr_rx_plan& p)
@@ -1245,6 +1444,7 @@ static const BackVariant* find_back(const uhsdr_rx_plan& p)
 // host runtime
 
 constexpr int TAPS2_MAX = (UHSDR_MAX_FIR_TAPS + 7) & ~7;   // taps per pair table
+constexpr int BACK_FUSED_MIN_CHANNELS = 262144;
 
 struct uhsdr_rx_s
 {
@@ -1254,6 +1454,7 @@ struct uhsdr_rx_s
     const BackVariant* bv;
     int C, N, Nd, Nf;        // Nf: frames per front launch (N split into N / Nf launches)
     int lw;                  // front LDS window pitch (floats)
+    int back_fused;          // rx_back_fused (large batches) instead of the wave pipeline
     int T1, T2;
     hipStream_t stream;
     // front state
@@ -1415,6 +1616,13 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     if (N % h->Nf) { free(h); uhsdr_set_error("frames_per_call %d not a multiple of %d", N, h->Nf); return UHSDR_LENGTH_ERROR; }
     if (front_lds(h) > 64 * 1024) { free(h); uhsdr_set_error("frames_per_call too long for LDS"); return UHSDR_LENGTH_ERROR; }
     const int W = h->bv->w;
+    {
+        // Back end: the wave pipeline shortens the per-call critical path, which is what bounds
+        // small batches; from BACK_FUSED_MIN_CHANNELS on (>= 4 waves per SIMD of 64 channels)
+        // the fused kernel wins.  UHSDR_BACK_FUSED=0/1 forces either (tests, benchmarking).
+        const char* env = getenv("UHSDR_BACK_FUSED");
+        h->back_fused = h->bv->fused && (env ? atoi(env) != 0 : C >= BACK_FUSED_MIN_CHANNELS);
+    }
 
     size_t fl = 0;
     auto take = [&](size_t n) { size_t o = fl; fl += (n + 63) & ~(size_t)63; return o; };
@@ -1554,7 +1762,11 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
         h->cw_blocks_last = blocks;
     }
     time_mark(h, 1, 0);
-    hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH), back_lds(h), h->stream, ba);
+    if (h->back_fused)
+        hipLaunchKernelGGL(h->bv->fused, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, h->stream, ba);
+    else
+        hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH),
+                           back_lds(h), h->stream, ba);
     HIPCHK(hipGetLastError());
     time_mark(h, 1, 1);
     if (h->timing) h->nev++;

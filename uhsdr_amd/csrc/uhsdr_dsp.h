@@ -223,8 +223,9 @@ __device__ __forceinline__ void front_fill(float* W, float* row, int c, bool act
 
 // front_fill for a FIR pair: the window holds interleaved pairs {x0[n], x1[n]} (8 bytes per
 // sample) built from the two history rows (row0 / row1, prefetched as buf0 / buf1) and NV new
-// pairs per lane; the next call's history rows are de-interleaved back to HBM.
-template <int T, int HQM>
+// pairs per lane; the next call's history rows are de-interleaved back to HBM.  DUP: both
+// filters of the pair run on the same signal (the TX Hilbert pair): one row, written once.
+template <int T, int HQM, bool DUP = false>
 __device__ __forceinline__ void front_fill2(float* W, float* row0, float* row1, int c, bool act, bool live, int b,
                                             int nb, const vf4 (&buf0)[HQM], const vf4 (&buf1)[HQM],
                                             const v2f* vals, int NV)
@@ -273,7 +274,7 @@ __device__ __forceinline__ void front_fill2(float* W, float* row0, float* row1, 
         if (live)
         {
             *(vf4*)(row0 + ro + 4 * q) = vf4{ p0.x, p0.z, p1.x, p1.z };
-            *(vf4*)(row1 + ro + 4 * q) = vf4{ p0.y, p0.w, p1.y, p1.w };
+            if (!DUP) *(vf4*)(row1 + ro + 4 * q) = vf4{ p0.y, p0.w, p1.y, p1.w };
         }
     }
 }

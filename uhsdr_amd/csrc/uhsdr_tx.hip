@@ -221,6 +221,7 @@ struct TxIqArgs
     const float* osc_in;     // [2] oscillator {I, Q} at launch start
     float* osc_out;          // [2]
     int2* iq;                // [C][ld] DAC frames, frame 0 of this launch
+    const float* taps2;      // Hilbert pair {hilbert_i[k], hilbert_q[k]} interleaved (fir_block2)
     int C, N, ld, lw;
 };
 
@@ -234,7 +235,7 @@ __global__ void __launch_bounds__(64) tx_iq(TxIqArgs a)
     const int nb = N / R;
     const int CPW = 64 / nb;
     int g, b;
-    front_lane(lane, nb, R, g, b);
+    front_lane(lane, nb, 2 * R, g, b);               // lane map for the pair window (2R floats per lane)
     const int c = blockIdx.x * CPW + g;
     const bool act = g < CPW;
     const bool live = act && c < C;
@@ -276,10 +277,16 @@ __global__ void __launch_bounds__(64) tx_iq(TxIqArgs a)
         }
         if (blockIdx.x == 0) { a.osc_out[0] = vi; a.osc_out[1] = vq; }
     }
-    front_fill<TX_T>(W, a.hist, c, act, live, b, nb, hA, xv, R);
+    // the Hilbert pair as one packed FIR pair over the window {x[n], x[n]} (fir_block2)
+    v2f x2[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) x2[j] = v2f{ xv[j], xv[j] };
+    front_fill2<TX_T, HQ, true>(W, a.hist, a.hist, c, act, live, b, nb, hA, hA, x2, R);
+    v2f h2[R];
+    fir_block2<TX_T, R, 1>(W + 2 * b * R, as_taps2(a.taps2), h2);
     float hi[R], hq[R];
-    fir_block<TX_T, R, 1>(W + b * R, as_taps(P->hilbert_i), hi);
-    fir_block<TX_T, R, 1>(W + b * R, as_taps(P->hilbert_q), hq);
+#pragma unroll
+    for (int r = 0; r < R; ++r) { hi[r] = h2[r].x; hq[r] = h2[r].y; }
     const bool up = P->shift_up;
     const float gi = P->final_i_gain, gq = P->final_q_gain, ph = P->phase_balance;
     int out[2 * R];
@@ -334,6 +341,7 @@ struct uhsdr_tx_s
 {
     uhsdr_tx_plan plan;
     uhsdr_tx_plan* d_plan;
+    float* d_taps2;          // Hilbert pair, interleaved for fir_block2
     int C, N, Nf, R, lw;
     hipStream_t stream;
     float *lat, *bq, *alc, *delay, *hist, *osc, *txa;
@@ -348,11 +356,11 @@ struct uhsdr_tx_s
 static int tx_pitch(int Nf, int R)
 {
     const int nb = Nf / R, cpw = 64 / nb;
-    const int need = (TX_T - 1 + Nf + FRONT_TAIL + 3) & ~3;
+    const int need = (2 * (TX_T - 1 + Nf + FRONT_TAIL) + 3) & ~3;   // pair window {x, x}
     int best = need, best_cost = 1 << 30;
     for (int lw = need; lw < need + 64; lw += 4)
     {
-        const int cost = window_conflicts(lw, nb, cpw, R, R, 4);
+        const int cost = window_conflicts(lw, nb, cpw, 2 * R, 2 * R, 4);
         if (cost < best_cost) { best_cost = cost; best = lw; }
     }
     return best;
@@ -400,7 +408,9 @@ extern "C" uhsdr_status uhsdr_tx_create(const uhsdr_tx_config* cfg, int32_t C, i
     const size_t o_osc = take(4), o_txa = take(h->plan.fm ? 0 : (size_t)C * N);
     const size_t o_fm = take(h->plan.fm ? (size_t)4 * C : 0);
     h->arena_bytes = fl * sizeof(float);
-    if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess || hipMalloc((void**)&h->d_plan, sizeof(uhsdr_tx_plan)) != hipSuccess)
+    constexpr int T2N = (TX_T + 7) & ~7;
+    if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess || hipMalloc((void**)&h->d_plan, sizeof(uhsdr_tx_plan)) != hipSuccess ||
+        hipMalloc((void**)&h->d_taps2, sizeof(float) * 2 * T2N) != hipSuccess)
     {
         uhsdr_set_error("hipMalloc failed (%zu bytes state)", h->arena_bytes);
         if (h->arena) (void)hipFree(h->arena);
@@ -411,6 +421,19 @@ extern "C" uhsdr_status uhsdr_tx_create(const uhsdr_tx_config* cfg, int32_t C, i
     h->lat = A + o_lat; h->bq = A + o_bq; h->alc = A + o_alc; h->delay = A + o_dly;
     h->hist = A + o_hist; h->osc = A + o_osc; h->txa = A + o_txa;
     h->fm = h->plan.fm ? (uint32_t*)(A + o_fm) : nullptr;
+    {
+        float t2[2 * T2N];
+        for (int k = 0; k < T2N; ++k)
+        {
+            t2[2 * k] = k < TX_T ? h->plan.hilbert_i[k] : 0.0f;
+            t2[2 * k + 1] = k < TX_T ? h->plan.hilbert_q[k] : 0.0f;
+        }
+        if (hipMemcpy(h->d_taps2, t2, sizeof t2, hipMemcpyHostToDevice) != hipSuccess)
+        {
+            uhsdr_set_error("tap upload failed");
+            return UHSDR_DEVICE_ERROR;
+        }
+    }
     if (hipMemcpy(h->d_plan, &h->plan, sizeof(uhsdr_tx_plan), hipMemcpyHostToDevice) != hipSuccess)
     {
         uhsdr_set_error("plan upload failed");
@@ -449,6 +472,7 @@ extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio
         ia.osc_out = h->osc + 2 * ((h->iq_launches + 1) & 1);
         ia.iq = (int2*)iq + f0;
         ia.C = h->C; ia.N = h->Nf; ia.ld = h->N; ia.lw = h->lw;
+        ia.taps2 = h->d_taps2;
         hipLaunchKernelGGL(tx_iq<8>, dim3((h->C + cpw - 1) / cpw), dim3(64), lds, h->stream, ia);
         HIPCHK(hipGetLastError());
         h->iq_launches += 1;
@@ -470,6 +494,7 @@ extern "C" uhsdr_status uhsdr_tx_destroy(uhsdr_tx_handle h)
     (void)hipStreamSynchronize(h->stream);
     (void)hipFree(h->arena);
     (void)hipFree(h->d_plan);
+    (void)hipFree(h->d_taps2);
     free(h);
     return UHSDR_OK;
 }

@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Per-GPU throughput of the BASELINE.json configs other than the headline C2 (which bench.py
+measures): C3 (SAM P70 + 1024-point spectrum), C4's per-GPU share (FM-RX P1 and SSB-TX),
+C5's per-GPU share (CW P4 with the CW decoder front end).
+
+    python tools/bench_configs.py [--steps K] [--only c3,c4fm,c4tx,c5] > profiles/rNN_configs.jsonl
+
+One JSON line per workload: Msamples/s of 48 kHz frames, ms per call, per-kernel device ms
+(RX: HIP events on the library stream), algorithmic HBM bytes per frame and the fraction of
+the 8 TB/s roofline they imply.  Inputs: 4096 distinct synthetic channels (uhsdr_amd.synth)
+tiled over the batch, resident in HBM before timing.  C4 / C5 are 8-GPU configs; a GPU's
+share is 1/8 of the channels (weak scaling: no data-path collective, bench.py --gpus N).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0
+
+
+def tiled(fn, C, N, distinct=4096):
+    import numpy as np
+    import torch
+    d = min(C, distinct)
+    base = fn(np.arange(d), 0, N)
+    reps = (C + d - 1) // d
+    t = torch.from_numpy(np.ascontiguousarray(base)).cuda()
+    return t.repeat((reps,) + (1,) * (t.dim() - 1))[:C].contiguous()
+
+
+def time_calls(fn, steps, warmup):
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(steps):
+        fn()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+def rx_line(name, cfg, C, N, iq, steps, warmup, cw=False):
+    import torch
+    import bench
+    import uhsdr_amd as U
+    s = torch.cuda.current_stream()
+    chain = U.RxChain(cfg, channels=C, frames=N, stream=s.cuda_stream)
+    audio = torch.empty((C, N), dtype=torch.float32, device="cuda")
+    if cw:
+        sig = torch.empty((C, N // 32), dtype=torch.uint8, device="cuda")
+        en = torch.empty((C, max(1, chain.cw_blocks_max)), dtype=torch.float32, device="cuda")
+        chain.set_cw_outputs(sig, en)
+    ms = time_calls(lambda: chain.process(iq, audio, None), steps, warmup)
+    chain.enable_timing(True)
+    time_calls(lambda: chain.process(iq, audio, None), steps, 0)
+    kt = chain.kernel_times()
+    chain.enable_timing(False)
+    ab = bench.algorithmic_bytes(chain.plan, C, N, False)
+    per = ab["chain"] / (C * N)
+    out = {"workload": name, "channels": C, "frames_per_call": N, "ms_per_call": round(ms, 4),
+           "msamples_per_s": round(C * N / ms / 1e3, 1),
+           "kernel_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kt.items()},
+           "alg_bytes_per_frame": round(per, 2), "hbm_frac": round(C * N * per / ms / 1e6 / HBM_PEAK_GBS, 4),
+           "finite": bool(torch.isfinite(audio).all().item())}
+    chain.close()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--only", default="c3,c3spec,c4fm,c4tx,c5")
+    a = ap.parse_args()
+    import torch
+    import uhsdr_amd as U
+    from uhsdr_amd import synth
+    want = set(a.only.split(","))
+    lines = []
+    if "c3" in want:
+        C, N = 32768, 1024
+        cfg = U.default_config(filter_path=70, dmod_mode=U.DEMOD_SAM)
+        lines.append(rx_line("C3 SAM P70 RX (PLL 2500/0.65/250, fade on)", cfg, C, N,
+                             tiled(synth.am_iq, C, N), a.steps, a.warmup))
+    if "c3spec" in want:
+        C, N, L = 32768, 1024, 1024
+        s = torch.cuda.current_stream()
+        spec = U.Spectrum(U.default_spectrum_config(fft_len=L), channels=C, frames=N, stream=s.cuda_stream)
+        iq = tiled(synth.am_iq, C, N)
+        avg = torch.empty(spec.out_shape, dtype=torch.float32, device="cuda")
+        ms = time_calls(lambda: spec.process(iq, None, avg), a.steps, a.warmup)
+        byts = C * N * (8 + 4) + C * L * 8
+        lines.append({"workload": "C3 spectrum 1024-point (Hann, CFFT, magnitude, IIR average)", "channels": C,
+                      "frames_per_call": N, "ms_per_call": round(ms, 4), "msamples_per_s": round(C * N / ms / 1e3, 1),
+                      "alg_bytes_per_frame": round(byts / (C * N), 2),
+                      "hbm_frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4)})
+        spec.close()
+    if "c4fm" in want:
+        C, N = 262144 // 8, 256
+        cfg = U.default_config(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=12)
+        lines.append(rx_line("C4 per-GPU share: FM-RX P1 (squelch 12)", cfg, C, N,
+                             tiled(synth.fm_iq, C, N), a.steps, a.warmup))
+    if "c4tx" in want:
+        C, N = 262144 // 8, 256
+        s = torch.cuda.current_stream()
+        tx = U.TxChain(channels=C, frames=N, stream=s.cuda_stream)
+        audio = tiled(synth.tx_audio, C, N)
+        iq = torch.empty((C, N, 2), dtype=torch.int32, device="cuda")
+        ms = time_calls(lambda: tx.process(audio, iq), a.steps, a.warmup)
+        # 8 B audio frame in, 8 B I/Q frame out, state (Hilbert 200, lattice 10, biquads 12, ALC,
+        # 320-sample delay line) read + written once per call, the f32 hand-off between kernels
+        state = 4 * (200 + 10 + 12 + 1 + 320)
+        per = 16 + 2 * state / N
+        lines.append({"workload": "C4 per-GPU share: SSB-TX (IIR_TX_SOPRANO + biquads + ALC + 201-tap Hilbert + Fs/4)",
+                      "channels": C, "frames_per_call": N, "ms_per_call": round(ms, 4),
+                      "msamples_per_s": round(C * N / ms / 1e3, 1), "alg_bytes_per_frame": round(per, 2),
+                      "hbm_frac": round(C * N * per / ms / 1e6 / HBM_PEAK_GBS, 4)})
+        tx.close()
+    if "c5" in want:
+        C, N = 1048576 // 8, 256
+        cfg = U.default_config(filter_path=4, dmod_mode=U.DEMOD_CW)
+        lines.append(rx_line("C5 per-GPU share: CW P4 (199-tap Hilbert @12k, 300 Hz lattice) + CW decoder Goertzel",
+                             cfg, C, N, tiled(synth.cw_iq, C, N), a.steps, a.warmup, cw=True))
+    for ln in lines:
+        ln["data"] = "synthetic: 4096 distinct channels tiled"
+        print(json.dumps(ln), flush=True)
+
+
+if __name__ == "__main__":
+    main()

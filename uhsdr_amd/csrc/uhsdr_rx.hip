@@ -1444,7 +1444,7 @@ static const BackVariant* find_back(const uhsdr_rx_plan& p)
 // host runtime
 
 constexpr int TAPS2_MAX = (UHSDR_MAX_FIR_TAPS + 7) & ~7;   // taps per pair table
-constexpr int BACK_FUSED_MIN_CHANNELS = 262144;
+constexpr int BACK_FUSED_MIN_CHANNELS = 131072;   // measured crossover (64-frame calls)
 
 struct uhsdr_rx_s
 {

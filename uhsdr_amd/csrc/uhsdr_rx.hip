@@ -422,31 +422,40 @@ __device__ __forceinline__ int to_dma(float f)
 // demodulator kinds of rx_back (DM): the SSB/CW/DIGI sum I +- Q happens in rx_front
 enum { DM_NONE = 0, DM_AM = 1, DM_SAM = 2, DM_SAM_SB = 3 /* SAM with the allpass sideband selector */,
        DM_FM = 4 /* separate kernel, rx_fm */ };
-__host__ __device__ constexpr int back_roles(int dm) { return dm == DM_FM ? 2 : dm ? 4 : 3; }
+__host__ __device__ constexpr int back_roles(int dm) { return dm == DM_FM ? 2 : dm ? 6 : 5; }
 
 // The back end of one channel group runs as a pipeline over 32-frame calls, one wave per
 // stage (lane == channel); stage s works on call it - s in iteration it and hands its results
 // to stage s+1 through double-buffered LDS, one workgroup barrier per iteration:
 //   [demod]  AM envelope / SAM PLL (AM, SAM only)              (decimated rate)
-//   agc      lattice pre-filter -> WDSP AGC                    (decimated rate)
+//   pre      IIR lattice pre-filter                            (decimated rate)
+//   agc      WDSP AGC                                          (decimated rate)
 //   audio    post-AGC scale -> biquad_1 -> polyphase interp    (decimated rate -> 48 ksps)
-//   output   anti-alias lattice -> biquad_2 -> line-out scale -> f32 / int32 stores (48 ksps)
-// Splitting the serial chain shortens the critical path per call (small batches) and keeps
-// each wave's coefficients + state small enough for 3-4 waves per SIMD (large ones).
+//   aa       anti-alias lattice                                (48 ksps)
+//   output   biquad_2 -> line-out scale -> f32 / int32 stores  (48 ksps)
+// Splitting the serial chain shortens the critical path per call, which is what bounds small
+// batches (one wave per SIMD).  Large batches use rx_back_fused (all stages in one wave).
 struct BackLds
 {
-    float* dem;   // [2][NDC][64]  demod -> agc
+    float* dem;   // [2][NDC][64]  demod -> pre
+    float* pre;   // [2][NDC][64]  pre -> agc
     float* agc;   // [2][NDC][64]  agc -> audio
-    float* mid;   // [2][BLK][64]  audio -> output
+    float* mid;   // [2][BLK][64]  audio -> aa
+    float* aa;    // [2][BLK][64]  aa -> output
 };
+
+// floats of the hand-off buffers (host: back_lds)
+__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (3 * ndc + 2 * BLK); }
 
 template <int NDC>
 __device__ __forceinline__ BackLds back_lds_carve(float* smem)
 {
     BackLds l;
     l.mid = smem;
-    l.agc = smem + 2 * BLK * BACK_CH;
-    l.dem = l.agc + 2 * NDC * BACK_CH;
+    l.aa = l.mid + 2 * BLK * BACK_CH;
+    l.agc = l.aa + 2 * BLK * BACK_CH;
+    l.pre = l.agc + 2 * NDC * BACK_CH;
+    l.dem = l.pre + 2 * NDC * BACK_CH;
     return l;
 }
 
@@ -471,9 +480,66 @@ struct BackLane
 // arithmetic, store() writes it back.  The pipelined kernel (rx_back) runs each stage in its own
 // wave; the fused kernel (rx_back_fused) runs all of them per sample in one wave.
 
-// ---- agc stage: IIR lattice pre-filter (audio_driver.c:2473-2482) + AudioAgc_RunAgcWdsp ----
-// input: adec from HBM (SSB: rx_front summed I +- Q), or the demod stage's output
-template <int PRE, int L, int W, int DM>
+// ---- input stage (SSB / CW / DIGI): rx_front's decimated I +- Q, fetched one call ahead ----
+template <int L>
+struct InStage
+{
+    static constexpr int NDC = BLK / L;
+    float xnext[NDC];
+
+    __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
+    {
+        const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
+#pragma unroll
+        for (int m = 0; m < NDC; m += 4)
+        {
+            const float4 v = *(const float4*)(src + m);
+            xnext[m] = v.x; xnext[m + 1] = v.y; xnext[m + 2] = v.z; xnext[m + 3] = v.w;
+        }
+    }
+
+    __device__ __forceinline__ void begin(const BackArgs& a, const BackLane& l, int call, float (&xin)[NDC])
+    {
+#pragma unroll
+        for (int m = 0; m < NDC; ++m) xin[m] = xnext[m];
+        if (call + 1 < l.calls) fetch(a, l, call + 1);
+    }
+};
+
+// ---- IIR lattice (arm_iir_lattice_f32): the pre-filter on a_buffer[0] at the decimated rate
+//      (IIR_PreFilter, audio_driver.c:2473-2482) or the anti-alias filter at 48 ksps
+//      (IIR_AntiAlias, :2581-2590); state [S][C] in `st` ----
+template <int S>
+struct LatticeStage
+{
+    float k[S > 0 ? S : 1], v[S + 1], g[S > 0 ? S : 1];
+
+    __device__ __forceinline__ void load(const BackLane& l, const float* kc, const float* vc, const float* st)
+    {
+#pragma unroll
+        for (int i = 0; i < S; ++i) k[i] = kc[i];
+#pragma unroll
+        for (int i = 0; i <= S; ++i) v[i] = vc[i];
+#pragma unroll
+        for (int i = 0; i < S; ++i) g[i] = st[i * l.C + l.cl];
+    }
+
+    __device__ __forceinline__ float step(float x)
+    {
+        if constexpr (S > 0) return lattice_step<S>(x, g, k, v);
+        return x;
+    }
+
+    __device__ __forceinline__ void store(const BackLane& l, float* st)
+    {
+        if (!l.live) return;
+#pragma unroll
+        for (int i = 0; i < S; ++i) st[i * l.C + l.c] = g[i];
+    }
+};
+
+// ---- agc stage: AudioAgc_RunAgcWdsp (audio_agc.c:349-595) on the pre-filtered samples ----
+template <int L, int W>
 struct AgcStage
 {
     static constexpr int NDC = BLK / L;
@@ -481,26 +547,18 @@ struct AgcStage
     // The AGC plan values live in the caller's local copy of P->agc, passed to step() (uniform
     // -> SGPRs; reading them through P inside the loop would reload them every sample since the
     // state stores may alias, and a struct member copy of it defeats SROA and lands in scratch).
-    float pk[PRE > 0 ? PRE : 1], pv[PRE + 1], pre[PRE > 0 ? PRE : 1];
     bool agc_on;
     float volts, save_volts, fast_bavg, hang_bavg, wold;
     float cmax[AGC_Q - 1];                               // maxima of calls k-Q+1 .. k-1 (oldest first)
     float leave_last;                                    // last sample of call k-Q-1
     int hang_counter, decay_type, state;
-    float xnext[NDC], rnext[NDC];                        // input and ring slot of the next call
+    float rnext[NDC];                                    // ring slot of the next call
     float old[NDC], sfx[NDC], wmax, pmax;                // this call's ring slot, suffix maxima
     float* ring_out;
 
     __device__ __forceinline__ void load(const BackArgs& a, const BackLane& l, const uhsdr_agc_plan& A)
     {
-        const uhsdr_rx_plan* __restrict__ P = a.plan;
         const int C = l.C, cl = l.cl;
-#pragma unroll
-        for (int i = 0; i < PRE; ++i) pk[i] = P->pre_k[i];
-#pragma unroll
-        for (int i = 0; i <= PRE; ++i) pv[i] = P->pre_v[i];
-#pragma unroll
-        for (int i = 0; i < PRE; ++i) pre[i] = a.s.pre[i * C + cl];
         agc_on = A.mode != 5;
         volts = a.s.agc[1 * C + cl];
         save_volts = a.s.agc[2 * C + cl];
@@ -515,19 +573,9 @@ struct AgcStage
         state = a.s.agci[2 * C + cl];
     }
 
-    // the decimated input and the ring slot of a call are fetched one call ahead
+    // the ring slot of a call is fetched one call ahead
     __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
     {
-        if (!DM)
-        {
-            const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
-#pragma unroll
-            for (int m = 0; m < NDC; m += 4)
-            {
-                const float4 v = *(const float4*)(src + m);
-                xnext[m] = v.x; xnext[m + 1] = v.y; xnext[m + 2] = v.z; xnext[m + 3] = v.w;
-            }
-        }
         if (agc_on)
         {
             const int slot = (a.ring_phase + call) % AGC_Q;
@@ -537,13 +585,12 @@ struct AgcStage
         }
     }
 
-    // start of call `call`: take the fetched data (xin: SSB input; AM/SAM get theirs from the
-    // demod stage), issue the next call's fetch, suffix maxima of call k-Q, maximum of the
-    // whole calls k-Q+1 .. k-1
-    __device__ __forceinline__ void begin(const BackArgs& a, const BackLane& l, int call, float (&xin)[NDC])
+    // start of call `call`: take the fetched ring slot, issue the next call's fetch, suffix
+    // maxima of call k-Q, maximum of the whole calls k-Q+1 .. k-1
+    __device__ __forceinline__ void begin(const BackArgs& a, const BackLane& l, int call)
     {
 #pragma unroll
-        for (int m = 0; m < NDC; ++m) { if (!DM) xin[m] = xnext[m]; old[m] = rnext[m]; }
+        for (int m = 0; m < NDC; ++m) old[m] = rnext[m];
         if (call + 1 < l.calls) fetch(a, l, call + 1);
         sfx[NDC - 1] = fabsf(old[NDC - 1]);
 #pragma unroll
@@ -558,7 +605,6 @@ struct AgcStage
     // sample m of the call
     __device__ __forceinline__ float step(int m, float x, const BackLane& l, const uhsdr_agc_plan& A)
     {
-        if (PRE > 0) x = lattice_step<PRE>(x, pre, pk, pv);
         // ---- AudioAgc_RunAgcWdsp, audio_agc.c:349-595 ----
         if (!agc_on)
         {
@@ -652,8 +698,6 @@ struct AgcStage
     {
         if (!l.live) return;
         const int C = l.C, c = l.c;
-#pragma unroll
-        for (int i = 0; i < PRE; ++i) a.s.pre[i * C + c] = pre[i];
         a.s.agc[1 * C + c] = volts;
         a.s.agc[2 * C + c] = save_volts;
         a.s.agc[3 * C + c] = fast_bavg;
@@ -787,34 +831,24 @@ struct AudioStage
     }
 };
 
-// ---- output stage: anti-alias lattice (audio_driver.c:2581-2590), biquad_2 (:2832), line-out
-//      scale (:2860); f32 audio and int32 codec frames (:2911-2923) by the caller ----
-template <int AA>
+// ---- output stage: biquad_2 (audio_driver.c:2832), line-out scale (:2860); f32 audio and
+//      int32 codec frames (:2911-2923) by the caller ----
 struct OutputStage
 {
-    float aa[AA > 0 ? AA : 1], bq2[4];
-    float ak[AA > 0 ? AA : 1], av[AA + 1], b2[5], lo;
+    float bq2[4], b2[5], lo;
 
     __device__ __forceinline__ void load(const BackArgs& a, const BackLane& l)
     {
         const uhsdr_rx_plan* __restrict__ P = a.plan;
-        const int C = l.C, cl = l.cl;
-#pragma unroll
-        for (int i = 0; i < AA; ++i) ak[i] = P->aa_k[i];
-#pragma unroll
-        for (int i = 0; i <= AA; ++i) av[i] = P->aa_v[i];
 #pragma unroll
         for (int i = 0; i < 5; ++i) b2[i] = P->biquad2[i];
 #pragma unroll
-        for (int i = 0; i < AA; ++i) aa[i] = a.s.aa[i * C + cl];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) bq2[i] = a.s.bq2[i * C + cl];
+        for (int i = 0; i < 4; ++i) bq2[i] = a.s.bq2[i * l.C + l.cl];
         lo = P->line_out_scale;
     }
 
     __device__ __forceinline__ float step(float v)
     {
-        if (AA > 0) v = lattice_step<AA>(v, aa, ak, av);
         v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
         return v * lo;
     }
@@ -822,8 +856,6 @@ struct OutputStage
     __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l)
     {
         if (!l.live) return;
-#pragma unroll
-        for (int i = 0; i < AA; ++i) a.s.aa[i * l.C + l.c] = aa[i];
 #pragma unroll
         for (int i = 0; i < 4; ++i) a.s.bq2[i * l.C + l.c] = bq2[i];
     }
@@ -992,36 +1024,80 @@ struct DemodStage
 
 // ---- pipelined roles (rx_back): stage s of the wave pipeline works on call it - s in
 //      iteration it; hand-offs through double-buffered LDS, one barrier per iteration ----
-template <int PRE, int L, int W, int DM>
+#define BACK_ROLE_LOOP(ST)                                                                     \
+    for (int it = 0; it < l.calls + back_roles(DM) - 1; ++it)                                  \
+    {                                                                                          \
+        const int call = it - (ST);                                                            \
+        if (call >= 0 && call < l.calls)                                                       \
+        {
+#define BACK_ROLE_END                                                                          \
+        }                                                                                      \
+        __syncthreads();                                                                       \
+    }
+
+template <int L, int DM>
+__device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
+{
+    const BackLane l(a);
+    constexpr int NDC = BLK / L;
+    DemodStage<L, DM> s;
+    s.load(a, l);
+    s.fetch(a, l, 0);
+    BACK_ROLE_LOOP(0)
+        s.begin(a, l, call);
+        float* dout = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
+#pragma unroll
+        for (int m = 0; m < NDC; ++m) dout[m * BACK_CH] = s.step(m);
+    BACK_ROLE_END
+    s.store(a, l);
+}
+
+// IIR lattice pre-filter; input: rx_front's decimated I +- Q (SSB) or the demod role's output
+template <int PRE, int L, int DM>
+__device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
+{
+    const BackLane l(a);
+    constexpr int NDC = BLK / L;
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    InStage<L> in;
+    LatticeStage<PRE> s;
+    s.load(l, P->pre_k, P->pre_v, a.s.pre);
+    if (!DM) in.fetch(a, l, 0);
+    BACK_ROLE_LOOP(DM ? 1 : 0)
+        float xin[NDC];
+        if (DM)
+        {
+            const float* di = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) xin[m] = di[m * BACK_CH];
+        }
+        else
+            in.begin(a, l, call, xin);
+        float* po = lds.pre + (call & 1) * NDC * BACK_CH + l.lane;
+#pragma unroll
+        for (int m = 0; m < NDC; ++m) po[m * BACK_CH] = s.step(xin[m]);
+    BACK_ROLE_END
+    s.store(l, a.s.pre);
+}
+
+template <int L, int W, int DM>
 __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
-    constexpr int NDC = BLK / L, ROLES = back_roles(DM), ST = DM ? 1 : 0;
+    constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     const uhsdr_agc_plan A = P->agc;
-    AgcStage<PRE, L, W, DM> s;
+    AgcStage<L, W> s;
     s.load(a, l, A);
     s.fetch(a, l, 0);
-    for (int it = 0; it < l.calls + ROLES - 1; ++it)
-    {
-        const int call = it - ST;
-        if (call >= 0 && call < l.calls)
-        {
-            float xin[NDC];
-            if (DM)
-            {
-                const float* di = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
+    BACK_ROLE_LOOP(DM ? 2 : 1)
+        const float* pi = lds.pre + (call & 1) * NDC * BACK_CH + l.lane;
+        float* ao = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
+        s.begin(a, l, call);
 #pragma unroll
-                for (int m = 0; m < NDC; ++m) xin[m] = di[m * BACK_CH];
-            }
-            s.begin(a, l, call, xin);
-            float* ao = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
-#pragma unroll
-            for (int m = 0; m < NDC; ++m) ao[m * BACK_CH] = s.step(m, xin[m], l, A);
-            s.end();
-        }
-        __syncthreads();
-    }
+        for (int m = 0; m < NDC; ++m) ao[m * BACK_CH] = s.step(m, pi[m * BACK_CH], l, A);
+        s.end();
+    BACK_ROLE_END
     s.store(a, l);
 }
 
@@ -1029,84 +1105,68 @@ template <int L, int PH, int DM>
 __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
-    constexpr int NDC = BLK / L, ROLES = back_roles(DM), ST = DM ? 2 : 1;
+    constexpr int NDC = BLK / L;
     AudioStage<L, PH, DM> s;
     s.load(a, l);
-    for (int it = 0; it < l.calls + ROLES - 1; ++it)
-    {
-        const int call = it - ST;
-        if (call >= 0 && call < l.calls)
+    BACK_ROLE_LOOP(DM ? 3 : 2)
+        const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
+        float* mo = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
+#pragma unroll
+        for (int m = 0; m < NDC; ++m)
         {
-            const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
-            float* mo = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
+            float u[L];
+            s.step(ai[m * BACK_CH], u);
 #pragma unroll
-            for (int m = 0; m < NDC; ++m)
-            {
-                float u[L];
-                s.step(ai[m * BACK_CH], u);
-#pragma unroll
-                for (int j = 0; j < L; ++j) mo[(m * L + j) * BACK_CH] = u[j];
-            }
-            s.end(a, l, call);
+            for (int j = 0; j < L; ++j) mo[(m * L + j) * BACK_CH] = u[j];
         }
-        __syncthreads();
-    }
+        s.end(a, l, call);
+    BACK_ROLE_END
     s.store(a, l);
 }
 
-template <int AA, int L, int DM>
+// anti-alias lattice at 48 ksps
+template <int AA, int DM>
+__device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
+{
+    const BackLane l(a);
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    LatticeStage<AA> s;
+    s.load(l, P->aa_k, P->aa_v, a.s.aa);
+    BACK_ROLE_LOOP(DM ? 4 : 3)
+        const float* mi = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
+        float* mo = lds.aa + (call & 1) * BLK * BACK_CH + l.lane;
+#pragma unroll 4
+        for (int n = 0; n < BLK; ++n) mo[n * BACK_CH] = s.step(mi[n * BACK_CH]);
+    BACK_ROLE_END
+    s.store(l, a.s.aa);
+}
+
+template <int DM>
 __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
-    constexpr int ROLES = back_roles(DM), ST = DM ? 3 : 2;
-    OutputStage<AA> s;
+    OutputStage s;
     s.load(a, l);
-    for (int it = 0; it < l.calls + ROLES - 1; ++it)
-    {
-        const int call = it - ST;
-        if (call >= 0)
-        {
-            const float* mi = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
+    BACK_ROLE_LOOP(DM ? 5 : 4)
+        const float* mi = lds.aa + (call & 1) * BLK * BACK_CH + l.lane;
 #pragma unroll 2
-            for (int n0 = 0; n0 < BLK; n0 += 4)
-            {
-                float y[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) y[j] = s.step(mi[(n0 + j) * BACK_CH]);
-                back_store4(a, l, call, n0, y);
-            }
-        }
-        __syncthreads();
-    }
-    s.store(a, l);
-}
-
-template <int L, int DM>
-__device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
-{
-    const BackLane l(a);
-    constexpr int NDC = BLK / L, ROLES = back_roles(DM);
-    DemodStage<L, DM> s;
-    s.load(a, l);
-    s.fetch(a, l, 0);
-    for (int it = 0; it < l.calls + ROLES - 1; ++it)
-    {
-        if (it < l.calls)
+        for (int n0 = 0; n0 < BLK; n0 += 4)
         {
-            s.begin(a, l, it);
-            float* dout = lds.dem + (it & 1) * NDC * BACK_CH + l.lane;
+            float y[4];
 #pragma unroll
-            for (int m = 0; m < NDC; ++m) dout[m * BACK_CH] = s.step(m);
+            for (int j = 0; j < 4; ++j) y[j] = s.step(mi[(n0 + j) * BACK_CH]);
+            back_store4(a, l, call, n0, y);
         }
-        __syncthreads();
-    }
+    BACK_ROLE_END
     s.store(a, l);
 }
+#undef BACK_ROLE_LOOP
+#undef BACK_ROLE_END
 
 // PRE / AA lattice stages, L interpolation factor, PH polyphase length, W AGC window,
 // DM demodulator (DM_NONE: SSB/CW/DIGI)
 template <int PRE, int AA, int L, int PH, int W, int DM>
-__global__ void __launch_bounds__(4 * BACK_CH) rx_back(BackArgs a)
+__global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const BackLds lds = back_lds_carve<BLK / L>(smem);
@@ -1115,11 +1175,15 @@ __global__ void __launch_bounds__(4 * BACK_CH) rx_back(BackArgs a)
     if (role < 0)
         rx_back_demod<L, DM>(a, lds);
     else if (role == 0)
-        rx_back_agc<PRE, L, W, DM>(a, lds);
+        rx_back_pre<PRE, L, DM>(a, lds);
     else if (role == 1)
+        rx_back_agc<L, W, DM>(a, lds);
+    else if (role == 2)
         rx_back_audio<L, PH, DM>(a, lds);
+    else if (role == 3)
+        rx_back_aa<AA, DM>(a, lds);
     else
-        rx_back_output<AA, L, DM>(a, lds);
+        rx_back_output<DM>(a, lds);
 }
 
 // Fused back end for large batches: one wave per 64 channels runs every stage per sample with
@@ -1132,16 +1196,22 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     static_assert(L == 2 || L == 4, "4 output frames per 1 or 2 decimated samples");
-    DemodStage<L, DM> dm;
-    AgcStage<PRE, L, W, DM> ag;
-    AudioStage<L, PH, DM> au;
-    OutputStage<AA> ou;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     const uhsdr_agc_plan A = P->agc;
+    DemodStage<L, DM> dm;
+    InStage<L> in;
+    LatticeStage<PRE> pre;
+    AgcStage<L, W> ag;
+    AudioStage<L, PH, DM> au;
+    LatticeStage<AA> aa;
+    OutputStage ou;
     if (DM) { dm.load(a, l); dm.fetch(a, l, 0); }
+    else in.fetch(a, l, 0);
+    pre.load(l, P->pre_k, P->pre_v, a.s.pre);
     ag.load(a, l, A);
     ag.fetch(a, l, 0);
     au.load(a, l);
+    aa.load(l, P->aa_k, P->aa_v, a.s.aa);
     ou.load(a, l);
     for (int call = 0; call < l.calls; ++call)
     {
@@ -1152,7 +1222,9 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
 #pragma unroll
             for (int m = 0; m < NDC; ++m) xin[m] = dm.step(m);
         }
-        ag.begin(a, l, call, xin);
+        else
+            in.begin(a, l, call, xin);
+        ag.begin(a, l, call);
         // the call's 32 output frames are stored in one burst at its end: interleaved with the
         // chain's arithmetic, the partial-line stores of 64 rows get evicted from L2 before
         // their lines fill, doubling the HBM write bytes
@@ -1161,9 +1233,9 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
         for (int m = 0; m < NDC; ++m)
         {
             float u[L];
-            au.step(ag.step(m, xin[m], l, A), u);
+            au.step(ag.step(m, pre.step(xin[m]), l, A), u);
 #pragma unroll
-            for (int j = 0; j < L; ++j) y[m * L + j] = ou.step(u[j]);
+            for (int j = 0; j < L; ++j) y[m * L + j] = ou.step(aa.step(u[j]));
         }
 #pragma unroll
         for (int n0 = 0; n0 < BLK; n0 += 4)
@@ -1175,11 +1247,12 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
         au.end(a, l, call);
     }
     if (DM) dm.store(a, l);
+    pre.store(l, a.s.pre);
     ag.store(a, l);
     au.store(a, l);
+    aa.store(l, a.s.aa);
     ou.store(a, l);
 }
-
 
 // ------------------------------------------------------------------------------------
 // rx_fm: FM receive after the Hilbert pair (AudioDriver_DemodFM, audio_driver.c:1544-1737,
@@ -1556,7 +1629,7 @@ static size_t front_lds(const uhsdr_rx_s* h)
 static size_t back_lds(const uhsdr_rx_s* h)
 {
     if (h->bv->dm == DM_FM) return sizeof(float) * (size_t)BACK_CH * 2 * (BLK + 1);
-    return sizeof(float) * (size_t)BACK_CH * 2 * (BLK + 2 * (BLK / h->plan.interp_L));
+    return sizeof(float) * (size_t)back_lds_floats(BLK / h->plan.interp_L);
 }
 
 extern "C" int uhsdr_rx_plan_supported(const uhsdr_rx_plan* p)

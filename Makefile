@@ -14,6 +14,7 @@ HOSTCFLAGS := -O2 -fPIC -ffp-contract=off -std=gnu11 -Wall -Wno-unused-function
 HIPFLAGS   := --offload-arch=$(ARCH) -O3 -fPIC -ffp-contract=off -fno-slp-vectorize -std=c++17 -Wno-unused-result
 
 LIB     := uhsdr_amd/lib/libuhsdr_amd.so
+CMSISLIB := uhsdr_amd/lib/libuhsdr_cmsis.so
 ORACLE  := oracle/build/libuhsdr_oracle.so
 OBJDIR  := uhsdr_amd/build
 
@@ -21,11 +22,11 @@ HOST_SRCS := uhsdr_amd/csrc/uhsdr_setup.c uhsdr_amd/csrc/uhsdr_filter_tables.c
 HIP_SRCS  := uhsdr_amd/csrc/uhsdr_rx.hip uhsdr_amd/csrc/uhsdr_tx.hip uhsdr_amd/csrc/uhsdr_spectrum.hip
 HOST_OBJS := $(patsubst uhsdr_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS  := $(patsubst uhsdr_amd/csrc/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
-HDRS := include/uhsdr.h uhsdr_amd/csrc/uhsdr_internal.h uhsdr_amd/csrc/uhsdr_dsp.h uhsdr_amd/csrc/uhsdr_libm.h
+HDRS := include/uhsdr.h uhsdr_amd/csrc/uhsdr_internal.h uhsdr_amd/csrc/uhsdr_dsp.h uhsdr_amd/csrc/uhsdr_libm.h uhsdr_amd/csrc/uhsdr_cfft.h
 
 EXAMPLE := examples/build/rx_batch
 
-all: $(LIB) $(ORACLE) $(EXAMPLE)
+all: $(LIB) $(CMSISLIB) $(ORACLE) $(EXAMPLE)
 
 $(OBJDIR) uhsdr_amd/lib oracle/build:
 	mkdir -p $@
@@ -38,6 +39,14 @@ $(OBJDIR)/%.o: uhsdr_amd/csrc/%.hip $(HDRS) | $(OBJDIR)
 
 $(LIB): $(HOST_OBJS) $(HIP_OBJS) | uhsdr_amd/lib
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -lm
+
+# CMSIS-DSP signature shims (include/uhsdr_cmsis.h): a library of their own, so the arm_* names
+# never collide with a CMSIS build linked elsewhere; uses libuhsdr_amd.so's setup layer
+$(OBJDIR)/uhsdr_cmsis.o: uhsdr_amd/csrc/uhsdr_cmsis.hip include/uhsdr_cmsis.h $(HDRS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CMSISLIB): $(OBJDIR)/uhsdr_cmsis.o $(LIB) | uhsdr_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJDIR)/uhsdr_cmsis.o -Luhsdr_amd/lib -luhsdr_amd -Wl,-rpath,'$$ORIGIN' -lm
 
 $(ORACLE): oracle/uhsdr_oracle.c oracle/uhsdr_oracle.h include/uhsdr.h | oracle/build
 	$(CC) $(HOSTCFLAGS) -shared -o $@ $< -lm -lpthread

@@ -1,0 +1,247 @@
+/*
+ * ORACLE TEST INFRASTRUCTURE -- golden vectors of the CMSIS-DSP f32 functions the firmware's
+ * RX/TX path calls, from the reference's own CMSIS-DSP V1.4.5 build (oracle/ref/Makefile),
+ * for the CMSIS-signature shims of libuhsdr_cmsis.so (include/uhsdr_cmsis.h).
+ *
+ *   uhsdr_ref dump=cmsis out=<dir>
+ *
+ * writes one raw little-endian float32 file per array, <dir>/<case>.<field>.f32, and prints a
+ * JSON manifest {case: {"params": {...}, "fields": {field: count}}}.  Every stateful case runs
+ * several consecutive calls on one instance, so the state carried in pState is exercised.
+ * Inputs come from a fixed LCG; coefficients of the IIR cases are drawn stable.
+ *
+ * arm_cfft_f32 (TransformFunctions/arm_cfft_f32.c:574-628) is dropped from the link (its bit
+ * reversal is ARM assembly, see ref_spectrum.c), so its wrapper -- input conjugation for the
+ * inverse, length switch, bit reversal, conjugate-and-scale by 1/L -- is restated in
+ * cfft_wrapper() around the reference's radix stages (ref_cfft_stages, ref_spectrum.c).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "arm_math.h"
+
+void ref_cfft_stages(int L, float* p, int bitrev);
+
+static uint32_t lcg_state = 0x5EED1234u;
+static float urand(void)   /* [-1, 1) */
+{
+    lcg_state = lcg_state * 1664525u + 1013904223u;
+    return (float)((int32_t)lcg_state) * (1.0f / 2147483648.0f);
+}
+
+static const char* g_dir;
+static int g_first_case = 1, g_first_field;
+
+static void case_begin(const char* name, const char* params_json)
+{
+    printf("%s\"%s\": {\"params\": %s, \"fields\": {", g_first_case ? "" : ", ", name, params_json);
+    g_first_case = 0;
+    g_first_field = 1;
+}
+
+static void case_end(void) { printf("}}"); }
+
+static void put(const char* cname, const char* field, const float* x, size_t n)
+{
+    char path[512];
+    snprintf(path, sizeof path, "%s/%s.%s.f32", g_dir, cname, field);
+    FILE* f = fopen(path, "wb");
+    if (!f || fwrite(x, sizeof(float), n, f) != n) { fprintf(stderr, "write %s failed\n", path); exit(2); }
+    fclose(f);
+    printf("%s\"%s\": %zu", g_first_field ? "" : ", ", field, n);
+    g_first_field = 0;
+}
+
+static float* frand(size_t n, float scale)
+{
+    float* x = malloc(sizeof(float) * (n ? n : 1));
+    for (size_t i = 0; i < n; ++i) x[i] = urand() * scale;
+    return x;
+}
+
+/* arm_fir_f32: numTaps T, blockSize B, K calls */
+static void fir_case(const char* name, int T, int B, int K)
+{
+    char p[128];
+    snprintf(p, sizeof p, "{\"numTaps\": %d, \"blockSize\": %d, \"calls\": %d}", T, B, K);
+    case_begin(name, p);
+    float* c = frand(T, 0.25f);
+    float* x = frand((size_t)B * K, 1.0f);
+    float* y = calloc((size_t)B * K, sizeof(float));
+    float* st = calloc(T + B - 1, sizeof(float));
+    arm_fir_instance_f32 S;
+    arm_fir_init_f32(&S, T, c, st, B);
+    for (int k = 0; k < K; ++k) arm_fir_f32(&S, x + (size_t)k * B, y + (size_t)k * B, B);
+    put(name, "coeffs", c, T); put(name, "src", x, (size_t)B * K); put(name, "dst", y, (size_t)B * K);
+    put(name, "state", st, T - 1);
+    case_end();
+    free(c); free(x); free(y); free(st);
+}
+
+/* arm_fir_decimate_f32: numTaps T, factor M, blockSize B (input samples), K calls */
+static void decim_case(const char* name, int T, int M, int B, int K)
+{
+    char p[160];
+    snprintf(p, sizeof p, "{\"numTaps\": %d, \"M\": %d, \"blockSize\": %d, \"calls\": %d}", T, M, B, K);
+    case_begin(name, p);
+    float* c = frand(T, 0.25f);
+    float* x = frand((size_t)B * K, 1.0f);
+    float* y = calloc((size_t)B / M * K, sizeof(float));
+    float* st = calloc(T + B - 1, sizeof(float));
+    arm_fir_decimate_instance_f32 S;
+    if (arm_fir_decimate_init_f32(&S, T, M, c, st, B) != ARM_MATH_SUCCESS) exit(3);
+    for (int k = 0; k < K; ++k) arm_fir_decimate_f32(&S, x + (size_t)k * B, y + (size_t)k * B / M, B);
+    put(name, "coeffs", c, T); put(name, "src", x, (size_t)B * K); put(name, "dst", y, (size_t)B / M * K);
+    put(name, "state", st, T - 1);
+    case_end();
+    free(c); free(x); free(y); free(st);
+}
+
+/* arm_fir_interpolate_f32: factor L, numTaps T (phaseLength T/L), blockSize B, K calls */
+static void interp_case(const char* name, int L, int T, int B, int K)
+{
+    char p[160];
+    snprintf(p, sizeof p, "{\"L\": %d, \"numTaps\": %d, \"blockSize\": %d, \"calls\": %d}", L, T, B, K);
+    case_begin(name, p);
+    const int ph = T / L;
+    float* c = frand(T, 0.5f);
+    float* x = frand((size_t)B * K, 1.0f);
+    float* y = calloc((size_t)B * L * K, sizeof(float));
+    float* st = calloc(ph + B - 1, sizeof(float));
+    arm_fir_interpolate_instance_f32 S;
+    if (arm_fir_interpolate_init_f32(&S, L, T, c, st, B) != ARM_MATH_SUCCESS) exit(3);
+    for (int k = 0; k < K; ++k) arm_fir_interpolate_f32(&S, x + (size_t)k * B, y + (size_t)k * B * L, B);
+    put(name, "coeffs", c, T); put(name, "src", x, (size_t)B * K); put(name, "dst", y, (size_t)B * L * K);
+    put(name, "state", st, ph - 1 > 0 ? ph - 1 : 0);
+    case_end();
+    free(c); free(x); free(y); free(st);
+}
+
+/* arm_iir_lattice_f32: numStages S, blockSize B, K calls; reflection coefficients |k| < 0.8 */
+static void lattice_case(const char* name, int NS, int B, int K)
+{
+    char p[128];
+    snprintf(p, sizeof p, "{\"numStages\": %d, \"blockSize\": %d, \"calls\": %d}", NS, B, K);
+    case_begin(name, p);
+    float* kc = frand(NS, 0.8f);
+    float* vc = frand(NS + 1, 0.5f);
+    float* x = frand((size_t)B * K, 1.0f);
+    float* y = calloc((size_t)B * K, sizeof(float));
+    float* st = calloc(NS + B, sizeof(float));
+    arm_iir_lattice_instance_f32 S;
+    arm_iir_lattice_init_f32(&S, NS, kc, vc, st, B);
+    for (int k = 0; k < K; ++k) arm_iir_lattice_f32(&S, x + (size_t)k * B, y + (size_t)k * B, B);
+    put(name, "k", kc, NS); put(name, "v", vc, NS + 1); put(name, "src", x, (size_t)B * K);
+    put(name, "dst", y, (size_t)B * K); put(name, "state", st, NS);
+    case_end();
+    free(kc); free(vc); free(x); free(y); free(st);
+}
+
+/* arm_biquad_cascade_df1_f32: numStages S, blockSize B, K calls; each stage a stable pair of
+   poles (radius < 0.95) with CMSIS's sign convention (a1, a2 enter as + a1 y[n-1] + a2 y[n-2]) */
+static void biquad_case(const char* name, int NS, int B, int K)
+{
+    char p[128];
+    snprintf(p, sizeof p, "{\"numStages\": %d, \"blockSize\": %d, \"calls\": %d}", NS, B, K);
+    case_begin(name, p);
+    float* c = malloc(sizeof(float) * 5 * NS);
+    for (int s = 0; s < NS; ++s)
+    {
+        const float r = 0.5f + 0.45f * (0.5f * urand() + 0.5f), th = 3.14159265f * (0.5f * urand() + 0.5f);
+        c[5 * s + 0] = 0.5f * urand(); c[5 * s + 1] = 0.5f * urand(); c[5 * s + 2] = 0.5f * urand();
+        c[5 * s + 3] = 2.0f * r * cosf(th);
+        c[5 * s + 4] = -r * r;
+    }
+    float* x = frand((size_t)B * K, 1.0f);
+    float* y = calloc((size_t)B * K, sizeof(float));
+    float* st = calloc(4 * NS, sizeof(float));
+    arm_biquad_casd_df1_inst_f32 S;
+    arm_biquad_cascade_df1_init_f32(&S, NS, c, st);
+    for (int k = 0; k < K; ++k) arm_biquad_cascade_df1_f32(&S, x + (size_t)k * B, y + (size_t)k * B, B);
+    put(name, "coeffs", c, 5 * NS); put(name, "src", x, (size_t)B * K); put(name, "dst", y, (size_t)B * K);
+    put(name, "state", st, 4 * NS);
+    case_end();
+    free(c); free(x); free(y); free(st);
+}
+
+/* arm_cfft_f32(S, p1, ifftFlag, bitReverseFlag), arm_cfft_f32.c:574-628 */
+static void cfft_wrapper(int L, float* p1, int ifft, int bitrev)
+{
+    if (ifft == 1)
+    {
+        float* p = p1 + 1;
+        for (int l = 0; l < L; ++l) { *p = -*p; p += 2; }
+    }
+    ref_cfft_stages(L, p1, bitrev);
+    if (ifft == 1)
+    {
+        const float invL = 1.0f / (float32_t)L;
+        float* p = p1;
+        for (int l = 0; l < L; ++l)
+        {
+            *p++ *= invL;
+            *p = -(*p) * invL;
+            p++;
+        }
+    }
+}
+
+static void cfft_case(const char* name, int L, int ifft, int bitrev)
+{
+    char p[128];
+    snprintf(p, sizeof p, "{\"fftLen\": %d, \"ifftFlag\": %d, \"bitReverseFlag\": %d}", L, ifft, bitrev);
+    case_begin(name, p);
+    float* x = frand(2 * (size_t)L, 1.0f);
+    float* y = malloc(sizeof(float) * 2 * L);
+    memcpy(y, x, sizeof(float) * 2 * L);
+    cfft_wrapper(L, y, ifft, bitrev);
+    put(name, "src", x, 2 * (size_t)L); put(name, "dst", y, 2 * (size_t)L);
+    case_end();
+    free(x); free(y);
+}
+
+static void mag_case(const char* name, int n)
+{
+    char p[64];
+    snprintf(p, sizeof p, "{\"numSamples\": %d}", n);
+    case_begin(name, p);
+    float* x = frand(2 * (size_t)n, 100.0f);
+    float* y = malloc(sizeof(float) * n);
+    arm_cmplx_mag_f32(x, y, n);
+    put(name, "src", x, 2 * (size_t)n); put(name, "dst", y, n);
+    case_end();
+    free(x); free(y);
+}
+
+int ref_cmsis_dump(const char* dir)
+{
+    g_dir = dir;
+    printf("{");
+    fir_case("fir_89x32", 89, 32, 5);
+    fir_case("fir_199x8", 199, 8, 40);
+    fir_case("fir_7x13", 7, 13, 4);
+    fir_case("fir_1x5", 1, 5, 3);
+    decim_case("decim_43_m4", 43, 4, 32, 5);
+    decim_case("decim_83_m4", 83, 4, 128, 3);
+    decim_case("decim_5_m2", 5, 2, 10, 4);
+    interp_case("interp_l4_t16", 4, 16, 8, 5);
+    interp_case("interp_l4_t4", 4, 4, 8, 3);
+    interp_case("interp_l2_t6", 2, 6, 7, 4);
+    interp_case("interp_l3_t21", 3, 21, 9, 3);
+    lattice_case("lattice_10x8", 10, 8, 6);
+    lattice_case("lattice_6x32", 6, 32, 4);
+    lattice_case("lattice_3x5", 3, 5, 3);
+    biquad_case("biquad_4x8", 4, 8, 6);
+    biquad_case("biquad_1x37", 1, 37, 3);
+    biquad_case("biquad_3x1", 3, 1, 9);
+    cfft_case("cfft_256", 256, 0, 1);
+    cfft_case("cfft_512", 512, 0, 1);
+    cfft_case("cfft_1024", 1024, 0, 1);
+    cfft_case("cfft_512_nobitrev", 512, 0, 0);
+    cfft_case("cfft_1024_nobitrev", 1024, 0, 0);
+    cfft_case("icfft_256", 256, 1, 1);
+    cfft_case("icfft_1024", 1024, 1, 1);
+    mag_case("mag_1000", 1000);
+    printf("}\n");
+    return 0;
+}

@@ -194,6 +194,7 @@ int main(int argc, char** argv)
     if (strcmp(dump, "paths") == 0) { dump_paths(); return 0; }
     if (strcmp(dump, "spectrum") == 0) { ref_spec_dump(); return 0; }
     if (strcmp(dump, "txextra") == 0) { dump_txextra(); return 0; }
+    if (strcmp(dump, "cmsis") == 0) { extern int ref_cmsis_dump(const char*); return ref_cmsis_dump(arg(argc, argv, "out", ".")); }
 
     const int mode = (int)iarg(argc, argv, "mode", DEMOD_USB);
     const int path = (int)iarg(argc, argv, "path", 0);

@@ -84,8 +84,9 @@ static void bitreverse(float* p, uint16_t len, const uint16_t* tab)
         }
 }
 
-/* arm_cfft_f32(S, p1, 0, 1) for L in {256, 512, 1024} */
-void ref_cfft(int L, float* p)
+/* the length switch and optional bit reversal of arm_cfft_f32 (arm_cfft_f32.c:594-614) for L
+   in {256, 512, 1024} */
+void ref_cfft_stages(int L, float* p, int bitrev)
 {
     const arm_cfft_instance_f32* S = instance(L);
     switch (L)
@@ -94,8 +95,11 @@ void ref_cfft(int L, float* p)
     case 256: arm_cfft_radix8by4_f32((arm_cfft_instance_f32*)S, p); break;
     case 512: arm_radix8_butterfly_f32(p, L, (float32_t*)S->pTwiddle, 1); break;
     }
-    bitreverse(p, S->bitRevLength, S->pBitRevTable);
+    if (bitrev) bitreverse(p, S->bitRevLength, S->pBitRevTable);
 }
+
+/* arm_cfft_f32(S, p1, 0, 1) for L in {256, 512, 1024} */
+void ref_cfft(int L, float* p) { ref_cfft_stages(L, p, 1); }
 
 /* UiSpectrum_FFTWindowFunction(FFT_WINDOW_HANN) on fft_iq_len = 2L floats */
 void ref_spec_window(int L, float* x)

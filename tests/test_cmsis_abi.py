@@ -1,0 +1,62 @@
+"""CMSIS-signature shims (include/uhsdr_cmsis.h, libuhsdr_cmsis.so), checks that need no GPU:
+the header, the ctypes binding and the library's exports agree; the instance structs have the
+CMSIS layout (checked against gcc on the header); the init functions follow CMSIS's argument
+rules (arm_fir_decimate_init_f32.c, arm_fir_interpolate_init_f32.c) and zero the state."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from uhsdr_amd import cmsis
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "uhsdr_cmsis.h")
+
+
+def declared():
+    src = re.sub(r"/\*.*?\*/", "", open(HDR).read(), flags=re.S)
+    return sorted(set(re.findall(r"\b((?:arm|uhsdr)_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_and_bindings_agree():
+    assert set(declared()) == set(cmsis.SIGNATURES), set(declared()) ^ set(cmsis.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = cmsis.load()
+    for name in declared():
+        assert hasattr(lib, name), name
+
+
+@pytest.mark.parametrize("name", ["arm_fir_instance_f32", "arm_fir_decimate_instance_f32",
+                                  "arm_fir_interpolate_instance_f32", "arm_iir_lattice_instance_f32",
+                                  "arm_biquad_casd_df1_inst_f32", "arm_cfft_instance_f32"])
+def test_instance_layout_matches_header(name, tmp_path):
+    st = getattr(cmsis, name)
+    src = tmp_path / "sz.c"
+    fields = [f for f, _ in st._fields_]
+    body = " ".join(f'printf("%zu ", (size_t)offsetof({name}, {f}));' for f in fields)
+    src.write_text(f'#include <stdio.h>\n#include <stddef.h>\n#include "uhsdr_cmsis.h"\n'
+                   f'int main(void) {{ printf("%zu ", sizeof({name})); {body} return 0; }}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got == [C.sizeof(st)] + [getattr(st, f).offset for f in fields]
+
+
+def test_init_functions_follow_cmsis_rules():
+    lib = cmsis.load()
+    c = np.ones(8, np.float32)
+    state = np.full(8 + 12 - 1, 7.0, np.float32)
+    S = cmsis.arm_fir_decimate_instance_f32()
+    assert lib.arm_fir_decimate_init_f32(C.byref(S), 8, 4, cmsis._fp(c), cmsis._fp(state), 10) == -2
+    assert lib.arm_fir_decimate_init_f32(C.byref(S), 8, 4, cmsis._fp(c), cmsis._fp(state), 12) == 0
+    assert (S.M, S.numTaps) == (4, 8) and not state.any()
+    I = cmsis.arm_fir_interpolate_instance_f32()
+    st2 = np.full(16, 3.0, np.float32)
+    assert lib.arm_fir_interpolate_init_f32(C.byref(I), 3, 8, cmsis._fp(c), cmsis._fp(st2), 4) == -2
+    assert lib.arm_fir_interpolate_init_f32(C.byref(I), 4, 8, cmsis._fp(c), cmsis._fp(st2), 4) == 0
+    assert I.phaseLength == 2 and not st2[:5].any()

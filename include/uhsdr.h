@@ -299,8 +299,34 @@ uhsdr_status uhsdr_tx_reset(uhsdr_tx_handle h);
 uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio, int32_t* iq, float* a0);
 uhsdr_status uhsdr_tx_get_plan(uhsdr_tx_handle h, uhsdr_tx_plan* plan);
 uhsdr_status uhsdr_tx_destroy(uhsdr_tx_handle h);
+/* TxProcessor_PrepareRun (tx_processor.c:63-66): clear the ALC look-ahead delay line only,
+   the first time back to TX; all other TX state carries on */
+uhsdr_status uhsdr_tx_prepare_run(uhsdr_tx_handle h);
 int32_t      uhsdr_sizeof_tx_config(void);
 int32_t      uhsdr_sizeof_tx_plan(void);
+
+/* ---- the firmware's ISR entry for one transceiver ----
+ * AudioDriver_I2SCallback(audio, iq, audioDst, blockSize) (audio_driver.c:2962-3049) with the
+ * firmware's own DMA half-buffers in host memory: AudioSample_t / IqSample_t = {int32 l, r}.
+ * One receiver (uhsdr_rx_* with 1 channel) and optionally one transmitter (uhsdr_tx_*), both
+ * with frames_per_call = block_size (32 on the firmware).
+ *   RX (txrx_mode 0): iq in, codec frames out in `audio`.  The first call after TX, and while
+ *       the input-mute counter runs, the firmware silences iq in place, still runs the chain
+ *       and mutes the output (AudioDriver_IqFillSilence, RxProcessor external_mute :2845-2853).
+ *   TX (txrx_mode 1): mic / line frames in `audio`, DAC I/Q out in `iq`, the codec sidetone in
+ *       `audioDst` (zero for the voice modes, tx_processor.c:154-163, radio_management.c:450).
+ *       The first call after RX runs TxProcessor_PrepareRun and, like a counted input mute,
+ *       silences `audio` and skips the chain (external_mute: "do nothing", :946-949), so the I/Q
+ *       out is zero and the TX state does not advance.
+ * A call is synchronous: outputs are in the host buffers on return. */
+typedef struct uhsdr_i2s_s* uhsdr_i2s_handle;
+
+uhsdr_status uhsdr_i2s_create(const uhsdr_rx_config* rx, const uhsdr_tx_config* tx /* NULL: receive only */,
+                              int32_t block_size, void* stream, uhsdr_i2s_handle* out);
+uhsdr_status uhsdr_i2s_set_txrx_mode(uhsdr_i2s_handle h, int32_t txrx_mode);   /* ts.txrx_mode: 0 RX, 1 TX */
+uhsdr_status uhsdr_i2s_set_input_mute(uhsdr_i2s_handle h, int32_t calls);      /* ts.audio_processor_input_mute_counter */
+uhsdr_status uhsdr_i2s_callback(uhsdr_i2s_handle h, int32_t* audio, int32_t* iq, int32_t* audioDst, int16_t blockSize);
+uhsdr_status uhsdr_i2s_destroy(uhsdr_i2s_handle h);
 
 /* ---- spectrum display ----
  * Replaces the no-zoom producer AudioDriver_SpectrumNoZoomProcessSamples (audio_driver.c:

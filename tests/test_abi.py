@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_functions():
     src = open(os.path.join(ROOT, "include", "uhsdr.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(uhsdr_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(uhsdr_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_and_bindings_agree():

@@ -11,3 +11,4 @@ from ._abi import (RxConfig, RxPlan, build_plan, config_from_ref_args, default_c
 from .rx import RxChain  # noqa: F401
 from .tx import TxChain  # noqa: F401
 from .spectrum import Spectrum  # noqa: F401
+from .i2s import Transceiver  # noqa: F401

@@ -173,6 +173,13 @@ SIGNATURES = {
     "uhsdr_tx_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "uhsdr_tx_get_plan": (C.c_int, [C.c_void_p, C.POINTER(TxPlan)]),
     "uhsdr_tx_destroy": (C.c_int, [C.c_void_p]),
+    "uhsdr_tx_prepare_run": (C.c_int, [C.c_void_p]),
+    "uhsdr_i2s_create": (C.c_int, [C.POINTER(RxConfig), C.POINTER(TxConfig), C.c_int32, C.c_void_p,
+                                   C.POINTER(C.c_void_p)]),
+    "uhsdr_i2s_set_txrx_mode": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_i2s_set_input_mute": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_i2s_callback": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int16]),
+    "uhsdr_i2s_destroy": (C.c_int, [C.c_void_p]),
     "uhsdr_sizeof_tx_config": (C.c_int32, []),
     "uhsdr_sizeof_tx_plan": (C.c_int32, []),
     "uhsdr_spectrum_config_default": (None, [C.POINTER(SpectrumConfig)]),

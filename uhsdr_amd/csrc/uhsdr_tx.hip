@@ -383,6 +383,14 @@ extern "C" uhsdr_status uhsdr_tx_reset(uhsdr_tx_handle h)
     return UHSDR_OK;
 }
 
+extern "C" uhsdr_status uhsdr_tx_prepare_run(uhsdr_tx_handle h)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    // TxProcessor_PrepareRun (tx_processor.c:63-66): arm_fill_f32(0, audio_delay_buffer, ...)
+    HIPCHK(hipMemsetAsync(h->delay, 0, sizeof(float) * UHSDR_TX_DELAY * (size_t)h->C, h->stream));
+    return UHSDR_OK;
+}
+
 extern "C" uhsdr_status uhsdr_tx_create(const uhsdr_tx_config* cfg, int32_t C, int32_t N, void* stream,
                                         uhsdr_tx_handle* out)
 {

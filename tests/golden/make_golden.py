@@ -14,7 +14,8 @@ freq_shift.c / CMSIS-DSP compiled for x86 by ``oracle/ref/Makefile`` -- once per
         args    json             the uhsdr_ref key=value configuration
 
 plus tests/golden/filter_paths.json (FilterPathInfo[], audio_filter.c:147-922, as raw
-float bits).  Only runs where /root/reference exists (build container); the fixtures
+float bits), the TX / spectrum / CW fixtures (tx_*, spec_*, cw_*.npz) and
+tests/golden/cmsis_vectors.npz (CMSIS-DSP f32 call sequences, dump=cmsis, oracle/ref/ref_cmsis.c).  Only runs where /root/reference exists (build container); the fixtures
 are committed and the GPU box never needs the reference.
 
     python tests/golden/make_golden.py [--only NAME]

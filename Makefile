@@ -19,7 +19,7 @@ ORACLE  := oracle/build/libuhsdr_oracle.so
 OBJDIR  := uhsdr_amd/build
 
 HOST_SRCS := uhsdr_amd/csrc/uhsdr_setup.c uhsdr_amd/csrc/uhsdr_filter_tables.c
-HIP_SRCS  := uhsdr_amd/csrc/uhsdr_rx.hip uhsdr_amd/csrc/uhsdr_tx.hip uhsdr_amd/csrc/uhsdr_spectrum.hip uhsdr_amd/csrc/uhsdr_i2s.hip
+HIP_SRCS  := uhsdr_amd/csrc/uhsdr_rx.hip uhsdr_amd/csrc/uhsdr_tx.hip uhsdr_amd/csrc/uhsdr_spectrum.hip uhsdr_amd/csrc/uhsdr_i2s.hip uhsdr_amd/csrc/uhsdr_fir.hip
 HOST_OBJS := $(patsubst uhsdr_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS  := $(patsubst uhsdr_amd/csrc/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
 HDRS := include/uhsdr.h uhsdr_amd/csrc/uhsdr_internal.h uhsdr_amd/csrc/uhsdr_dsp.h uhsdr_amd/csrc/uhsdr_libm.h uhsdr_amd/csrc/uhsdr_cfft.h

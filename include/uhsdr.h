@@ -319,6 +319,24 @@ int32_t      uhsdr_sizeof_tx_plan(void);
  *       silences `audio` and skips the chain (external_mute: "do nothing", :946-949), so the I/Q
  *       out is zero and the TX state does not advance.
  * A call is synchronous: outputs are in the host buffers on return. */
+/* ---- batched arm_fir_f32 (CMSIS FilteringFunctions/arm_fir_f32.c:482-560) ----
+ * C channels, one shared tap set (CMSIS order, time-reversed), each channel's T-1 carried samples
+ * on the device; one call == arm_fir_f32(S_c, src_c, dst_c, B) on every channel.  C5's long
+ * narrow filter and the north_star's FIR-as-GEMM:
+ *   UHSDR_FIR_EXACT  bit-identical to arm_fir_f32 (VALU, the reference's operation order)
+ *   UHSDR_FIR_MFMA   the FIR as a GEMM on v_mfma_f32_16x16x4_f32 (fused multiply-adds in tap
+ *                    order: within 1e-5 relative of the reference, not bit-identical)
+ * block_size B: a multiple of 256.  src / dst: device f32 [C][B]. */
+enum { UHSDR_FIR_EXACT = 0, UHSDR_FIR_MFMA = 1 };
+typedef struct uhsdr_fir_s* uhsdr_fir_handle;
+
+uhsdr_status uhsdr_fir_create(const float* coeffs, int32_t num_taps, int32_t num_channels, int32_t block_size,
+                              int32_t mode, void* stream, uhsdr_fir_handle* out);
+uhsdr_status uhsdr_fir_reset(uhsdr_fir_handle h);
+uhsdr_status uhsdr_fir_process(uhsdr_fir_handle h, const float* src, float* dst);
+uhsdr_status uhsdr_fir_synchronize(uhsdr_fir_handle h);
+uhsdr_status uhsdr_fir_destroy(uhsdr_fir_handle h);
+
 typedef struct uhsdr_i2s_s* uhsdr_i2s_handle;
 
 uhsdr_status uhsdr_i2s_create(const uhsdr_rx_config* rx, const uhsdr_tx_config* tx /* NULL: receive only */,

@@ -40,6 +40,7 @@ def load():
         lib.uo_cfft.argtypes = [C.c_void_p, C.c_void_p]
         lib.uo_spec_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                               C.c_void_p, C.c_void_p, C.c_int]
+        lib.uo_fir_batch.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
         _lib = lib
     return _lib
 
@@ -143,3 +144,21 @@ class OracleSpectrum:
         x = np.ascontiguousarray(x, dtype=np.float32).copy()
         self.lib.uo_cfft(C.byref(self.plan), x.ctypes.data_as(C.c_void_p))
         return x
+
+
+class OracleFir:
+    """C channels of CMSIS arm_fir_f32 sharing one tap set, state carried across calls."""
+
+    def __init__(self, taps, channels: int):
+        self.lib = load()
+        self.c = np.ascontiguousarray(taps, np.float32)
+        self.channels = channels
+        self.hist = np.zeros((channels, len(self.c) - 1), np.float32)
+
+    def process(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, np.float32)
+        assert x.shape[0] == self.channels
+        y = np.empty_like(x)
+        self.lib.uo_fir_batch(self.c.ctypes.data_as(C.c_void_p), len(self.c), self.hist.ctypes.data_as(C.c_void_p),
+                              self.channels, x.ctypes.data_as(C.c_void_p), x.shape[1], y.ctypes.data_as(C.c_void_p))
+        return y

@@ -221,6 +221,7 @@ int ref_cmsis_dump(const char* dir)
     fir_case("fir_199x8", 199, 8, 40);
     fir_case("fir_7x13", 7, 13, 4);
     fir_case("fir_1x5", 1, 5, 3);
+    fir_case("fir_513x256", 513, 256, 6);   /* C5's synthetic long FIR */
     decim_case("decim_43_m4", 43, 4, 32, 5);
     decim_case("decim_83_m4", 83, 4, 128, 3);
     decim_case("decim_5_m2", 5, 2, 10, 4);

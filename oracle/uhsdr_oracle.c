@@ -10,6 +10,7 @@
  * (auto I/Q statistics, oscillator gain renormalisation).
  */
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
 #include "uhsdr_oracle.h"
@@ -1215,4 +1216,27 @@ int uo_spec_process_batch(const uhsdr_spectrum_plan* p, uo_spec_state* states, i
     if (threads > 1)
         for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
     return jobs[0].frames;
+}
+
+/* ---- batched arm_fir_f32 (CMSIS FilteringFunctions/arm_fir_f32.c:482-560): per channel the
+   window [T-1 carried samples | block], y[n] = sum_{k<T} c[k] * w[n + k] accumulated from +0.0f
+   in tap order, separate multiply and add; the carried samples become the window's last T-1.
+   The checker for uhsdr_fir_* (C5's synthetic long FIR). */
+void uo_fir_batch(const float* c, int T, float* hist, int C, const float* x, int n, float* y)
+{
+    float* w = (float*)malloc(sizeof(float) * (size_t)(T - 1 + n));
+    for (int ch = 0; ch < C; ++ch)
+    {
+        float* h = hist + (size_t)ch * (T - 1);
+        memcpy(w, h, sizeof(float) * (size_t)(T - 1));
+        memcpy(w + T - 1, x + (size_t)ch * n, sizeof(float) * (size_t)n);
+        for (int i = 0; i < n; ++i)
+        {
+            float acc = 0.0f;
+            for (int k = 0; k < T; ++k) acc += w[i + k] * c[k];
+            y[(size_t)ch * n + i] = acc;
+        }
+        memcpy(h, w + n, sizeof(float) * (size_t)(T - 1));
+    }
+    free(w);
 }

@@ -105,6 +105,8 @@ size_t uo_spec_state_size(void);
 void uo_spec_state_init(const uhsdr_spectrum_plan* p, uo_spec_state* s);
 /* arm_cfft_f32(S, x, 0, 1) restated: forward CFFT in place, natural order out */
 void uo_cfft(const uhsdr_spectrum_plan* p, float* x);
+/* batched arm_fir_f32: hist [C][T-1] carried in / out, x / y [C][n] */
+void uo_fir_batch(const float* c, int T, float* hist, int C, const float* x, int n, float* y);
 /* n samples of C channels; mag / avg [C][F][L] with F = frames completed (same for every
    channel); returns F, or a negative status */
 int uo_spec_process_batch(const uhsdr_spectrum_plan* p, uo_spec_state* states, int C, const int32_t* iq, int n,

@@ -78,7 +78,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--only", default="c3,c3spec,c4fm,c4tx,c5")
+    ap.add_argument("--only", default="c3,c3spec,c4fm,c4tx,c5,c5fir")
     a = ap.parse_args()
     import torch
     import uhsdr_amd as U
@@ -129,6 +129,29 @@ def main():
         cfg = U.default_config(filter_path=4, dmod_mode=U.DEMOD_CW)
         lines.append(rx_line("C5 per-GPU share: CW P4 (199-tap Hilbert @12k, 300 Hz lattice) + CW decoder Goertzel",
                              cfg, C, N, tiled(synth.cw_iq, C, N), a.steps, a.warmup, cw=True))
+    if "c5fir" in want:
+        import numpy as np
+        C, N = 1048576 // 8, 256
+        taps = np.load(os.path.join(ROOT, "tests", "golden", "fir513_kaiser.npy"))
+        T = len(taps)
+        x = torch.randn((min(C, 4096), N), device="cuda").mul_(1000.0).repeat((C + 4095) // 4096, 1)[:C].contiguous()
+        y = torch.empty_like(x)
+        s = torch.cuda.current_stream()
+        for mode, name in ((U.fir.EXACT, "exact, bit-identical to arm_fir_f32"),
+                           (U.fir.MFMA, "MFMA v_mfma_f32_16x16x4_f32, FIR as GEMM, fused MACs")):
+            fir = U.FirBatch(taps, C, N, mode, stream=s.cuda_stream)
+            ms = time_calls(lambda: fir.process(x, y), a.steps, a.warmup)
+            fir.close()
+            per = 8 + 2 * 4 * (T - 1) / N                 # 4 B in + 4 B out, carried samples in + out
+            K = (T + 15 + 3) & ~3
+            line = {"workload": f"C5 per-GPU share: batched 513-tap FIR at 12 ksps ({name})", "channels": C,
+                    "frames_per_call": N, "ms_per_call": round(ms, 4), "msamples_per_s": round(C * N / ms / 1e3, 1),
+                    "alg_bytes_per_frame": round(per, 2), "hbm_frac": round(C * N * per / ms / 1e6 / HBM_PEAK_GBS, 4),
+                    "alg_tflops": round(C * N * 2 * T / ms / 1e9, 1)}
+            if mode == U.fir.MFMA:
+                line["mfma_tflops_issued"] = round(C * N * 2 * K / ms / 1e9, 1)
+                line["mfma_f32_peak_tflops"] = 157.3
+            lines.append(line)
     for ln in lines:
         ln["data"] = "synthetic: 4096 distinct channels tiled"
         print(json.dumps(ln), flush=True)

@@ -12,3 +12,4 @@ from .rx import RxChain  # noqa: F401
 from .tx import TxChain  # noqa: F401
 from .spectrum import Spectrum  # noqa: F401
 from .i2s import Transceiver  # noqa: F401
+from .fir import FirBatch  # noqa: F401

@@ -174,6 +174,12 @@ SIGNATURES = {
     "uhsdr_tx_get_plan": (C.c_int, [C.c_void_p, C.POINTER(TxPlan)]),
     "uhsdr_tx_destroy": (C.c_int, [C.c_void_p]),
     "uhsdr_tx_prepare_run": (C.c_int, [C.c_void_p]),
+    "uhsdr_fir_create": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                   C.POINTER(C.c_void_p)]),
+    "uhsdr_fir_reset": (C.c_int, [C.c_void_p]),
+    "uhsdr_fir_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "uhsdr_fir_synchronize": (C.c_int, [C.c_void_p]),
+    "uhsdr_fir_destroy": (C.c_int, [C.c_void_p]),
     "uhsdr_i2s_create": (C.c_int, [C.POINTER(RxConfig), C.POINTER(TxConfig), C.c_int32, C.c_void_p,
                                    C.POINTER(C.c_void_p)]),
     "uhsdr_i2s_set_txrx_mode": (C.c_int, [C.c_void_p, C.c_int32]),

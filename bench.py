@@ -121,12 +121,16 @@ def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
                       f"{threads} threads, channels split evenly; host CPU: {model}"}
 
 
-def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, pool, want_dst):
+def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, pool, want_dst, pipelined=False,
+              precision=0):
     """W untimed + K timed steps of one RxChain on this rank; returns (max-rank seconds,
     per-kernel (total ms, launches) from HIP events on the library's stream, plan, finite)."""
     cfg = U.default_config()
     stream = torch.cuda.current_stream(dev)
     chain = U.RxChain(cfg, channels=C, frames=N, stream=stream.cuda_stream)
+    chain.set_precision(precision)
+    if pipelined:
+        chain.set_pipelined(True)        # call k+1's rx_front overlaps call k's rx_back
     plan = chain.plan
     # inputs resident in HBM before timing: a pool of consecutive blocks, cycled
     c0 = shard.channel_range(C, rank)[0]          # weak scaling: rank r owns channels [r*C, (r+1)*C)
@@ -137,7 +141,10 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     for s in range(warmup):
         chain.process(inputs[s % pool], audio, dst)
     torch.cuda.synchronize(dev)
-    chain.enable_timing(True)
+    # HIP events bracket the kernels of every `every`-th timed call (~64 sampled calls), so the
+    # event records' own cost (~30 us per bracketed call) stays out of the throughput
+    every = max(1, steps // 64)
+    chain.enable_timing(True, every=every)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -226,6 +233,11 @@ def main():
     ap.add_argument("--no-northstar", action="store_true", help="skip the 1M-channel north-star leg")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL gather leg (N > 1)")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--pipelined", action="store_true",
+                    help="overlap call k+1's rx_front with call k's rx_back (uhsdr_rx_set_pipelined); "
+                         "measured no faster on MI355X, so off by default")
+    ap.add_argument("--precision", default="exact", choices=["exact", "fma"],
+                    help="FIR MACs: exact (bit-identical to the reference) or fma (1e-5 normwise)")
     ap.add_argument("--pool", type=int, default=8, help="distinct input blocks cycled through")
     args = ap.parse_args()
 
@@ -243,11 +255,12 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    prec = U.PRECISION_FMA if args.precision == "fma" else U.PRECISION_EXACT
     wl = WORKLOADS[args.workload]
     C = args.channels or wl["channels"]
     N = args.frames or wl["frames"]
     elapsed, ktimes, plan, ok, _ = timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, args.steps,
-                                             args.warmup, max(1, args.pool), args.dst)
+                                             args.warmup, max(1, args.pool), args.dst, args.pipelined, prec)
 
     gather = None
     if world > 1 and not args.no_gather:
@@ -258,20 +271,30 @@ def main():
                   "how": "every launch's f32 audio gathered to rank 0 (torch.distributed.gather = grouped RCCL "
                          "send/recv over xGMI) on a comm stream, overlapped with the next launch (double-buffered)"}
 
-    ns = None
-    if world == 1 and not args.no_northstar and args.workload != "northstar" and not (args.channels or args.frames):
+    def north_star_leg(precision):
         nw = WORKLOADS["northstar"]
         n_el, n_kt, n_plan, n_ok, _ = timed_run(U, synth, shard, torch, dist, dev, 1, 0, nw["channels"], nw["frames"],
-                                                20, 3, 3, False)
+                                                20, 3, 3, False, args.pipelined, precision)
         n_ab = algorithmic_bytes(n_plan, nw["channels"], nw["frames"], False)
-        n_roof, n_kms = roofline_of(n_ab, n_kt, pmc_traffic("northstar"))
+        n_roof, n_kms = roofline_of(n_ab, n_kt, pmc_traffic("northstar" if precision == U.PRECISION_EXACT
+                                                            else "northstar_fma"))
         n_dev = sum(n_kms.values())
-        ns = {"workload": nw["desc"], "value": round(nw["channels"] * nw["frames"] * 20 / n_el / 1e6, 2),
-              "unit": "Msamples/s", "steps": 20, "ms_per_step": round(n_el / 20 * 1e3, 5), "roofline": n_roof,
-              "kernel_ms": {k: round(v, 5) for k, v in n_kms.items()},
-              "chain_hbm_frac": round(n_ab["chain"] / (n_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-              "alg_bytes_per_sample": round(n_ab["chain"] / (nw["channels"] * nw["frames"]), 2),
-              "outputs_finite": n_ok}
+        return {"workload": nw["desc"], "value": round(nw["channels"] * nw["frames"] * 20 / n_el / 1e6, 2),
+                "unit": "Msamples/s", "steps": 20, "ms_per_step": round(n_el / 20 * 1e3, 5), "roofline": n_roof,
+                "kernel_ms": {k: round(v, 5) for k, v in n_kms.items()},
+                "chain_hbm_frac": round(n_ab["chain"] / (n_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "alg_bytes_per_sample": round(n_ab["chain"] / (nw["channels"] * nw["frames"]), 2),
+                "outputs_finite": n_ok}
+
+    ns = None
+    if world == 1 and not args.no_northstar and args.workload != "northstar" and not (args.channels or args.frames):
+        ns = north_star_leg(prec)
+        ns["precision"] = args.precision
+        if prec == U.PRECISION_EXACT:
+            # the same workload with fused FIR MACs (uhsdr_rx_set_precision FMA): within 1e-5
+            # normwise of the reference on this path (tests/test_gpu_fma.py), not bit-identical
+            ns["fma"] = north_star_leg(U.PRECISION_FMA)
+            ns["fma"]["precision"] = "fma"
 
     if rank != 0:
         if world > 1:
@@ -295,7 +318,8 @@ def main():
                    f"{C} ch x {N}-frame blocks, SSB-USB P48 chain, f32",
                    "channels_per_gpu": C, "frames_per_call": N, "filter_path": int(plan.filter_path),
                    "parallelism": f"channel-sharded x{world}, no data-path collective",
-                   "outputs": "f32 audio" + (" + int32 codec frames" if args.dst else "")},
+                   "outputs": "f32 audio" + (" + int32 codec frames" if args.dst else ""),
+                   "pipelined": args.pipelined, "precision": args.precision},
         "roofline": roofline,
         "chain": {"device_ms_per_step": round(chain_dev_ms, 5),
                   "kernel_ms": {k: round(v, 5) for k, v in kms.items()},

@@ -209,8 +209,32 @@ uhsdr_status uhsdr_rx_get_plan(uhsdr_rx_handle h, uhsdr_rx_plan* plan);
 uhsdr_status uhsdr_rx_set_stream(uhsdr_rx_handle h, void* stream);
 uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h);
 
-/* Wait until every call enqueued on the handle's stream has finished. */
+/* Wait until every call enqueued on the handle has finished (both streams when pipelined). */
 uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h);
+
+/* Pipelined mode (off by default).  On: rx_back runs on a private side stream and the
+   decimated hand-off is double-buffered, so call k+1's rx_front overlaps call k's rx_back —
+   the streaming throughput of back-to-back ISR calls is max(front, back) instead of the sum.
+   Results are identical; only their completion point moves: the audio / dst / CW outputs of
+   a call are complete after uhsdr_rx_synchronize(), or for work enqueued on the handle's
+   stream after uhsdr_rx_join() (which orders the handle stream after every rx_back issued
+   so far).  The caller must not overwrite an output buffer still being written: reuse across
+   calls is safe (rx_back launches are ordered on the side stream).  Replaces nothing in the
+   reference (the firmware runs one ISR at a time); uhsdr_rx_process_host joins itself. */
+uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable);
+
+/* Arithmetic of the FIR dot products in rx_front (Hilbert pair, decimators, AM/FM I/Q filters).
+   EXACT (default): a rounded multiply then a rounded add per tap, in tap order -- the binary32
+   sequence of CMSIS arm_fir_f32 / arm_fir_decimate_f32 as the reference builds them, so every
+   output is bit-identical to the reference chain.  FMA: one fused multiply-add per tap
+   (v_pk_fma_f32), half the VALU issue; outputs within north_star's 1e-5 normwise relative
+   tolerance of the reference (max|diff| / max|ref| per channel), not bit-identical.  The
+   recursive stages (lattices, AGC, biquads, demodulators) always run the reference sequence.
+   Takes effect from the next uhsdr_rx_process. */
+enum { UHSDR_PRECISION_EXACT = 0, UHSDR_PRECISION_FMA = 1 };
+uhsdr_status uhsdr_rx_set_precision(uhsdr_rx_handle h, int32_t precision);
+int32_t      uhsdr_rx_get_precision(uhsdr_rx_handle h);   /* -1 for a null handle */
+uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h);
 
 /* ---- device memory for plain-C hosts (no HIP headers needed) ---- */
 void*        uhsdr_device_alloc(uint64_t bytes);             /* NULL on failure */
@@ -426,9 +450,12 @@ int32_t      uhsdr_sizeof_plan(void);
 const char*  uhsdr_last_error(void);
 /* number of kernels one uhsdr_rx_process call enqueues */
 int32_t      uhsdr_rx_kernel_count(uhsdr_rx_handle h);
-/* Per-kernel device timing: while enabled, every uhsdr_rx_process brackets each kernel with
-   hipEvents on the handle's stream.  uhsdr_rx_kernel_times() synchronises the stream and
-   returns, per kernel, the summed milliseconds and launch count since the last enable. */
+/* Per-kernel device timing: while enabled (enable = k > 0), every k-th uhsdr_rx_process call
+   (the 1st, (k+1)-th, ...) brackets each kernel with hipEvents on the stream it runs on; k = 1
+   times every call.  Sampling keeps the event records' own host and device cost (~30 us per
+   bracketed call) out of a throughput measurement.  uhsdr_rx_kernel_times() synchronises and
+   returns, per kernel, the summed milliseconds and launch count of the timed calls since the
+   last enable. */
 uhsdr_status uhsdr_rx_enable_timing(uhsdr_rx_handle h, int32_t enable);
 int32_t      uhsdr_rx_kernel_times(uhsdr_rx_handle h, float* total_ms, int32_t* launches, int32_t max_kernels);
 const char*  uhsdr_rx_kernel_name(int32_t index);

@@ -1,0 +1,121 @@
+"""UHSDR_PRECISION_FMA (uhsdr_rx_set_precision): rx_front's FIR dot products as fused
+multiply-adds.  Not bit-identical to the reference; the bar is north_star's "within 1e-5
+relative f32", read normwise per channel: max_n |gpu[c][n] - ref[c][n]| / max_n |ref[c][n]|
+<= 1e-5 for every channel c, against the CPU oracle (bit-exact to the reference build) on the
+same seeded inputs.  At full size (no oracle) the FMA output is held to the same bound against
+the EXACT GPU output, which the other tests pin bit-for-bit to the oracle.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import uhsdr_amd as U
+from uhsdr_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5          # north_star: outputs within 1e-5 relative (normwise per channel)
+# Paths whose chain amplifies the FIR rounding difference past north_star's bound (measured on
+# MI355X, 8 calls: P35 1.7e-5, P70 AM 1.8e-5 / SAM 1.3e-5, P4 CW 1.3e-5): FMA stays opt-in
+# there and is held to this looser bound; EXACT is the mode that meets the bar on every path.
+TOL_NARROW = 3e-5
+
+
+def normwise(got, ref):
+    num = np.abs(got.astype(np.float64) - ref.astype(np.float64)).max(axis=1)
+    den = np.abs(ref.astype(np.float64)).max(axis=1)
+    return num / np.maximum(den, 1e-30)
+
+
+def run(cfg, iq, N, precision):
+    import torch
+    C, n, _ = iq.shape
+    chain = U.RxChain(cfg, channels=C, frames=N)
+    chain.set_precision(precision)
+    assert chain.precision == precision
+    audio = torch.empty((C, N), dtype=torch.float32, device="cuda")
+    out = []
+    for k in range(n // N):
+        chain.process(torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda(), audio, None)
+        out.append(audio.cpu().numpy())
+    chain.close()
+    return np.concatenate(out, axis=1)
+
+
+CASES = [
+    ("p48_usb", dict(filter_path=48, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 256, 256, TOL),
+    ("p48_lsb_n64", dict(filter_path=48, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 128, 64, TOL),
+    ("p60_usb_24k", dict(filter_path=60, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 96, 256, TOL),
+    ("p35_usb", dict(filter_path=35, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 130, 256, TOL_NARROW),
+    ("p70_am", dict(filter_path=70, dmod_mode=U.DEMOD_AM), synth.am_iq, 128, 256, TOL_NARROW),
+    ("p70_sam", dict(filter_path=70, dmod_mode=U.DEMOD_SAM), synth.am_iq, 128, 256, TOL_NARROW),
+    ("p1_fm", dict(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=12), synth.fm_iq, 96, 256, TOL),
+    ("p4_cw", dict(filter_path=4, dmod_mode=U.DEMOD_CW), synth.cw_iq, 96, 256, TOL_NARROW),
+]
+
+
+@pytest.mark.parametrize("name,kw,gen,C,N,tol", CASES, ids=[c[0] for c in CASES])
+def test_fma_within_tolerance(cuda, back, name, kw, gen, C, N, tol):
+    cfg = U.default_config(**kw)
+    iq = gen(np.arange(C), 0, 8 * N)
+    got = run(cfg, iq, N, U.PRECISION_FMA)
+    ref, _ = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    err = normwise(got, ref)
+    assert np.isfinite(got).all()
+    assert err.max() <= tol, f"{name}: normwise error {err.max():.3g} (median {np.median(err):.3g}) > {tol}"
+    # FMA really changes the arithmetic (a silent EXACT path would pass the bound trivially);
+    # the FM discriminator's atan2 of a ratio absorbs the FIR's last-bit differences here
+    if kw["dmod_mode"] != U.DEMOD_FM:
+        assert not np.array_equal(got.view(np.uint32), ref.view(np.uint32)), f"{name}: FMA output is bit-exact"
+
+
+def test_fma_toggle_back_to_exact(cuda):
+    """Switching to FMA and back: the EXACT calls stay bit-identical to the oracle."""
+    import torch
+    cfg = U.default_config()
+    C, N = 64, 256
+    iq = synth.ssb_iq(np.arange(C), 0, 2 * N)
+    ref, _ = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    chain = U.RxChain(cfg, channels=C, frames=N)
+    chain.set_precision(U.PRECISION_FMA)
+    chain.set_precision(U.PRECISION_EXACT)
+    audio = torch.empty((C, N), dtype=torch.float32, device="cuda")
+    out = []
+    for k in range(2):
+        chain.process(torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda(), audio, None)
+        out.append(audio.cpu().numpy())
+    chain.close()
+    got = np.concatenate(out, axis=1)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_fma_rejects_unknown_precision(cuda):
+    chain = U.RxChain(U.default_config(), channels=64, frames=64)
+    with pytest.raises(Exception):
+        chain.set_precision(7)
+    assert chain.precision == U.PRECISION_EXACT
+    chain.close()
+
+
+def test_fma_full_size_against_exact(cuda):
+    """North-star shape (1 M channels x 64 frames, 4 calls): FMA vs the EXACT GPU chain."""
+    import torch
+    cfg = U.default_config()
+    C, N, calls = 1 << 20, 64, 4
+    dev = torch.device("cuda", 0)
+    outs = {}
+    for prec in (U.PRECISION_EXACT, U.PRECISION_FMA):
+        chain = U.RxChain(cfg, channels=C, frames=N)
+        chain.set_precision(prec)
+        audio = torch.empty((C, N), dtype=torch.float32, device=dev)
+        acc = []
+        for k in range(calls):
+            chain.process(synth.ssb_iq_torch(0, C, k * N, N, dev), audio, None)
+            acc.append(audio.clone())
+        chain.close()
+        outs[prec] = torch.cat(acc, dim=1)
+    e, f = outs[U.PRECISION_EXACT].double(), outs[U.PRECISION_FMA].double()
+    assert torch.isfinite(f).all()
+    err = (f - e).abs().amax(dim=1) / e.abs().amax(dim=1).clamp_min(1e-30)
+    worst = float(err.max())
+    assert worst <= TOL, f"full size: normwise error {worst:.3g} > {TOL}"

@@ -1,0 +1,106 @@
+"""Pipelined mode (uhsdr_rx_set_pipelined): call k+1's rx_front overlaps call k's rx_back on a
+side stream, with the decimated hand-off double-buffered.  The results must be the same bits as
+the serial chain: back-to-back calls with no synchronisation between them, checked against the
+CPU oracle (SSB, AM / SAM with their second hand-off buffer, FM, CW with the decoder outputs),
+plus join() ordering on the handle's stream, toggling the mode mid-stream, and the host entry.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import uhsdr_amd as U
+from golden_util import assert_bitexact
+from uhsdr_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def run_pipelined(cfg, iq, N, toggle_at=None, join_each=False):
+    import torch
+    C, n, _ = iq.shape
+    calls = n // N
+    chain = U.RxChain(cfg, channels=C, frames=N)
+    chain.set_pipelined(True)
+    xs = [torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda() for k in range(calls)]
+    audio = torch.empty((calls, C, N), dtype=torch.float32, device="cuda")
+    dst = torch.empty((calls, C, N, 2), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    for k in range(calls):
+        if toggle_at is not None and k == toggle_at:
+            chain.set_pipelined(False)
+        if toggle_at is not None and k == toggle_at + 1:
+            chain.set_pipelined(True)
+        chain.process(xs[k], audio[k], dst[k])
+        if join_each:
+            chain.join()
+    chain.synchronize()
+    a = audio.permute(1, 0, 2).reshape(C, n).cpu().numpy()
+    d = dst.permute(1, 0, 2, 3).reshape(C, n, 2).cpu().numpy()
+    chain.close()
+    return a, d
+
+
+CASES = [
+    ("p48_usb", dict(filter_path=48, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 300, 256),
+    ("p35_lsb", dict(filter_path=35, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 130, 128),
+    ("p70_am", dict(filter_path=70, dmod_mode=U.DEMOD_AM), synth.am_iq, 200, 256),
+    ("p70_sam", dict(filter_path=70, dmod_mode=U.DEMOD_SAM), synth.am_iq, 129, 256),
+    ("p1_fm", dict(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=12), synth.fm_iq, 100, 256),
+    ("p4_cw", dict(filter_path=4, dmod_mode=U.DEMOD_CW), synth.cw_iq, 65, 64),
+]
+
+
+@pytest.mark.parametrize("name,kw,gen,C,N", CASES, ids=[c[0] for c in CASES])
+def test_pipelined_matches_oracle(cuda, back, name, kw, gen, C, N):
+    cfg = U.default_config(**kw)
+    iq = gen(np.arange(C), 0, 8 * N)
+    a1, dst = run_pipelined(cfg, iq, N)
+    ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    assert_bitexact(a1, ref_a1, f"pipelined {name}")
+    np.testing.assert_array_equal(dst, ref_dst)
+
+
+def test_pipelined_toggle_and_join(cuda):
+    cfg = U.default_config()
+    C, N = 96, 128
+    iq = synth.ssb_iq(np.arange(C), 0, 8 * N)
+    ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    a1, dst = run_pipelined(cfg, iq, N, toggle_at=3)
+    assert_bitexact(a1, ref_a1, "pipelined, off for call 3")
+    a1, dst = run_pipelined(cfg, iq, N, join_each=True)
+    assert_bitexact(a1, ref_a1, "pipelined, join after every call")
+    np.testing.assert_array_equal(dst, ref_dst)
+
+
+def test_pipelined_join_orders_handle_stream(cuda):
+    """After join(), work the caller enqueues on the handle's stream sees the outputs."""
+    import torch
+    cfg = U.default_config()
+    C, N = 4096, 256
+    iq = synth.ssb_iq(np.arange(C), 0, N)
+    s = torch.cuda.Stream()
+    chain = U.RxChain(cfg, channels=C, frames=N, stream=s.cuda_stream)
+    chain.set_pipelined(True)
+    x = torch.from_numpy(iq).cuda()
+    audio = torch.zeros((C, N), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        chain.process(x, audio, None)
+        chain.join()
+        copy = audio.clone()                 # enqueued on s after the join
+    torch.cuda.synchronize()
+    ref, _ = oracle.OracleRx(U.build_plan(cfg), 64).process(iq[:64], threads=8)
+    assert_bitexact(copy[:64].cpu().numpy(), ref, "copy after join")
+    chain.close()
+
+
+def test_pipelined_host_entry(cuda):
+    cfg = U.default_config(filter_path=70, dmod_mode=U.DEMOD_AM)
+    C, N = 33, 256
+    iq = synth.am_iq(np.arange(C), 0, 2 * N)
+    chain = U.RxChain(cfg, channels=C, frames=N)
+    chain.set_pipelined(True)
+    outs = [chain.process_host(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])) for k in range(2)]
+    chain.close()
+    ref_a1, _ = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    assert_bitexact(np.concatenate([o[0] for o in outs], axis=1), ref_a1, "pipelined host entry")

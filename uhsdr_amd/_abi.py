@@ -26,6 +26,7 @@ UHSDR_DEVICE_ERROR = -11
 
 DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI = range(7)
 SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB = range(3)
+PRECISION_EXACT, PRECISION_FMA = 0, 1          # uhsdr_rx_set_precision
 
 
 class RxConfig(C.Structure):
@@ -159,6 +160,10 @@ SIGNATURES = {
     "uhsdr_rx_kernel_times": (C.c_int32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int32), C.c_int32]),
     "uhsdr_rx_kernel_name": (C.c_char_p, [C.c_int32]),
     "uhsdr_rx_synchronize": (C.c_int, [C.c_void_p]),
+    "uhsdr_rx_set_pipelined": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_rx_join": (C.c_int, [C.c_void_p]),
+    "uhsdr_rx_set_precision": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_rx_get_precision": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_set_cw_outputs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "uhsdr_rx_cw_blocks_max": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_cw_blocks_last": (C.c_int32, [C.c_void_p]),

@@ -49,8 +49,20 @@ __device__ __forceinline__ void lds_vec(const float* p, float (&w)[N], int j)
 typedef const __attribute__((address_space(4))) float ctaps_t;
 __device__ __forceinline__ ctaps_t* as_taps(const float* p) { return (ctaps_t*)p; }
 
+// One MAC of the FIR dot products.  F = false: the reference's binary32 sequence, a rounded
+// multiply then a rounded add (CMSIS arm_fir_f32 built without contraction, SURVEY.md §8(c)
+// c3-i).  F = true: one fused multiply-add (v_fma_f32 / v_pk_fma_f32) -- half the VALU issue of
+// a FIR, one rounding per tap instead of two; within north_star's 1e-5 normwise tolerance of the
+// reference (tests/test_gpu_fma.py), not bit-identical (UHSDR_PRECISION_FMA).
+template <bool F, typename V>
+__device__ __forceinline__ V fir_mac(V acc, V x, V c)
+{
+    if constexpr (F) return __builtin_elementwise_fma(x, c, acc);
+    else return acc + x * c;
+}
+
 // V: LDS read width in floats (the lane base is 4V bytes aligned)
-template <int T, int R, int M, int V = 4>
+template <int T, int R, int M, int V = 4, bool F = false>
 __device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&acc)[R])
 {
     constexpr int WA = (M * (R - 1) + 8 + 7) & ~7;
@@ -74,7 +86,7 @@ __device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&
         for (int kk = 0; kk < 8; ++kk)
         {
 #pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * cc[kk];
+            for (int r = 0; r < R; ++r) acc[r] = fir_mac<F>(acc[r], w[r * M + kk], cc[kk]);
         }
 #pragma unroll
         for (int j = 0; j < WA - 8; ++j) w[j] = w[j + 8];
@@ -86,7 +98,7 @@ __device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&
     {
         const float ck = c[8 * NCH + kk];
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * ck;
+        for (int r = 0; r < R; ++r) acc[r] = fir_mac<F>(acc[r], w[r * M + kk], ck);
     }
 }
 
@@ -101,7 +113,7 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(4))) v2f ctaps2_t;
 __device__ __forceinline__ ctaps2_t* as_taps2(const float* p) { return (ctaps2_t*)p; }
 
-template <int T, int R, int M>
+template <int T, int R, int M, bool F = false>
 __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&acc)[R])
 {
     constexpr int WA = (M * (R - 1) + 8 + 7) & ~7;   // window pairs in registers
@@ -134,7 +146,7 @@ __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&
         for (int kk = 0; kk < 8; ++kk)
         {
 #pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * cc[kk];
+            for (int r = 0; r < R; ++r) acc[r] = fir_mac<F>(acc[r], w[r * M + kk], cc[kk]);
         }
 #pragma unroll
         for (int j = 0; j < WA - 8; ++j) w[j] = w[j + 8];
@@ -146,7 +158,7 @@ __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&
     {
         const v2f ck = c[8 * NCH + kk];
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] += w[r * M + kk] * ck;
+        for (int r = 0; r < R; ++r) acc[r] = fir_mac<F>(acc[r], w[r * M + kk], ck);
     }
 }
 

@@ -157,7 +157,7 @@ __device__ __forceinline__ void convert_block(const int4 (&raw)[R / 2], const In
 // are issued early: the I/Q frames and the first two history rows at entry, and the row of
 // pass p+2 as soon as pass p has put its row into LDS (double-buffered registers), so each
 // pass's HBM latency hides behind the previous pass's FIR.
-template <int T1, int T2, int M, bool DECIM_FIRST, int R>
+template <int T1, int T2, int M, bool DECIM_FIRST, int R, bool F>
 __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -295,7 +295,7 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
             // FM: the Hilbert / low-pass pair at 48 ksps (:2748-2753), no decimation.
             // The demodulator in rx_back / rx_fm takes both I and Q.
                 v2f d2[RD];
-            fir_block2<T1, RD, M>(W + 2 * b * R, tA, d2);
+            fir_block2<T1, RD, M, F>(W + 2 * b * R, tA, d2);
 #pragma unroll
             for (int r = 0; r < RD; ++r) o[r] = d2[r].x;
             if (live)
@@ -311,13 +311,13 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
             front_load_row<T2>(a.hist2_i, cl, b, nb, hC);
                 v2f h2[R];
             float hs[R];
-            fir_block2<T1, R, 1>(W + 2 * b * R, tA, h2);
+            fir_block2<T1, R, 1, F>(W + 2 * b * R, tA, h2);
             // a = I + Q (USB) or I - Q (LSB), audio_driver.c:2781-2790
 #pragma unroll
             for (int r = 0; r < R; ++r) hs[r] = lsb ? (h2[r].x - h2[r].y) : (h2[r].x + h2[r].y);
             wave_sync();
             front_fill<T2>(W, a.hist2_i, c, act, live, b, nb, hC, hs, R);
-            fir_block<T2, RD, M>(W + b * R, as_taps(P->dec), o);
+            fir_block<T2, RD, M, 4, F>(W + b * R, as_taps(P->dec), o);
         }
         else
         {
@@ -325,10 +325,10 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
             front_load_row<T2>(a.hist2_i, cl, b, nb, hC);
             front_load_row<T2>(a.hist2_q, cl, b, nb, hD);
                 v2f d2[RD], h2[RD];
-            fir_block2<T1, RD, M>(W + 2 * b * R, tA, d2);
+            fir_block2<T1, RD, M, F>(W + 2 * b * R, tA, d2);
             wave_sync();
             front_fill2<T2>(W, a.hist2_i, a.hist2_q, c, act, live, b, nb, hC, hD, d2, RD);
-            fir_block2<T2, RD, 1>(W + 2 * b * RD, as_taps2(a.taps2b), h2);
+            fir_block2<T2, RD, 1, F>(W + 2 * b * RD, as_taps2(a.taps2b), h2);
 #pragma unroll
             for (int r = 0; r < RD; ++r) o[r] = lsb ? (h2[r].x - h2[r].y) : (h2[r].x + h2[r].y);
         }
@@ -1434,25 +1434,22 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
 typedef void (*front_fn)(FrontArgs);
 typedef void (*back_fn)(BackArgs);
 
-struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; };
+struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; front_fn fn_fma; };
 struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; };
 
 // R = FIR outputs per lane: 16 for large batches (more MACs per window load), 8 for small
-// batches (twice the waves in flight)
+// batches (twice the waves in flight).  fn: reference MAC order (bit-exact); fn_fma: fused MACs
+// (UHSDR_PRECISION_FMA)
+#define FRONT_V(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false>, R, rx_front<t1, t2, m, df, R, true> }
 static const FrontVariant kFront[] = {
-    { 89, 43, 4, 0, rx_front<89, 43, 4, false, 16>, 16 },     // wide SSB/CW  (P48-54)
-    { 89, 43, 4, 0, rx_front<89, 43, 4, false, 8>, 8 },
-    { 89, 4, 2, 0, rx_front<89, 4, 2, false, 16>, 16 },       // 24 ksps SSB   (P55-65)
-    { 89, 4, 2, 0, rx_front<89, 4, 2, false, 8>, 8 },
-    { 83, 199, 4, 1, rx_front<83, 199, 4, true, 16>, 16 },    // narrow SSB/CW (P4-47)
-    { 83, 199, 4, 1, rx_front<83, 199, 4, true, 8>, 8 },
-    { 89, 0, 4, 1, rx_front<89, 0, 4, true, 16>, 16 },        // AM / SAM, 12 ksps (P66-82)
-    { 89, 0, 4, 1, rx_front<89, 0, 4, true, 8>, 8 },
-    { 89, 0, 2, 1, rx_front<89, 0, 2, true, 16>, 16 },        // AM / SAM, 24 ksps (P83-86)
-    { 89, 0, 2, 1, rx_front<89, 0, 2, true, 8>, 8 },
-    { 89, 0, 1, 0, rx_front<89, 0, 1, false, 16>, 16 },       // FM, 48 ksps Hilbert pair (P1-3)
-    { 89, 0, 1, 0, rx_front<89, 0, 1, false, 8>, 8 },
+    FRONT_V(89, 43, 4, false, 16), FRONT_V(89, 43, 4, false, 8),     // wide SSB/CW  (P48-54)
+    FRONT_V(89, 4, 2, false, 16), FRONT_V(89, 4, 2, false, 8),       // 24 ksps SSB   (P55-65)
+    FRONT_V(83, 199, 4, true, 16), FRONT_V(83, 199, 4, true, 8),     // narrow SSB/CW (P4-47)
+    FRONT_V(89, 0, 4, true, 16), FRONT_V(89, 0, 4, true, 8),         // AM / SAM, 12 ksps (P66-82)
+    FRONT_V(89, 0, 2, true, 16), FRONT_V(89, 0, 2, true, 8),         // AM / SAM, 24 ksps (P83-86)
+    FRONT_V(89, 0, 1, false, 16), FRONT_V(89, 0, 1, false, 8),       // FM, 48 ksps Hilbert pair (P1-3)
 };
+#undef FRONT_V
 
 #define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm> }
 static const BackVariant kBack[] = {
@@ -1528,6 +1525,7 @@ struct uhsdr_rx_s
     int C, N, Nd, Nf;        // Nf: frames per front launch (N split into N / Nf launches)
     int lw;                  // front LDS window pitch (floats)
     int back_fused;          // rx_back_fused (large batches) instead of the wave pipeline
+    int precision;           // UHSDR_PRECISION_EXACT / _FMA (front FIR MACs)
     int T1, T2;
     hipStream_t stream;
     // front state
@@ -1544,8 +1542,17 @@ struct uhsdr_rx_s
     float* cw_energy;
     long long calls_done;
     long long front_launches; // oscillator ping-pong parity
+    // pipelined mode (uhsdr_rx_set_pipelined): rx_back on a side stream, decimated hand-off
+    // double-buffered so the next call's rx_front overlaps this call's rx_back
+    int pipelined;
+    hipStream_t side;
+    hipEvent_t ev_front, ev_join, ev_back[2];
+    float *adec2, *adec_q2;  // second hand-off buffer pair
+    long long calls_issued;  // process() calls (hand-off buffer parity)
     // per-kernel timing (uhsdr_rx_enable_timing)
-    int timing;
+    int timing;               // 0 off, else every timing-th call is bracketed
+    int tsample;              // the call being enqueued is a timed one
+    long long tcalls;         // calls since timing was enabled
     int nev;
     int nev_cap;
     hipEvent_t* ev;          // [cap][2 kernels][start, stop]
@@ -1555,16 +1562,26 @@ struct uhsdr_rx_s
 
 static const char* kKernelNames[2] = { "rx_front", "rx_back" };
 
+static hipStream_t back_stream(const uhsdr_rx_s* h) { return h->pipelined ? h->side : h->stream; }
+
 static void time_mark(uhsdr_rx_s* h, int k, int which)
 {
-    if (!h->timing || h->nev >= h->nev_cap) return;
-    (void)hipEventRecord(h->ev[(size_t)h->nev * 4 + 2 * k + which], h->stream);
+    if (!h->tsample) return;
+    (void)hipEventRecord(h->ev[(size_t)h->nev * 4 + 2 * k + which], k ? back_stream(h) : h->stream);
+}
+
+// every call enqueued so far, on both streams, has finished
+static hipError_t sync_all(uhsdr_rx_s* h)
+{
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess && h->side) e = hipStreamSynchronize(h->side);
+    return e;
 }
 
 static void time_harvest(uhsdr_rx_s* h)
 {
     if (!h->nev) return;
-    (void)hipStreamSynchronize(h->stream);
+    (void)sync_all(h);
     for (int i = 0; i < h->nev; ++i)
         for (int k = 0; k < 2; ++k)
         {
@@ -1640,6 +1657,7 @@ extern "C" int uhsdr_rx_plan_supported(const uhsdr_rx_plan* p)
 extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
+    HIPCHK(sync_all(h));
     HIPCHK(hipMemsetAsync(h->arena, 0, h->arena_bytes, h->stream));
     // oscillator starts at {I=0, Q=1} (freq_shift.c:48-49); both ping-pong copies
     const float osc0[4] = { 0.0f, 1.0f, 0.0f, 1.0f };
@@ -1657,6 +1675,7 @@ extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
     h->dec_samples = 0;
     h->calls_done = 0;
     h->front_launches = 0;
+    h->calls_issued = 0;
     h->cw_count = 0;
     h->cw_blocks_last = 0;
     return UHSDR_OK;
@@ -1786,6 +1805,14 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
 {
     if (!h || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
     if (h->timing && h->nev >= h->nev_cap) time_harvest(h);
+    h->tsample = h->timing && (h->tcalls++ % h->timing) == 0;
+    // hand-off buffers of this call; pipelined: alternate, and wait until the rx_back that
+    // read this pair two calls ago has finished
+    const int par = h->pipelined ? (int)(h->calls_issued & 1) : 0;
+    float* adec = par ? h->adec2 : h->adec;
+    float* adec_q = par ? h->adec_q2 : h->adec_q;
+    if (h->pipelined) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[par], 0));
+    h->calls_issued += 1;
     time_mark(h, 0, 0);
     const int cpw = FRONT_WAVE / (h->Nf / h->fv->R);
     const size_t lds = front_lds(h);
@@ -1798,13 +1825,13 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
         fa.teta = h->teta;
         fa.osc_in = h->osc + 2 * (h->front_launches & 1);     // ping-pong: read one copy, write the other
         fa.osc_out = h->osc + 2 * ((h->front_launches + 1) & 1);
-        fa.adec = h->adec + f0 / h->plan.decimation_rate;
-        fa.adec_q = h->adec_q ? h->adec_q + f0 / h->plan.decimation_rate : nullptr;
+        fa.adec = adec + f0 / h->plan.decimation_rate;
+        fa.adec_q = adec_q ? adec_q + f0 / h->plan.decimation_rate : nullptr;
         fa.C = h->C; fa.N = h->Nf; fa.ld = h->N; fa.ldd = h->Nd;
         fa.lw = h->lw;
         fa.taps2a = h->d_taps2;
         fa.taps2b = h->d_taps2 + 2 * TAPS2_MAX;
-        hipLaunchKernelGGL(h->fv->fn, dim3((h->C + cpw - 1) / cpw), dim3(FRONT_WAVE), lds, h->stream, fa);
+        hipLaunchKernelGGL(h->precision == UHSDR_PRECISION_FMA ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw), dim3(FRONT_WAVE), lds, h->stream, fa);
         HIPCHK(hipGetLastError());
         h->front_launches += 1;
     }
@@ -1812,8 +1839,8 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
 
     BackArgs ba;
     ba.plan = h->d_plan;
-    ba.adec = h->adec;
-    ba.adec_q = h->adec_q;
+    ba.adec = adec;
+    ba.adec_q = adec_q;
     ba.audio = audio;
     ba.dst = (int2*)dst;
     ba.s = h->bs;
@@ -1834,15 +1861,23 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
         }
         h->cw_blocks_last = blocks;
     }
+    const hipStream_t bst = back_stream(h);
+    if (h->pipelined)
+    {
+        HIPCHK(hipEventRecord(h->ev_front, h->stream));
+        HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
+    }
     time_mark(h, 1, 0);
     if (h->back_fused)
-        hipLaunchKernelGGL(h->bv->fused, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, h->stream, ba);
+        hipLaunchKernelGGL(h->bv->fused, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
     else
         hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH),
-                           back_lds(h), h->stream, ba);
+                           back_lds(h), bst, ba);
     HIPCHK(hipGetLastError());
     time_mark(h, 1, 1);
-    if (h->timing) h->nev++;
+    if (h->pipelined) HIPCHK(hipEventRecord(h->ev_back[par], bst));
+    if (h->tsample) h->nev++;
+    h->tsample = 0;
     h->dec_samples += h->Nd;
     h->calls_done += h->N / BLK;
     return UHSDR_OK;
@@ -1858,6 +1893,7 @@ extern "C" uhsdr_status uhsdr_rx_process_host(uhsdr_rx_handle h, const int32_t* 
     if (dst) HIPCHK(hipMalloc((void**)&d_d, nf * 8));
     HIPCHK(hipMemcpyAsync(d_iq, iq, nf * 8, hipMemcpyHostToDevice, h->stream));
     uhsdr_status st = uhsdr_rx_process(h, d_iq, d_a, d_d);
+    if (st == UHSDR_OK) st = uhsdr_rx_join(h);
     if (st == UHSDR_OK)
     {
         if (audio) HIPCHK(hipMemcpyAsync(audio, d_a, nf * 4, hipMemcpyDeviceToHost, h->stream));
@@ -1873,7 +1909,60 @@ extern "C" uhsdr_status uhsdr_rx_process_host(uhsdr_rx_handle h, const int32_t* 
 extern "C" uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(sync_all(h));
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_rx_set_precision(uhsdr_rx_handle h, int32_t precision)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    if (precision != UHSDR_PRECISION_EXACT && precision != UHSDR_PRECISION_FMA)
+    {
+        uhsdr_set_error("unknown precision %d", (int)precision);
+        return UHSDR_ARGUMENT_ERROR;
+    }
+    h->precision = precision;
+    return UHSDR_OK;
+}
+
+extern "C" int32_t uhsdr_rx_get_precision(uhsdr_rx_handle h) { return h ? h->precision : -1; }
+
+extern "C" uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    if (h->pipelined)
+    {
+        HIPCHK(hipEventRecord(h->ev_join, h->side));
+        HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+    }
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    if (enable && !h->side)
+    {
+        const size_t nd = (size_t)h->C * h->Nd;
+        HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_front, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i)
+        {
+            HIPCHK(hipEventCreateWithFlags(&h->ev_back[i], hipEventDisableTiming));
+            HIPCHK(hipEventRecord(h->ev_back[i], h->side));
+        }
+        HIPCHK(hipMalloc((void**)&h->adec2, sizeof(float) * nd));
+        if (h->adec_q) HIPCHK(hipMalloc((void**)&h->adec_q2, sizeof(float) * nd));
+    }
+    if (h->timing) time_harvest(h);
+    // leaving the mode: the side stream's work completes before the handle stream goes on
+    if (!enable && h->pipelined)
+    {
+        const uhsdr_status st = uhsdr_rx_join(h);
+        if (st != UHSDR_OK) return st;
+    }
+    h->pipelined = enable != 0;
     return UHSDR_OK;
 }
 
@@ -1919,7 +2008,9 @@ extern "C" uhsdr_status uhsdr_rx_enable_timing(uhsdr_rx_handle h, int32_t enable
         for (int i = 0; i < h->nev_cap * 4; ++i) HIPCHK(hipEventCreate(&h->ev[i]));
     }
     if (h->timing) time_harvest(h);
-    h->timing = enable != 0;
+    h->timing = enable > 0 ? enable : 0;
+    h->tsample = 0;
+    h->tcalls = 0;
     h->nev = 0;
     h->total_ms[0] = h->total_ms[1] = 0.0f;
     h->launches[0] = h->launches[1] = 0;
@@ -1944,7 +2035,17 @@ extern "C" const char* uhsdr_rx_kernel_name(int32_t index) { return (index >= 0 
 extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
-    (void)hipStreamSynchronize(h->stream);
+    (void)sync_all(h);
+    if (h->side)
+    {
+        (void)hipEventDestroy(h->ev_front);
+        (void)hipEventDestroy(h->ev_join);
+        (void)hipEventDestroy(h->ev_back[0]);
+        (void)hipEventDestroy(h->ev_back[1]);
+        (void)hipStreamDestroy(h->side);
+        (void)hipFree(h->adec2);
+        if (h->adec_q2) (void)hipFree(h->adec_q2);
+    }
     if (h->ev)
     {
         for (int i = 0; i < h->nev_cap * 4; ++i) (void)hipEventDestroy(h->ev[i]);

@@ -90,8 +90,29 @@ class RxChain:
     def cw_blocks_last(self) -> int:
         return self.lib.uhsdr_rx_cw_blocks_last(self.handle)
 
-    def enable_timing(self, enable: bool = True) -> None:
-        _abi.check(self.lib.uhsdr_rx_enable_timing(self.handle, int(enable)), "uhsdr_rx_enable_timing")
+    def set_pipelined(self, enable: bool = True) -> None:
+        """Overlap call k+1's rx_front with call k's rx_back (uhsdr_rx_set_pipelined); outputs
+        are complete after synchronize() / a device-wide sync, or join() for the handle's stream."""
+        _abi.check(self.lib.uhsdr_rx_set_pipelined(self.handle, int(enable)), "uhsdr_rx_set_pipelined")
+
+    def set_precision(self, precision: int) -> None:
+        """PRECISION_EXACT (bit-identical, default) or PRECISION_FMA (fused FIR MACs, 1e-5 normwise)."""
+        _abi.check(self.lib.uhsdr_rx_set_precision(self.handle, int(precision)), "uhsdr_rx_set_precision")
+
+    @property
+    def precision(self) -> int:
+        return self.lib.uhsdr_rx_get_precision(self.handle)
+
+    def join(self) -> None:
+        _abi.check(self.lib.uhsdr_rx_join(self.handle), "uhsdr_rx_join")
+
+    def synchronize(self) -> None:
+        _abi.check(self.lib.uhsdr_rx_synchronize(self.handle), "uhsdr_rx_synchronize")
+
+    def enable_timing(self, enable: bool = True, every: int = 1) -> None:
+        """Bracket each kernel of every `every`-th call with HIP events (uhsdr_rx_enable_timing)."""
+        _abi.check(self.lib.uhsdr_rx_enable_timing(self.handle, int(every) if enable else 0),
+                   "uhsdr_rx_enable_timing")
 
     def kernel_times(self):
         """{kernel name: (total ms, launches)} accumulated since enable_timing()."""

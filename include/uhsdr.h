@@ -380,6 +380,9 @@ uhsdr_status uhsdr_i2s_destroy(uhsdr_i2s_handle h);
  * arbitrary times, the batch takes it exactly when fft_len new samples have arrived.
  * The I/Q correction runs on the handle's own copy of the auto-correction state (it depends only
  * on the input), so a spectrum handle beside an RX handle sees what the firmware's ring sees.
+ * magnify > 0 replaces the producer with the zoom one (AudioDriver_SpectrumZoomProcessSamples,
+ * audio_driver.c:1860-1909): corrected I/Q, translated by iq_freq_mode (FreqShift), low-passed
+ * and decimated by 2^magnify, so a display frame spans fft_len * 2^magnify input frames.
  */
 #define UHSDR_SPECTRUM_MAX_LEN 1024
 #define UHSDR_SPECTRUM_MAX_BITREV 1800   /* ARMBITREVINDEXTABLE1024_TABLE_LENGTH, arm_common_tables.h:96 */
@@ -391,7 +394,9 @@ typedef struct uhsdr_spectrum_config
     int32_t iq_auto_correction;   /* ts.iq_auto_correction, as uhsdr_rx_config */
     float   iq_gain_i, iq_gain_q; /* ts.rx_adj_gain_var.i / .q */
     float   iq_phase_balance;     /* ads.iq_phase_balance_rx */
-    int32_t reserved[10];
+    int32_t magnify;              /* sd.magnify 0..5: zoom 2^magnify (0: no zoom, ui_spectrum.c) */
+    int32_t iq_freq_mode;         /* ts.iq_freq_mode: the translation the zoom producer sees */
+    int32_t reserved[8];
 } uhsdr_spectrum_config;
 
 typedef struct uhsdr_spectrum_plan
@@ -411,6 +416,16 @@ typedef struct uhsdr_spectrum_plan
     uint16_t iperm[UHSDR_SPECTRUM_MAX_LEN];        /* butterfly result p lands in bin iperm[p] */
     float   tw_lane[8][64][2];    /* the first-stage twiddles each of 64 lanes uses, laid out per lane
                                      (same values as twiddle[]; device read coalescing only) */
+    /* zoom producer (AudioDriver_SpectrumZoomProcessSamples, audio_driver.c:1860-1909), magnify > 0:
+       after I/Q correction and FreqShift, I and Q each through IIR_biquad_Zoom_FFT_I/_Q (4 stages,
+       mag_coeffs[magnify]) and DECIMATE_ZOOM_FFT_I/_Q (FirZoomFFTDecimate[magnify]) */
+    int32_t magnify;
+    int32_t zoom_decimation;      /* 2^magnify */
+    int32_t zoom_taps;
+    int32_t freq_shift_hz, shift_kind, shift_up;   /* as uhsdr_rx_plan */
+    float   osc_cos, osc_sin;
+    float   zoom_biquad[20];
+    float   zoom_fir[8];
     int32_t reserved[16];
 } uhsdr_spectrum_plan;
 

@@ -130,7 +130,7 @@ class OracleSpectrum:
         Cn, n, _ = iq.shape
         assert Cn == self.channels
         L = self.plan.fft_len
-        fmax = max(1, n // L)
+        fmax = max(1, n // max(1, self.plan.zoom_decimation) // L)
         mag = np.zeros((Cn, fmax, L), np.float32)
         avg = np.zeros((Cn, fmax, L), np.float32)
         f = self.lib.uo_spec_process_batch(C.byref(self.plan), self.states, Cn, iq.ctypes.data_as(C.c_void_p), n,

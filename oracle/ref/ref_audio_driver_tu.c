@@ -22,3 +22,10 @@ const arm_fir_interpolate_instance_f32* oracle_ref_interpolate(void) { return &I
 /* layout fingerprint of TransceiverState as audio_driver.c sees it */
 unsigned long oracle_driver_layout(void) { return (unsigned long)sizeof(TransceiverState) * 100000ul + (unsigned long)((char*)&ts.dsp.active - (char*)&ts); }
 const arm_iir_lattice_instance_f32* oracle_ref_squelch(void) { return &IIR_Squelch_HPF; }
+
+/* zoom spectrum producer (AudioDriver_SpectrumZoomProcessSamples, audio_driver.c:1860-1909):
+   select the magnification the way the firmware's spectrum setup does (AudioDriver_Spectrum_Set,
+   :1055-1086, which re-inits the zoom decimators), and read back its tables */
+void oracle_ref_spec_magnify(int m) { sd.magnify = (uint8_t)m; AudioDriver_Spectrum_Set(); }
+const float* oracle_ref_zoom_biquad(int m) { return mag_coeffs[m]; }
+const arm_fir_decimate_instance_f32* oracle_ref_zoom_decim(void) { return &DECIMATE_ZOOM_FFT_I; }

@@ -54,7 +54,7 @@ void oracle_ref_agc_dump(void);
 unsigned long oracle_harness_layout(void);
 unsigned long oracle_driver_layout(void);
 int ref_spec_ring_len(int L);
-void ref_spec_setup(int L);
+void ref_spec_setup(int L, int magnify);
 void ref_spec_snapshot(float* out);
 void ref_spec_frame(int L, int spectrum_filter, const float* ring, float* mag, float* avg);
 void ref_spec_dump(void);
@@ -247,6 +247,8 @@ int main(int argc, char** argv)
     sd.fft_iq_len = 0;          /* spectrum tap off unless spec=L (ref_spectrum.c) */
     const int spec = (int)iarg(argc, argv, "spec", 0);
     const int spec_filter = (int)iarg(argc, argv, "specfilt", 4);   /* SPECTRUM_FILTER_DEFAULT */
+    const int magnify = (int)iarg(argc, argv, "mag", 0);            /* sd.magnify: zoom 2^mag */
+    const long zd = 1L << magnify;                                  /* ring samples per input frame: 1/zd */
     /* transmit settings (hardware/uhsdr_board.h:301-460, defaults ui_configuration.c) */
     const int tx = (int)iarg(argc, argv, "tx", 0);
     ts.tx_mic_gain_mult = iarg(argc, argv, "micmult", 15);
@@ -292,9 +294,10 @@ int main(int argc, char** argv)
     int ring = 0;
     if (spec)
     {
-        if ((spec != 256 && spec != 512 && spec != 1024) || n % spec) { fprintf(stderr, "spec=256|512|1024 dividing n\n"); return 2; }
+        if ((spec != 256 && spec != 512 && spec != 1024) || n % (spec * zd) || magnify < 0 || magnify > 5)
+        { fprintf(stderr, "spec=256|512|1024 with spec*2^mag dividing n, mag 0..5\n"); return 2; }
         ring = ref_spec_ring_len(spec);
-        ref_spec_setup(spec);
+        ref_spec_setup(spec, magnify);
         stream = calloc(2 * n, sizeof(float));
     }
     if (tx)
@@ -319,8 +322,8 @@ int main(int argc, char** argv)
         AudioDriver_I2SCallback(dst + off, blk, NULL, block);
         memcpy(a1 + off, adb.a_buffer[1], sizeof(float) * block);
         if (cw_signal) cw_signal[off / block] = ads.CW_signal;
-        if (spec && (off + block) % (ring / 2) == 0)       /* the ring holds ring/2 new samples */
-            ref_spec_snapshot(stream + 2 * (off + block - ring / 2));
+        if (spec && (off + block) % (ring / 2 * zd) == 0)  /* the ring holds ring/2 new samples */
+            ref_spec_snapshot(stream + 2 * ((off + block) / zd - ring / 2));
     }
     if (spec)
     {
@@ -329,7 +332,7 @@ int main(int argc, char** argv)
         float* mag = calloc(n, sizeof(float));
         float* avgs = calloc(n, sizeof(float));
         float avg[1024] = { 0 };                /* sd.FFT_AVGData starts zeroed (global) */
-        for (long fr = 0; fr < n / spec; ++fr)
+        for (long fr = 0; fr < n / zd / spec; ++fr)
         {
             ref_spec_frame(spec, spec_filter, stream + 2 * fr * spec, mag + fr * spec, avg);
             memcpy(avgs + fr * spec, avg, sizeof(float) * spec);

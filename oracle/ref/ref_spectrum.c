@@ -53,12 +53,16 @@ static const arm_cfft_instance_f32* instance(int L)
    consecutive 512-point snapshots of the same producer */
 int ref_spec_ring_len(int L) { return L >= 512 ? 1024 : 2 * L; }
 
-void ref_spec_setup(int L)
+void oracle_ref_spec_magnify(int m);
+const float* oracle_ref_zoom_biquad(int m);
+const arm_fir_decimate_instance_f32* oracle_ref_zoom_decim(void);
+
+void ref_spec_setup(int L, int magnify)
 {
     sd.fft_iq_len = (uint16_t)ref_spec_ring_len(L);
     sd.samp_ptr = 0;
-    sd.magnify = 0;
     sd.reading_ringbuffer = false;
+    oracle_ref_spec_magnify(magnify);       /* 0: no zoom (the no-zoom producer fills the ring) */
 }
 
 /* UiSpectrum_RedrawSpectrum state 0 copy (ui_spectrum.c:1362-1367) */
@@ -163,5 +167,21 @@ void ref_spec_dump(void)
         const float32_t w = (1 - (arm_cos_f32(PI * 2 * (float32_t)i / (float32_t)(fft_iq_len - 1))));
         printf("%s%u", i ? "," : "", fb(w));
     }
-    printf("]}\n");
+    /* zoom producer tables per magnification 1..5 (2x .. 32x): the 4-stage lowpass biquad
+       mag_coeffs[m] (audio_driver.c:204-363) and the decimator FirZoomFFTDecimate[m]
+       (filters/fir_rx_decimate_4.c:108), read back from the instance Spectrum_Set configured */
+    printf("]");
+    for (int m = 1; m <= 5; ++m)
+    {
+        oracle_ref_spec_magnify(m);
+        const float* bq = oracle_ref_zoom_biquad(m);
+        const arm_fir_decimate_instance_f32* d = oracle_ref_zoom_decim();
+        printf(", \"zoom_biquad_%d\": [", m);
+        for (int i = 0; i < 20; ++i) printf("%s%u", i ? "," : "", fb(bq[i]));
+        printf("], \"zoom_decim_%d\": {\"M\": %d, \"taps\": [", m, d->M);
+        for (int i = 0; i < d->numTaps; ++i) printf("%s%u", i ? "," : "", fb(d->pCoeffs[i]));
+        printf("]}");
+    }
+    oracle_ref_spec_magnify(0);
+    printf("}\n");
 }

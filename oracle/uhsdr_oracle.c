@@ -894,6 +894,42 @@ void uo_spec_state_init(const uhsdr_spectrum_plan* p, uo_spec_state* s)
 {
     (void)p;
     memset(s, 0, sizeof *s);
+    s->osc_vq = 1.0f;          /* FreqShift_Approx oscillator starts at {I=0, Q=1} (freq_shift.c:48-49) */
+}
+
+/* FreqShift (freq_shift.c:275-334) on one 32-frame call, as rx_call */
+static void spec_freq_shift(const uhsdr_spectrum_plan* p, uo_spec_state* s, float* ib, float* qb, int n)
+{
+    float* ip = p->shift_up ? ib : qb;
+    float* qp = p->shift_up ? qb : ib;
+    if (p->shift_kind == 1)
+    {
+        for (int i = 0; i < n; i += 4)   /* FreqShift_QuarterFs :219-262 */
+        {
+            float h1 = qp[i + 1], h2 = -ip[i + 1];
+            ip[i + 1] = h1; qp[i + 1] = h2;
+            h1 = -ip[i + 2]; h2 = -qp[i + 2];
+            ip[i + 2] = h1; qp[i + 2] = h2;
+            h1 = -qp[i + 3]; h2 = ip[i + 3];
+            ip[i + 3] = h1; qp[i + 3] = h2;
+        }
+    }
+    else
+    {
+        for (int i = 0; i < n; i++)      /* FreqShift_Approx :57-101 */
+        {
+            const float oq = (s->osc_vq * p->osc_cos) - (s->osc_vi * p->osc_sin);
+            const float oi = (s->osc_vi * p->osc_cos) + (s->osc_vq * p->osc_sin);
+            const float qt = qp[i], it = ip[i];
+            qp[i] = (qt * oq) - (it * oi);
+            ip[i] = (it * oq) + (qt * oi);
+            s->osc_vq = oq;
+            s->osc_vi = oi;
+        }
+        const float g = (3 - ((s->osc_vq * s->osc_vq) + (s->osc_vi * s->osc_vi))) / 2;
+        s->osc_vq = g * s->osc_vq;
+        s->osc_vi = g * s->osc_vi;
+    }
 }
 
 /* 8-point DFT core of arm_radix8_butterfly_f32 (CMSIS TransformFunctions/arm_cfft_radix8_f32.c:
@@ -1161,7 +1197,21 @@ static int spec_channel(const uhsdr_spectrum_plan* p, uo_spec_state* s, const in
             for (int i = 0; i < BLK; i++) qb[i] += M_c1 * ib[i];
             for (int i = 0; i < BLK; i++) ib[i] = ib[i] * M_c2;
         }
-        for (int i = 0; i < BLK; i++)
+        int nout = BLK;
+        if (p->magnify > 0)
+        {
+            /* AudioDriver_SpectrumZoomProcessSamples (audio_driver.c:1860-1909), after FreqShift
+               (:2694-2705): biquad low-pass on I and Q, decimate by 2^magnify, BLK / 2^magnify
+               samples into the ring */
+            if (p->freq_shift_hz != 0) spec_freq_shift(p, s, ib, qb, BLK);
+            biquad_df1(p->zoom_biquad, 4, s->zbq_i, ib, BLK);
+            biquad_df1(p->zoom_biquad, 4, s->zbq_q, qb, BLK);
+            const int M = p->zoom_decimation;
+            fir_decimate(p->zoom_fir, p->zoom_taps, M, s->zdec_i, ib, ib, BLK);
+            fir_decimate(p->zoom_fir, p->zoom_taps, M, s->zdec_q, qb, qb, BLK);
+            nout = BLK / M;
+        }
+        for (int i = 0; i < nout; i++)
         {
             s->frame[2 * s->fill] = qb[i];
             s->frame[2 * s->fill + 1] = ib[i];
@@ -1199,8 +1249,9 @@ int uo_spec_process_batch(const uhsdr_spectrum_plan* p, uo_spec_state* states, i
                           float* mag, float* avg, int threads)
 {
     const int L = p->fft_len;
-    if (n <= 0 || n % BLK || !(L == 256 || L == 512 || L == 1024) || (n % L && L % n)) return UHSDR_LENGTH_ERROR;
-    const int fmax = n >= L ? n / L : 1;
+    const int nd = n / (p->magnify > 0 ? p->zoom_decimation : 1);     /* ring samples per call */
+    if (n <= 0 || n % BLK || !(L == 256 || L == 512 || L == 1024) || (nd % L && L % nd)) return UHSDR_LENGTH_ERROR;
+    const int fmax = nd >= L ? nd / L : 1;
     if (threads < 1) threads = 1;
     if (threads > C) threads = C;
     if (threads > 256) threads = 256;

@@ -99,6 +99,11 @@ typedef struct uo_spec_state
     float frame[2 * UHSDR_SPECTRUM_MAX_LEN];        /* the [Q, I] ring, oldest first */
     float avg[UHSDR_SPECTRUM_MAX_LEN];              /* sd.FFT_AVGData */
     int32_t fill;                                   /* samples in frame[] */
+    /* zoom producer (magnify > 0): IIR_biquad_Zoom_FFT_I/_Q states, DECIMATE_ZOOM_FFT_I/_Q
+       histories, FreqShift_Approx oscillator */
+    float zbq_i[16], zbq_q[16];
+    float zdec_i[8], zdec_q[8];
+    float osc_vi, osc_vq;
 } uo_spec_state;
 
 size_t uo_spec_state_size(void);

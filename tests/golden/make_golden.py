@@ -59,7 +59,7 @@ CONFIGS = {
     "p48_agchang": ({"mode": 0, "path": 48, "agc_mode": 1, "agc_hang": 1}, {}),
     "p48_agcfrank": ({"mode": 0, "path": 48, "agc_mode": 0}, {}),
     "p48_p12k": ({"mode": 0, "path": 48, "iqmode": 3}, {"center": -12000.0}),
-    "p48_m6k": ({"mode": 0, "path": 48, "iqmode": 2}, {"center": 6000.0}),
+    "p48_m6k": ({"mode": 0, "path": 48, "iqmode": 2}, {"carrier": 6000.0}),
     "p48_p6k": ({"mode": 0, "path": 48, "iqmode": 1}, {"center": -6000.0}),
     "p48_off": ({"mode": 0, "path": 48, "iqmode": 0}, {"center": 0.0}),
     # AM / SAM (C3): AM carrier at +12 kHz +- 200 Hz, 50 % modulation with a 1 kHz tone
@@ -140,6 +140,16 @@ SPEC_CONFIGS = {
                         "phase": -0.0125, "specfilt": 20}, {}),
     "p48_iqman2_512": ({"mode": 0, "path": 48, "spec": 512, "gain_i": 0.98, "gain_q": 1.01, "phase": 0.02,
                         "specfilt": 7}, {}),
+    # zoom FFT producer (audio_driver.c:1860-1909): sd.magnify = mag, the ring gets the
+    # translated I/Q low-passed (4-stage biquad) and decimated by 2^mag; signal center 0 Hz after
+    # the translation (the default -12 kHz conversion puts the SSB tones at +12.7/13.9 kHz)
+    "p48_zoom2_256": ({"mode": 0, "path": 48, "spec": 256, "mag": 1}, {}),
+    "p48_zoom8_512_iqauto": ({"mode": 0, "path": 48, "spec": 512, "mag": 3, "iq_auto": 1}, {"frames": 16384}),
+    "p48_zoom32_256_m6k": ({"mode": 0, "path": 48, "spec": 256, "mag": 5, "iqmode": 2, "specfilt": 2},
+                           {"frames": 16384, "carrier": 6000.0}),
+    "p48_zoom4_1024_off": ({"mode": 0, "path": 48, "spec": 1024, "mag": 2, "iqmode": 0,
+                            "gain_i": 1.03125, "gain_q": 0.96875, "phase": -0.0125}, {"frames": 16384, "carrier": 0.0}),
+    "p48_zoom16_256_p12k": ({"mode": 0, "path": 48, "spec": 256, "mag": 4, "iqmode": 3}, {"frames": 8192, "carrier": -12000.0}),
 }
 SPEC_FRAMES = 4096
 
@@ -185,21 +195,25 @@ def make_cw(name: str):
 
 def make_spec(name: str):
     args, sig = SPEC_CONFIGS[name]
-    if sig.get("am"):
-        iq = synth.am_iq(np.arange(NCH), 0, SPEC_FRAMES)
+    sig = dict(sig)
+    nfr = sig.pop("frames", SPEC_FRAMES)
+    if sig.pop("am", False):
+        iq = synth.am_iq(np.arange(NCH), 0, nfr)
     else:
-        iq = synth.ssb_iq(np.arange(NCH), 0, SPEC_FRAMES)
+        iq = synth.ssb_iq(np.arange(NCH), 0, nfr, **sig)
     L = args["spec"]
-    mag = np.empty((NCH, SPEC_FRAMES // L, L), np.float32)
+    zd = 1 << args.get("mag", 0)
+    mag = np.empty((NCH, nfr // zd // L, L), np.float32)
     avg = np.empty_like(mag)
     for c in range(NCH):
         with tempfile.TemporaryDirectory() as td:
             fin, fm, fa = (os.path.join(td, x) for x in ("in.bin", "m.bin", "a.bin"))
             iq[c].astype(np.int32).tofile(fin)
-            cmd = [REF, f"in={fin}", f"n={SPEC_FRAMES}", f"out_mag={fm}", f"out_avg={fa}"]
+            cmd = [REF, f"in={fin}", f"n={nfr}", f"out_mag={fm}", f"out_avg={fa}"]
             subprocess.run(cmd + [f"{k}={v}" for k, v in args.items()], check=True)
-            mag[c] = np.fromfile(fm, dtype=np.float32).reshape(-1, L)
-            avg[c] = np.fromfile(fa, dtype=np.float32).reshape(-1, L)
+            F = mag.shape[1]                        # the harness writes n floats: frames first
+            mag[c] = np.fromfile(fm, dtype=np.float32)[:F * L].reshape(-1, L)
+            avg[c] = np.fromfile(fa, dtype=np.float32)[:F * L].reshape(-1, L)
     np.savez_compressed(os.path.join(HERE, f"spec_{name}.npz"), iq=iq, mag=mag, avg=avg, args=json.dumps(args))
     print(f"spec_{name:14s} peak mag={float(mag.max()):10.2f}  min avg={float(avg.min()):6.2f}")
 

@@ -118,3 +118,45 @@ def test_plan_rejects_bad_config():
     assert lib.uhsdr_spectrum_create(C.byref(cfg), 4, 1000, None, C.byref(h)) == -2   # N % 32
     assert lib.uhsdr_spectrum_create(C.byref(cfg), 0, 1024, None, C.byref(h)) == -1
     assert lib.uhsdr_spectrum_process(None, None, None, None, None) == -1
+
+
+def zoom_files():
+    return [p for p in spec_files() if "_zoom" in p]
+
+
+@pytest.mark.parametrize("path", zoom_files(), ids=lambda p: os.path.basename(p)[5:-4])
+@pytest.mark.parametrize("step", [32, 1024, 4096])
+def test_oracle_zoom_call_granularity(path, step):
+    """zoom producer (audio_driver.c:1860-1909): biquad / decimator / oscillator state and the
+    ring carry across calls of any size"""
+    g = load_spec(path)
+    plan = U.build_spectrum_plan(U.spectrum_config_from_ref_args(g["args"]))
+    L, D = plan.fft_len, plan.zoom_decimation
+    nd = step // D
+    if nd == 0 or (nd % L and L % nd):
+        pytest.skip("call size gives a ring count that neither divides nor is divided by fft_len")
+    o = oracle.OracleSpectrum(plan, g["iq"].shape[0])
+    mags, avgs = [], []
+    for off in range(0, g["iq"].shape[1], step):
+        m, a = o.process(g["iq"][:, off:off + step])
+        if nd >= L or (off + step) // D % L == 0:
+            mags.append(m)
+            avgs.append(a)
+    assert_bitexact(np.concatenate(mags, axis=1), g["mag"], "mag")
+    assert_bitexact(np.concatenate(avgs, axis=1), g["avg"], "avg")
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 4, 5])
+def test_zoom_plan_tables_match_reference_dump(m):
+    t = tables()
+    p = U.build_spectrum_plan(U.default_spectrum_config(fft_len=256, magnify=m))
+    assert p.magnify == m and p.zoom_decimation == t[f"zoom_decim_{m}"]["M"] == 1 << m
+    taps = t[f"zoom_decim_{m}"]["taps"]
+    assert p.zoom_taps == len(taps)
+    np.testing.assert_array_equal(np.frombuffer(bytes(p.zoom_fir), np.uint32)[:len(taps)], np.array(taps, np.uint32))
+    np.testing.assert_array_equal(np.frombuffer(bytes(p.zoom_biquad), np.uint32), np.array(t[f"zoom_biquad_{m}"], np.uint32))
+
+
+def test_zoom_magnify_out_of_range_rejected():
+    with pytest.raises(RuntimeError):
+        U.build_spectrum_plan(U.default_spectrum_config(fft_len=256, magnify=6))

@@ -123,7 +123,8 @@ class SpectrumConfig(C.Structure):
     _fields_ = [
         ("fft_len", C.c_int32), ("spectrum_filter", C.c_int32), ("iq_auto_correction", C.c_int32),
         ("iq_gain_i", C.c_float), ("iq_gain_q", C.c_float), ("iq_phase_balance", C.c_float),
-        ("reserved", C.c_int32 * 10),
+        ("magnify", C.c_int32), ("iq_freq_mode", C.c_int32),
+        ("reserved", C.c_int32 * 8),
     ]
 
 
@@ -135,6 +136,10 @@ class SpectrumPlan(C.Structure):
         ("window", C.c_float * (2 * SPECTRUM_MAX_LEN)), ("twiddle", C.c_float * (2 * SPECTRUM_MAX_LEN)),
         ("bitrev", C.c_uint16 * SPECTRUM_MAX_BITREV), ("perm", C.c_uint16 * SPECTRUM_MAX_LEN),
         ("iperm", C.c_uint16 * SPECTRUM_MAX_LEN), ("tw_lane", C.c_float * (8 * 64 * 2)),
+        ("magnify", C.c_int32), ("zoom_decimation", C.c_int32), ("zoom_taps", C.c_int32),
+        ("freq_shift_hz", C.c_int32), ("shift_kind", C.c_int32), ("shift_up", C.c_int32),
+        ("osc_cos", C.c_float), ("osc_sin", C.c_float),
+        ("zoom_biquad", C.c_float * 20), ("zoom_fir", C.c_float * 8),
         ("reserved", C.c_int32 * 16),
     ]
 
@@ -305,6 +310,7 @@ def build_tx_plan(cfg: TxConfig) -> TxPlan:
 SPEC_ARG_MAP = {
     "spec": "fft_len", "specfilt": "spectrum_filter", "iq_auto": "iq_auto_correction",
     "gain_i": "iq_gain_i", "gain_q": "iq_gain_q", "phase": "iq_phase_balance",
+    "mag": "magnify", "iqmode": "iq_freq_mode",
 }
 
 

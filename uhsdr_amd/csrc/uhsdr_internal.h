@@ -59,6 +59,13 @@ typedef struct
     int bitrev_len;
 } uhsdr_spectrum_desc;
 extern const uhsdr_spectrum_desc uhsdr_spectrum_tables[3];
+typedef struct
+{
+    int decimation, taps;
+    const uint32_t* biquad;       /* 4 stages x {b0, b1, b2, a1, a2} */
+    const uint32_t* fir;          /* taps */
+} uhsdr_zoom_desc;
+extern const uhsdr_zoom_desc uhsdr_zoom_tables[5];
 
 int uhsdr_rx_mode_supported(const uhsdr_rx_plan* p);
 

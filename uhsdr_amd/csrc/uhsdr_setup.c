@@ -272,6 +272,30 @@ static void setup_agc(uhsdr_agc_plan* a, const uhsdr_rx_config* cfg, float sampl
     a->hang_counter_init = (int)(a->hangtime * a->sample_rate);   /* audio_agc.c:469 */
 }
 
+/* FreqShift parameters for ts.iq_freq_mode: AudioDriver_GetTranslateFreq (audio_driver.c:445-464),
+   FreqShift's kind selection (freq_shift.c:294-319) and FreqShift_Approx_Prepare (:40-52) */
+static void shift_plan(int32_t iq_freq_mode, int32_t* hz, int32_t* kind, int32_t* up, float* oc, float* os)
+{
+    switch (iq_freq_mode)
+    {
+    case UHSDR_IQ_CONV_P6KHZ: *hz = 6000; break;
+    case UHSDR_IQ_CONV_M6KHZ: *hz = -6000; break;
+    case UHSDR_IQ_CONV_P12KHZ: *hz = 12000; break;
+    case UHSDR_IQ_CONV_M12KHZ: *hz = -12000; break;
+    default: *hz = 0; break;
+    }
+    if (*hz != 0)
+    {
+        const int32_t conv = *hz < 0 ? -*hz : *hz;
+        const float rate = conv / (float)IQ_SAMPLE_RATE;       /* IQ_SAMPLE_RATE_F */
+        *kind = (rate == 0.25) ? 1 : 2;                /* freq_shift.c:294-319 */
+        const double r = (2 * M_PI * conv) / (float)IQ_SAMPLE_RATE;
+        *oc = cos(r);
+        *os = sin(r);
+        *up = !(*hz > 0);                 /* dir = shift > 0 => DOWN */
+    }
+}
+
 uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
 {
     if (!cfg || !p) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
@@ -311,24 +335,7 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
     p->iq_gain_i = cfg->iq_gain_i;
     p->iq_gain_q = cfg->iq_gain_q;
     p->iq_phase_balance = cfg->iq_phase_balance;
-    switch (cfg->iq_freq_mode)
-    {
-    case UHSDR_IQ_CONV_P6KHZ: p->freq_shift_hz = 6000; break;
-    case UHSDR_IQ_CONV_M6KHZ: p->freq_shift_hz = -6000; break;
-    case UHSDR_IQ_CONV_P12KHZ: p->freq_shift_hz = 12000; break;
-    case UHSDR_IQ_CONV_M12KHZ: p->freq_shift_hz = -12000; break;
-    default: p->freq_shift_hz = 0; break;
-    }
-    if (p->freq_shift_hz != 0)
-    {
-        const int32_t conv = p->freq_shift_hz < 0 ? -p->freq_shift_hz : p->freq_shift_hz;
-        const float rate = conv / (float)IQ_SAMPLE_RATE;       /* IQ_SAMPLE_RATE_F */
-        p->shift_kind = (rate == 0.25) ? 1 : 2;                /* freq_shift.c:294-319 */
-        const double r = (2 * M_PI * conv) / (float)IQ_SAMPLE_RATE;
-        p->osc_cos = cos(r);
-        p->osc_sin = sin(r);
-        p->shift_up = !(p->freq_shift_hz > 0);                 /* dir = shift > 0 => DOWN */
-    }
+    shift_plan(cfg->iq_freq_mode, &p->freq_shift_hz, &p->shift_kind, &p->shift_up, &p->osc_cos, &p->osc_sin);
 
     /* Hilbert / decimation FIRs, audio_filter.c:1134-1223 and audio_driver.c:2718-2720 */
     const int is_am = (mode == UHSDR_DEMOD_AM || mode == UHSDR_DEMOD_SAM);
@@ -623,6 +630,8 @@ void uhsdr_spectrum_config_default(uhsdr_spectrum_config* cfg)
     cfg->iq_gain_i = 1.0f;
     cfg->iq_gain_q = 1.0f;
     cfg->iq_phase_balance = 0.0f;
+    cfg->magnify = 0;
+    cfg->iq_freq_mode = UHSDR_IQ_CONV_M12KHZ;   /* as uhsdr_rx_config_default */
 }
 
 uhsdr_status uhsdr_spectrum_plan_build(const uhsdr_spectrum_config* cfg, uhsdr_spectrum_plan* p)
@@ -643,6 +652,18 @@ uhsdr_status uhsdr_spectrum_plan_build(const uhsdr_spectrum_config* cfg, uhsdr_s
     p->iq_gain_q = cfg->iq_gain_q;
     p->iq_phase_balance = cfg->iq_phase_balance;
     p->filt_factor = 1 / (float)cfg->spectrum_filter;
+    if (cfg->magnify < 0 || cfg->magnify > 5)
+    { uhsdr_set_error("magnify %d outside 0..5 (MAGNIFY_MIN..MAGNIFY_MAX)", cfg->magnify); return UHSDR_ARGUMENT_ERROR; }
+    p->magnify = cfg->magnify;
+    p->zoom_decimation = 1 << cfg->magnify;
+    shift_plan(cfg->iq_freq_mode, &p->freq_shift_hz, &p->shift_kind, &p->shift_up, &p->osc_cos, &p->osc_sin);
+    if (cfg->magnify > 0)
+    {
+        const uhsdr_zoom_desc* z = &uhsdr_zoom_tables[cfg->magnify - 1];
+        p->zoom_taps = z->taps;
+        memcpy(p->zoom_biquad, z->biquad, sizeof p->zoom_biquad);
+        memcpy(p->zoom_fir, z->fir, sizeof(float) * z->taps);
+    }
     p->bitrev_len = d->bitrev_len;
     memcpy(p->window, d->window, sizeof(float) * 2 * L);
     memcpy(p->twiddle, d->twiddle, sizeof(float) * 2 * L);

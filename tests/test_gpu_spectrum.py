@@ -18,7 +18,7 @@ def run_spec(cfg, iq, frames, want_mag=True, want_avg=True):
     import torch
     C, n, _ = iq.shape
     spec = U.Spectrum(cfg, channels=C, frames=frames)
-    L = spec.fft_len
+    L, D = spec.fft_len, spec.decimation
     mags, avgs = [], []
     d_mag = torch.full(spec.out_shape, -1.0, dtype=torch.float32, device="cuda") if want_mag else None
     d_avg = torch.full(spec.out_shape, -1.0, dtype=torch.float32, device="cuda") if want_avg else None
@@ -27,7 +27,8 @@ def run_spec(cfg, iq, frames, want_mag=True, want_avg=True):
         d_iq.copy_(torch.from_numpy(np.ascontiguousarray(iq[:, off:off + frames])))
         nf = spec.process(d_iq, d_mag, d_avg)
         torch.cuda.synchronize()
-        assert nf == (min(frames, n - off) // L if frames >= L else int((off + frames) % L == 0))
+        nd = frames // D
+        assert nf == (nd // L if nd >= L else int((off + frames) // D % L == 0))
         if nf:
             if want_mag:
                 mags.append(d_mag[:, :nf].cpu().numpy())
@@ -110,3 +111,57 @@ def test_device_spectrum_c3_sampled(cuda):
     assert_bitexact(d_mag.cpu().numpy()[pick], om, "mag")
     assert_bitexact(d_avg.cpu().numpy()[pick], oa, "avg")
     spec.close()
+
+
+def zoom_names():
+    return [n.split("spec_")[-1][:-4] for n in spec_files() if "_zoom" in n]
+
+
+@pytest.mark.parametrize("frames", [32, 256, 2048, 8192])
+@pytest.mark.parametrize("name", zoom_names())
+def test_device_zoom_call_granularity(cuda, frames, name):
+    """zoom producer (spectrum_zoom: biquad / decimator / oscillator / auto-I/Q state carried
+    across calls) against the reference firmware's zoom fixtures, for call sizes from one ISR
+    call to several display frames"""
+    g = load_spec(spec_files()[[n.split("spec_")[-1][:-4] for n in spec_files()].index(name)])
+    cfg = U.spectrum_config_from_ref_args(g["args"])
+    L, D = cfg.fft_len, 1 << cfg.magnify
+    nd = frames // D
+    if nd == 0 or (nd % L and L % nd) or g["iq"].shape[1] % frames:
+        pytest.skip("call size not allowed for this zoom / fft_len")
+    mag, avg = run_spec(cfg, g["iq"], frames)
+    assert_bitexact(mag, g["mag"], f"zoom mag N={frames}")
+    assert_bitexact(avg, g["avg"], f"zoom avg N={frames}")
+
+
+@pytest.mark.parametrize("m,L,iqmode,auto,channels", [(1, 512, 4, 0, 333), (3, 256, 2, 1, 130), (5, 1024, 0, 0, 65),
+                                                      (2, 256, 3, 1, 200)])
+def test_device_zoom_matches_oracle_ragged(cuda, m, L, iqmode, auto, channels):
+    cfg = U.default_spectrum_config(fft_len=L, magnify=m, iq_freq_mode=iqmode, iq_auto_correction=auto,
+                                    iq_gain_i=1.01, iq_gain_q=0.99, iq_phase_balance=0.004)
+    n = max(4096, 2 * L << m)
+    iq = synth.ssb_iq(np.arange(channels), 3, n)
+    plan = U.build_spectrum_plan(cfg)
+    om, oa = oracle.OracleSpectrum(plan, channels).process(iq, threads=8)
+    mag, avg = run_spec(cfg, iq, 1024)
+    assert_bitexact(mag, om, "zoom mag")
+    assert_bitexact(avg, oa, "zoom avg")
+
+
+def test_device_zoom_reset(cuda):
+    """reset() restarts the zoom filters, decimator, oscillator and ring"""
+    import torch
+    cfg = U.default_spectrum_config(fft_len=256, magnify=2, iq_freq_mode=2)
+    C, N = 64, 1024
+    iq = synth.ssb_iq(np.arange(C), 0, N)
+    spec = U.Spectrum(cfg, channels=C, frames=N)
+    d_iq = torch.from_numpy(iq).cuda()
+    d_mag = torch.empty(spec.out_shape, dtype=torch.float32, device="cuda")
+    spec.process(d_iq, d_mag, None)
+    first = d_mag.cpu().numpy()
+    spec.process(d_iq, d_mag, None)
+    spec.reset()
+    spec.process(d_iq, d_mag, None)
+    again = d_mag.cpu().numpy()
+    spec.close()
+    assert_bitexact(again, first, "after reset")

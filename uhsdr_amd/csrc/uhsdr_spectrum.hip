@@ -21,6 +21,7 @@
 #include <string.h>
 #include <stdlib.h>
 #include <math.h>
+#include <type_traits>
 #include "uhsdr_internal.h"
 #include "uhsdr_dsp.h"
 #include "uhsdr_cfft.h"
@@ -33,6 +34,7 @@ struct SpecArgs
 {
     const uhsdr_spectrum_plan* plan;
     const int2* iq;          // [C][ld] IqSample_t
+    const float2* zq;        // zoom: [C][ld] {Q, I} from spectrum_zoom (corrected, translated, decimated)
     float* teta;             // [3][C] auto I/Q correction low-pass state
     float* avg_state;        // [C][L] sd.FFT_AVGData
     float* carry;            // [C][2L] windowed ring of an incomplete frame (positions < fill)
@@ -55,8 +57,8 @@ struct SpecParams
 // statistics summed in sample order through LDS), window (ui_spectrum.c:402-414).  PART: the
 // segment does not start at 0 (positions below fill hold the carried, already windowed values)
 // or does not reach L.  Positions outside [fill, end) are left alone.
-template <int L, bool PART, bool AUTO>
-__device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2* __restrict__ src, int fill, int end,
+template <int L, bool PART, bool AUTO, bool ZM = false, typename SrcT = typename std::conditional<ZM, float2, int2>::type>
+__device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const SrcT* __restrict__ src, int fill, int end,
                                         const SpecParams& sp, float* S, float* T, float& o1, float& o2, float& o3,
                                         int lane)
 {
@@ -70,11 +72,15 @@ __device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2*
         const int p = lane + 64 * k;
         if (in_seg(p))
         {
-            const int2 v = src[p - fill];
-            float I = (float)v.x, Q = (float)v.y;
-            I = I * IQ_BIT_SCALE_DOWN;
-            Q = Q * IQ_BIT_SCALE_DOWN;
-            z[k] = make_float2(Q, I);
+            if constexpr (ZM) z[k] = src[p - fill];          // zoom ring samples, ready to window
+            else
+            {
+                const int2 v = src[p - fill];
+                float I = (float)v.x, Q = (float)v.y;
+                I = I * IQ_BIT_SCALE_DOWN;
+                Q = Q * IQ_BIT_SCALE_DOWN;
+                z[k] = make_float2(Q, I);
+            }
         }
     }
     if constexpr (AUTO)
@@ -141,7 +147,8 @@ __device__ __forceinline__ void produce(float2 (&z)[SpecGeom<L>::K], const int2*
         if (in_seg(p))
         {
             float Q = z[k].x, I = z[k].y;
-            if constexpr (!AUTO)
+            if constexpr (ZM) {}
+            else if constexpr (!AUTO)
             {
                 I = I * sp.gi;
                 Q = Q * sp.gq;
@@ -228,7 +235,7 @@ __device__ __forceinline__ void spectrum_frame(float2 (&z)[SpecGeom<L>::K], floa
 }
 
 // A call that completes no frame (frames_per_call < fft_len): produce into the carried ring.
-template <int L, bool AUTO>
+template <int L, bool AUTO, bool ZM>
 __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_accumulate(SpecArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -242,7 +249,8 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_accumulate(SpecArgs 
     if (AUTO) { o1 = a.teta[c]; o2 = a.teta[a.C + c]; o3 = a.teta[2 * a.C + c]; }
     const int fill = a.fill0, end = a.fill0 + a.N;
     float2 z[G::K];
-    produce<L, true, AUTO>(z, a.iq + (size_t)c * a.ld, fill, end, sp, S, S + G::REGION, o1, o2, o3, lane);
+    if constexpr (ZM) produce<L, true, false, true>(z, a.zq + (size_t)c * a.ld, fill, end, sp, S, S + G::REGION, o1, o2, o3, lane);
+    else produce<L, true, AUTO>(z, a.iq + (size_t)c * a.ld, fill, end, sp, S, S + G::REGION, o1, o2, o3, lane);
     float2* __restrict__ carry = (float2*)a.carry + (size_t)c * L;
 #pragma unroll
     for (int k = 0; k < G::K; ++k)
@@ -254,7 +262,7 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_accumulate(SpecArgs 
 }
 
 // Calls that complete frames: every segment ends a frame; the first may start from the carry.
-template <int L, bool AUTO>
+template <int L, bool AUTO, bool ZM>
 __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -285,7 +293,10 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
     }
     float o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
     if (AUTO) { o1 = a.teta[c]; o2 = a.teta[C + c]; o3 = a.teta[2 * C + c]; }
-    const int2* __restrict__ src = a.iq + (size_t)c * a.ld;
+    using SrcT = typename std::conditional<ZM, float2, int2>::type;
+    const SrcT* __restrict__ src;
+    if constexpr (ZM) src = a.zq + (size_t)c * a.ld;
+    else src = a.iq + (size_t)c * a.ld;
 
     int n0 = 0, frame = 0;
     if (a.fill0)
@@ -299,7 +310,7 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
             const int p = lane + 64 * k;
             z[k] = carry[p < a.fill0 ? p : 0];
         }
-        produce<L, true, AUTO>(z, src, a.fill0, L, sp, S, T, o1, o2, o3, lane);
+        produce<L, true, AUTO && !ZM, ZM>(z, src, a.fill0, L, sp, S, T, o1, o2, o3, lane);
         spectrum_frame<L>(z, X, tw, av, f, a, c, frame, lane);
         n0 = L - a.fill0;
         ++frame;
@@ -312,7 +323,7 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
         const float* __restrict__ twf = tw;
         asm volatile("" : "+s"(spf.win), "+s"(twf));
         float2 z[K];
-        produce<L, false, AUTO>(z, src + n0, 0, L, spf, S, T, o1, o2, o3, lane);
+        produce<L, false, AUTO && !ZM, ZM>(z, src + n0, 0, L, spf, S, T, o1, o2, o3, lane);
         spectrum_frame<L>(z, X, twf, av, f, a, c, frame, lane);
     }
 #pragma unroll
@@ -326,6 +337,180 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
     if (AUTO && lane == 0) { a.teta[c] = o1; a.teta[C + c] = o2; a.teta[2 * C + c] = o3; }
 }
 
+
+// ---- zoom producer (AudioDriver_SpectrumZoomProcessSamples, audio_driver.c:1860-1909) ----
+// One lane per channel walks the launch's 32-frame calls in order, each exactly as the ISR:
+// convert, I/Q correction (:2254-2316), FreqShift (freq_shift.c:275-334; the ring sees the
+// translated I/Q, :2694-2705), IIR_biquad_Zoom_FFT_I/_Q (arm_biquad_cascade_df1_f32, 4 stages)
+// and DECIMATE_ZOOM_FFT_I/_Q (arm_fir_decimate_f32 by 2^magnify), writing the BLK / 2^magnify
+// ring samples {Q, I} of every call to zq[c][*].  All recursions are per channel and sequential
+// (lane == channel); state is field-major [field][C], so a wave's loads and stores coalesce.
+struct ZoomState
+{
+    float* bq_i;     // [16][C]  x1 x2 y1 y2 per stage (IIR_biquad_Zoom_FFT_I pState)
+    float* bq_q;     // [16][C]
+    float* dec_i;    // [3][C]   decimator history (numTaps - 1)
+    float* dec_q;    // [3][C]
+    float* osc;      // [2][C]   FreqShift_Approx oscillator {vi, vq}
+};
+
+struct ZoomArgs
+{
+    const uhsdr_spectrum_plan* plan;
+    const int2* iq;  // [C][N]
+    float2* zq;      // [C][N / D]
+    float* teta;     // [3][C]
+    ZoomState s;
+    int C, N;
+};
+
+constexpr int ZOOM_TAPS = 4;        // every FirZoomFFTDecimate entry (checked on the host)
+
+template <int D>
+__global__ void __launch_bounds__(64) spectrum_zoom(ZoomArgs a)
+{
+    const uhsdr_spectrum_plan* __restrict__ P = a.plan;
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= a.C) return;
+    const int C = a.C;
+    constexpr int T = ZOOM_TAPS;
+    const bool auto_iq = P->iq_auto_correction != 0;
+    const int shift = P->freq_shift_hz != 0 ? P->shift_kind : 0;
+    float bqi[16], bqq[16], hi[T - 1], hq[T - 1];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { bqi[k] = a.s.bq_i[k * C + c]; bqq[k] = a.s.bq_q[k * C + c]; }
+#pragma unroll
+    for (int k = 0; k < T - 1; ++k) { hi[k] = a.s.dec_i[k * C + c]; hq[k] = a.s.dec_q[k * C + c]; }
+    float vi = a.s.osc[c], vq = a.s.osc[C + c];
+    float o1 = a.teta[c], o2 = a.teta[C + c], o3 = a.teta[2 * C + c];
+    const int4* __restrict__ src = (const int4*)(a.iq + (size_t)c * a.N);
+    float2* __restrict__ dst = a.zq + (size_t)c * (a.N / D);
+    for (int n0 = 0; n0 < a.N; n0 += BLK)
+    {
+        float ib[BLK], qb[BLK];
+#pragma unroll
+        for (int j = 0; j < BLK / 2; ++j)
+        {
+            const int4 v = src[n0 / 2 + j];
+            ib[2 * j] = ((float)v.x) * IQ_BIT_SCALE_DOWN; qb[2 * j] = ((float)v.y) * IQ_BIT_SCALE_DOWN;
+            ib[2 * j + 1] = ((float)v.z) * IQ_BIT_SCALE_DOWN; qb[2 * j + 1] = ((float)v.w) * IQ_BIT_SCALE_DOWN;
+        }
+        if (!auto_iq)
+        {
+            const float gi = P->iq_gain_i, gq = P->iq_gain_q, ph = P->iq_phase_balance;
+#pragma unroll
+            for (int i = 0; i < BLK; ++i) { ib[i] = ib[i] * gi; qb[i] = qb[i] * gq; }
+            if (ph < 0)
+            {
+#pragma unroll
+                for (int i = 0; i < BLK; ++i) { const float e = ib[i] * ph; qb[i] = qb[i] + e; }
+            }
+            else if (ph > 0)
+            {
+#pragma unroll
+                for (int i = 0; i < BLK; ++i) { const float e = qb[i] * ph; ib[i] = ib[i] + e; }
+            }
+        }
+        else
+        {
+            float t1 = 0.0f, t2 = 0.0f, t3 = 0.0f;
+#pragma unroll
+            for (int i = 0; i < BLK; ++i)
+            {
+                t1 += sign_new(ib[i]) * qb[i];
+                t2 += sign_new(ib[i]) * ib[i];
+                t3 += sign_new(qb[i]) * qb[i];
+            }
+            t1 = (float)(-0.003 * (double)(t1 / (float)BLK) + 0.997 * (double)o1);
+            t2 = (float)(0.003 * (double)(t2 / (float)BLK) + 0.997 * (double)o2);
+            t3 = (float)(0.003 * (double)(t3 / (float)BLK) + 0.997 * (double)o3);
+            const float M_c1 = (t2 != 0.0f) ? t1 / t2 : 0.0f;
+            float help = (t2 * t2);
+            if (help > 0.0f) help = (t3 * t3 - t1 * t1) / help;
+            const float M_c2 = (help > 0.0f) ? sqrtf(help) : 1.0f;
+            o1 = t1; o2 = t2; o3 = t3;
+#pragma unroll
+            for (int i = 0; i < BLK; ++i) { qb[i] += M_c1 * ib[i]; ib[i] = ib[i] * M_c2; }
+        }
+        if (shift)
+        {
+            float* ip = P->shift_up ? ib : qb;
+            float* qp = P->shift_up ? qb : ib;
+            if (shift == 1)
+            {
+#pragma unroll
+                for (int i = 0; i < BLK; i += 4)   // FreqShift_QuarterFs, freq_shift.c:219-262
+                {
+                    float h1 = qp[i + 1], h2 = -ip[i + 1];
+                    ip[i + 1] = h1; qp[i + 1] = h2;
+                    h1 = -ip[i + 2]; h2 = -qp[i + 2];
+                    ip[i + 2] = h1; qp[i + 2] = h2;
+                    h1 = -qp[i + 3]; h2 = ip[i + 3];
+                    ip[i + 3] = h1; qp[i + 3] = h2;
+                }
+            }
+            else
+            {
+                const float oc = P->osc_cos, os = P->osc_sin;
+#pragma unroll
+                for (int i = 0; i < BLK; ++i)      // FreqShift_Approx, freq_shift.c:57-101
+                {
+                    const float oq = (vq * oc) - (vi * os);
+                    const float oi = (vi * oc) + (vq * os);
+                    const float qt = qp[i], it = ip[i];
+                    qp[i] = (qt * oq) - (it * oi);
+                    ip[i] = (it * oq) + (qt * oi);
+                    vq = oq; vi = oi;
+                }
+                const float g = (3 - ((vq * vq) + (vi * vi))) / 2;
+                vq = g * vq; vi = g * vi;
+            }
+        }
+        // IIR_biquad_Zoom_FFT_I / _Q: stage by stage over the call (arm_biquad_cascade_df1_f32)
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+        {
+            const float* cf = P->zoom_biquad + 5 * st;
+#pragma unroll
+            for (int i = 0; i < BLK; ++i)
+            {
+                ib[i] = biquad_step(ib[i], bqi[4 * st], bqi[4 * st + 1], bqi[4 * st + 2], bqi[4 * st + 3], cf);
+                qb[i] = biquad_step(qb[i], bqq[4 * st], bqq[4 * st + 1], bqq[4 * st + 2], bqq[4 * st + 3], cf);
+            }
+        }
+        // DECIMATE_ZOOM_FFT_I / _Q: y[m] = sum_k c[k] * w[m D + k], w = [T-1 history | call]
+#pragma unroll
+        for (int m = 0; m < BLK / D; ++m)
+        {
+            float si = 0.0f, sq = 0.0f;
+#pragma unroll
+            for (int k = 0; k < T; ++k)
+            {
+                const int j = m * D + k - (T - 1);      // < 0: history
+                const float ck = P->zoom_fir[k];
+                const float xi = j < 0 ? hi[j + T - 1] : ib[j];
+                const float xq = j < 0 ? hq[j + T - 1] : qb[j];
+                si += xi * ck;
+                sq += xq * ck;
+            }
+            dst[n0 / D + m] = make_float2(sq, si);
+        }
+#pragma unroll
+        for (int k = 0; k < T - 1; ++k)
+        {
+            const int j = BLK - (T - 1) + k;
+            hi[k] = ib[j];
+            hq[k] = qb[j];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { a.s.bq_i[k * C + c] = bqi[k]; a.s.bq_q[k * C + c] = bqq[k]; }
+#pragma unroll
+    for (int k = 0; k < T - 1; ++k) { a.s.dec_i[k * C + c] = hi[k]; a.s.dec_q[k * C + c] = hq[k]; }
+    a.s.osc[c] = vi; a.s.osc[C + c] = vq;
+    a.teta[c] = o1; a.teta[C + c] = o2; a.teta[2 * C + c] = o3;
+}
+
 } // namespace
 
 struct uhsdr_spectrum_s
@@ -333,8 +518,11 @@ struct uhsdr_spectrum_s
     uhsdr_spectrum_plan plan;
     uhsdr_spectrum_plan* d_plan;
     int C, N, L, F, fill;
+    int D, Nd;               // zoom decimation (1: no zoom), ring samples per call N / D
     hipStream_t stream;
     float *teta, *avg, *carry;
+    float2* zq;              // zoom ring samples of the current call [C][Nd]
+    ZoomState zs;
     void* arena;
     size_t arena_bytes;
 };
@@ -354,6 +542,16 @@ extern "C" uhsdr_status uhsdr_spectrum_reset(uhsdr_spectrum_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
     HIPCHK(hipMemsetAsync(h->arena, 0, h->arena_bytes, h->stream));   // sd.FFT_AVGData / iq_corr start zeroed
+    if (h->D > 1)
+    {
+        // FreqShift_Approx oscillator starts at {I=0, Q=1} (freq_shift.c:48-49)
+        float* ones = (float*)malloc(sizeof(float) * h->C);
+        for (int i = 0; i < h->C; ++i) ones[i] = 1.0f;
+        const hipError_t e = hipMemcpyAsync(h->zs.osc + h->C, ones, sizeof(float) * h->C, hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) (void)hipStreamSynchronize(h->stream);
+        free(ones);
+        HIPCHK(e);
+    }
     HIPCHK(hipStreamSynchronize(h->stream));
     h->fill = 0;
     return UHSDR_OK;
@@ -374,18 +572,31 @@ extern "C" uhsdr_status uhsdr_spectrum_create(const uhsdr_spectrum_config* cfg, 
         uhsdr_set_error("window kind does not match fft_len %d", L);
         return UHSDR_UNSUPPORTED;
     }
-    if (N % BLK || (N % L && L % N))
+    const int D = h->plan.magnify > 0 ? h->plan.zoom_decimation : 1, Nd = N / D;
+    if (h->plan.magnify > 0 && h->plan.zoom_taps != ZOOM_TAPS)
     {
         free(h);
-        uhsdr_set_error("frames_per_call %d: need a multiple of %d that is a multiple or a divisor of fft_len %d", N, BLK, L);
+        uhsdr_set_error("zoom decimator with %d taps (kernel built for %d)", h->plan.zoom_taps, ZOOM_TAPS);
+        return UHSDR_UNSUPPORTED;
+    }
+    if (N % BLK || (Nd % L && L % Nd))
+    {
+        free(h);
+        uhsdr_set_error("frames_per_call %d: need a multiple of %d whose ring samples (frames / %d) are a multiple "
+                        "or a divisor of fft_len %d", N, BLK, D, L);
         return UHSDR_LENGTH_ERROR;
     }
     h->C = C; h->N = N; h->L = L;
-    h->F = N >= L ? N / L : 1;
+    h->D = D; h->Nd = Nd;
+    h->F = Nd >= L ? Nd / L : 1;
     h->stream = (hipStream_t)stream;
     size_t fl = 0;
     auto take = [&](size_t n) { size_t o = fl; fl += (n + 63) & ~(size_t)63; return o; };
-    const size_t o_teta = take((size_t)3 * C), o_avg = take((size_t)C * L), o_carry = take(N < L ? (size_t)C * 2 * L : 0);
+    const size_t o_teta = take((size_t)3 * C), o_avg = take((size_t)C * L), o_carry = take(Nd < L ? (size_t)C * 2 * L : 0);
+    const bool zoom = D > 1;
+    const size_t o_zq = take(zoom ? (size_t)C * 2 * Nd : 0), o_bqi = take(zoom ? (size_t)16 * C : 0),
+                 o_bqq = take(zoom ? (size_t)16 * C : 0), o_di = take(zoom ? (size_t)(ZOOM_TAPS - 1) * C : 0),
+                 o_dq = take(zoom ? (size_t)(ZOOM_TAPS - 1) * C : 0), o_osc = take(zoom ? (size_t)2 * C : 0);
     h->arena_bytes = fl * sizeof(float);
     if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess ||
         hipMalloc((void**)&h->d_plan, sizeof(uhsdr_spectrum_plan)) != hipSuccess)
@@ -397,6 +608,8 @@ extern "C" uhsdr_status uhsdr_spectrum_create(const uhsdr_spectrum_config* cfg, 
     }
     float* A = (float*)h->arena;
     h->teta = A + o_teta; h->avg = A + o_avg; h->carry = A + o_carry;
+    h->zq = (float2*)(A + o_zq);
+    h->zs.bq_i = A + o_bqi; h->zs.bq_q = A + o_bqq; h->zs.dec_i = A + o_di; h->zs.dec_q = A + o_dq; h->zs.osc = A + o_osc;
     if (hipMemcpy(h->d_plan, &h->plan, sizeof(uhsdr_spectrum_plan), hipMemcpyHostToDevice) != hipSuccess)
     {
         uhsdr_set_error("plan upload failed");
@@ -410,19 +623,37 @@ extern "C" uhsdr_status uhsdr_spectrum_process(uhsdr_spectrum_handle h, const in
                                                int32_t* frames)
 {
     if (!h || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
+    const bool zoom = h->D > 1;
+    if (zoom)
+    {
+        ZoomArgs za;
+        za.plan = h->d_plan; za.iq = (const int2*)iq; za.zq = h->zq; za.teta = h->teta; za.s = h->zs;
+        za.C = h->C; za.N = h->N;
+        const dim3 zg((h->C + 63) / 64), zb(64);
+        switch (h->D)
+        {
+        case 2: hipLaunchKernelGGL(spectrum_zoom<2>, zg, zb, 0, h->stream, za); break;
+        case 4: hipLaunchKernelGGL(spectrum_zoom<4>, zg, zb, 0, h->stream, za); break;
+        case 8: hipLaunchKernelGGL(spectrum_zoom<8>, zg, zb, 0, h->stream, za); break;
+        case 16: hipLaunchKernelGGL(spectrum_zoom<16>, zg, zb, 0, h->stream, za); break;
+        default: hipLaunchKernelGGL(spectrum_zoom<32>, zg, zb, 0, h->stream, za); break;
+        }
+        HIPCHK(hipGetLastError());
+    }
     SpecArgs sa;
-    sa.plan = h->d_plan; sa.iq = (const int2*)iq;
+    sa.plan = h->d_plan; sa.iq = (const int2*)iq; sa.zq = h->zq;
     sa.teta = h->teta; sa.avg_state = h->avg; sa.carry = h->carry;
     sa.mag = mag; sa.avg = avg;
-    sa.C = h->C; sa.N = h->N; sa.ld = h->N; sa.F = h->F; sa.fill0 = h->fill;
-    sa.lds_pitch = spec_pitch(h->L, h->plan.iq_auto_correction != 0);
+    sa.C = h->C; sa.N = h->Nd; sa.ld = h->Nd; sa.F = h->F; sa.fill0 = h->fill;
+    const bool au = h->plan.iq_auto_correction != 0 && !zoom;   // zoom: corrected by spectrum_zoom
+    sa.lds_pitch = spec_pitch(h->L, au);
     const size_t lds = sizeof(float) * (size_t)SPEC_WAVES * sa.lds_pitch;
     const dim3 grid((h->C + SPEC_WAVES - 1) / SPEC_WAVES), block(64 * SPEC_WAVES);
-    const bool completes = h->fill + h->N >= h->L;
-    const bool au = h->plan.iq_auto_correction != 0;
-#define SPEC_LAUNCH2(LEN, AU) do { if (completes) hipLaunchKernelGGL((spectrum_frames<LEN, AU>), grid, block, lds, h->stream, sa); \
-                                   else hipLaunchKernelGGL((spectrum_accumulate<LEN, AU>), grid, block, lds, h->stream, sa); } while (0)
-#define SPEC_LAUNCH(LEN) do { if (au) SPEC_LAUNCH2(LEN, true); else SPEC_LAUNCH2(LEN, false); } while (0)
+    const bool completes = h->fill + h->Nd >= h->L;
+#define SPEC_LAUNCH3(LEN, AU, ZM) do { if (completes) hipLaunchKernelGGL((spectrum_frames<LEN, AU, ZM>), grid, block, lds, h->stream, sa); \
+                                       else hipLaunchKernelGGL((spectrum_accumulate<LEN, AU, ZM>), grid, block, lds, h->stream, sa); } while (0)
+#define SPEC_LAUNCH(LEN) do { if (zoom) SPEC_LAUNCH3(LEN, false, true); else if (au) SPEC_LAUNCH3(LEN, true, false); \
+                              else SPEC_LAUNCH3(LEN, false, false); } while (0)
     switch (h->L)
     {
     case 256: SPEC_LAUNCH(256); break;
@@ -430,10 +661,10 @@ extern "C" uhsdr_status uhsdr_spectrum_process(uhsdr_spectrum_handle h, const in
     default: SPEC_LAUNCH(1024); break;
     }
 #undef SPEC_LAUNCH
-#undef SPEC_LAUNCH2
+#undef SPEC_LAUNCH3
     HIPCHK(hipGetLastError());
-    const int done = (h->fill + h->N) / h->L;
-    h->fill = (h->fill + h->N) % h->L;
+    const int done = (h->fill + h->Nd) / h->L;
+    h->fill = (h->fill + h->Nd) % h->L;
     if (frames) *frames = done;
     return UHSDR_OK;
 }

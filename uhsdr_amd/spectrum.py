@@ -28,7 +28,8 @@ class Spectrum:
         self.plan = _abi.SpectrumPlan()
         _abi.check(self.lib.uhsdr_spectrum_get_plan(h, C.byref(self.plan)), "uhsdr_spectrum_get_plan")
         self.fft_len = self.plan.fft_len
-        self.frames_out = max(1, self.frames // self.fft_len)
+        self.decimation = 1 << int(self.config.magnify)          # zoom: ring samples per frame
+        self.frames_out = max(1, self.frames // self.decimation // self.fft_len)
 
     @property
     def out_shape(self):

@@ -78,7 +78,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--only", default="c3,c3spec,c4fm,c4tx,c5,c5fir")
+    ap.add_argument("--only", default="c3,c3spec,c3zoom,c4fm,c4tx,c5,c5fir")
     a = ap.parse_args()
     import torch
     import uhsdr_amd as U
@@ -101,6 +101,23 @@ def main():
         lines.append({"workload": "C3 spectrum 1024-point (Hann, CFFT, magnitude, IIR average)", "channels": C,
                       "frames_per_call": N, "ms_per_call": round(ms, 4), "msamples_per_s": round(C * N / ms / 1e3, 1),
                       "alg_bytes_per_frame": round(byts / (C * N), 2),
+                      "hbm_frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4)})
+        spec.close()
+    if "c3zoom" in want:
+        # zoom producer (spectrum_zoom) 8x + 256-point display: 8 B in per frame, the ring
+        # scratch written and read once (8 / D B each way), zoom state (2 x (16 + 3) + 2 + 3
+        # floats) and the display state per call
+        C, N, L, m = 32768, 2048, 256, 3
+        D = 1 << m
+        s = torch.cuda.current_stream()
+        spec = U.Spectrum(U.default_spectrum_config(fft_len=L, magnify=m), channels=C, frames=N, stream=s.cuda_stream)
+        iq = tiled(synth.ssb_iq, C, N)
+        avg = torch.empty(spec.out_shape, dtype=torch.float32, device="cuda")
+        ms = time_calls(lambda: spec.process(iq, None, avg), a.steps, a.warmup)
+        byts = C * N * (8 + 2 * 8 / D) + C * (2 * 4 * (2 * 19 + 5) + 2 * 4 * L) + C * (N // D // L) * L * 4
+        lines.append({"workload": f"C3-size zoom spectrum {D}x, {L}-point (FreqShift, zoom biquad, decimate, CFFT)",
+                      "channels": C, "frames_per_call": N, "ms_per_call": round(ms, 4),
+                      "msamples_per_s": round(C * N / ms / 1e3, 1), "alg_bytes_per_frame": round(byts / (C * N), 2),
                       "hbm_frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4)})
         spec.close()
     if "c4fm" in want:

@@ -344,7 +344,8 @@ __global__ void __launch_bounds__(64 * SPEC_WAVES) spectrum_frames(SpecArgs a)
 // translated I/Q, :2694-2705), IIR_biquad_Zoom_FFT_I/_Q (arm_biquad_cascade_df1_f32, 4 stages)
 // and DECIMATE_ZOOM_FFT_I/_Q (arm_fir_decimate_f32 by 2^magnify), writing the BLK / 2^magnify
 // ring samples {Q, I} of every call to zq[c][*].  All recursions are per channel and sequential
-// (lane == channel); state is field-major [field][C], so a wave's loads and stores coalesce.
+// (a lane pair per channel: I and Q); state is field-major [field][C], so loads and stores
+// coalesce.
 struct ZoomState
 {
     float* bq_i;     // [16][C]  x1 x2 y1 y2 per stage (IIR_biquad_Zoom_FFT_I pState)
@@ -370,21 +371,27 @@ template <int D>
 __global__ void __launch_bounds__(64) spectrum_zoom(ZoomArgs a)
 {
     const uhsdr_spectrum_plan* __restrict__ P = a.plan;
-    const int c = blockIdx.x * 64 + threadIdx.x;
+    // two lanes per channel: both run the correction / translation (they mix I and Q), then
+    // lane q = 0 filters and decimates I, lane q = 1 Q -- twice the waves of lane == channel,
+    // half the recursive work per lane
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    const int c = t >> 1, q = t & 1;
     if (c >= a.C) return;
     const int C = a.C;
     constexpr int T = ZOOM_TAPS;
     const bool auto_iq = P->iq_auto_correction != 0;
     const int shift = P->freq_shift_hz != 0 ? P->shift_kind : 0;
-    float bqi[16], bqq[16], hi[T - 1], hq[T - 1];
+    float* __restrict__ bq_g = q ? a.s.bq_q : a.s.bq_i;
+    float* __restrict__ dec_g = q ? a.s.dec_q : a.s.dec_i;
+    float bq[16], h[T - 1];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { bqi[k] = a.s.bq_i[k * C + c]; bqq[k] = a.s.bq_q[k * C + c]; }
+    for (int k = 0; k < 16; ++k) bq[k] = bq_g[k * C + c];
 #pragma unroll
-    for (int k = 0; k < T - 1; ++k) { hi[k] = a.s.dec_i[k * C + c]; hq[k] = a.s.dec_q[k * C + c]; }
+    for (int k = 0; k < T - 1; ++k) h[k] = dec_g[k * C + c];
     float vi = a.s.osc[c], vq = a.s.osc[C + c];
     float o1 = a.teta[c], o2 = a.teta[C + c], o3 = a.teta[2 * C + c];
     const int4* __restrict__ src = (const int4*)(a.iq + (size_t)c * a.N);
-    float2* __restrict__ dst = a.zq + (size_t)c * (a.N / D);
+    float* __restrict__ dst = (float*)(a.zq + (size_t)c * (a.N / D)) + (q ? 0 : 1);   // {Q, I} pairs
     for (int n0 = 0; n0 < a.N; n0 += BLK)
     {
         float ib[BLK], qb[BLK];
@@ -467,48 +474,42 @@ __global__ void __launch_bounds__(64) spectrum_zoom(ZoomArgs a)
             }
         }
         // IIR_biquad_Zoom_FFT_I / _Q: stage by stage over the call (arm_biquad_cascade_df1_f32)
+        float x[BLK];
+#pragma unroll
+        for (int i = 0; i < BLK; ++i) x[i] = q ? qb[i] : ib[i];
 #pragma unroll
         for (int st = 0; st < 4; ++st)
         {
             const float* cf = P->zoom_biquad + 5 * st;
 #pragma unroll
             for (int i = 0; i < BLK; ++i)
-            {
-                ib[i] = biquad_step(ib[i], bqi[4 * st], bqi[4 * st + 1], bqi[4 * st + 2], bqi[4 * st + 3], cf);
-                qb[i] = biquad_step(qb[i], bqq[4 * st], bqq[4 * st + 1], bqq[4 * st + 2], bqq[4 * st + 3], cf);
-            }
+                x[i] = biquad_step(x[i], bq[4 * st], bq[4 * st + 1], bq[4 * st + 2], bq[4 * st + 3], cf);
         }
         // DECIMATE_ZOOM_FFT_I / _Q: y[m] = sum_k c[k] * w[m D + k], w = [T-1 history | call]
 #pragma unroll
         for (int m = 0; m < BLK / D; ++m)
         {
-            float si = 0.0f, sq = 0.0f;
+            float sum = 0.0f;
 #pragma unroll
             for (int k = 0; k < T; ++k)
             {
                 const int j = m * D + k - (T - 1);      // < 0: history
-                const float ck = P->zoom_fir[k];
-                const float xi = j < 0 ? hi[j + T - 1] : ib[j];
-                const float xq = j < 0 ? hq[j + T - 1] : qb[j];
-                si += xi * ck;
-                sq += xq * ck;
+                sum += (j < 0 ? h[j + T - 1] : x[j]) * P->zoom_fir[k];
             }
-            dst[n0 / D + m] = make_float2(sq, si);
+            dst[2 * (n0 / D + m)] = sum;
         }
 #pragma unroll
-        for (int k = 0; k < T - 1; ++k)
-        {
-            const int j = BLK - (T - 1) + k;
-            hi[k] = ib[j];
-            hq[k] = qb[j];
-        }
+        for (int k = 0; k < T - 1; ++k) h[k] = x[BLK - (T - 1) + k];
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { a.s.bq_i[k * C + c] = bqi[k]; a.s.bq_q[k * C + c] = bqq[k]; }
+    for (int k = 0; k < 16; ++k) bq_g[k * C + c] = bq[k];
 #pragma unroll
-    for (int k = 0; k < T - 1; ++k) { a.s.dec_i[k * C + c] = hi[k]; a.s.dec_q[k * C + c] = hq[k]; }
-    a.s.osc[c] = vi; a.s.osc[C + c] = vq;
-    a.teta[c] = o1; a.teta[C + c] = o2; a.teta[2 * C + c] = o3;
+    for (int k = 0; k < T - 1; ++k) dec_g[k * C + c] = h[k];
+    if (q == 0)
+    {
+        a.s.osc[c] = vi; a.s.osc[C + c] = vq;
+        a.teta[c] = o1; a.teta[C + c] = o2; a.teta[2 * C + c] = o3;
+    }
 }
 
 } // namespace
@@ -629,7 +630,7 @@ extern "C" uhsdr_status uhsdr_spectrum_process(uhsdr_spectrum_handle h, const in
         ZoomArgs za;
         za.plan = h->d_plan; za.iq = (const int2*)iq; za.zq = h->zq; za.teta = h->teta; za.s = h->zs;
         za.C = h->C; za.N = h->N;
-        const dim3 zg((h->C + 63) / 64), zb(64);
+        const dim3 zg((2 * h->C + 63) / 64), zb(64);      // two lanes per channel
         switch (h->D)
         {
         case 2: hipLaunchKernelGGL(spectrum_zoom<2>, zg, zb, 0, h->stream, za); break;

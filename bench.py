@@ -89,24 +89,12 @@ def pmc_traffic(workload: str):
     return out or None
 
 
-def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
-    import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 64))
-    from uhsdr_amd import synth
-    C = 32 * threads
-    o = oracle.OracleRx(plan, C)
-    blocks = [synth.ssb_iq(np.arange(C), k * frames, frames) for k in range(4)]
-    o.process(blocks[0], threads=threads)          # warm-up
-    done, t0 = 0, time.perf_counter()
-    while True:
-        o.process(blocks[done % 4], threads=threads)
-        done += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or done >= 100000:
-            break
-    samples = C * frames * done
-    import platform
+def host_cpus():
+    """CPUs this process may run on (its affinity mask), and the host CPU model."""
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = os.cpu_count() or 1
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -114,11 +102,31 @@ def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
                 model = line.split(":", 1)[1].strip()
                 break
     except OSError:
-        model = platform.processor()
+        pass
+    return cpus, model
+
+
+def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
+    """The bit-exact CPU restatement (oracle/uhsdr_oracle.c) on the host cores (SURVEY.md
+    §8(d) d4): one persistent worker thread per CPU, pinned (sched affinity), channels split
+    evenly, no thread creation inside the timed loop.  Threads = the CPUs of this process's
+    affinity mask, capped by OMP_NUM_THREADS when the box sets it (the GPU box's per-GPU CPU
+    share)."""
+    import oracle
+    from uhsdr_amd import synth
+    cpus, model = host_cpus()
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(cpus, cap) if cap > 0 else cpus)
+    C = 16 * threads
+    blocks = np.stack([synth.ssb_iq(np.arange(C), k * frames, frames) for k in range(4)])
+    oracle.rx_bench(plan, blocks, threads, 0.5)                 # warm-up (pages, caches, clocks)
+    done, el = oracle.rx_bench(plan, blocks, threads, budget_s)
+    samples = done * frames
     return {"value": round(samples / el / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{C} channels x {done} blocks of {frames} frames ({samples} samples, {el:.1f} s) "
-                      f"through oracle/uhsdr_oracle.c (bit-exact to the reference build), "
-                      f"{threads} threads, channels split evenly; host CPU: {model}"}
+            "sample": f"{C} channels x {frames}-frame calls, {done // C} calls per channel on average "
+                      f"({samples} samples, {el:.1f} s) through oracle/uhsdr_oracle.c (bit-exact to the "
+                      f"reference build); {threads} persistent worker threads pinned one per CPU "
+                      f"(affinity mask has {cpus} CPUs), channels split evenly; host CPU: {model}"}
 
 
 def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, pool, want_dst, pipelined=False,
@@ -141,10 +149,7 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     for s in range(warmup):
         chain.process(inputs[s % pool], audio, dst)
     torch.cuda.synchronize(dev)
-    # HIP events bracket the kernels of every `every`-th timed call (~64 sampled calls), so the
-    # event records' own cost (~30 us per bracketed call) stays out of the throughput
-    every = max(1, steps // 64)
-    chain.enable_timing(True, every=every)
+    # throughput: K calls with nothing but the calls themselves inside the timed region
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -155,6 +160,14 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # per-kernel breakdown in a separate pass: HIP events on the library's own stream bracket
+    # every kernel of every call (the records cost host time, so they never share a clock with
+    # the throughput loop above)
+    tsteps = max(10, min(steps, 200))
+    chain.enable_timing(True, every=1)
+    for s in range(tsteps):
+        chain.process(inputs[s % pool], audio, dst)
+    torch.cuda.synchronize(dev)
     ktimes = chain.kernel_times()
     chain.enable_timing(False)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -167,39 +180,28 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
 
 
 def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup):
-    """The same chain with every launch's f32 audio gathered to rank 0 over RCCL (SURVEY.md
-    §8(e) e1; RCCL has no gather primitive, torch.distributed.gather issues grouped send/recv,
-    so rank 0 receives from every peer over its own xGMI link): the gather of launch k runs on
-    a communication stream while launch k+1 computes (double-buffered outputs).  Returns
-    max-rank seconds for `steps` steps."""
+    """The same chain with every launch's f32 audio gathered to rank 0
+    through shard.GatherPipeline: double-buffered outputs, the gather of launch k (RCCL
+    grouped send/recv over xGMI, rank 0 receiving from every peer on its own link) in flight
+    while launch k+1 computes.  Returns max-rank seconds for `steps` steps."""
     cfg = U.default_config()
     comp = torch.cuda.current_stream(dev)
-    comm = torch.cuda.Stream(dev)
     chain = U.RxChain(cfg, channels=C, frames=N, stream=comp.cuda_stream)
     x = synth.ssb_iq_torch(shard.channel_range(C, rank)[0], C, 0, N, dev)
-    outs = [torch.empty((C, N), dtype=torch.float32, device=dev) for _ in range(2)]
-    recv = [[torch.empty((C, N), dtype=torch.float32, device=dev) for _ in range(world)] if rank == 0 else None
-            for _ in range(2)]
-    done = [torch.cuda.Event() for _ in range(2)]
-    gdone = [torch.cuda.Event() for _ in range(2)]
+    pipe = shard.GatherPipeline(dist, world, rank,
+                                lambda: torch.empty((C, N), dtype=torch.float32, device=dev))
 
-    def step(s):
-        k = s & 1
-        if s >= 2:
-            comp.wait_event(gdone[k])                  # buffer k's previous gather has finished
-        chain.process(x, outs[k], None)
-        done[k].record(comp)
-        with torch.cuda.stream(comm):
-            comm.wait_event(done[k])
-            dist.gather(outs[k], gather_list=recv[k], dst=0)
-            gdone[k].record(comm)
+    def compute(out):
+        chain.process(x, out, None)
     for s in range(warmup):
-        step(s)
+        pipe.step(compute)
+    pipe.drain()
     torch.cuda.synchronize(dev)
     dist.barrier()
     t0 = time.perf_counter()
     for s in range(steps):
-        step(s)
+        pipe.step(compute)
+    pipe.drain()
     torch.cuda.synchronize(dev)
     dist.barrier()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)

@@ -230,6 +230,10 @@ uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable);
    (v_pk_fma_f32), half the VALU issue; outputs within north_star's 1e-5 normwise relative
    tolerance of the reference (max|diff| / max|ref| per channel), not bit-identical.  The
    recursive stages (lattices, AGC, biquads, demodulators) always run the reference sequence.
+   FMA is accepted only on the Hilbert-first families (wide SSB / CW / DIGI at 12 and 24 ksps,
+   FM), where it stays within 1e-5; the decimate-first families (narrow SSB / CW, AM, SAM)
+   amplify the FIR rounding difference past 1e-5 (1.3e-5 .. 1.8e-5 measured), so there the call
+   returns UHSDR_UNSUPPORTED and the handle stays EXACT.
    Takes effect from the next uhsdr_rx_process. */
 enum { UHSDR_PRECISION_EXACT = 0, UHSDR_PRECISION_FMA = 1 };
 uhsdr_status uhsdr_rx_set_precision(uhsdr_rx_handle h, int32_t precision);

@@ -29,6 +29,9 @@ def load():
         lib.uo_rx_process.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         lib.uo_rx_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                             C.c_void_p, C.c_void_p, C.c_int]
+        lib.uo_rx_bench.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                    C.c_void_p, C.c_int, C.c_int, C.c_double, C.POINTER(C.c_double)]
+        lib.uo_rx_bench.restype = C.c_longlong
         lib.uo_rx_process_batch_cw.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
                                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         lib.uo_tx_state_size.restype = C.c_size_t
@@ -68,6 +71,26 @@ class OracleRx:
         if st != 0:
             raise RuntimeError(f"uo_rx_process_batch status {st}")
         return a1, dst
+
+
+def rx_bench(plan, blocks: np.ndarray, threads: int, budget_s: float, pin: bool = True):
+    """CPU baseline (bench.py): `threads` persistent workers pinned one per CPU of the affinity
+    mask, each owning a contiguous channel slice, cycling through blocks [pool][C][n][2] until
+    budget_s has passed.  Returns (channel-calls done, slowest worker's seconds)."""
+    lib = load()
+    blocks = np.ascontiguousarray(blocks, dtype=np.int32)
+    pool, Cn, n, _ = blocks.shape
+    ssize = lib.uo_rx_state_size()
+    states = (C.c_char * (ssize * Cn))()
+    for c in range(Cn):
+        lib.uo_rx_state_init(C.byref(plan), C.byref(states, c * ssize))
+    a1 = np.empty((Cn, n), np.float32)
+    el = C.c_double(0.0)
+    done = lib.uo_rx_bench(C.byref(plan), states, Cn, blocks.ctypes.data_as(C.c_void_p), pool, n,
+                           a1.ctypes.data_as(C.c_void_p), None, threads, 1 if pin else 0, budget_s, C.byref(el))
+    if done < 0:
+        raise RuntimeError("uo_rx_bench: bad arguments")
+    return int(done), float(el.value)
 
 
 class OracleTx:

@@ -703,6 +703,99 @@ int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, cons
     return UHSDR_OK;
 }
 
+/* CPU baseline for bench.py: `threads` persistent workers, worker t pinned
+   to the t-th CPU of the process's affinity mask, each running its own contiguous channel slice
+   (states and outputs private to the worker) call after call over a pool of `pool` input blocks
+   [pool][C][n][2], until `budget_s` seconds have passed.  No thread is created or joined inside
+   the timed loop.  Returns the total channel-calls done (sum over workers of channels x calls);
+   *elapsed gets the slowest worker's wall time. */
+typedef struct
+{
+    const uhsdr_rx_plan* p;
+    uo_rx_state* states;
+    const int32_t* iq;
+    float* a1;
+    int32_t* dst;
+    int c0, c1, n, C, pool, cpu;
+    double budget;
+    pthread_barrier_t* bar;
+    long long done;
+    double el;
+} uo_bench_job;
+
+static double uo_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+static void* uo_bench_worker(void* arg)
+{
+    uo_bench_job* j = (uo_bench_job*)arg;
+    if (j->cpu >= 0)
+    {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(j->cpu, &set);
+        pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+    }
+    const int nc = j->c1 - j->c0;
+    pthread_barrier_wait(j->bar);
+    const double t0 = uo_now();
+    long long calls = 0;
+    double el = 0.0;
+    do
+    {
+        const int32_t* blk = j->iq + (size_t)(calls % j->pool) * j->C * j->n * 2;
+        for (int c = j->c0; c < j->c1; c++)
+            uo_rx_process(j->p, &j->states[c], blk + (size_t)c * j->n * 2, j->n, j->a1 + (size_t)c * j->n,
+                          j->dst ? j->dst + (size_t)c * j->n * 2 : NULL);
+        ++calls;
+        el = uo_now() - t0;
+    } while (el < j->budget);
+    j->done = calls * nc;
+    j->el = el;
+    return NULL;
+}
+
+long long uo_rx_bench(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int pool, int n,
+                      float* a1, int32_t* dst, int threads, int pin, double budget_s, double* elapsed)
+{
+    if (n % BLK || C < 1 || pool < 1) return -1;
+    cpu_set_t allowed;
+    int cpus[1024], ncpu = 0;
+    if (sched_getaffinity(0, sizeof allowed, &allowed) == 0)
+        for (int i = 0; i < CPU_SETSIZE && ncpu < 1024; i++)
+            if (CPU_ISSET(i, &allowed)) cpus[ncpu++] = i;
+    if (threads < 1) threads = 1;
+    if (threads > C) threads = C;
+    if (threads > 1024) threads = 1024;
+    pthread_t* tid = (pthread_t*)calloc(threads, sizeof(pthread_t));
+    uo_bench_job* jobs = (uo_bench_job*)calloc(threads, sizeof(uo_bench_job));
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, threads);
+    for (int t = 0; t < threads; t++)
+    {
+        jobs[t] = (uo_bench_job){ p, states, iq, a1, dst, (int)((long)C * t / threads), (int)((long)C * (t + 1) / threads),
+                                  n, C, pool, (pin && ncpu) ? cpus[t % ncpu] : -1, budget_s, &bar, 0, 0.0 };
+        pthread_create(&tid[t], NULL, uo_bench_worker, &jobs[t]);
+    }
+    long long total = 0;
+    double mx = 0.0;
+    for (int t = 0; t < threads; t++)
+    {
+        pthread_join(tid[t], NULL);
+        total += jobs[t].done;
+        if (jobs[t].el > mx) mx = jobs[t].el;
+    }
+    pthread_barrier_destroy(&bar);
+    free(tid);
+    free(jobs);
+    if (elapsed) *elapsed = mx;
+    return total;
+}
+
 /* ================================ transmit ================================ */
 
 size_t uo_tx_state_size(void) { return sizeof(uo_tx_state); }

@@ -64,6 +64,8 @@ void uo_rx_state_init(const uhsdr_rx_plan* p, uo_rx_state* s);
 /* one channel, n frames (n % 32 == 0): iq [n][2] int32 -> a1 [n] f32, dst [n][2] int32 */
 int uo_rx_process(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, int n, float* a1, int32_t* dst);
 /* C channels, channel-major buffers, `threads` POSIX threads (0 = 1) */
+long long uo_rx_bench(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int pool, int n,
+                      float* a1, int32_t* dst, int threads, int pin, double budget_s, double* elapsed);
 int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
                         float* a1, int32_t* dst, int threads);
 /* the same, also recording the CW decoder front end: cw_signal [C][n/32] (ads.CW_signal after

@@ -15,10 +15,6 @@ from uhsdr_amd import synth
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-5          # north_star: outputs within 1e-5 relative (normwise per channel)
-# Paths whose chain amplifies the FIR rounding difference past north_star's bound (measured on
-# MI355X, 8 calls: P35 1.7e-5, P70 AM 1.8e-5 / SAM 1.3e-5, P4 CW 1.3e-5): FMA stays opt-in
-# there and is held to this looser bound; EXACT is the mode that meets the bar on every path.
-TOL_NARROW = 3e-5
 
 
 def normwise(got, ref):
@@ -46,12 +42,26 @@ CASES = [
     ("p48_usb", dict(filter_path=48, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 256, 256, TOL),
     ("p48_lsb_n64", dict(filter_path=48, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 128, 64, TOL),
     ("p60_usb_24k", dict(filter_path=60, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 96, 256, TOL),
-    ("p35_usb", dict(filter_path=35, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 130, 256, TOL_NARROW),
-    ("p70_am", dict(filter_path=70, dmod_mode=U.DEMOD_AM), synth.am_iq, 128, 256, TOL_NARROW),
-    ("p70_sam", dict(filter_path=70, dmod_mode=U.DEMOD_SAM), synth.am_iq, 128, 256, TOL_NARROW),
     ("p1_fm", dict(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=12), synth.fm_iq, 96, 256, TOL),
-    ("p4_cw", dict(filter_path=4, dmod_mode=U.DEMOD_CW), synth.cw_iq, 96, 256, TOL_NARROW),
 ]
+
+# decimate-first families: FMA measured past 1e-5 (P35 1.7e-5, P70 AM 1.8e-5 / SAM 1.3e-5,
+# P4 CW 1.3e-5), so the library refuses it there
+REFUSED = [
+    ("p35_usb", dict(filter_path=35, dmod_mode=U.DEMOD_USB)),
+    ("p70_am", dict(filter_path=70, dmod_mode=U.DEMOD_AM)),
+    ("p70_sam", dict(filter_path=70, dmod_mode=U.DEMOD_SAM)),
+    ("p4_cw", dict(filter_path=4, dmod_mode=U.DEMOD_CW)),
+]
+
+
+@pytest.mark.parametrize("name,kw", REFUSED, ids=[c[0] for c in REFUSED])
+def test_fma_refused_where_past_tolerance(cuda, name, kw):
+    chain = U.RxChain(U.default_config(**kw), channels=64, frames=64)
+    with pytest.raises(Exception):
+        chain.set_precision(U.PRECISION_FMA)
+    assert chain.precision == U.PRECISION_EXACT
+    chain.close()
 
 
 @pytest.mark.parametrize("name,kw,gen,C,N,tol", CASES, ids=[c[0] for c in CASES])

@@ -99,8 +99,14 @@ def _check(lib):
 class _Inst:
     """One instance with its caller-owned arrays (kept alive here)."""
 
+    in_place = False   # pDst == pSrc, as the firmware calls FIR / decimate / lattice / biquad
+
     def _run(self, fn, x: np.ndarray, nout: int) -> np.ndarray:
-        x = np.ascontiguousarray(x, np.float32)
+        x = np.array(x, np.float32, copy=True)
+        if self.in_place and nout <= len(x):
+            fn(C.byref(self.S), _fp(x), _fp(x), len(x))
+            _check(self.lib)
+            return x[:nout].copy()
         y = np.zeros(nout, np.float32)
         fn(C.byref(self.S), _fp(x), _fp(y), len(x))
         _check(self.lib)

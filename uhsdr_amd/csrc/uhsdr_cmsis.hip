@@ -245,17 +245,14 @@ void fir_run(float* pState, const float* pCoeffs, const float* pSrc, float* pDst
     float* dy = d + yoff;
     if (e != hipSuccess) { fail(UHSDR_DEVICE_ERROR, "arm_fir upload", e); return; }
     hipLaunchKernelGGL(shim_fir, dim3(grid(nout)), dim3(SHIM_THREADS), 0, t_ctx.stream, d, d + coff, dy, T, nout, M);
-    if ((e = hipGetLastError()) != hipSuccess || !finish(pDst, dy, nout)) { fail(UHSDR_DEVICE_ERROR, "arm_fir", e); return; }
-    // carried samples for the next call: the last T-1 of [history | block] (host data movement)
-    if (T > 1)
-    {
-        if (B >= T - 1) memcpy(pState, pSrc + B - (T - 1), sizeof(float) * (T - 1));
-        else
-        {
-            memmove(pState, pState + B, sizeof(float) * (T - 1 - B));
-            memcpy(pState + (T - 1 - B), pSrc, sizeof(float) * B);
-        }
-    }
+    e = hipGetLastError();
+    // carried samples for the next call: the last T-1 of the device window [history | block],
+    // which still holds this call's input -- the reference decimates and filters in place
+    // (pSrc == pDst, audio_driver.c:2744-2745, 2751-2752, 2803), so pSrc may already hold outputs
+    // once finish() has copied them back
+    if (e == hipSuccess && T > 1)
+        e = hipMemcpyAsync(pState, d + B, sizeof(float) * (T - 1), hipMemcpyDeviceToHost, t_ctx.stream);
+    if (e != hipSuccess || !finish(pDst, dy, nout)) { fail(UHSDR_DEVICE_ERROR, "arm_fir", e); return; }
 }
 
 template <int L>
@@ -360,18 +357,12 @@ void arm_fir_interpolate_f32(const arm_fir_interpolate_instance_f32* S, float32_
     if (e != hipSuccess) { fail(UHSDR_DEVICE_ERROR, "arm_fir_interpolate_f32 upload", e); return; }
     hipLaunchKernelGGL(shim_interp, dim3(grid((size_t)B * L)), dim3(SHIM_THREADS), 0, t_ctx.stream, d + woff, d + coff,
                        d + yoff, L, ph, B);
-    if ((e = hipGetLastError()) != hipSuccess || !finish(pDst, d + yoff, (size_t)B * L))
+    e = hipGetLastError();
+    // carried samples: the last phaseLength-1 of the device window (pSrc may alias pDst)
+    if (e == hipSuccess && ph > 1)
+        e = hipMemcpyAsync(S->pState, d + woff + B, sizeof(float) * (ph - 1), hipMemcpyDeviceToHost, t_ctx.stream);
+    if (e != hipSuccess || !finish(pDst, d + yoff, (size_t)B * L))
     { fail(UHSDR_DEVICE_ERROR, "arm_fir_interpolate_f32", e); return; }
-    if (ph > 1)
-    {
-        const int H = ph - 1;
-        if (B >= H) memcpy(S->pState, pSrc + B - H, sizeof(float) * H);
-        else
-        {
-            memmove(S->pState, S->pState + B, sizeof(float) * (H - B));
-            memcpy(S->pState + (H - B), pSrc, sizeof(float) * B);
-        }
-    }
 }
 
 void arm_iir_lattice_init_f32(arm_iir_lattice_instance_f32* S, uint16_t numStages, float32_t* pkCoeffs,

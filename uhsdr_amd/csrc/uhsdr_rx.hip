@@ -1547,6 +1547,7 @@ struct uhsdr_rx_s
     int pipelined;
     hipStream_t side;
     hipEvent_t ev_front, ev_join, ev_back[2];
+    hipEvent_t ev_switch;    // uhsdr_rx_set_stream: new stream after the old one's work
     float *adec2, *adec_q2;  // second hand-off buffer pair
     long long calls_issued;  // process() calls (hand-off buffer parity)
     // per-kernel timing (uhsdr_rx_enable_timing)
@@ -1736,9 +1737,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         hipMalloc((void**)&h->d_taps2, sizeof(float) * 4 * TAPS2_MAX) != hipSuccess)
     {
         uhsdr_set_error("hipMalloc failed (%zu bytes state)", h->arena_bytes);
-        if (h->arena) (void)hipFree(h->arena);
-        if (h->adec) (void)hipFree(h->adec);
-        free(h);
+        (void)uhsdr_rx_destroy(h);
         return UHSDR_DEVICE_ERROR;
     }
     float* A = (float*)h->arena;
@@ -1771,16 +1770,20 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         if (hipMemcpy(h->d_taps2, t2, sizeof t2, hipMemcpyHostToDevice) != hipSuccess)
         {
             uhsdr_set_error("tap upload failed");
+            (void)uhsdr_rx_destroy(h);
             return UHSDR_DEVICE_ERROR;
         }
     }
     if (hipMemcpy(h->d_plan, &h->plan, sizeof(uhsdr_rx_plan), hipMemcpyHostToDevice) != hipSuccess)
     {
         uhsdr_set_error("plan upload failed");
+        (void)uhsdr_rx_destroy(h);
         return UHSDR_DEVICE_ERROR;
     }
+    const uhsdr_status rs = uhsdr_rx_reset(h);
+    if (rs != UHSDR_OK) { (void)uhsdr_rx_destroy(h); return rs; }
     *out = h;
-    return uhsdr_rx_reset(h);
+    return UHSDR_OK;
 }
 
 extern "C" uhsdr_status uhsdr_rx_set_cw_outputs(uhsdr_rx_handle h, uint8_t* signal, float* energy)
@@ -1797,6 +1800,17 @@ extern "C" int32_t uhsdr_rx_cw_blocks_last(uhsdr_rx_handle h) { return h ? h->cw
 extern "C" uhsdr_status uhsdr_rx_set_stream(uhsdr_rx_handle h, void* stream)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
+    if ((hipStream_t)stream == h->stream) return UHSDR_OK;
+    // the next call's kernels read and write the state the calls already queued on the old
+    // stream (and, pipelined, on the side stream) are still using: order the new stream after them
+    if (h->pipelined)
+    {
+        const uhsdr_status st = uhsdr_rx_join(h);
+        if (st != UHSDR_OK) return st;
+    }
+    if (!h->ev_switch) HIPCHK(hipEventCreateWithFlags(&h->ev_switch, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(h->ev_switch, h->stream));
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, h->ev_switch, 0));
     h->stream = (hipStream_t)stream;
     return UHSDR_OK;
 }
@@ -1920,6 +1934,14 @@ extern "C" uhsdr_status uhsdr_rx_set_precision(uhsdr_rx_handle h, int32_t precis
     {
         uhsdr_set_error("unknown precision %d", (int)precision);
         return UHSDR_ARGUMENT_ERROR;
+    }
+    if (precision == UHSDR_PRECISION_FMA && h->plan.use_decimated_iq)
+    {
+        // decimate-first families (narrow SSB / CW, AM, SAM): the fused FIR MACs move the output
+        // by more than north_star's 1e-5 normwise (tests/test_gpu_fma.py), so EXACT only
+        uhsdr_set_error("FMA precision exceeds 1e-5 on filter path %d (decimate-first family): EXACT only",
+                        (int)h->plan.filter_path);
+        return UHSDR_UNSUPPORTED;
     }
     h->precision = precision;
     return UHSDR_OK;
@@ -2051,10 +2073,11 @@ extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
         for (int i = 0; i < h->nev_cap * 4; ++i) (void)hipEventDestroy(h->ev[i]);
         free(h->ev);
     }
-    (void)hipFree(h->arena);
-    (void)hipFree(h->adec);
-    (void)hipFree(h->d_plan);
-    (void)hipFree(h->d_taps2);
+    if (h->ev_switch) (void)hipEventDestroy(h->ev_switch);
+    if (h->arena) (void)hipFree(h->arena);
+    if (h->adec) (void)hipFree(h->adec);
+    if (h->d_plan) (void)hipFree(h->d_plan);
+    if (h->d_taps2) (void)hipFree(h->d_taps2);
     free(h);
     return UHSDR_OK;
 }

@@ -603,8 +603,7 @@ extern "C" uhsdr_status uhsdr_spectrum_create(const uhsdr_spectrum_config* cfg, 
         hipMalloc((void**)&h->d_plan, sizeof(uhsdr_spectrum_plan)) != hipSuccess)
     {
         uhsdr_set_error("hipMalloc failed (%zu bytes state)", h->arena_bytes);
-        if (h->arena) (void)hipFree(h->arena);
-        free(h);
+        (void)uhsdr_spectrum_destroy(h);
         return UHSDR_DEVICE_ERROR;
     }
     float* A = (float*)h->arena;
@@ -614,10 +613,13 @@ extern "C" uhsdr_status uhsdr_spectrum_create(const uhsdr_spectrum_config* cfg, 
     if (hipMemcpy(h->d_plan, &h->plan, sizeof(uhsdr_spectrum_plan), hipMemcpyHostToDevice) != hipSuccess)
     {
         uhsdr_set_error("plan upload failed");
+        (void)uhsdr_spectrum_destroy(h);
         return UHSDR_DEVICE_ERROR;
     }
+    const uhsdr_status rs = uhsdr_spectrum_reset(h);
+    if (rs != UHSDR_OK) { (void)uhsdr_spectrum_destroy(h); return rs; }
     *out = h;
-    return uhsdr_spectrum_reset(h);
+    return UHSDR_OK;
 }
 
 extern "C" uhsdr_status uhsdr_spectrum_process(uhsdr_spectrum_handle h, const int32_t* iq, float* mag, float* avg,
@@ -681,8 +683,8 @@ extern "C" uhsdr_status uhsdr_spectrum_destroy(uhsdr_spectrum_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
     (void)hipStreamSynchronize(h->stream);
-    (void)hipFree(h->arena);
-    (void)hipFree(h->d_plan);
+    if (h->arena) (void)hipFree(h->arena);
+    if (h->d_plan) (void)hipFree(h->d_plan);
     free(h);
     return UHSDR_OK;
 }

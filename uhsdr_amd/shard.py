@@ -31,3 +31,58 @@ def gather_to_root(local, dist, world: int, rank: int):
     parts = [torch.empty_like(local) for _ in range(world)] if rank == 0 else None
     dist.gather(local, gather_list=parts, dst=0)
     return torch.cat(parts, dim=0) if rank == 0 else None
+
+
+class GatherPipeline:
+    """Per-launch outputs gathered to rank 0 while the next launch computes.
+
+    `depth` output buffers are used round robin.  Step s computes into buffer s % depth and
+    issues its gather asynchronously (``dist.gather(..., async_op=True)``); before buffer k is
+    reused, the gather that last read it is waited for.  With RCCL the collective runs on the
+    process group's own stream, ordered after the compute stream at issue time, and
+    ``Work.wait()`` orders the compute stream after it, so the whole pipeline stays on the
+    device queues (no host sync); with gloo (CPU tests) ``wait()`` blocks the caller.
+
+    Rank 0 hands every completed step to ``sink(step, parts)`` (parts: one tensor per rank,
+    in rank order) in step order, right before the receive buffers are reused or at drain().
+    Backend-agnostic: only ``dist.gather`` and ``Work.wait`` are used.
+    """
+
+    def __init__(self, dist, world: int, rank: int, make_buffer, depth: int = 2, sink=None):
+        if depth < 1:
+            raise ValueError("depth >= 1")
+        self.dist, self.world, self.rank, self.depth, self.sink = dist, world, rank, depth, sink
+        self.bufs = [make_buffer() for _ in range(depth)]
+        self.recv = [[make_buffer() for _ in range(world)] if rank == 0 else None for _ in range(depth)]
+        self.work = [None] * depth
+        self.issued = 0          # steps issued
+        self.retired = 0         # steps whose gather has been waited for
+
+    def _retire(self, k: int) -> None:
+        w = self.work[k]
+        if w is None:
+            return
+        w.wait()
+        self.work[k] = None
+        if self.rank == 0 and self.sink is not None:
+            self.sink(self.retired, self.recv[k])
+        self.retired += 1
+
+    def step(self, compute) -> None:
+        """compute(out) fills this step's output buffer (enqueue only)."""
+        k = self.issued % self.depth
+        self._retire(k)                       # the gather of step issued - depth read buffer k
+        compute(self.bufs[k])
+        if self.world == 1:
+            if self.sink is not None:
+                self.sink(self.issued, [self.bufs[k]])
+            self.retired += 1
+        else:
+            self.work[k] = self.dist.gather(self.bufs[k], gather_list=self.recv[k], dst=0, async_op=True)
+        self.issued += 1
+
+    def drain(self) -> None:
+        """Wait for every gather in flight, oldest first."""
+        for i in range(self.issued - self.depth, self.issued):
+            if i >= 0:
+                self._retire(i % self.depth)

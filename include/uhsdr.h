@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define UHSDR_ABI_VERSION 1
+#define UHSDR_ABI_VERSION 2
 
 typedef enum
 {
@@ -49,18 +49,21 @@ typedef enum
     UHSDR_DEVICE_ERROR = -11      /* HIP runtime error */
 } uhsdr_status;
 
-/* sam_sideband_t, drivers/audio/audio_driver.h:181-190 */
-enum { UHSDR_SAM_SIDEBAND_BOTH = 0, UHSDR_SAM_SIDEBAND_LSB = 1, UHSDR_SAM_SIDEBAND_USB = 2 };
+/* sam_sideband_t, drivers/audio/audio_driver.h:181-190 (STEREO: USE_TWO_CHANNEL_AUDIO, OVI40) */
+enum { UHSDR_SAM_SIDEBAND_BOTH = 0, UHSDR_SAM_SIDEBAND_LSB = 1, UHSDR_SAM_SIDEBAND_USB = 2,
+       UHSDR_SAM_SIDEBAND_STEREO = 3 };
 
-/* DemodModes_t, hardware/uhsdr_board.h:72-85 */
+/* DemodModes_t, hardware/uhsdr_board.h:72-85 (SSBSTEREO / IQ: USE_TWO_CHANNEL_AUDIO, OVI40) */
 enum { UHSDR_DEMOD_USB = 0, UHSDR_DEMOD_LSB = 1, UHSDR_DEMOD_CW = 2, UHSDR_DEMOD_AM = 3,
-       UHSDR_DEMOD_SAM = 4, UHSDR_DEMOD_FM = 5, UHSDR_DEMOD_DIGI = 6 };
+       UHSDR_DEMOD_SAM = 4, UHSDR_DEMOD_FM = 5, UHSDR_DEMOD_DIGI = 6, UHSDR_DEMOD_SSBSTEREO = 7,
+       UHSDR_DEMOD_IQ = 8 };
 
 /* FREQ_IQ_CONV_*, drivers/audio/audio_driver.h:520-526 */
 enum { UHSDR_IQ_CONV_OFF = 0, UHSDR_IQ_CONV_P6KHZ = 1, UHSDR_IQ_CONV_M6KHZ = 2,
        UHSDR_IQ_CONV_P12KHZ = 3, UHSDR_IQ_CONV_M12KHZ = 4 };
 
-/* ts.dsp.active bits honoured by the chain (drivers/ui/ui_driver.c:425-433) */
+/* ts.dsp.active bits honoured by the chain (drivers/audio/audio_driver.h:195-200) */
+#define UHSDR_DSP_NOTCH_ENABLE  0x04      /* LMS auto notch (AudioDriver_NotchFilter) */
 #define UHSDR_DSP_MNOTCH_ENABLE 0x10
 #define UHSDR_DSP_MPEAK_ENABLE  0x20
 
@@ -112,7 +115,16 @@ typedef struct uhsdr_rx_config
     int32_t cw_decoder_blocksize; /* cw_decoder_config.blocksize (88, 8..128, cw_decoder.h:12-13) */
     int32_t cw_decoder_thresh;    /* cw_decoder_config.thresh (32000, cw_decoder.h:15-17) */
     int32_t cw_decoder_noisecancel; /* cw_decoder_config.noisecancel_enable (1) */
-    int32_t reserved[5];
+    /* ABI 2 */
+    int32_t notch_mu;             /* ts.dsp.notch_mu (DSP_NOTCH_MU_DEFAULT 10, 0..40): LMS auto notch
+                                     convergence; the notch runs with UHSDR_DSP_NOTCH_ENABLE in dsp_active */
+    int32_t fm_tone_det;          /* ts.fm_subaudible_tone_det_select: 0 off, else index into
+                                     fm_subaudible_tone_table (FM subaudible tone detector) */
+    int32_t beep_frequency;       /* ts.beep_frequency (DEFAULT_BEEP_FREQUENCY 1000 Hz) */
+    int32_t beep_loudness;        /* ts.beep_loudness (DEFAULT_BEEP_LOUDNESS 10) */
+    int32_t stereo_enable;        /* ts.stereo_enable: two-channel audio in DEMOD_SSBSTEREO, DEMOD_IQ and
+                                     SAM with UHSDR_SAM_SIDEBAND_STEREO (audio_driver.c:2618) */
+    int32_t reserved[11];
 } uhsdr_rx_config;
 
 /* AudioAgc_SetupAgcWdsp() results (audio_agc.c:126-339) */
@@ -184,7 +196,25 @@ typedef struct uhsdr_rx_plan
     int32_t cw_enabled, cw_blocksize, cw_noisecancel;
     float   cw_thresh;
     float   cw_r, cw_cos, cw_sin;     /* AudioFilter_CalcGoertzel (audio_filter.c:1281-1288) */
-    int32_t reserved[57];
+    /* ABI 2 */
+    /* LMS auto notch: AudioDriver_NotchFilter (audio_driver.c:1746-1763) -> arm_lms_norm_f32 on
+       a_buffer[0] at the decimated rate, before the pre-filter (:2443-2456); set up at :1166-1186 */
+    int32_t notch_enabled;        /* DSP_NOTCH_ENABLE, not in CW, not in SAM at 24 ksps */
+    int32_t notch_taps;           /* ts.dsp.notch_numtaps (DSP_NOTCH_NUMTAPS_DEFAULT 64) */
+    int32_t notch_delay_len;      /* ts.dsp.notch_delaybuf_len (DSP_NOTCH_DELAYBUF_DEFAULT 128) */
+    float   notch_mu;             /* log10f(((notch_mu + 1.0) / 1500.0) + 1.0) */
+    /* FM subaudible tone detector (audio_driver.c:1665-1734), Goertzels of
+       AudioManagement_CalcSubaudibleDetFreq (audio_management.c:313-326): FM_HIGH, FM_LOW, FM_CTR */
+    int32_t tone_det_enabled;
+    float   tone_r[3], tone_cos[3], tone_sin[3];
+    /* key beep: softdds step and loudness (AudioManagement_KeyBeepPrepare, audio_management.c:354-363) */
+    uint32_t beep_step;
+    float   beep_scale;
+    /* OVI40 two-channel audio (use_stereo, audio_driver.c:2618): 0 mono, 1 SSB stereo
+       (a_buffer[0] = I + Q, [1] = I - Q), 2 IQ (a_buffer[0] = I, [1] = Q), 3 SAM stereo */
+    int32_t stereo;
+    int16_t dds_table[1024];      /* softdds DDS_TABLE (softdds/dds_table.c) */
+    int32_t reserved[32];
 } uhsdr_rx_plan;
 
 typedef struct uhsdr_rx_s* uhsdr_rx_handle;
@@ -460,6 +490,13 @@ int32_t      uhsdr_sizeof_spectrum_plan(void);
 uhsdr_status uhsdr_rx_set_cw_outputs(uhsdr_rx_handle h, uint8_t* signal, float* energy);
 int32_t      uhsdr_rx_cw_blocks_max(uhsdr_rx_handle h);
 int32_t      uhsdr_rx_cw_blocks_last(uhsdr_rx_handle h);
+
+/* Key beep (AudioManagement_KeyBeep, audio_management.c:368-375 -> the softdds tone added to the
+   output at audio_driver.c:2891-2898): the beep's DDS accumulator restarts at 0 and the tone
+   (config beep_frequency / beep_loudness) is added to every channel's output for the next
+   `calls` 32-frame calls (the firmware's ts.beep_timing countdown, here counted in ISR calls);
+   0 stops a running beep.  Like the firmware's single key beep, it is common to all channels. */
+uhsdr_status uhsdr_rx_key_beep(uhsdr_rx_handle h, int32_t calls);
 
 /* ---- diagnostics ---- */
 const char*  uhsdr_version(void);

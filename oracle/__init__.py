@@ -29,6 +29,7 @@ def load():
         lib.uo_rx_process.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         lib.uo_rx_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                             C.c_void_p, C.c_void_p, C.c_int]
+        lib.uo_rx_key_beep.argtypes = [C.c_void_p, C.c_int, C.c_int]
         lib.uo_rx_bench.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                                     C.c_void_p, C.c_int, C.c_int, C.c_double, C.POINTER(C.c_double)]
         lib.uo_rx_bench.restype = C.c_longlong
@@ -59,6 +60,10 @@ class OracleRx:
         self.states = (C.c_char * (self.ssize * channels))()
         for c in range(channels):
             self.lib.uo_rx_state_init(C.byref(plan), C.byref(self.states, c * self.ssize))
+
+    def key_beep(self, calls: int) -> None:
+        """AudioManagement_KeyBeep on every channel: the next `calls` calls get the beep."""
+        self.lib.uo_rx_key_beep(self.states, self.channels, calls)
 
     def process(self, iq: np.ndarray, threads: int = 1):
         iq = np.ascontiguousarray(iq, dtype=np.int32)

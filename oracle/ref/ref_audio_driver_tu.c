@@ -29,3 +29,6 @@ const arm_iir_lattice_instance_f32* oracle_ref_squelch(void) { return &IIR_Squel
 void oracle_ref_spec_magnify(int m) { sd.magnify = (uint8_t)m; AudioDriver_Spectrum_Set(); }
 const float* oracle_ref_zoom_biquad(int m) { return mag_coeffs[m]; }
 const arm_fir_decimate_instance_f32* oracle_ref_zoom_decim(void) { return &DECIMATE_ZOOM_FFT_I; }
+
+/* LMS auto notch instance (AudioDriver_NotchFilter, audio_driver.c:1746-1763) */
+float oracle_ref_notch_mu(void) { return lmsData.lms2Norm_instance.mu; }

@@ -17,6 +17,14 @@
  *   mode= path= iqmode= agc_mode= agc_thresh= agc_slope= agc_hang= bass= treble=
  *   iq_auto= gain_i= gain_q= phase= dsp= notch= peak= sam_sb= pll_fmax= zeta= omegan=
  *   fade= sql= fm5k= block=
+ *   notch_mu=      ts.dsp.notch_mu (LMS auto notch, on with dsp=4 / DSP_NOTCH_ENABLE)
+ *   tonedet=       ts.fm_subaudible_tone_det_select (FM subaudible tone detector)
+ *   beep=b0:K      key beep on calls b0 .. b0+K-1 (AudioManagement_KeyBeep at call b0)
+ *   beepfreq= beeploud=   ts.beep_frequency / ts.beep_loudness
+ *   stereo=1       ts.stereo_enable (two-channel modes: mode=7 SSB stereo, mode=8 IQ, SAM sam_sb=3)
+ *   out_a0=<file>  f32 adb.a_buffer[0] after each call (the second channel in stereo)
+ *   out_clip=<file> uint8 per call: ads.adc_clip | adc_half_clip << 1 | adc_quarter_clip << 2,
+ *                  read and cleared after every call (the UI's role)
  *   tx=1           transmit: in= holds codec audio frames {l,r}, out_dst= gets the IQ frames
  *                  TxProcessor_Run writes (tx_processor.c:891-1078), out_a= a_buffer[0]
  *   micmult= boost= comp= txfilter= txbass= txtreble= txpwr= txgi= txgq= txphase=
@@ -32,6 +40,7 @@
 #include "filters.h"
 #include "cw_decoder.h"
 #include "dds_table.h"
+#include "audio_management.h"
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -47,6 +56,7 @@ const arm_iir_lattice_instance_f32* oracle_ref_prefilter(void);
 const arm_iir_lattice_instance_f32* oracle_ref_antialias(void);
 const arm_fir_interpolate_instance_f32* oracle_ref_interpolate(void);
 const arm_iir_lattice_instance_f32* oracle_ref_squelch(void);
+float oracle_ref_notch_mu(void);
 const arm_iir_lattice_instance_f32* oracle_ref_tx_lattice(void);
 const arm_biquad_casd_df1_inst_f32* oracle_ref_tx_biquad(void);
 extern arm_fir_instance_f32 Fir_Tx_Hilbert_I, Fir_Tx_Hilbert_Q;
@@ -172,6 +182,19 @@ static void dump_setup(void)
         const float alc[2] = { ads.alc_decay, (float)ts.alc_tx_postfilt_gain_var };
         print_fvec("tx_alc", alc, 2, 0);
     }
+    {   /* LMS auto notch mu (audio_driver.c:1170), key beep (AudioManagement_KeyBeepPrepare,
+           audio_management.c:354-363), FM subaudible tone detector Goertzels (audio_management.c:313-326) */
+        const float nm[1] = { oracle_ref_notch_mu() };
+        print_fvec("notch_mu", nm, 1, 0);
+        printf("  \"beep_step\": %u,\n", (unsigned)ads.beep.step);
+        const float bl[1] = { ads.beep_loudness_factor };
+        print_fvec("beep_scale", bl, 1, 0);
+        const float tg[9] = { ads.fm_conf.goertzel[FM_HIGH].r, ads.fm_conf.goertzel[FM_HIGH].cos, ads.fm_conf.goertzel[FM_HIGH].sin,
+                              ads.fm_conf.goertzel[FM_LOW].r, ads.fm_conf.goertzel[FM_LOW].cos, ads.fm_conf.goertzel[FM_LOW].sin,
+                              ads.fm_conf.goertzel[FM_CTR].r, ads.fm_conf.goertzel[FM_CTR].cos, ads.fm_conf.goertzel[FM_CTR].sin };
+        print_fvec("tone_goertzel", tg, 9, 0);
+        printf("  \"tone_det_freq\": %u,\n", bits(ads.fm_conf.subaudible_tone_det_freq));
+    }
     {   /* CW decoder Goertzel (CwDecode_Filter_Set via SetProcessingChain, audio_driver.c:1158) */
         const Goertzel* g = oracle_ref_cw_goertzel();
         const float cw[3] = { g->r, g->cos, g->sin };
@@ -204,8 +227,6 @@ int main(int argc, char** argv)
        (drivers/ui/ui_configuration.c:70-230 defaults unless overridden) */
     ts.txrx_mode = TRX_MODE_RX;                    /* src/uhsdr_main.c:181-182 */
     ts.samp_rate = IQ_SAMPLE_RATE;
-    ts.beep_frequency = DEFAULT_BEEP_FREQUENCY;    /* ui_configuration.c defaults */
-    ts.beep_loudness = DEFAULT_BEEP_LOUDNESS;
     ts.dmod_mode = mode;
     ts.rx_iq_source = RX_IQ_CODEC;
     ts.tx_audio_source = TX_AUDIO_MIC;
@@ -219,7 +240,14 @@ int main(int argc, char** argv)
     ts.dsp.peak_frequency = iarg(argc, argv, "peak", 750);
     ts.dsp.bass_gain = iarg(argc, argv, "bass", 2);
     ts.dsp.treble_gain = iarg(argc, argv, "treble", 0);
-    ts.stereo_enable = false;
+    ts.stereo_enable = iarg(argc, argv, "stereo", 0);
+    /* LMS auto notch (audio_driver.c:1166-1186; defaults audio_driver.h:486-495) */
+    ts.dsp.notch_numtaps = DSP_NOTCH_NUMTAPS_DEFAULT;
+    ts.dsp.notch_delaybuf_len = DSP_NOTCH_DELAYBUF_DEFAULT;
+    ts.dsp.notch_mu = iarg(argc, argv, "notch_mu", DSP_NOTCH_MU_DEFAULT);
+    ts.fm_subaudible_tone_det_select = iarg(argc, argv, "tonedet", 0);
+    ts.beep_frequency = iarg(argc, argv, "beepfreq", DEFAULT_BEEP_FREQUENCY);
+    ts.beep_loudness = iarg(argc, argv, "beeploud", DEFAULT_BEEP_LOUDNESS);
     ts.cw_sidetone_freq = iarg(argc, argv, "sidetone", CW_SIDETONE_FREQ_DEFAULT);   /* CW decoder Goertzel */
     ts.cw_keyer_speed = 20;                        /* CW_KEYER_SPEED_DEFAULT (ui_configuration.h:59) */
     ts.cw_keyer_weight = CW_KEYER_WEIGHT_DEFAULT;
@@ -287,6 +315,16 @@ int main(int argc, char** argv)
     fclose(f);
 
     IqSample_t blk[IQ_BLOCK_SIZE];
+    long beep0 = -1, beepn = 0;
+    {
+        const char* b = arg(argc, argv, "beep", NULL);
+        if (b && sscanf(b, "%ld:%ld", &beep0, &beepn) != 2) { fprintf(stderr, "beep=b0:K\n"); return 2; }
+        if (b) ts.flags2 |= FLAGS2_KEY_BEEP_ENABLE;
+    }
+    const char* out_a0 = arg(argc, argv, "out_a0", NULL);
+    const char* out_clip = arg(argc, argv, "out_clip", NULL);
+    float* a0s = out_a0 ? calloc(n, sizeof(float)) : NULL;
+    uint8_t* clips = out_clip ? calloc(n / block, 1) : NULL;
     const char* out_cw = arg(argc, argv, "out_cw", NULL);        /* Goertzel energy per CW block */
     const char* out_cws = arg(argc, argv, "out_cws", NULL);      /* ads.CW_signal after each call */
     uint8_t* cw_signal = out_cws ? calloc(n / block, 1) : NULL;
@@ -319,8 +357,22 @@ int main(int argc, char** argv)
     for (long off = 0; off < n; off += block)
     {
         memcpy(blk, iq + off, sizeof(IqSample_t) * block);   /* the ISR's DMA half-buffer */
+        const long call = off / block;
+        if (beep0 >= 0)
+        {
+            /* AudioManagement_KeyBeep (audio_management.c:368-375) at call b0, then the UI's
+               countdown of ts.beep_timing (ui_driver.c:7214-7216) held to K calls */
+            if (call == beep0) AudioManagement_KeyBeep();
+            ts.beep_timing = (call >= beep0 && call < beep0 + beepn) ? 1 : 0;
+        }
         AudioDriver_I2SCallback(dst + off, blk, NULL, block);
         memcpy(a1 + off, adb.a_buffer[1], sizeof(float) * block);
+        if (a0s) memcpy(a0s + off, adb.a_buffer[0], sizeof(float) * block);
+        if (clips)
+        {
+            clips[call] = (uint8_t)((ads.adc_clip ? 1 : 0) | (ads.adc_half_clip ? 2 : 0) | (ads.adc_quarter_clip ? 4 : 0));
+            ads.adc_clip = ads.adc_half_clip = ads.adc_quarter_clip = 0;
+        }
         if (cw_signal) cw_signal[off / block] = ads.CW_signal;
         if (spec && (off + block) % (ring / 2 * zd) == 0)  /* the ring holds ring/2 new samples */
             ref_spec_snapshot(stream + 2 * ((off + block) / zd - ring / 2));
@@ -349,6 +401,8 @@ int main(int argc, char** argv)
     }
     if (out_cws) { f = fopen(out_cws, "wb"); fwrite(cw_signal, 1, n / block, f); fclose(f); free(cw_signal); }
     if (out_dst) { f = fopen(out_dst, "wb"); fwrite(dst, sizeof(AudioSample_t), n, f); fclose(f); }
+    if (a0s) { f = fopen(out_a0, "wb"); fwrite(a0s, sizeof(float), n, f); fclose(f); free(a0s); }
+    if (clips) { f = fopen(out_clip, "wb"); fwrite(clips, 1, n / block, f); fclose(f); free(clips); }
     free(iq); free(dst); free(a1);
     return 0;
 }

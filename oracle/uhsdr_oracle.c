@@ -401,12 +401,29 @@ static void demod_sam(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, c
     }
 }
 
-/* AudioDriver_DemodFM, audio_driver.c:1544-1737 (subaudible tone detection off); returns
-   signal_active = !squelched after this call's squelch update */
+/* AudioFilter_GoertzelInput / _Energy, audio_filter.c:1290-1305 */
+static void goertzel_in(float r, float* b, float in)
+{
+    const float b0 = r * b[0] - b[1] + in;
+    b[1] = b[0];
+    b[0] = b0;
+}
+static float goertzel_energy(float co, float si, float* b)
+{
+    const float a = (b[0] - (b[1] * co));
+    const float bb = (b[1] * si);
+    b[0] = 0;
+    b[1] = 0;
+    return sqrtf(a * a + bb * bb);
+}
+
+/* AudioDriver_DemodFM, audio_driver.c:1544-1737, with the subaudible tone detector (:1665-1734);
+   returns signal_active = !squelched after this call's squelch update */
 static int demod_fm(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, const float* qb, float* a0, int n)
 {
-    float sq[BLK];
+    float sq[BLK], gbuf[BLK];
     if (p->freq_shift_hz == 0) return !s->fm_squelched;      /* bails out without translation (:1548) */
+    const int tone_en = p->tone_det_enabled;
     for (int i = 0; i < n; i++)
     {
         const float y = (s->fm_i_prev * qb[i]) - (ib[i] * s->fm_q_prev);
@@ -415,7 +432,8 @@ static int demod_fm(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, con
         sq[i] = angle;
         const float a = s->fm_lpf_prev + (0.05 * (angle - s->fm_lpf_prev));     /* FM_RX_LPF_ALPHA */
         s->fm_lpf_prev = a;
-        if (!s->fm_squelched || !p->fm_sql_threshold)
+        gbuf[i] = a;
+        if ((!s->fm_squelched && !tone_en) || (s->fm_tone_detected && tone_en) || !p->fm_sql_threshold)
         {
             const float b = 0.96 * (s->fm_hpf_prev_b + a - s->fm_hpf_prev_a);  /* FM_RX_HPF_ALPHA */
             s->fm_hpf_prev_a = a;
@@ -453,7 +471,72 @@ static int demod_fm(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, con
             s->fm_squelched = 1;
         }
     }
+    if (tone_en)
+    {
+        s->fm_gcount++;
+        for (int i = 0; i < n; i++)
+        {
+            goertzel_in(p->tone_r[0], s->fm_g[0], gbuf[i]);     /* FM_HIGH */
+            goertzel_in(p->tone_r[1], s->fm_g[1], gbuf[i]);     /* FM_LOW */
+            goertzel_in(p->tone_r[2], s->fm_g[2], gbuf[i]);     /* FM_CTR */
+        }
+        if (s->fm_gcount >= 400)                                /* FM_SUBAUDIBLE_GOERTZEL_WINDOW */
+        {
+            const float so = goertzel_energy(p->tone_cos[0], p->tone_sin[0], s->fm_g[0])
+                           + goertzel_energy(p->tone_cos[1], p->tone_sin[1], s->fm_g[1]);
+            const float r = goertzel_energy(p->tone_cos[2], p->tone_sin[2], s->fm_g[2]);
+            s->fm_subdet = ((1 - 0.9) * s->fm_subdet) + (r / (so / 2) * 0.9);    /* FM_TONE_DETECT_ALPHA */
+            if (s->fm_subdet > 1.75)                            /* FM_SUBAUDIBLE_TONE_DET_THRESHOLD */
+            {
+                s->fm_tdet++;
+                if (s->fm_tdet > 5) s->fm_tdet = 5;             /* FM_SUBAUDIBLE_DEBOUNCE_MAX */
+            }
+            else if (s->fm_tdet)
+                s->fm_tdet--;
+            s->fm_tone_detected = s->fm_tdet >= 2;              /* FM_SUBAUDIBLE_TONE_DEBOUNCE_THRESHOLD */
+            s->fm_gcount = 0;
+        }
+    }
     return !s->fm_squelched;
+}
+
+/* AudioDriver_NotchFilter (audio_driver.c:1746-1763): delay line + arm_lms_norm_f32
+   (CMSIS .../arm_lms_norm_f32.c, sequential tap order) in place on a0 */
+static void notch_run(const uhsdr_rx_plan* p, uo_rx_state* s, float* a0, int n)
+{
+    const int T = p->notch_taps, D = p->notch_delay_len;
+    memcpy(&s->notch_delay[s->notch_in], a0, sizeof(float) * n);
+    const float* ref = &s->notch_delay[s->notch_out];
+    float* st = s->notch_st;                  /* [0 .. T-2] carried, new samples appended */
+    const float mu = p->notch_mu;
+    for (int i = 0; i < n; i++)
+    {
+        const float in = a0[i];
+        st[T - 1 + i] = in;
+        s->notch_energy -= s->notch_x0 * s->notch_x0;
+        s->notch_energy += in * in;
+        float sum = 0.0f;
+        for (int k = 0; k < T; k++) sum += st[i + k] * s->notch_w[k];
+        const float e = ref[i] - sum;
+        a0[i] = e;
+        const float w = (e * mu) / (s->notch_energy + 0.000000119209289f);
+        for (int k = 0; k < T; k++) s->notch_w[k] += w * st[i + k];
+        s->notch_x0 = st[i];
+    }
+    memmove(st, st + n, sizeof(float) * (T - 1));
+    s->notch_in += n;
+    s->notch_out = s->notch_in + n;
+    s->notch_in %= D;
+    s->notch_out %= D;
+}
+
+void uo_rx_key_beep(uo_rx_state* states, int C, int calls)
+{
+    for (int c = 0; c < C; c++)
+    {
+        states[c].beep_acc = 0;               /* AudioManagement_KeyBeep, audio_management.c:372 */
+        states[c].beep_left = calls;
+    }
 }
 
 /* float -> int32 as x86 cvttss2si does it (out of range / NaN -> INT32_MIN), then the
@@ -462,6 +545,21 @@ static int32_t to_dma(float f)
 {
     int32_t v = (f > -2147483904.0f && f < 2147483648.0f) ? (int32_t)f : INT32_MIN;
     return (int32_t)((uint32_t)v << 16);
+}
+
+/* key beep (audio_driver.c:2891-2898): is it on for this call (ts.beep_timing > 0)? */
+static int beep_on(const uhsdr_rx_plan* p, uo_rx_state* s)
+{
+    if (s->beep_left <= 0 || p->beep_step == 0) return 0;
+    s->beep_left--;
+    return 1;
+}
+/* softdds_nextSample (softdds.h:48-66) x ads.beep_loudness_factor */
+static float beep_next(const uhsdr_rx_plan* p, uo_rx_state* s)
+{
+    const uint32_t k = (s->beep_acc >> 22) % 1024;
+    s->beep_acc += p->beep_step;
+    return (float)p->dds_table[k] * p->beep_scale;
 }
 
 /* one AudioDriver_RxProcessor call on BLK frames, audio_driver.c:2603-2942 */
@@ -566,9 +664,11 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
         const int active = demod_fm(p, s, ib, qb, a0, n);
         for (int i = 0; i < n; i++) a1[i] = a0[i] * p->fm_scale;
         biquad_df1(p->biquad2, 1, s->bq2, a1, n);      /* audio_driver.c:2832 */
+        const int beep = beep_on(p, s);
         for (int i = 0; i < n; i++)
         {
-            const float v = active ? a1[i] * p->line_out_scale : 0.0f;    /* mute when squelched, :2843-2850 */
+            float v = active ? a1[i] * p->line_out_scale : 0.0f;    /* mute when squelched, :2843-2850 */
+            if (beep) v += beep_next(p, s);
             out_a1[i] = v;
             const int32_t d = active ? to_dma(v) : 0;
             if (dst) { dst[2 * i] = d; dst[2 * i + 1] = d; }
@@ -586,6 +686,7 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
         fir_decimate(p->dec, p->dec_taps, p->decimation_rate, s->dec_i, a0, a0, niq);
 
     /* RxProcessor_DemodAudioPostprocessing, audio_driver.c:2436-2592 */
+    if (p->notch_enabled) notch_run(p, s, a0, nd);
     if (p->pre_stages > 0) iir_lattice(p->pre_k, p->pre_v, p->pre_stages, s->pre, a0, a0, nd);
     agc_run(&p->agc, s, a0, nd);
     for (int i = 0; i < nd; i++) a0[i] = a0[i] * p->post_agc_scale;
@@ -596,6 +697,8 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
 
     biquad_df1(p->biquad2, 1, s->bq2, a1, n);          /* audio_driver.c:2832 */
     for (int i = 0; i < n; i++) a1[i] = a1[i] * p->line_out_scale;   /* :2860 (OVI40) */
+    if (beep_on(p, s))
+        for (int i = 0; i < n; i++) a1[i] += beep_next(p, s);
     for (int i = 0; i < n; i++)
     {
         out_a1[i] = a1[i];

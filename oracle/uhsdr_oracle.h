@@ -57,12 +57,25 @@ typedef struct uo_rx_state
     /* outputs of the current call: energies of blocks completed, ads.CW_signal */
     float cw_energy_out;
     int32_t cw_blocks_out, cw_signal_out;
+    /* lmsData (audio_driver.c:58-66) and AudioDriver_NotchFilter's statics lms2_inbuf/_outbuf */
+    float notch_w[64], notch_st[64 + 16], notch_delay[128];
+    float notch_energy, notch_x0;
+    int32_t notch_in, notch_out;
+    /* FM subaudible tone detector: ads.fm_conf.goertzel[3].buf[1..2], fm_data.subdet / tdet /
+       gcount, ads.fm_conf.subaudible_tone_detected */
+    float fm_g[3][2], fm_subdet;
+    int32_t fm_tdet, fm_gcount, fm_tone_detected;
+    /* key beep: ts.beep_timing as calls left, ads.beep.acc */
+    int32_t beep_left;
+    uint32_t beep_acc;
 } uo_rx_state;
 
 size_t uo_rx_state_size(void);
 void uo_rx_state_init(const uhsdr_rx_plan* p, uo_rx_state* s);
 /* one channel, n frames (n % 32 == 0): iq [n][2] int32 -> a1 [n] f32, dst [n][2] int32 */
 int uo_rx_process(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, int n, float* a1, int32_t* dst);
+/* AudioManagement_KeyBeep on C channel states: the next `calls` calls get the beep tone */
+void uo_rx_key_beep(uo_rx_state* states, int C, int calls);
 /* C channels, channel-major buffers, `threads` POSIX threads (0 = 1) */
 long long uo_rx_bench(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int pool, int n,
                       float* a1, int32_t* dst, int threads, int pin, double budget_s, double* elapsed);

@@ -79,6 +79,29 @@ CONFIGS = {
     "p1_fm_sql0": ({"mode": 5, "path": 1, "sql": 0}, {"fm": True, "frames": 8192}),
     "p2_fm5k": ({"mode": 5, "path": 2, "sql": 2, "fm5k": 1}, {"fm": True, "frames": 8192, "deviation": 5000.0}),
     "p3_fm_noise": ({"mode": 5, "path": 3, "sql": 18}, {"fm": True, "frames": 8192, "amplitude": 40.0}),
+    # LMS auto notch (DSP_NOTCH_ENABLE = 4; AudioDriver_NotchFilter, audio_driver.c:1746-1763,
+    # called at :2443-2456 except in CW and in SAM at 24 ksps)
+    "p48_notch": ({"mode": 0, "path": 48, "dsp": 4}, {}),
+    "p48_notch_mu25_lsb": ({"mode": 1, "path": 48, "dsp": 4 | 0x30, "notch_mu": 25}, {"lsb": True}),
+    "p35_notch": ({"mode": 0, "path": 35, "dsp": 4, "notch_mu": 3}, {}),
+    "p55_notch": ({"mode": 0, "path": 55, "dsp": 4, "notch_mu": 40}, {}),
+    "p70_am_notch": ({"mode": 3, "path": 70, "dsp": 4}, {"am": True}),
+    "p70_sam_notch": ({"mode": 4, "path": 70, "dsp": 4, "notch_mu": 20}, {"am": True}),
+    "p83_am_notch": ({"mode": 3, "path": 83, "dsp": 4}, {"am": True}),
+    "p83_sam_notch": ({"mode": 4, "path": 83, "dsp": 4}, {"am": True}),
+    "p4_cw_notch": ({"mode": 2, "path": 4, "dsp": 4}, {}),
+    # key beep (audio_driver.c:2891-2898, softdds): AudioManagement_KeyBeep at call b0, tone for
+    # K calls (beep=b0:K; b0 on an 8-call boundary so 256-frame device calls can replay it)
+    "p48_beep": ({"mode": 0, "path": 48, "beep": "8:20"}, {}),
+    "p48_beep_loud": ({"mode": 0, "path": 48, "beep": "0:64", "beepfreq": 740, "beeploud": 20}, {}),
+    "p70_sam_beep": ({"mode": 4, "path": 70, "beep": "16:33", "beepfreq": 1750}, {"am": True}),
+    "p1_fm_beep": ({"mode": 5, "path": 1, "sql": 0, "beep": "40:100"}, {"fm": True, "frames": 8192}),
+    # FM subaudible tone detector (audio_driver.c:1665-1734): Goertzel window of 400 calls,
+    # debounce 2, so 1280 calls (40960 frames) see three detector decisions
+    "p1_fm_tone": ({"mode": 5, "path": 1, "tonedet": 10}, {"fm": True, "frames": 40960, "subtone": 91.5, "nch": 2}),
+    "p1_fm_tone_absent": ({"mode": 5, "path": 1, "tonedet": 10, "sql": 0}, {"fm": True, "frames": 40960, "nch": 2}),
+    "p2_fm_tone_sql3": ({"mode": 5, "path": 2, "tonedet": 10, "fm5k": 1, "sql": 3},
+                        {"fm": True, "frames": 40960, "subtone": 91.5, "deviation": 5000.0, "nch": 2}),
 }
 
 # SSB transmit (C4, TxProcessor_Run): microphone two-tone in, IQ frames out (tests/golden/tx_*.npz)
@@ -227,16 +250,20 @@ def spectrum_tables():
         json.dump(d, fo, separators=(",", ":"))
 
 
-def run_ref(args: dict, iq: np.ndarray):
+def run_ref(args: dict, iq: np.ndarray, want_a0: bool = False):
     n = iq.shape[0]
     with tempfile.TemporaryDirectory() as td:
-        fin, fa, fd = (os.path.join(td, x) for x in ("in.bin", "a.bin", "d.bin"))
+        fin, fa, fd, fa0 = (os.path.join(td, x) for x in ("in.bin", "a.bin", "d.bin", "a0.bin"))
         iq.astype(np.int32).tofile(fin)
         cmd = [REF, f"in={fin}", f"n={n}", f"out_a={fa}", f"out_dst={fd}"]
+        if want_a0:
+            cmd.append(f"out_a0={fa0}")
         cmd += [f"{k}={v}" for k, v in args.items()]
         subprocess.run(cmd, check=True)
         a1 = np.fromfile(fa, dtype=np.float32)
         dst = np.fromfile(fd, dtype=np.int32).reshape(n, 2)
+        if want_a0:
+            return a1, dst, np.fromfile(fa0, dtype=np.float32)
     return a1, dst
 
 
@@ -250,17 +277,26 @@ def make(name: str):
     sig = dict(sig)
     center = sig.pop("center", None)
     nframes = sig.pop("frames", NFRAMES)
+    nch = sig.pop("nch", NCH)
     if sig.pop("fm", False):
-        iq = synth.fm_iq(np.arange(NCH), 0, nframes, **sig)
+        iq = synth.fm_iq(np.arange(nch), 0, nframes, **sig)
     elif sig.pop("am", False):
         iq = synth.am_iq(np.arange(NCH), 0, NFRAMES)
     else:
         iq = synth.ssb_iq(np.arange(NCH), 0, NFRAMES, carrier=center if center is not None else 12000.0, **sig)
-    a1 = np.empty((NCH, iq.shape[1]), np.float32)
-    dst = np.empty((NCH, iq.shape[1], 2), np.int32)
-    for c in range(NCH):
-        a1[c], dst[c] = run_ref(args, iq[c])
-    np.savez_compressed(os.path.join(HERE, f"rx_{name}.npz"), iq=iq, a1=a1, dst=dst,
+    C = iq.shape[0]
+    a1 = np.empty((C, iq.shape[1]), np.float32)
+    dst = np.empty((C, iq.shape[1], 2), np.int32)
+    extra = {}
+    stereo = bool(args.get("stereo", 0))
+    if stereo:
+        extra["a0"] = np.empty((C, iq.shape[1]), np.float32)
+    for c in range(C):
+        if stereo:
+            a1[c], dst[c], extra["a0"][c] = run_ref(args, iq[c], want_a0=True)
+        else:
+            a1[c], dst[c] = run_ref(args, iq[c])
+    np.savez_compressed(os.path.join(HERE, f"rx_{name}.npz"), iq=iq, a1=a1, dst=dst, **extra,
                         setup=json.dumps(ref_json(args, "setup")), agc=json.dumps(ref_json(args, "agc")),
                         args=json.dumps(args))
     peak = float(np.abs(a1).max())

@@ -13,7 +13,7 @@ import pytest
 
 import oracle
 import uhsdr_amd as U
-from golden_util import assert_bitexact, golden_file, golden_files, load
+from golden_util import assert_bitexact, drive, golden_file, golden_files, load
 from uhsdr_amd import synth
 
 pytestmark = pytest.mark.gpu
@@ -38,11 +38,29 @@ def run_device(cfg, iq, frames_per_call, want_dst=True):
     return a_out, d_out
 
 
+class DeviceStream:
+    """One RxChain fed block by block (golden_util.drive), outputs copied back per call."""
+
+    def __init__(self, cfg, channels, frames):
+        import torch
+        self.torch = torch
+        self.chain = U.RxChain(cfg, channels=channels, frames=frames)
+        self.audio = torch.empty((channels, frames), dtype=torch.float32, device="cuda")
+        self.dst = torch.empty((channels, frames, 2), dtype=torch.int32, device="cuda")
+
+    def __call__(self, iq_block):
+        self.chain.process(self.torch.from_numpy(iq_block).cuda(), self.audio, self.dst)
+        self.torch.cuda.synchronize()
+        return self.audio.cpu().numpy(), self.dst.cpu().numpy()
+
+
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("rx_")[-1][:-4])
 def test_device_matches_reference_firmware(cuda, back, path):
     g = load(path)
     cfg = U.config_from_ref_args(g["args"])
-    a1, dst = run_device(cfg, g["iq"], 256)
+    dev = DeviceStream(cfg, g["iq"].shape[0], 256)
+    a1, dst = drive(g, 256, dev, dev.chain.key_beep)
+    dev.chain.close()
     assert_bitexact(a1, g["a1"], g["name"])
     np.testing.assert_array_equal(dst, g["dst"])
 
@@ -64,6 +82,67 @@ def test_device_matches_oracle_ragged_batches(cuda, back, path, channels):
     ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), channels).process(iq, threads=8)
     assert_bitexact(a1, ref_a1, f"P{path} C={channels}")
     np.testing.assert_array_equal(dst, ref_dst)
+
+
+NOTCH_CASES = [
+    ("p48_usb", dict(filter_path=48), synth.ssb_iq, 200),
+    ("p35_lsb", dict(filter_path=35, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 130),
+    ("p55_usb", dict(filter_path=55, notch_mu=40), synth.ssb_iq, 70),
+    ("p70_am", dict(filter_path=70, dmod_mode=U.DEMOD_AM), synth.am_iq, 129),
+    ("p70_sam", dict(filter_path=70, dmod_mode=U.DEMOD_SAM, notch_mu=25), synth.am_iq, 96),
+    ("p75_sam_lsb", dict(filter_path=75, dmod_mode=U.DEMOD_SAM, sam_sideband=U.SAM_SIDEBAND_LSB), synth.am_iq, 65),
+    ("p83_am", dict(filter_path=83, dmod_mode=U.DEMOD_AM), synth.am_iq, 64),
+]
+
+
+@pytest.mark.parametrize("name,kw,gen,C", NOTCH_CASES, ids=[c[0] for c in NOTCH_CASES])
+def test_device_notch_matches_oracle(cuda, back, name, kw, gen, C):
+    """LMS auto notch (rx_notch, + the AM / SAM demodulator ahead of it) on ragged batches over
+    the 128-sample delay line's full cycle (1024 calls of 32 frames would be 4 cycles; 48 calls
+    here pass the wrap at 16 / 8 calls and the first-call self reference)."""
+    cfg = U.default_config(dsp_active=U.DSP_NOTCH_ENABLE, **kw)
+    assert U.build_plan(cfg).notch_enabled
+    iq = gen(np.arange(C), 0, 48 * 32)
+    a1, dst = run_device(cfg, iq, 256)
+    ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    assert_bitexact(a1, ref_a1, f"notch {name}")
+    np.testing.assert_array_equal(dst, ref_dst)
+
+
+@pytest.mark.parametrize("frames", [32, 64, 512])
+def test_device_beep_call_sizes(cuda, back, frames):
+    """Key beep across call sizes: started between launches, ending inside one, restarted."""
+    import torch
+    cfg = U.default_config(beep_frequency=880, beep_loudness=15)
+    C, n = 70, 2048
+    iq = synth.ssb_iq(np.arange(C), 0, n)
+    o = oracle.OracleRx(U.build_plan(cfg), C)
+    chain = U.RxChain(cfg, channels=C, frames=frames)
+    audio = torch.empty((C, frames), dtype=torch.float32, device="cuda")
+    got, ref = [], []
+    for k, off in enumerate(range(0, n, frames)):
+        if k in (1, 5):
+            chain.key_beep(21 if k == 1 else 3)
+            o.key_beep(21 if k == 1 else 3)
+        blk = np.ascontiguousarray(iq[:, off:off + frames])
+        chain.process(torch.from_numpy(blk).cuda(), audio, None)
+        torch.cuda.synchronize()
+        got.append(audio.cpu().numpy())
+        ref.append(o.process(blk)[0])
+    chain.close()
+    assert_bitexact(np.concatenate(got, axis=1), np.concatenate(ref, axis=1), f"beep frames={frames}")
+
+
+def test_device_fm_tone_detector_matches_oracle(cuda):
+    """FM subaudible tone detector on 100 channels, half carrying the selected CTCSS tone."""
+    cfg = U.default_config(filter_path=1, dmod_mode=U.DEMOD_FM, fm_tone_det=10)
+    C, n = 100, 1600 * 32
+    iq = np.concatenate([synth.fm_iq(np.arange(50), 0, n, subtone=91.5), synth.fm_iq(np.arange(50, 100), 0, n)])
+    a1, dst = run_device(cfg, iq, 2048)
+    ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    assert_bitexact(a1, ref_a1, "fm tone detector")
+    np.testing.assert_array_equal(dst, ref_dst)
+    assert np.abs(a1[:50, -2048:]).max() > 1000 and np.abs(a1[50:, -2048:]).max() == 0
 
 
 def test_device_c2_batch_sampled_channels(cuda):

@@ -8,7 +8,7 @@ import pytest
 
 import oracle
 import uhsdr_amd as U
-from golden_util import assert_bitexact, golden_file, golden_files, load
+from golden_util import assert_bitexact, drive, golden_file, golden_files, load
 
 
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("rx_")[-1][:-4])
@@ -16,7 +16,7 @@ def test_oracle_matches_reference(path):
     g = load(path)
     plan = U.build_plan(U.config_from_ref_args(g["args"]))
     o = oracle.OracleRx(plan, g["iq"].shape[0])
-    a1, dst = o.process(g["iq"])
+    a1, dst = drive(g, 256, o.process, o.key_beep)
     assert_bitexact(a1, g["a1"], g["name"])
     np.testing.assert_array_equal(dst, g["dst"])
 

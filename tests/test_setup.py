@@ -66,3 +66,27 @@ def test_plan_rejects_bad_config():
                  dict(filter_path=1)]:   # FM-only path for USB
         cfg = U.default_config(**over)
         assert lib.uhsdr_rx_plan_build(C.byref(cfg), C.byref(plan)) == -1, over
+
+
+@pytest.mark.parametrize("path", [p for p in golden_files() if "notch_mu" in load(p)["setup"]],
+                         ids=lambda p: p.split("rx_")[-1][:-4])
+def test_notch_beep_tone_setup_matches_reference(path):
+    """ABI 2 plan fields against the reference build's own setup: the LMS notch mu
+    (audio_driver.c:1170), the key beep's softdds step and loudness (audio_management.c:354-363)
+    and the FM subaudible tone detector's three Goertzels (audio_management.c:313-326)."""
+    g = load(path)
+    s = g["setup"]
+    p = U.build_plan(U.config_from_ref_args(g["args"]))
+    assert np.array([p.notch_mu], np.float32).view(np.uint32)[0] == s["notch_mu"][0]
+    assert p.beep_step == s["beep_step"]
+    assert np.array([p.beep_scale], np.float32).view(np.uint32)[0] == s["beep_scale"][0]
+    det = np.array([s["tone_det_freq"]], np.uint32).view(np.float32)[0]
+    assert bool(p.tone_det_enabled) == (det != 0)
+    if det:
+        mine = np.array([[p.tone_r[i], p.tone_cos[i], p.tone_sin[i]] for i in range(3)], np.float32).ravel()
+        np.testing.assert_array_equal(mine.view(np.uint32), np.array(s["tone_goertzel"], np.uint32))
+    dsp = g["args"].get("dsp", 0)
+    mode = g["args"]["mode"]
+    expect_notch = bool(dsp & 4) and mode not in (U.DEMOD_CW, U.DEMOD_FM) and not (mode == U.DEMOD_SAM and
+                                                                                  p.decimated_freq == 24000)
+    assert bool(p.notch_enabled) == expect_notch

@@ -24,8 +24,9 @@ UHSDR_LENGTH_ERROR = -2
 UHSDR_UNSUPPORTED = -10
 UHSDR_DEVICE_ERROR = -11
 
-DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI = range(7)
-SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB = range(3)
+DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI, DEMOD_SSBSTEREO, DEMOD_IQ = range(9)
+SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB, SAM_SIDEBAND_STEREO = range(4)
+DSP_NOTCH_ENABLE, DSP_MNOTCH_ENABLE, DSP_MPEAK_ENABLE = 0x04, 0x10, 0x20
 PRECISION_EXACT, PRECISION_FMA = 0, 1          # uhsdr_rx_set_precision
 
 
@@ -41,7 +42,9 @@ class RxConfig(C.Structure):
         ("sam_sideband", C.c_int32), ("sam_pll_fmax", C.c_int32), ("sam_zeta", C.c_int32), ("sam_omega_n", C.c_int32),
         ("fade_leveler", C.c_int32), ("fm_sql_threshold", C.c_int32), ("fm_deviation_5k", C.c_int32),
         ("cw_sidetone_freq", C.c_int32), ("cw_decoder_blocksize", C.c_int32), ("cw_decoder_thresh", C.c_int32),
-        ("cw_decoder_noisecancel", C.c_int32), ("reserved", C.c_int32 * 5),
+        ("cw_decoder_noisecancel", C.c_int32),
+        ("notch_mu", C.c_int32), ("fm_tone_det", C.c_int32), ("beep_frequency", C.c_int32),
+        ("beep_loudness", C.c_int32), ("stereo_enable", C.c_int32), ("reserved", C.c_int32 * 11),
     ]
 
 
@@ -80,7 +83,11 @@ class RxPlan(C.Structure):
         ("sq_k", C.c_float * MAX_LATTICE), ("sq_v", C.c_float * (MAX_LATTICE + 1)),
         ("cw_enabled", C.c_int32), ("cw_blocksize", C.c_int32), ("cw_noisecancel", C.c_int32),
         ("cw_thresh", C.c_float), ("cw_r", C.c_float), ("cw_cos", C.c_float), ("cw_sin", C.c_float),
-        ("reserved", C.c_int32 * 57),
+        ("notch_enabled", C.c_int32), ("notch_taps", C.c_int32), ("notch_delay_len", C.c_int32),
+        ("notch_mu", C.c_float), ("tone_det_enabled", C.c_int32), ("tone_r", C.c_float * 3),
+        ("tone_cos", C.c_float * 3), ("tone_sin", C.c_float * 3), ("beep_step", C.c_uint32),
+        ("beep_scale", C.c_float), ("stereo", C.c_int32), ("dds_table", C.c_int16 * 1024),
+        ("reserved", C.c_int32 * 32),
     ]
 
 
@@ -172,6 +179,7 @@ SIGNATURES = {
     "uhsdr_rx_set_cw_outputs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "uhsdr_rx_cw_blocks_max": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_cw_blocks_last": (C.c_int32, [C.c_void_p]),
+    "uhsdr_rx_key_beep": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_device_alloc": (C.c_void_p, [C.c_uint64]),
     "uhsdr_device_free": (None, [C.c_void_p]),
     "uhsdr_copy_to_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
@@ -271,12 +279,15 @@ REF_ARG_MAP = {
     "sam_sb": "sam_sideband", "pll_fmax": "sam_pll_fmax", "zeta": "sam_zeta", "omegan": "sam_omega_n",
     "fade": "fade_leveler", "sql": "fm_sql_threshold", "fm5k": "fm_deviation_5k",
     "sidetone": "cw_sidetone_freq", "cwblock": "cw_decoder_blocksize", "cwthresh": "cw_decoder_thresh",
-    "cwnc": "cw_decoder_noisecancel",
+    "cwnc": "cw_decoder_noisecancel", "notch_mu": "notch_mu", "tonedet": "fm_tone_det",
+    "beepfreq": "beep_frequency", "beeploud": "beep_loudness", "stereo": "stereo_enable",
 }
+# uhsdr_ref run-time controls that are calls, not configuration (tests drive them through the ABI)
+REF_RUNTIME_ARGS = {"beep"}
 
 
 def config_from_ref_args(args: dict) -> RxConfig:
-    return default_config(**{REF_ARG_MAP[k]: v for k, v in args.items()})
+    return default_config(**{REF_ARG_MAP[k]: v for k, v in args.items() if k not in REF_RUNTIME_ARGS})
 
 
 # uhsdr_ref TX key=value names (tests/golden/tx_*.npz) -> TxConfig fields

@@ -375,6 +375,8 @@ struct BackState
     int* agci;       // [3][C]   hang_counter decay_type state
     float* sam;      // AM / SAM: [7 + 96][C] phs omega2 fil_out dsI dsQ dc27 dc_insert | allpass a,b,c,d[24]
     float* cw;       // CW decoder front end: [5][C] goertzel buf[1] buf[2], old_siglevel, cw_state, change
+    float* notch;    // LMS auto notch: [64][C] coefficients, [64][C] state (63 used), [2][C] energy x0,
+                     // [128][C] de-correlation delay line (lmsData, audio_driver.c:58-66)
 };
 
 struct BackArgs
@@ -391,7 +393,24 @@ struct BackArgs
     float* cw_energy;    // optional [C][cw_bmax]: Goertzel energy per completed CW block
     int cw_count0;       // CwDecode_RxProcessor's sample_counter at launch start (same for all channels)
     int cw_bmax;
+    // LMS notch delay line (AudioDriver_NotchFilter's lms2_inbuf / lms2_outbuf, audio_driver.c:
+    // 1749-1761): slot of the launch's first call in units of one call's samples, and whether that
+    // call is the first since reset (both statics start at 0, so call 0 reads its own input back)
+    int notch_slot0, notch_first;
+    // key beep (audio_driver.c:2891-2898): frames [beep_n0, beep_n1) of this launch get the softdds
+    // tone; beep_acc = the DDS accumulator at frame beep_n0 (common to all channels)
+    int beep_n0, beep_n1;
+    uint32_t beep_acc;
+    int tone_phase;      // FM subaudible tone detector: fm_data.gcount at launch start (mod 400)
 };
+
+// softdds_addSingleToneToTwobuffers (softdds.c:142-152): the tone of launch frame n
+__device__ __forceinline__ float beep_tone(const BackArgs& a, int n)
+{
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    const uint32_t acc = a.beep_acc + (uint32_t)(n - a.beep_n0) * P->beep_step;
+    return (float)P->dds_table[(acc >> 22) % 1024] * P->beep_scale;
+}
 
 // Math_log10f_fast, misc/uhsdr_math.c:26-39
 __device__ __forceinline__ float log10f_fast(float X)
@@ -1154,7 +1173,12 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
         {
             float y[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) y[j] = s.step(mi[(n0 + j) * BACK_CH]);
+            for (int j = 0; j < 4; ++j)
+            {
+                y[j] = s.step(mi[(n0 + j) * BACK_CH]);
+                const int fr = call * BLK + n0 + j;
+                if (fr >= a.beep_n0 && fr < a.beep_n1) y[j] += beep_tone(a, fr);
+            }
             back_store4(a, l, call, n0, y);
         }
     BACK_ROLE_END
@@ -1237,6 +1261,15 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
 #pragma unroll
             for (int j = 0; j < L; ++j) y[m * L + j] = ou.step(aa.step(u[j]));
         }
+        if (a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK)
+        {
+#pragma unroll
+            for (int n = 0; n < BLK; ++n)
+            {
+                const int fr = call * BLK + n;
+                if (fr >= a.beep_n0 && fr < a.beep_n1) y[n] += beep_tone(a, fr);
+            }
+        }
 #pragma unroll
         for (int n0 = 0; n0 < BLK; n0 += 4)
         {
@@ -1255,6 +1288,104 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
 }
 
 // ------------------------------------------------------------------------------------
+// rx_notch: the LMS auto notch (AudioDriver_NotchFilter, audio_driver.c:1746-1763, called from
+// RxProcessor_DemodAudioPostprocessing :2443-2456 when DSP_NOTCH_ENABLE is set), in place on the
+// decimated audio a_buffer[0] between the demodulator and the IIR pre-filter.  Lane == channel:
+// arm_lms_norm_f32 (CMSIS .../FilteringFunctions/arm_lms_norm_f32.c) is a per-sample recursion
+// over its 64 coefficients, so each lane holds its channel's coefficients and the 63-sample
+// state window in registers for the launch.  Per call:
+//   arm_copy_f32(a_buffer[0] -> delay[inbuf])            (the de-correlation delay line)
+//   arm_lms_norm_f32(src = a_buffer[0], ref = delay[outbuf], out = errsig2, err = a_buffer[0])
+//   inbuf += B; outbuf = inbuf + B (mod 128)
+// and per sample, in CMSIS order: state[63] = in; energy -= x0*x0; energy += in*in;
+// y = sum_k state[k] * w[k] (k = 0..63 from +0.0f); e = ref - y; out = e;
+// mu_w = (e * mu) / (energy + 1.19209289e-7); w[k] += mu_w * state[k]; x0 = state[0]; slide.
+// AM / SAM (DM != DM_NONE): the demodulator runs here first (DemodStage, its state in
+// BackState.sam), the notched audio goes to adec and rx_back runs its DM_NONE variant.
+constexpr int NOTCH_TAPS = 64, NOTCH_DELAY = 128;
+
+template <int L, int DM>
+__global__ void __launch_bounds__(BACK_CH) rx_notch(BackArgs a)
+{
+    const BackLane l(a);
+    constexpr int NDC = BLK / L;
+    constexpr int SLOTS = NOTCH_DELAY / NDC;             // delay line in units of one call
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    const int C = l.C, cl = l.cl;
+    DemodStage<L, DM> dm;
+    InStage<L> in;
+    if (DM) { dm.load(a, l); dm.fetch(a, l, 0); }
+    else in.fetch(a, l, 0);
+    float* const W = a.s.notch;                          // [64][C] coefficients
+    float* const H = W + (size_t)NOTCH_TAPS * C;         // [64][C] state (63 carried samples)
+    float* const E = H + (size_t)NOTCH_TAPS * C;         // [2][C]  energy, x0
+    float* const R = E + (size_t)2 * C;                  // [128][C] delay line
+    float w[NOTCH_TAPS], st[NOTCH_TAPS - 1 + NDC];
+#pragma unroll
+    for (int k = 0; k < NOTCH_TAPS; ++k) w[k] = W[(size_t)k * C + cl];
+#pragma unroll
+    for (int k = 0; k < NOTCH_TAPS - 1; ++k) st[k] = H[(size_t)k * C + cl];
+    float energy = E[cl], x0 = E[C + cl];
+    const float mu = P->notch_mu;
+    for (int call = 0; call < l.calls; ++call)
+    {
+        float x[NDC];
+        if (DM)
+        {
+            dm.begin(a, l, call);
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) x[m] = dm.step(m);
+        }
+        else
+            in.begin(a, l, call, x);
+        const int si = (a.notch_slot0 + call) % SLOTS, so = (a.notch_slot0 + call + 1) % SLOTS;
+        const bool first = a.notch_first && call == 0;   // lms2_outbuf == lms2_inbuf == 0
+        float d[NDC];
+#pragma unroll
+        for (int m = 0; m < NDC; ++m) d[m] = first ? x[m] : R[(size_t)(so * NDC + m) * C + cl];
+        if (l.live)
+        {
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) R[(size_t)(si * NDC + m) * C + l.c] = x[m];
+        }
+        float o[NDC];
+#pragma unroll
+        for (int m = 0; m < NDC; ++m)
+        {
+            const float xin = x[m];
+            st[NOTCH_TAPS - 1 + m] = xin;
+            energy -= x0 * x0;
+            energy += xin * xin;
+            float sum = 0.0f;
+#pragma unroll
+            for (int k = 0; k < NOTCH_TAPS; ++k) sum += st[m + k] * w[k];
+            const float e = d[m] - sum;
+            o[m] = e;
+            const float wf = (e * mu) / (energy + 0.000000119209289f);
+#pragma unroll
+            for (int k = 0; k < NOTCH_TAPS; ++k) w[k] += wf * st[m + k];
+            x0 = st[m];
+        }
+#pragma unroll
+        for (int k = 0; k < NOTCH_TAPS - 1; ++k) st[k] = st[k + NDC];
+        if (l.live)
+        {
+            float* dst = const_cast<float*>(a.adec) + (size_t)l.c * a.Nd + call * NDC;
+#pragma unroll
+            for (int m = 0; m < NDC; m += 4) *(float4*)(dst + m) = make_float4(o[m], o[m + 1], o[m + 2], o[m + 3]);
+        }
+    }
+    if (!l.live) return;
+    if (DM) dm.store(a, l);
+#pragma unroll
+    for (int k = 0; k < NOTCH_TAPS; ++k) W[(size_t)k * C + l.c] = w[k];
+#pragma unroll
+    for (int k = 0; k < NOTCH_TAPS - 1; ++k) H[(size_t)k * C + l.c] = st[k];
+    E[l.c] = energy;
+    E[C + l.c] = x0;
+}
+
+// ------------------------------------------------------------------------------------
 // rx_fm: FM receive after the Hilbert pair (AudioDriver_DemodFM, audio_driver.c:1544-1737,
 // and the FM branch of AudioDriver_RxProcessor, :2818-2850).  Two waves over 64 channels:
 //   wave 0  discriminator atan2f -> de-emphasis LPF -> HPF (or 0 when squelched) per sample;
@@ -1264,9 +1395,11 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
 //           f32 audio and int32 codec frames
 // The AGC the reference runs on a_buffer[0] in FM (:2827) is not run: the output stage
 // overwrites that buffer with the line-out copy (:2868), so it never reaches the audio.
-// Subaudible tone detection (:1665-1734) is off (ui_configuration.c default); a plan with it
-// on is not offered to this kernel.  FM state: [field][C] in BackState.sam:
-//   0 i_prev 1 q_prev 2 lpf_prev 3 hpf_prev_a 4 hpf_prev_b 5 sql_avg 6 open (!squelched) 7.. lattice
+// Subaudible tone detection (:1665-1734, ts.fm_subaudible_tone_det_select): three Goertzels on the
+// de-emphasised audio, a decision every FM_SUBAUDIBLE_GOERTZEL_WINDOW = 400 calls; with it on, the
+// audio passes only while a tone is detected.  FM state: [field][C] in BackState.sam:
+//   0 i_prev 1 q_prev 2 lpf_prev 3 hpf_prev_a 4 hpf_prev_b 5 sql_avg 6 open (!squelched) 7..12 lattice
+//   13..18 Goertzel buf[1], buf[2] of FM_HIGH, FM_LOW, FM_CTR  19 subdet  20 tdet  21 tone detected
 template <int SQ>
 __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
 {
@@ -1295,6 +1428,13 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
         float hpf_a = S[3 * C + cl], hpf_b = S[4 * C + cl], sql_avg = S[5 * C + cl];
         bool squelched = S[6 * C + cl] == 0.0f;          // field 6 = "open": zeroed state starts squelched (:475)
         const int thr = P->fm_sql_threshold;
+        const bool tone_en = P->tone_det_enabled;
+        float tg[6];                                     // {buf[1], buf[2]} of FM_HIGH, FM_LOW, FM_CTR
+#pragma unroll
+        for (int i = 0; i < 6; ++i) tg[i] = tone_en ? S[(13 + i) * C + cl] : 0.0f;
+        float subdet = tone_en ? S[19 * C + cl] : 0.0f;
+        int tdet = tone_en ? (int)S[20 * C + cl] : 0;
+        bool detected = tone_en && S[21 * C + cl] != 0.0f;
         const bool translate = P->freq_shift_hz != 0;   // no translation: the demod bails out (:1548)
         float inext[BLK], qnext[BLK];
         auto fetch = [&](int call) {
@@ -1321,7 +1461,8 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                 float* out = dem + (it & 1) * BLK * BACK_CH + lane;
                 if (translate)
                 {
-                    const bool pass = !squelched || !thr;
+                    // audio gate (:1571-1586)
+                    const bool pass = (!squelched && !tone_en) || (detected && tone_en) || !thr;
                     float sq0 = 0.0f;
 #pragma unroll 4
                     for (int m = 0; m < BLK; ++m)
@@ -1331,6 +1472,17 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                         const float angle = ul_atan2f(y, x);
                         const float aa = (float)((double)lpf_prev + (0.05 * (double)(angle - lpf_prev)));
                         lpf_prev = aa;
+                        if (tone_en)
+                        {
+                            // AudioFilter_GoertzelInput (audio_filter.c:1290-1295) x 3 (:1683-1691)
+#pragma unroll
+                            for (int gi = 0; gi < 3; ++gi)
+                            {
+                                const float g0 = P->tone_r[gi] * tg[2 * gi] - tg[2 * gi + 1] + aa;
+                                tg[2 * gi + 1] = tg[2 * gi];
+                                tg[2 * gi] = g0;
+                            }
+                        }
                         float o = 0.0f;
                         if (pass)
                         {
@@ -1357,6 +1509,31 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                         else if (thr > 3) { if (scaled < (float)(thr - 3)) squelched = true; }
                         else if (scaled < (float)thr) squelched = true;
                     }
+                    if (tone_en && (a.tone_phase + it + 1) % 400 == 0)   // fm_data.gcount (:1679, 1693)
+                    {
+                        // AudioFilter_GoertzelEnergy (audio_filter.c:1296-1305), :1693-1725
+                        float en[3];
+#pragma unroll
+                        for (int gi = 0; gi < 3; ++gi)
+                        {
+                            const float ga = (tg[2 * gi] - (tg[2 * gi + 1] * P->tone_cos[gi]));
+                            const float gb = (tg[2 * gi + 1] * P->tone_sin[gi]);
+                            en[gi] = sqrtf(ga * ga + gb * gb);
+                            tg[2 * gi] = 0.0f;
+                            tg[2 * gi + 1] = 0.0f;
+                        }
+                        const float s_off = en[0] + en[1];
+                        const float r_on = en[2];
+                        subdet = (float)(((1 - 0.9) * (double)subdet) + ((double)(r_on / (s_off / 2)) * 0.9));
+                        if ((double)subdet > 1.75)
+                        {
+                            ++tdet;
+                            if (tdet > 5) tdet = 5;
+                        }
+                        else if (tdet)
+                            --tdet;
+                        detected = tdet >= 2;
+                    }
                 }
                 else
                 {
@@ -1375,6 +1552,14 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
             S[6 * C + c] = squelched ? 0.0f : 1.0f;
 #pragma unroll
             for (int i = 0; i < SQ; ++i) S[(7 + i) * C + c] = g[i];
+            if (tone_en)
+            {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) S[(13 + i) * C + c] = tg[i];
+                S[19 * C + c] = subdet;
+                S[20 * C + c] = (float)tdet;
+                S[21 * C + c] = detected ? 1.0f : 0.0f;
+            }
         }
     }
     else
@@ -1404,6 +1589,9 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                         float v = mi[(n0 + j) * BACK_CH] * fs;
                         v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
                         y[j] = on ? v * lo : 0.0f;
+                        // the beep is added after muting (audio_driver.c:2891-2898); dst stays 0 when muted
+                        const int fr = call * BLK + n0 + j;
+                        if (fr >= a.beep_n0 && fr < a.beep_n1) y[j] += beep_tone(a, fr);
                     }
                     if (live)
                     {
@@ -1469,6 +1657,15 @@ static const BackVariant kBack[] = {
 static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6>, nullptr };
 #undef BACK_V
 
+// LMS auto notch (+ the AM / SAM demodulator ahead of it): decimation L, demodulator DM
+struct NotchVariant { int L, dm; back_fn fn; };
+static const NotchVariant kNotch[] = {
+    { 4, DM_NONE, rx_notch<4, DM_NONE> }, { 2, DM_NONE, rx_notch<2, DM_NONE> },
+    { 4, DM_AM, rx_notch<4, DM_AM> }, { 2, DM_AM, rx_notch<2, DM_AM> },
+    { 4, DM_SAM, rx_notch<4, DM_SAM> }, { 2, DM_SAM, rx_notch<2, DM_SAM> },
+    { 4, DM_SAM_SB, rx_notch<4, DM_SAM_SB> }, { 2, DM_SAM_SB, rx_notch<2, DM_SAM_SB> },
+};
+
 static int plan_dm(const uhsdr_rx_plan& p)
 {
     if (p.dmod_mode == UHSDR_DEMOD_FM) return DM_FM;
@@ -1500,12 +1697,22 @@ static const FrontVariant* find_front(const uhsdr_rx_plan& p, long long C = 0, i
     return best;
 }
 
+static const NotchVariant* find_notch(const uhsdr_rx_plan& p)
+{
+    if (!p.notch_enabled) return nullptr;
+    for (const NotchVariant& v : kNotch)
+        if (v.L == p.decimation_rate && v.dm == plan_dm(p)) return &v;
+    return nullptr;
+}
+
+// with the notch on, the demodulator runs in rx_notch and rx_back takes its DM_NONE variant
 static const BackVariant* find_back(const uhsdr_rx_plan& p)
 {
     if (p.dmod_mode == UHSDR_DEMOD_FM) return p.sq_stages == 6 ? &kBackFm : nullptr;
+    const int dm = p.notch_enabled ? DM_NONE : plan_dm(p);
     for (const BackVariant& v : kBack)
         if (v.pre == p.pre_stages && v.aa == p.aa_stages && v.L == p.interp_L && v.ph == p.interp_phase &&
-            v.w == p.agc.attack_buffsize && v.dm == plan_dm(p))
+            v.w == p.agc.attack_buffsize && v.dm == dm)
             return &v;
     return nullptr;
 }
@@ -1522,6 +1729,7 @@ struct uhsdr_rx_s
     uhsdr_rx_plan* d_plan;
     const FrontVariant* fv;
     const BackVariant* bv;
+    const NotchVariant* nv;  // LMS auto notch kernel (null: notch off)
     int C, N, Nd, Nf;        // Nf: frames per front launch (N split into N / Nf launches)
     int lw;                  // front LDS window pitch (floats)
     int back_fused;          // rx_back_fused (large batches) instead of the wave pipeline
@@ -1538,6 +1746,8 @@ struct uhsdr_rx_s
     long long dec_samples;   // decimated samples processed (AGC ring phase)
     int cw_count;            // CW decoder sample_counter (uniform over channels)
     int cw_bmax, cw_blocks_last;
+    int beep_left;           // key beep: 32-frame calls still to get the tone (uhsdr_rx_key_beep)
+    uint32_t beep_acc;       // its softdds accumulator at the next beep frame
     uint8_t* cw_signal;      // user outputs (uhsdr_rx_set_cw_outputs)
     float* cw_energy;
     long long calls_done;
@@ -1652,7 +1862,7 @@ static size_t back_lds(const uhsdr_rx_s* h)
 
 extern "C" int uhsdr_rx_plan_supported(const uhsdr_rx_plan* p)
 {
-    return p && uhsdr_rx_mode_supported(p) && find_front(*p) && find_back(*p);
+    return p && uhsdr_rx_mode_supported(p) && find_front(*p) && find_back(*p) && (!p->notch_enabled || find_notch(*p));
 }
 
 extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
@@ -1679,6 +1889,16 @@ extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
     h->calls_issued = 0;
     h->cw_count = 0;
     h->cw_blocks_last = 0;
+    h->beep_left = 0;
+    h->beep_acc = 0;
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_rx_key_beep(uhsdr_rx_handle h, int32_t calls)
+{
+    if (!h || calls < 0) { uhsdr_set_error("bad argument"); return UHSDR_ARGUMENT_ERROR; }
+    h->beep_acc = 0;          // AudioManagement_KeyBeep: ads.beep.acc = 0 (audio_management.c:372)
+    h->beep_left = calls;
     return UHSDR_OK;
 }
 
@@ -1694,7 +1914,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const uhsdr_rx_plan& p = h->plan;
     h->fv = find_front(p, C, N);
     h->bv = find_back(p);
-    if (!uhsdr_rx_mode_supported(&p) || !h->fv || !h->bv)
+    h->nv = find_notch(p);
+    if (!uhsdr_rx_mode_supported(&p) || !h->fv || !h->bv || (p.notch_enabled && !h->nv))
     {
         free(h);
         uhsdr_set_error("demodulation mode %d / filter path %d not implemented on the device", cfg->dmod_mode,
@@ -1726,8 +1947,9 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const size_t o_pre = take((size_t)10 * C), o_aa = take((size_t)10 * C), o_bq1 = take((size_t)16 * C);
     const size_t o_bq2 = take((size_t)4 * C), o_ip = take((size_t)15 * C), o_ring = take(W > 0 ? (size_t)(W - 1) * C : 0);
     const size_t o_agc = take((size_t)(6 + AGC_Q) * C), o_agci = take((size_t)3 * C);
-    const bool am = h->bv->dm != DM_NONE;
+    const bool am = plan_dm(p) != DM_NONE;             // AM / SAM / FM demodulator state
     const size_t o_sam = take(am ? (size_t)(7 + 96) * C : 0), o_adq = take(am ? (size_t)C * h->Nd : 0);
+    const size_t o_notch = take(h->nv ? (size_t)(2 * NOTCH_TAPS + 2 + NOTCH_DELAY) * C : 0);
     const bool cw = p.cw_enabled && p.decimation_rate == 4;
     const size_t o_cw = take(cw ? (size_t)5 * C : 0);
     h->arena_bytes = fl * sizeof(float);
@@ -1747,6 +1969,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->bs.interp = A + o_ip; h->bs.ring = A + o_ring; h->bs.agc = A + o_agc; h->bs.agci = (int*)(A + o_agci);
     h->bs.sam = am ? A + o_sam : nullptr;
     h->bs.cw = cw ? A + o_cw : nullptr;
+    h->bs.notch = h->nv ? A + o_notch : nullptr;
     {
         // blocks per call: one completes at the end of every ceil(blocksize / NDC)-th call
         const int ndc = BLK / p.decimation_rate, cpb = (p.cw_blocksize + ndc - 1) / ndc;
@@ -1761,7 +1984,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         memset(t2, 0, sizeof t2);
         if (p.use_decimated_iq)
         {
-            const bool amq = h->bv->dm != DM_NONE;
+            const bool amq = plan_dm(p) != DM_NONE;
             pair_taps(t2, p.dec, amq ? p.dec_q : p.dec, p.dec_taps);
             if (h->T2) pair_taps(t2 + 2 * TAPS2_MAX, p.hilbert_i, p.hilbert_q, p.hilbert_taps);
         }
@@ -1864,6 +2087,22 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
     ba.cw_energy = h->bs.cw ? h->cw_energy : nullptr;
     ba.cw_count0 = h->cw_count;
     ba.cw_bmax = h->cw_bmax;
+    {
+        const int slots = NOTCH_DELAY / (BLK / h->plan.decimation_rate);
+        ba.notch_slot0 = (int)(h->calls_done % slots);
+        ba.notch_first = h->calls_done == 0;
+    }
+    ba.tone_phase = (int)(h->calls_done % 400);
+    {
+        // key beep: frames [0, beep_n1) of this launch while calls are left (uhsdr_rx_key_beep)
+        const int calls = h->N / BLK;
+        const int bc = h->plan.beep_step ? (h->beep_left < calls ? h->beep_left : calls) : 0;
+        ba.beep_n0 = 0;
+        ba.beep_n1 = bc * BLK;
+        ba.beep_acc = h->beep_acc;
+        h->beep_acc += (uint32_t)ba.beep_n1 * h->plan.beep_step;
+        h->beep_left -= bc;
+    }
     if (h->bs.cw)
     {
         const int ndc = BLK / h->plan.decimation_rate;
@@ -1882,6 +2121,11 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
         HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
     }
     time_mark(h, 1, 0);
+    if (h->nv)
+    {
+        hipLaunchKernelGGL(h->nv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
+        HIPCHK(hipGetLastError());
+    }
     if (h->back_fused)
         hipLaunchKernelGGL(h->bv->fused, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
     else

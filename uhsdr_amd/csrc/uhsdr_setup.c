@@ -87,6 +87,30 @@ void uhsdr_rx_config_default(uhsdr_rx_config* c)
     c->cw_decoder_blocksize = 88;                /* CW_DECODER_BLOCKSIZE_DEFAULT, cw_decoder.h:13 */
     c->cw_decoder_thresh = 32000;                /* CW_DECODER_THRESH_DEFAULT, cw_decoder.h:17 */
     c->cw_decoder_noisecancel = 1;               /* CW_DECODER_FLAGS_DEFAULT bit 0, cw_decoder.h:19 */
+    c->notch_mu = 10;                            /* DSP_NOTCH_MU_DEFAULT, audio_driver.h:495 */
+    c->fm_tone_det = 0;                          /* FM_SUBAUDIBLE_TONE_OFF */
+    c->beep_frequency = 1000;                    /* DEFAULT_BEEP_FREQUENCY, audio_driver.h:455 */
+    c->beep_loudness = 10;                       /* DEFAULT_BEEP_LOUDNESS, audio_driver.h:460 */
+    c->stereo_enable = 0;
+}
+
+/* AudioFilter_CalcGoertzel, audio_filter.c:1281-1288 (Goertzel.a is an int) */
+static void calc_goertzel(float* r, float* co, float* si, float freq, uint32_t size, float goertzel_coeff,
+                          float samplerate)
+{
+    const int a = (0.5 + (freq * goertzel_coeff) * size / samplerate);
+    const float b = (2 * CMSIS_PI * a) / size;
+    *si = sinf(b);
+    *co = cosf(b);
+    *r = 2 * *co;
+}
+
+/* softdds_stepForSampleRate, softdds.c:26-32 (DDS_TBL_SIZE 1024, SOFTDDS_ACC_SHIFT 22) */
+static uint32_t softdds_step(float freq, uint32_t samp_rate)
+{
+    uint64_t freq64_shifted = freq * 1024;
+    freq64_shifted <<= 22;
+    return (uint32_t)(freq64_shifted / samp_rate);
 }
 
 /* IIR_15k_hpf (drivers/audio/filters/iir_15k_hpf_fm_squelch.c): 6-stage lattice high-pass of
@@ -439,6 +463,42 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
         p->cw_cos = cosf(gb);
         p->cw_r = 2 * p->cw_cos;
     }
+    /* LMS auto notch: AudioDriver_SetProcessingChain (audio_driver.c:1166-1186) and the call
+       condition of RxProcessor_DemodAudioPostprocessing (:2441-2443): not in CW, not in SAM at
+       24 ksps, not in FM (FM skips the post-processing, :2792-2830) */
+    if (cfg->notch_mu < 0 || cfg->notch_mu > 40)
+    { uhsdr_set_error("notch_mu %d outside 0..40 (DSP_NOTCH_MU_MAX)", cfg->notch_mu); return UHSDR_ARGUMENT_ERROR; }
+    p->notch_enabled = (cfg->dsp_active & UHSDR_DSP_NOTCH_ENABLE) && mode != UHSDR_DEMOD_CW && mode != UHSDR_DEMOD_FM
+                       && !(mode == UHSDR_DEMOD_SAM && p->decimated_freq == 24000);
+    p->notch_taps = 64;                          /* DSP_NOTCH_NUMTAPS_DEFAULT (= MIN = MAX), audio_driver.h:486-488 */
+    p->notch_delay_len = 128;                    /* DSP_NOTCH_DELAYBUF_DEFAULT (= MIN = MAX), :490-492 */
+    p->notch_mu = log10f(((cfg->notch_mu + 1.0) / 1500.0) + 1.0);
+    /* FM subaudible tone detector: AudioManagement_CalcSubaudibleDetFreq (audio_management.c:313-326),
+       window FM_SUBAUDIBLE_GOERTZEL_WINDOW * AUDIO_BLOCK_SIZE = 400 * 32 samples */
+    if (cfg->fm_tone_det < 0 || cfg->fm_tone_det >= uhsdr_fm_subaudible_count)
+    { uhsdr_set_error("fm_tone_det %d outside 0..%d", cfg->fm_tone_det, uhsdr_fm_subaudible_count - 1); return UHSDR_ARGUMENT_ERROR; }
+    {
+        float freq;
+        memcpy(&freq, &uhsdr_fm_subaudible[cfg->fm_tone_det], 4);
+        p->tone_det_enabled = freq != 0;
+        if (freq > 0)
+        {
+            const uint32_t size = 400 * 32;
+            calc_goertzel(&p->tone_r[0], &p->tone_cos[0], &p->tone_sin[0], freq, size, 1.04, IQ_SAMPLE_RATE);  /* FM_HIGH */
+            calc_goertzel(&p->tone_r[1], &p->tone_cos[1], &p->tone_sin[1], freq, size, 0.95, IQ_SAMPLE_RATE);  /* FM_LOW */
+            calc_goertzel(&p->tone_r[2], &p->tone_cos[2], &p->tone_sin[2], freq, size, 1.0, IQ_SAMPLE_RATE);   /* FM_CTR */
+        }
+    }
+    /* key beep: AudioManagement_KeyBeepPrepare (audio_management.c:354-363), ts.samp_rate 48000 */
+    p->beep_step = softdds_step((float)cfg->beep_frequency, 48000);
+    {
+        float calc = (float)(cfg->beep_loudness - 1);
+        calc /= 2;
+        calc *= calc;
+        calc += 3;
+        p->beep_scale = calc / 400;
+    }
+    memcpy(p->dds_table, uhsdr_dds_table, sizeof p->dds_table);
     return UHSDR_OK;
 }
 

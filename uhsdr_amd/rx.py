@@ -90,6 +90,11 @@ class RxChain:
     def cw_blocks_last(self) -> int:
         return self.lib.uhsdr_rx_cw_blocks_last(self.handle)
 
+    def key_beep(self, calls: int) -> None:
+        """AudioManagement_KeyBeep for every channel: the beep tone is added to the next `calls`
+        32-frame calls (uhsdr_rx_key_beep)."""
+        _abi.check(self.lib.uhsdr_rx_key_beep(self.handle, int(calls)), "uhsdr_rx_key_beep")
+
     def set_pipelined(self, enable: bool = True) -> None:
         """Overlap call k+1's rx_front with call k's rx_back (uhsdr_rx_set_pipelined); outputs
         are complete after synchronize() / a device-wide sync, or join() for the handle's stream."""

@@ -146,9 +146,12 @@ def cw_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier
 
 
 def fm_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier: float = 12000.0,
-          deviation: float = 2500.0, tone: float = 1000.0, amplitude: float = 3000.0):
+          deviation: float = 2500.0, tone: float = 1000.0, amplitude: float = 3000.0,
+          subtone: float = 0.0, subtone_dev: float = 300.0):
     """C4 FM-RX: carrier at `carrier` Hz, a `tone` Hz audio tone at
-    `deviation` Hz peak deviation, `amplitude` LSB16, plus noise."""
+    `deviation` Hz peak deviation, `amplitude` LSB16, plus noise; optionally a CTCSS
+    subaudible tone of `subtone` Hz at `subtone_dev` Hz deviation (the FM tone detector's
+    input, audio_driver.c:1665-1734)."""
     channels = np.asarray(channels, dtype=np.int64)
     ch = channels.astype(np.uint64)
     base = (np.uint64(SEED_BASE) + ch) << np.uint64(20)
@@ -157,6 +160,8 @@ def fm_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier
     n = np.arange(start, start + nframes, dtype=np.float64)[None, :]
     ph = (2.0 * np.pi * carrier / FS * n + ph_c[:, None]
           + (deviation / tone) * np.sin(2.0 * np.pi * tone / FS * n + ph_m[:, None]))
+    if subtone > 0:
+        ph = ph + (subtone_dev / subtone) * np.sin(2.0 * np.pi * subtone / FS * n)
     i_sig, q_sig = amplitude * np.cos(ph), amplitude * np.sin(ph)
     if noise_sigma > 0:
         ni, nq = _noise(channels, start, nframes, noise_sigma)

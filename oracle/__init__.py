@@ -29,6 +29,8 @@ def load():
         lib.uo_rx_process.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         lib.uo_rx_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                             C.c_void_p, C.c_void_p, C.c_int]
+        lib.uo_rx_process_batch2.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         lib.uo_rx_key_beep.argtypes = [C.c_void_p, C.c_int, C.c_int]
         lib.uo_rx_bench.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                                     C.c_void_p, C.c_int, C.c_int, C.c_double, C.POINTER(C.c_double)]
@@ -66,16 +68,23 @@ class OracleRx:
         self.lib.uo_rx_key_beep(self.states, self.channels, calls)
 
     def process(self, iq: np.ndarray, threads: int = 1):
+        a1, _, dst = self.process2(iq, threads)
+        return a1, dst
+
+    def process2(self, iq: np.ndarray, threads: int = 1):
+        """(a_buffer[1], a_buffer[0], dst): a_buffer[0] is the second channel in stereo."""
         iq = np.ascontiguousarray(iq, dtype=np.int32)
         Cn, n, _ = iq.shape
         assert Cn == self.channels
         a1 = np.empty((Cn, n), np.float32)
+        a0 = np.empty((Cn, n), np.float32)
         dst = np.empty((Cn, n, 2), np.int32)
-        st = self.lib.uo_rx_process_batch(C.byref(self.plan), self.states, Cn, iq.ctypes.data_as(C.c_void_p), n,
-                                          a1.ctypes.data_as(C.c_void_p), dst.ctypes.data_as(C.c_void_p), threads)
+        st = self.lib.uo_rx_process_batch2(C.byref(self.plan), self.states, Cn, iq.ctypes.data_as(C.c_void_p), n,
+                                           a1.ctypes.data_as(C.c_void_p), a0.ctypes.data_as(C.c_void_p),
+                                           dst.ctypes.data_as(C.c_void_p), threads)
         if st != 0:
-            raise RuntimeError(f"uo_rx_process_batch status {st}")
-        return a1, dst
+            raise RuntimeError(f"uo_rx_process_batch2 status {st}")
+        return a1, a0, dst
 
 
 def rx_bench(plan, blocks: np.ndarray, threads: int, budget_s: float, pin: bool = True):

@@ -186,12 +186,17 @@ static float log10f_fast(float X)
 
 static float sign_new(float x) { return (x < 0) ? -1.0 : ((x > 0) ? 1.0 : 0.0); }  /* uhsdr_math.c:84-87 */
 
-/* AudioAgc_RunAgcWdsp, audio_agc.c:349-595 (mono) */
-static void agc_run(const uhsdr_agc_plan* a, uo_rx_state* s, float* buf, int n)
+/* AudioAgc_RunAgcWdsp, audio_agc.c:349-595; buf1 != NULL: use_stereo (second channel in the
+   odd ring slots, abs_ring = the larger magnitude, one gain for both) */
+static void agc_run(const uhsdr_agc_plan* a, uo_rx_state* s, float* buf, float* buf1, int n)
 {
     if (a->mode == 5)
     {
-        for (int i = 0; i < n; i++) buf[i] = buf[i] * a->fixed_gain;
+        for (int i = 0; i < n; i++)
+        {
+            buf[i] = buf[i] * a->fixed_gain;
+            if (buf1) buf1[i] = buf1[i] * a->fixed_gain;
+        }
         return;
     }
     for (int i = 0; i < n; i++)
@@ -199,9 +204,12 @@ static void agc_run(const uhsdr_agc_plan* a, uo_rx_state* s, float* buf, int n)
         if (++s->out_index >= a->ring_buffsize) s->out_index -= a->ring_buffsize;
         if (++s->in_index >= a->ring_buffsize) s->in_index -= a->ring_buffsize;
         const float out_sample = s->ring[s->out_index];
+        const float out_sample1 = s->ring1[s->out_index];
         const float abs_out_sample = s->abs_ring[s->out_index];
         s->ring[s->in_index] = buf[i];
+        if (buf1) s->ring1[s->in_index] = buf1[i];
         s->abs_ring[s->in_index] = fabsf(buf[i]);
+        if (buf1 && s->abs_ring[s->in_index] < fabsf(buf1[i])) s->abs_ring[s->in_index] = fabsf(buf1[i]);
 
         s->fast_backaverage = a->fast_backmult * abs_out_sample + a->onemfast_backmult * s->fast_backaverage;
         s->hang_backaverage = a->hang_backmult * abs_out_sample + a->onemhang_backmult * s->hang_backaverage;
@@ -304,6 +312,7 @@ static void agc_run(const uhsdr_agc_plan* a, uo_rx_state* s, float* buf, int n)
         if (vo > 0.0) vo = 0.0;
         const float mult = (a->out_target - a->slope_constant * vo) / s->volts;
         buf[i] = out_sample * mult;
+        if (buf1) buf1[i] = out_sample1 * mult;
     }
     if (a->remove_dc)
     {
@@ -312,6 +321,12 @@ static void agc_run(const uhsdr_agc_plan* a, uo_rx_state* s, float* buf, int n)
             const float w = buf[i] + s->wold * 0.9999;
             buf[i] = w - s->wold;
             s->wold = w;
+            if (buf1)
+            {
+                const float w1 = buf1[i] + s->wold1 * 0.9999;
+                buf1[i] = w1 - s->wold1;
+                s->wold1 = w1;
+            }
         }
     }
 }
@@ -324,6 +339,14 @@ static float fade_leveler(const uhsdr_rx_plan* p, uo_rx_state* s, float audio, f
     audio = audio + s->fade_dc_insert - s->fade_dc27;
     return audio;
 }
+/* channel 1 (only its output matters in stereo) */
+static float fade_leveler1(const uhsdr_rx_plan* p, uo_rx_state* s, float audio, float corr)
+{
+    s->fade_dc27_1 = p->fade_mtauR * s->fade_dc27_1 + p->fade_onem_mtauR * audio;
+    s->fade_dc_insert_1 = p->fade_mtauI * s->fade_dc_insert_1 + p->fade_onem_mtauI * corr;
+    audio = audio + s->fade_dc_insert_1 - s->fade_dc27_1;
+    return audio;
+}
 
 /* the 7-stage allpass pair of the SAM sideband selector, demod_sam_const (audio_driver.c:1931-1953) */
 static const float sam_c0[7] = { -0.328201924180698, -0.744171491539427, -0.923022915444215, -0.978490468768238,
@@ -333,7 +356,8 @@ static const float sam_c1[7] = { -0.0991227952747244, -0.565619728761389, -0.857
 
 /* AudioDriver_DemodSAM, audio_driver.c:1990-2166 (mono; the display-only carrier estimate
    at :2150-2162 does not touch the audio and is not restated) */
-static void demod_sam(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, const float* qb, float* a0, int n)
+static void demod_sam(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, const float* qb, float* a0, float* a1,
+                      int n)
 {
     if (p->dmod_mode == UHSDR_DEMOD_AM)
     {
@@ -354,7 +378,7 @@ static void demod_sam(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, c
         const float bi = Sin * ib[i];
         const float aq = Cos * qb[i];
         const float bq = Sin * qb[i];
-        float audio;
+        float audio, audio1 = 0;
         const float corr[2] = { ai + bq, -bi + aq };
         if (p->sam_sideband != UHSDR_SAM_SIDEBAND_BOTH)
         {
@@ -381,14 +405,24 @@ static void demod_sam(const uhsdr_rx_plan* p, uo_rx_state* s, const float* ib, c
                 s->sam_d[j] = s->sam_d[j - 1];
             }
             if (p->sam_sideband == UHSDR_SAM_SIDEBAND_LSB) audio = (ai_ps + bi_ps) - (aq_ps - bq_ps);
+            else if (p->sam_sideband == UHSDR_SAM_SIDEBAND_STEREO)
+            {
+                audio = (ai_ps + bi_ps) - (aq_ps - bq_ps);      /* audio_driver.c:2091-2094 */
+                audio1 = (ai_ps - bi_ps) + (aq_ps + bq_ps);
+            }
             else audio = (ai_ps - bi_ps) + (aq_ps + bq_ps);
         }
         else
         {
             audio = corr[0];
         }
-        if (p->fade_leveler) audio = fade_leveler(p, s, audio, corr[0]);
+        if (p->fade_leveler)
+        {
+            audio = fade_leveler(p, s, audio, corr[0]);
+            audio1 = fade_leveler1(p, s, audio1, corr[0]);
+        }
         a0[i] = audio;
+        if (a1) a1[i] = audio1;
         const float phzerror = atan2f(corr[1], corr[0]);
         const float del_out = s->sam_fil_out;
         s->sam_omega2 = s->sam_omega2 + p->sam_g2 * phzerror;
@@ -563,7 +597,8 @@ static float beep_next(const uhsdr_rx_plan* p, uo_rx_state* s)
 }
 
 /* one AudioDriver_RxProcessor call on BLK frames, audio_driver.c:2603-2942 */
-static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, float* out_a1, int32_t* dst)
+static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, float* out_a1, float* out_a0,
+                    int32_t* dst)
 {
     float ib[BLK], qb[BLK], a0[BLK], a1[BLK];
     const int n = BLK;
@@ -670,40 +705,84 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
             float v = active ? a1[i] * p->line_out_scale : 0.0f;    /* mute when squelched, :2843-2850 */
             if (beep) v += beep_next(p, s);
             out_a1[i] = v;
+            if (out_a0) out_a0[i] = v;
             const int32_t d = active ? to_dma(v) : 0;
             if (dst) { dst[2 * i] = d; dst[2 * i + 1] = d; }
         }
         return;
     }
+    /* second channel a_buffer[1] while at the decimated rate (use_stereo) */
+    const int st = p->stereo;
+    float b1[BLK], a0o[BLK];
     if (am)
-        demod_sam(p, s, ib, qb, a0, niq);
+        demod_sam(p, s, ib, qb, a0, st ? b1 : NULL, niq);
+    else if (p->dmod_mode == UHSDR_DEMOD_IQ)          /* audio_driver.c:2769-2772 */
+    {
+        for (int i = 0; i < niq; i++) a0[i] = ib[i];
+        if (st) for (int i = 0; i < niq; i++) b1[i] = qb[i];
+    }
+    else if (p->dmod_mode == UHSDR_DEMOD_SSBSTEREO)   /* :2773-2776 */
+    {
+        for (int i = 0; i < niq; i++) a0[i] = ib[i] + qb[i];
+        if (st) for (int i = 0; i < niq; i++) b1[i] = ib[i] - qb[i];
+    }
     else if (p->lsb)
         for (int i = 0; i < niq; i++) a0[i] = ib[i] - qb[i];
     else
         for (int i = 0; i < niq; i++) a0[i] = ib[i] + qb[i];
 
     if (!p->use_decimated_iq)
+    {
         fir_decimate(p->dec, p->dec_taps, p->decimation_rate, s->dec_i, a0, a0, niq);
+        if (st) fir_decimate(p->dec, p->dec_taps, p->decimation_rate, s->dec_q, b1, b1, niq);   /* DECIMATE_RX_Q, :2797-2801 */
+    }
 
     /* RxProcessor_DemodAudioPostprocessing, audio_driver.c:2436-2592 */
     if (p->notch_enabled) notch_run(p, s, a0, nd);
-    if (p->pre_stages > 0) iir_lattice(p->pre_k, p->pre_v, p->pre_stages, s->pre, a0, a0, nd);
-    agc_run(&p->agc, s, a0, nd);
+    if (p->pre_stages > 0)
+    {
+        iir_lattice(p->pre_k, p->pre_v, p->pre_stages, s->pre, a0, a0, nd);
+        if (st) iir_lattice(p->pre_k, p->pre_v, p->pre_stages, s->pre1, b1, b1, nd);
+    }
+    agc_run(&p->agc, s, a0, st ? b1 : NULL, nd);
     for (int i = 0; i < nd; i++) a0[i] = a0[i] * p->post_agc_scale;
     biquad_df1(p->biquad1, 4, s->bq1, a0, nd);
+    if (st)
+    {
+        for (int i = 0; i < nd; i++) b1[i] = b1[i] * p->post_agc_scale;
+        biquad_df1(p->biquad1, 4, s->bq1_1, b1, nd);
+    }
     if (p->cw_enabled) cw_front(p, s, a0, nd);         /* audio_driver.c:2550-2557 */
-    if (p->interp_phase > 0) fir_interpolate(p->interp, p->interp_L, p->interp_phase, s->interp, a0, a1, nd);
-    if (p->aa_stages > 0) iir_lattice(p->aa_k, p->aa_v, p->aa_stages, s->aa, a1, a1, n);
+    /* interpolation: channel 1 into a temporary that becomes a_buffer[0], channel 0 into
+       a_buffer[1] (:2560-2577) */
+    if (p->interp_phase > 0)
+    {
+        if (st) fir_interpolate(p->interp, p->interp_L, p->interp_phase, s->interp1, b1, a0o, nd);
+        fir_interpolate(p->interp, p->interp_L, p->interp_phase, s->interp, a0, a1, nd);
+    }
+    if (p->aa_stages > 0)
+    {
+        iir_lattice(p->aa_k, p->aa_v, p->aa_stages, s->aa, a1, a1, n);
+        if (st) iir_lattice(p->aa_k, p->aa_v, p->aa_stages, s->aa1, a0o, a0o, n);
+    }
 
     biquad_df1(p->biquad2, 1, s->bq2, a1, n);          /* audio_driver.c:2832 */
+    if (st) biquad_df1(p->biquad2, 1, s->bq2_1, a0o, n);
     for (int i = 0; i < n; i++) a1[i] = a1[i] * p->line_out_scale;   /* :2860 (OVI40) */
+    if (st) for (int i = 0; i < n; i++) a0o[i] = a0o[i] * p->line_out_scale;
+    else for (int i = 0; i < n; i++) a0o[i] = a1[i];                  /* :2868 copy */
     if (beep_on(p, s))
-        for (int i = 0; i < n; i++) a1[i] += beep_next(p, s);
+        for (int i = 0; i < n; i++)
+        {
+            const float t = beep_next(p, s);
+            a0o[i] += t;
+            a1[i] += t;
+        }
     for (int i = 0; i < n; i++)
     {
         out_a1[i] = a1[i];
-        const int32_t d = to_dma(a1[i]);                /* a_buffer[0] is a copy, :2868 */
-        if (dst) { dst[2 * i] = d; dst[2 * i + 1] = d; }
+        if (out_a0) out_a0[i] = a0o[i];
+        if (dst) { dst[2 * i] = to_dma(a1[i]); dst[2 * i + 1] = to_dma(a0o[i]); }
     }
 }
 
@@ -711,7 +790,16 @@ int uo_rx_process(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, int
 {
     if (n % BLK) return UHSDR_LENGTH_ERROR;
     for (int off = 0; off < n; off += BLK)
-        rx_call(p, s, iq + 2 * off, a1 + off, dst ? dst + 2 * off : NULL);
+        rx_call(p, s, iq + 2 * off, a1 + off, NULL, dst ? dst + 2 * off : NULL);
+    return UHSDR_OK;
+}
+
+int uo_rx_process2(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, int n, float* a1, float* a0,
+                   int32_t* dst)
+{
+    if (n % BLK) return UHSDR_LENGTH_ERROR;
+    for (int off = 0; off < n; off += BLK)
+        rx_call(p, s, iq + 2 * off, a1 + off, a0 ? a0 + off : NULL, dst ? dst + 2 * off : NULL);
     return UHSDR_OK;
 }
 
@@ -721,6 +809,7 @@ typedef struct
     uo_rx_state* states;
     const int32_t* iq;
     float* a1;
+    float* a0;
     int32_t* dst;
     int c0, c1, n;
 } uo_job;
@@ -729,8 +818,8 @@ static void* uo_worker(void* arg)
 {
     uo_job* j = (uo_job*)arg;
     for (int c = j->c0; c < j->c1; c++)
-        uo_rx_process(j->p, &j->states[c], j->iq + (size_t)c * j->n * 2, j->n, j->a1 + (size_t)c * j->n,
-                      j->dst ? j->dst + (size_t)c * j->n * 2 : NULL);
+        uo_rx_process2(j->p, &j->states[c], j->iq + (size_t)c * j->n * 2, j->n, j->a1 + (size_t)c * j->n,
+                       j->a0 ? j->a0 + (size_t)c * j->n : NULL, j->dst ? j->dst + (size_t)c * j->n * 2 : NULL);
     return NULL;
 }
 
@@ -755,7 +844,7 @@ static void* uo_cw_worker(void* arg)
         int nb = 0;
         for (int off = 0; off < j->n; off += BLK)
         {
-            rx_call(j->p, s, j->iq + ((size_t)c * j->n + off) * 2, j->a1 + (size_t)c * j->n + off,
+            rx_call(j->p, s, j->iq + ((size_t)c * j->n + off) * 2, j->a1 + (size_t)c * j->n + off, NULL,
                     j->dst ? j->dst + ((size_t)c * j->n + off) * 2 : NULL);
             if (j->sig) j->sig[(size_t)c * (j->n / BLK) + off / BLK] = (uint8_t)s->cw_signal_out;
             if (j->p->cw_enabled && s->cw_blocks_out && j->en && nb < j->bmax) j->en[(size_t)c * j->bmax + nb] = s->cw_energy_out;
@@ -786,8 +875,8 @@ int uo_rx_process_batch_cw(const uhsdr_rx_plan* p, uo_rx_state* states, int C, c
     return UHSDR_OK;
 }
 
-int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
-                        float* a1, int32_t* dst, int threads)
+int uo_rx_process_batch2(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
+                         float* a1, float* a0, int32_t* dst, int threads)
 {
     if (n % BLK) return UHSDR_LENGTH_ERROR;
     if (threads < 1) threads = 1;
@@ -797,13 +886,19 @@ int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, cons
     if (threads > 256) threads = 256;
     for (int t = 0; t < threads; t++)
     {
-        jobs[t] = (uo_job){ p, states, iq, a1, dst, (int)((long)C * t / threads), (int)((long)C * (t + 1) / threads), n };
+        jobs[t] = (uo_job){ p, states, iq, a1, a0, dst, (int)((long)C * t / threads), (int)((long)C * (t + 1) / threads), n };
         if (threads == 1) uo_worker(&jobs[t]);
         else pthread_create(&tid[t], NULL, uo_worker, &jobs[t]);
     }
     if (threads > 1)
         for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
     return UHSDR_OK;
+}
+
+int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
+                        float* a1, int32_t* dst, int threads)
+{
+    return uo_rx_process_batch2(p, states, C, iq, n, a1, NULL, dst, threads);
 }
 
 /* CPU baseline for bench.py: `threads` persistent workers, worker t pinned

@@ -65,6 +65,11 @@ typedef struct uo_rx_state
        gcount, ads.fm_conf.subaudible_tone_detected */
     float fm_g[3][2], fm_subdet;
     int32_t fm_tdet, fm_gcount, fm_tone_detected;
+    /* OVI40 second audio channel (use_stereo): instances [1] of IIR_PreFilter, IIR_AntiAlias,
+       IIR_biquad_1 / _2, INTERPOLATE_RX (audio_driver.c:78-161), agc ring[2*i+1], wold[1],
+       the fade leveler's dc27[1] / dc_insert[1] (:1915-1916) */
+    float pre1[UHSDR_MAX_LATTICE + 1], aa1[UHSDR_MAX_LATTICE + 1], bq1_1[16], bq2_1[4], interp1[UHSDR_MAX_INTERP];
+    float ring1[UHSDR_AGC_RING], wold1, fade_dc27_1, fade_dc_insert_1;
     /* key beep: ts.beep_timing as calls left, ads.beep.acc */
     int32_t beep_left;
     uint32_t beep_acc;
@@ -74,6 +79,10 @@ size_t uo_rx_state_size(void);
 void uo_rx_state_init(const uhsdr_rx_plan* p, uo_rx_state* s);
 /* one channel, n frames (n % 32 == 0): iq [n][2] int32 -> a1 [n] f32, dst [n][2] int32 */
 int uo_rx_process(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, int n, float* a1, int32_t* dst);
+/* the same with both output channels: a0 = adb.a_buffer[0] (the second channel in stereo, a copy
+   of a_buffer[1] otherwise) */
+int uo_rx_process2(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, int n, float* a1, float* a0,
+                   int32_t* dst);
 /* AudioManagement_KeyBeep on C channel states: the next `calls` calls get the beep tone */
 void uo_rx_key_beep(uo_rx_state* states, int C, int calls);
 /* C channels, channel-major buffers, `threads` POSIX threads (0 = 1) */
@@ -81,6 +90,8 @@ long long uo_rx_bench(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const 
                       float* a1, int32_t* dst, int threads, int pin, double budget_s, double* elapsed);
 int uo_rx_process_batch(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
                         float* a1, int32_t* dst, int threads);
+int uo_rx_process_batch2(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
+                         float* a1, float* a0, int32_t* dst, int threads);
 /* the same, also recording the CW decoder front end: cw_signal [C][n/32] (ads.CW_signal after
    each call), cw_energy [C][bmax] (Goertzel energy of each block completed, in order) */
 int uo_rx_process_batch_cw(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,

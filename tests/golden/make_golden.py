@@ -100,6 +100,20 @@ CONFIGS = {
     # debounce 2, so 1280 calls (40960 frames) see three detector decisions
     "p1_fm_tone": ({"mode": 5, "path": 1, "tonedet": 10}, {"fm": True, "frames": 40960, "subtone": 91.5, "nch": 2}),
     "p1_fm_tone_absent": ({"mode": 5, "path": 1, "tonedet": 10, "sql": 0}, {"fm": True, "frames": 40960, "nch": 2}),
+    # OVI40 two-channel audio (USE_TWO_CHANNEL_AUDIO, use_stereo at audio_driver.c:2618): SSB stereo
+    # (a_buffer[0] = I + Q, [1] = I - Q), IQ (I, Q), SAM stereo (LSB, USB); a0 stored too
+    "p48_ssbstereo": ({"mode": 7, "path": 48, "stereo": 1}, {}),
+    "p35_ssbstereo": ({"mode": 7, "path": 35, "stereo": 1}, {}),
+    "p55_ssbstereo": ({"mode": 7, "path": 55, "stereo": 1, "agc_mode": 4}, {}),
+    "p48_iq_stereo": ({"mode": 8, "path": 48, "stereo": 1, "dsp": 0x30}, {}),
+    "p35_iq_stereo": ({"mode": 8, "path": 35, "stereo": 1, "agc_mode": 5}, {}),
+    "p48_iq_mono": ({"mode": 8, "path": 48}, {}),
+    "p48_ssbstereo_mono": ({"mode": 7, "path": 48}, {}),
+    "p70_sam_stereo": ({"mode": 4, "path": 70, "sam_sb": 3, "stereo": 1}, {"am": True}),
+    "p83_sam_stereo": ({"mode": 4, "path": 83, "sam_sb": 3, "stereo": 1, "fade": 0}, {"am": True}),
+    "p70_sam_stereo_mono": ({"mode": 4, "path": 70, "sam_sb": 3}, {"am": True}),
+    "p48_ssbstereo_notch_beep": ({"mode": 7, "path": 48, "stereo": 1, "dsp": 4, "beep": "16:20"}, {}),
+    "p70_sam_stereo_notch": ({"mode": 4, "path": 70, "sam_sb": 3, "stereo": 1, "dsp": 4}, {"am": True}),
     "p2_fm_tone_sql3": ({"mode": 5, "path": 2, "tonedet": 10, "fm5k": 1, "sql": 3},
                         {"fm": True, "frames": 40960, "subtone": 91.5, "deviation": 5000.0, "nch": 2}),
 }
@@ -288,7 +302,7 @@ def make(name: str):
     a1 = np.empty((C, iq.shape[1]), np.float32)
     dst = np.empty((C, iq.shape[1], 2), np.int32)
     extra = {}
-    stereo = bool(args.get("stereo", 0))
+    stereo = True          # a_buffer[0] too: the second channel in stereo, a copy of [1] otherwise
     if stereo:
         extra["a0"] = np.empty((C, iq.shape[1]), np.float32)
     for c in range(C):

@@ -16,8 +16,10 @@ def test_oracle_matches_reference(path):
     g = load(path)
     plan = U.build_plan(U.config_from_ref_args(g["args"]))
     o = oracle.OracleRx(plan, g["iq"].shape[0])
-    a1, dst = drive(g, 256, o.process, o.key_beep)
+    a1, a0, dst = drive(g, 256, o.process2, o.key_beep)
     assert_bitexact(a1, g["a1"], g["name"])
+    if "a0" in g:
+        assert_bitexact(a0, g["a0"], g["name"] + " a_buffer[0]")
     np.testing.assert_array_equal(dst, g["dst"])
 
 

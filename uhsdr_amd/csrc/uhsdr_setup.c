@@ -328,7 +328,7 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
         uhsdr_set_error("filter_path %d out of range 1..%d", cfg->filter_path, UHSDR_FILTER_PATH_NUM - 1);
         return UHSDR_ARGUMENT_ERROR;
     }
-    if (cfg->dmod_mode < UHSDR_DEMOD_USB || cfg->dmod_mode > UHSDR_DEMOD_DIGI)
+    if (cfg->dmod_mode < UHSDR_DEMOD_USB || cfg->dmod_mode > UHSDR_DEMOD_IQ)
     {
         uhsdr_set_error("dmod_mode %d unknown", cfg->dmod_mode);
         return UHSDR_ARGUMENT_ERROR;
@@ -416,7 +416,15 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
     setup_agc(&p->agc, cfg, (float)p->decimated_freq, is_am);
 
     /* AudioDriver_SetSamPllParameters, audio_driver.c:709-745 (PI = 3.14159265358979f) */
+    if (cfg->sam_sideband < UHSDR_SAM_SIDEBAND_BOTH || cfg->sam_sideband > UHSDR_SAM_SIDEBAND_STEREO)
+    { uhsdr_set_error("sam_sideband %d outside 0..3", cfg->sam_sideband); return UHSDR_ARGUMENT_ERROR; }
     p->sam_sideband = cfg->sam_sideband;
+    /* OVI40 two-channel audio: use_stereo (audio_driver.c:2618) */
+    {
+        const int two = mode == UHSDR_DEMOD_IQ || mode == UHSDR_DEMOD_SSBSTEREO ||
+                        (mode == UHSDR_DEMOD_SAM && cfg->sam_sideband == UHSDR_SAM_SIDEBAND_STEREO);
+        p->stereo = (two && cfg->stereo_enable) ? (mode == UHSDR_DEMOD_SSBSTEREO ? 1 : mode == UHSDR_DEMOD_IQ ? 2 : 3) : 0;
+    }
     p->fade_leveler = cfg->fade_leveler != 0;
     {
         const float decimSampleRate = p->decimated_freq;

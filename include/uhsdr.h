@@ -233,6 +233,10 @@ uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h);
 /* iq, audio, dst: device pointers ([C][N][2] int32, [C][N] f32, [C][N][2] int32).
    audio or dst may be NULL (not written).  Asynchronous on the handle's stream. */
 uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, int32_t* dst);
+/* OVI40 two-channel modes (plan.stereo != 0): audio = adb.a_buffer[1] (channel 0, codec left),
+   audio0 = adb.a_buffer[0] (channel 1, codec right), dst = both channels {l, r}; either may be
+   NULL.  Without stereo, audio0 is not written (a_buffer[0] is a copy of a_buffer[1]). */
+uhsdr_status uhsdr_rx_process_stereo(uhsdr_rx_handle h, const int32_t* iq, float* audio, float* audio0, int32_t* dst);
 /* Same with host buffers: copies in, processes, copies out, synchronises. */
 uhsdr_status uhsdr_rx_process_host(uhsdr_rx_handle h, const int32_t* iq, float* audio, int32_t* dst);
 uhsdr_status uhsdr_rx_get_plan(uhsdr_rx_handle h, uhsdr_rx_plan* plan);

@@ -45,13 +45,17 @@ class DeviceStream:
         import torch
         self.torch = torch
         self.chain = U.RxChain(cfg, channels=channels, frames=frames)
+        self.stereo = bool(self.chain.plan.stereo)
         self.audio = torch.empty((channels, frames), dtype=torch.float32, device="cuda")
+        self.audio0 = torch.empty((channels, frames), dtype=torch.float32, device="cuda")
         self.dst = torch.empty((channels, frames, 2), dtype=torch.int32, device="cuda")
 
     def __call__(self, iq_block):
-        self.chain.process(self.torch.from_numpy(iq_block).cuda(), self.audio, self.dst)
+        """(a_buffer[1], a_buffer[0], dst); a_buffer[0] is a copy of [1] without stereo"""
+        self.chain.process_stereo(self.torch.from_numpy(iq_block).cuda(), self.audio, self.audio0, self.dst)
         self.torch.cuda.synchronize()
-        return self.audio.cpu().numpy(), self.dst.cpu().numpy()
+        a1 = self.audio.cpu().numpy()
+        return a1, (self.audio0.cpu().numpy() if self.stereo else a1.copy()), self.dst.cpu().numpy()
 
 
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("rx_")[-1][:-4])
@@ -59,9 +63,11 @@ def test_device_matches_reference_firmware(cuda, back, path):
     g = load(path)
     cfg = U.config_from_ref_args(g["args"])
     dev = DeviceStream(cfg, g["iq"].shape[0], 256)
-    a1, dst = drive(g, 256, dev, dev.chain.key_beep)
+    a1, a0, dst = drive(g, 256, dev, dev.chain.key_beep)
     dev.chain.close()
     assert_bitexact(a1, g["a1"], g["name"])
+    if "a0" in g:
+        assert_bitexact(a0, g["a0"], g["name"] + " a_buffer[0]")
     np.testing.assert_array_equal(dst, g["dst"])
 
 
@@ -143,6 +149,36 @@ def test_device_fm_tone_detector_matches_oracle(cuda):
     assert_bitexact(a1, ref_a1, "fm tone detector")
     np.testing.assert_array_equal(dst, ref_dst)
     assert np.abs(a1[:50, -2048:]).max() > 1000 and np.abs(a1[50:, -2048:]).max() == 0
+
+
+STEREO_CASES = [
+    ("p48_ssbstereo", dict(filter_path=48, dmod_mode=U.DEMOD_SSBSTEREO), synth.ssb_iq, 130, 256),
+    ("p35_ssbstereo", dict(filter_path=35, dmod_mode=U.DEMOD_SSBSTEREO), synth.ssb_iq, 65, 512),
+    ("p55_iq", dict(filter_path=55, dmod_mode=U.DEMOD_IQ), synth.ssb_iq, 100, 64),
+    ("p44_iq", dict(filter_path=44, dmod_mode=U.DEMOD_IQ, agc_mode=1, agc_hang_enable=1), synth.ssb_iq, 64, 256),
+    ("p70_sam_st", dict(filter_path=70, dmod_mode=U.DEMOD_SAM, sam_sideband=U.SAM_SIDEBAND_STEREO), synth.am_iq, 96, 256),
+    ("p86_sam_st", dict(filter_path=86, dmod_mode=U.DEMOD_SAM, sam_sideband=U.SAM_SIDEBAND_STEREO), synth.am_iq, 70, 128),
+    ("p48_ssbstereo_notch", dict(filter_path=48, dmod_mode=U.DEMOD_SSBSTEREO, dsp_active=U.DSP_NOTCH_ENABLE),
+     synth.ssb_iq, 66, 256),
+    ("p75_sam_st_notch", dict(filter_path=75, dmod_mode=U.DEMOD_SAM, sam_sideband=U.SAM_SIDEBAND_STEREO,
+                              dsp_active=U.DSP_NOTCH_ENABLE), synth.am_iq, 65, 256),
+]
+
+
+@pytest.mark.parametrize("name,kw,gen,C,N", STEREO_CASES, ids=[c[0] for c in STEREO_CASES])
+def test_device_stereo_matches_oracle(cuda, name, kw, gen, C, N):
+    """OVI40 two-channel modes on ragged batches: both output channels and the {l, r} codec frames."""
+    cfg = U.default_config(stereo_enable=1, **kw)
+    assert U.build_plan(cfg).stereo
+    iq = gen(np.arange(C), 0, 2048)
+    dev = DeviceStream(cfg, C, N)
+    outs = [dev(np.ascontiguousarray(iq[:, off:off + N])) for off in range(0, 2048, N)]
+    dev.chain.close()
+    a1, a0, dst = (np.concatenate([o[i] for o in outs], axis=1) for i in range(3))
+    r1, r0, rdst = oracle.OracleRx(U.build_plan(cfg), C).process2(iq, threads=8)
+    assert_bitexact(a1, r1, f"{name} a_buffer[1]")
+    assert_bitexact(a0, r0, f"{name} a_buffer[0]")
+    np.testing.assert_array_equal(dst, rdst)
 
 
 def test_device_c2_batch_sampled_channels(cuda):

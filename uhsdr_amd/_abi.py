@@ -160,6 +160,7 @@ SIGNATURES = {
     "uhsdr_rx_reset": (C.c_int, [C.c_void_p]),
     "uhsdr_rx_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "uhsdr_rx_process_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "uhsdr_rx_process_stereo": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "uhsdr_rx_get_plan": (C.c_int, [C.c_void_p, C.POINTER(RxPlan)]),
     "uhsdr_rx_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "uhsdr_rx_destroy": (C.c_int, [C.c_void_p]),

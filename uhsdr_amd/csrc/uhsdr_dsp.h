@@ -243,7 +243,6 @@ __device__ __forceinline__ void front_fill2(float* W, float* row0, float* row1, 
                                             const v2f* vals, int NV)
 {
     constexpr int hs4 = hist_stride(T) / 4, HQ = hist_q(T);
-    static_assert(((T - 1) & 1) == 0, "pair windows store new samples two pairs at a time");
     const int nnew = nb * NV;
     if (act)
     {
@@ -273,8 +272,11 @@ __device__ __forceinline__ void front_fill2(float* W, float* row0, float* row1, 
     if (act)
     {
         float* d = W + 2 * (T - 1 + b * NV);
-        for (int j = 0; j < NV; j += 2)
-            *(vf4*)(d + 2 * j) = vf4{ vals[j].x, vals[j].y, vals[j + 1].x, vals[j + 1].y };
+        if constexpr (((T - 1) & 1) == 0)           // 16-byte aligned: two pairs per store
+            for (int j = 0; j < NV; j += 2)
+                *(vf4*)(d + 2 * j) = vf4{ vals[j].x, vals[j].y, vals[j + 1].x, vals[j + 1].y };
+        else
+            for (int j = 0; j < NV; ++j) *(v2f*)(d + 2 * j) = vals[j];
         for (int t = b; t < FRONT_TAIL; t += nb) *(v2f*)(W + 2 * (T - 1 + nnew + t)) = v2f{ 0.0f, 0.0f };
     }
     wave_sync();

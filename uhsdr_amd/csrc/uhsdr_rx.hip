@@ -54,7 +54,24 @@ struct FrontArgs
     int C, N, ld, ldd;
     int lw;                  // LDS window pitch per channel (floats, multiple of 4; host picks it
                              // for conflict-free ds_read_b128, front_window_pitch)
+    int comb;                // demodulator of the Hilbert pair (audio_driver.c:2755-2790, FRONT_COMB_*)
 };
+
+// what rx_front makes of the Hilbert pair (I', Q'): a_buffer[0] (and a_buffer[1] in stereo)
+enum { FRONT_COMB_USB = 0,       // I + Q                      (USB, CW/DIGI upper, SSB stereo mono)
+       FRONT_COMB_LSB = 1,       // I - Q
+       FRONT_COMB_I = 2,         // I                          (DEMOD_IQ without stereo)
+       FRONT_COMB_SSB_ST = 3,    // {I + Q, I - Q}             (DEMOD_SSBSTEREO, use_stereo)
+       FRONT_COMB_IQ_ST = 4 };   // {I, Q}                     (DEMOD_IQ, use_stereo)
+
+__device__ __forceinline__ float front_comb(int comb, v2f h)
+{
+    return comb == FRONT_COMB_I ? h.x : comb == FRONT_COMB_LSB ? (h.x - h.y) : (h.x + h.y);
+}
+__device__ __forceinline__ v2f front_comb2(int comb, v2f h)
+{
+    return comb == FRONT_COMB_SSB_ST ? v2f{ h.x + h.y, h.x - h.y } : h;
+}
 
 // converted, corrected, frequency-shifted sample n of a channel (audio_driver.c:2660-2705)
 struct InputStage
@@ -157,7 +174,10 @@ __device__ __forceinline__ void convert_block(const int4 (&raw)[R / 2], const In
 // are issued early: the I/Q frames and the first two history rows at entry, and the row of
 // pass p+2 as soon as pass p has put its row into LDS (double-buffered registers), so each
 // pass's HBM latency hides behind the previous pass's FIR.
-template <int T1, int T2, int M, bool DECIM_FIRST, int R, bool F>
+// ST: use_stereo (DEMOD_SSBSTEREO / DEMOD_IQ): both channels of the pair continue -- through a
+// decimator pair (DECIMATE_RX_I / _Q, audio_driver.c:2792-2801) on the Hilbert-first paths --
+// into adec (a_buffer[0]) and adec_q (a_buffer[1])
+template <int T1, int T2, int M, bool DECIM_FIRST, int R, bool F, bool ST = false>
 __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -186,7 +206,7 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
     in.shift = P->freq_shift_hz != 0 ? P->shift_kind : 0;
     in.shift_up = P->shift_up;
     ctaps2_t* tA = as_taps2(a.taps2a);
-    const bool lsb = P->lsb;
+    const int comb = a.comb;
 
     // One wave per channel group.  The I/Q frames and the stage-1 history rows are issued at
     // entry; the stage-2 rows are issued before the stage-1 FIR, so their latency hides behind it.
@@ -305,6 +325,28 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
                 for (int r = 0; r < RD; ++r) dst[r] = d2[r].y;
             }
         }
+        else if constexpr (!DECIM_FIRST && ST)
+        {
+            // stereo: {a_buffer[0], a_buffer[1]} through the decimator pair (taps2b = {dec, dec})
+            vf4 hC[HQ2], hD[HQ2];
+            front_load_row<T2>(a.hist2_i, cl, b, nb, hC);
+            front_load_row<T2>(a.hist2_q, cl, b, nb, hD);
+            v2f h2[R], d2[RD];
+            fir_block2<T1, R, 1, F>(W + 2 * b * R, tA, h2);
+#pragma unroll
+            for (int r = 0; r < R; ++r) h2[r] = front_comb2(comb, h2[r]);
+            wave_sync();
+            front_fill2<T2>(W, a.hist2_i, a.hist2_q, c, act, live, b, nb, hC, hD, h2, R);
+            fir_block2<T2, RD, M, F>(W + 2 * b * R, as_taps2(a.taps2b), d2);
+#pragma unroll
+            for (int r = 0; r < RD; ++r) o[r] = d2[r].x;
+            if (live)
+            {
+                float* dst = a.adec_q + (size_t)c * a.ldd + b * RD;
+#pragma unroll
+                for (int r = 0; r < RD; ++r) dst[r] = d2[r].y;
+            }
+        }
         else if constexpr (!DECIM_FIRST)
         {
             vf4 hC[HQ2];
@@ -312,9 +354,9 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
                 v2f h2[R];
             float hs[R];
             fir_block2<T1, R, 1, F>(W + 2 * b * R, tA, h2);
-            // a = I + Q (USB) or I - Q (LSB), audio_driver.c:2781-2790
+            // a = I + Q (USB) or I - Q (LSB) or I (IQ mono), audio_driver.c:2755-2790
 #pragma unroll
-            for (int r = 0; r < R; ++r) hs[r] = lsb ? (h2[r].x - h2[r].y) : (h2[r].x + h2[r].y);
+            for (int r = 0; r < R; ++r) hs[r] = front_comb(comb, h2[r]);
             wave_sync();
             front_fill<T2>(W, a.hist2_i, c, act, live, b, nb, hC, hs, R);
             fir_block<T2, RD, M, 4, F>(W + b * R, as_taps(P->dec), o);
@@ -329,8 +371,27 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
             wave_sync();
             front_fill2<T2>(W, a.hist2_i, a.hist2_q, c, act, live, b, nb, hC, hD, d2, RD);
             fir_block2<T2, RD, 1, F>(W + 2 * b * RD, as_taps2(a.taps2b), h2);
+            if constexpr (ST)
+            {
 #pragma unroll
-            for (int r = 0; r < RD; ++r) o[r] = lsb ? (h2[r].x - h2[r].y) : (h2[r].x + h2[r].y);
+                for (int r = 0; r < RD; ++r)
+                {
+                    const v2f st2 = front_comb2(comb, h2[r]);
+                    o[r] = st2.x;
+                    h2[r].y = st2.y;
+                }
+                if (live)
+                {
+                    float* dst = a.adec_q + (size_t)c * a.ldd + b * RD;
+#pragma unroll
+                    for (int r = 0; r < RD; ++r) dst[r] = h2[r].y;
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int r = 0; r < RD; ++r) o[r] = front_comb(comb, h2[r]);
+            }
         }
         if (live)
         {
@@ -371,10 +432,13 @@ struct BackState
     float* bq2;      // [4][C]
     float* interp;   // [15][C]
     float* ring;     // [AGC_Q][B][C]  AGC inputs of the last AGC_Q calls
-    float* agc;      // [6 + AGC_Q][C]  spare volts save_volts fast_bavg hang_bavg wold | call maxima[Q-1], leaving sample
+    float* ring1;    // [AGC_Q][B][C]  stereo: the second channel's AGC inputs
+    float* agc;      // [8 + AGC_Q][C]  spare volts save_volts fast_bavg hang_bavg wold | call maxima[Q-1], leaving
+                     // sample | stereo: wold, leaving sample of the second channel
     int* agci;       // [3][C]   hang_counter decay_type state
     float* sam;      // AM / SAM: [7 + 96][C] phs omega2 fil_out dsI dsQ dc27 dc_insert | allpass a,b,c,d[24]
     float* cw;       // CW decoder front end: [5][C] goertzel buf[1] buf[2], old_siglevel, cw_state, change
+    float *pre1, *aa1, *bq1_1, *bq2_1, *interp1;   // stereo: instances [1] (audio_driver.c:78-161)
     float* notch;    // LMS auto notch: [64][C] coefficients, [64][C] state (63 used), [2][C] energy x0,
                      // [128][C] de-correlation delay line (lmsData, audio_driver.c:58-66)
 };
@@ -384,7 +448,8 @@ struct BackArgs
     const uhsdr_rx_plan* plan;
     const float* adec;   // [C][Nd]  (AM / SAM: decimated I)
     const float* adec_q; // [C][Nd]  AM / SAM: decimated Q
-    float* audio;        // [C][N]  or null
+    float* audio;        // [C][N]  or null: adb.a_buffer[1]
+    float* audio0;       // [C][N]  or null: adb.a_buffer[0], stereo only (the second channel)
     int2* dst;           // [C][N]  or null
     BackState s;
     int C, N, Nd;
@@ -440,7 +505,7 @@ __device__ __forceinline__ int to_dma(float f)
 
 // demodulator kinds of rx_back (DM): the SSB/CW/DIGI sum I +- Q happens in rx_front
 enum { DM_NONE = 0, DM_AM = 1, DM_SAM = 2, DM_SAM_SB = 3 /* SAM with the allpass sideband selector */,
-       DM_FM = 4 /* separate kernel, rx_fm */ };
+       DM_FM = 4 /* separate kernel, rx_fm */, DM_SAM_ST = 5 /* SAM stereo: LSB and USB channels */ };
 __host__ __device__ constexpr int back_roles(int dm) { return dm == DM_FM ? 2 : dm ? 6 : 5; }
 
 // The back end of one channel group runs as a pipeline over 32-frame calls, one wave per
@@ -558,7 +623,9 @@ struct LatticeStage
 };
 
 // ---- agc stage: AudioAgc_RunAgcWdsp (audio_agc.c:349-595) on the pre-filtered samples ----
-template <int L, int W>
+// NCH = 2: use_stereo (audio_agc.c:366-393, 575-593): both channels in the look-ahead ring, the
+// window maximum over the larger magnitude of the pair, one gain for both, DC removal per channel
+template <int L, int W, int NCH = 1>
 struct AgcStage
 {
     static constexpr int NDC = BLK / L;
@@ -567,13 +634,15 @@ struct AgcStage
     // -> SGPRs; reading them through P inside the loop would reload them every sample since the
     // state stores may alias, and a struct member copy of it defeats SROA and lands in scratch).
     bool agc_on;
-    float volts, save_volts, fast_bavg, hang_bavg, wold;
+    float volts, save_volts, fast_bavg, hang_bavg, wold[NCH];
     float cmax[AGC_Q - 1];                               // maxima of calls k-Q+1 .. k-1 (oldest first)
-    float leave_last;                                    // last sample of call k-Q-1
+    float leave_last[NCH];                               // last sample of call k-Q-1
     int hang_counter, decay_type, state;
-    float rnext[NDC];                                    // ring slot of the next call
-    float old[NDC], sfx[NDC], wmax, pmax;                // this call's ring slot, suffix maxima
-    float* ring_out;
+    float rnext[NCH][NDC];                               // ring slot of the next call
+    float old[NCH][NDC], sfx[NDC], wmax, pmax;           // this call's ring slot, suffix maxima
+    float* ring_out[NCH];
+
+    __device__ __forceinline__ static float* ring_of(const BackArgs& a, int ch) { return ch ? a.s.ring1 : a.s.ring; }
 
     __device__ __forceinline__ void load(const BackArgs& a, const BackLane& l, const uhsdr_agc_plan& A)
     {
@@ -583,10 +652,15 @@ struct AgcStage
         save_volts = a.s.agc[2 * C + cl];
         fast_bavg = a.s.agc[3 * C + cl];
         hang_bavg = a.s.agc[4 * C + cl];
-        wold = a.s.agc[5 * C + cl];
+        wold[0] = a.s.agc[5 * C + cl];
 #pragma unroll
         for (int i = 0; i < AGC_Q - 1; ++i) cmax[i] = a.s.agc[(6 + i) * C + cl];
-        leave_last = a.s.agc[(5 + AGC_Q) * C + cl];
+        leave_last[0] = a.s.agc[(5 + AGC_Q) * C + cl];
+        if (NCH == 2)
+        {
+            wold[NCH - 1] = a.s.agc[(6 + AGC_Q) * C + cl];
+            leave_last[NCH - 1] = a.s.agc[(7 + AGC_Q) * C + cl];
+        }
         hang_counter = a.s.agci[0 * C + cl];
         decay_type = a.s.agci[1 * C + cl];
         state = a.s.agci[2 * C + cl];
@@ -598,10 +672,24 @@ struct AgcStage
         if (agc_on)
         {
             const int slot = (a.ring_phase + call) % AGC_Q;
-            const float* rs = a.s.ring + (size_t)slot * NDC * l.C + l.cl;
 #pragma unroll
-            for (int m = 0; m < NDC; ++m) rnext[m] = rs[(size_t)m * l.C];
+            for (int ch = 0; ch < NCH; ++ch)
+            {
+                const float* rs = ring_of(a, ch) + (size_t)slot * NDC * l.C + l.cl;
+#pragma unroll
+                for (int m = 0; m < NDC; ++m) rnext[ch][m] = rs[(size_t)m * l.C];
+            }
         }
+    }
+
+    // |sample| as the reference's abs_ring holds it: the larger magnitude of the pair in stereo
+    template <typename F>
+    __device__ __forceinline__ static float absn(F&& v)
+    {
+        float r = fabsf(v(0));
+#pragma unroll
+        for (int ch = 1; ch < NCH; ++ch) r = fmaxf(r, fabsf(v(ch)));
+        return r;
     }
 
     // start of call `call`: take the fetched ring slot, issue the next call's fetch, suffix
@@ -609,34 +697,45 @@ struct AgcStage
     __device__ __forceinline__ void begin(const BackArgs& a, const BackLane& l, int call)
     {
 #pragma unroll
-        for (int m = 0; m < NDC; ++m) old[m] = rnext[m];
-        if (call + 1 < l.calls) fetch(a, l, call + 1);
-        sfx[NDC - 1] = fabsf(old[NDC - 1]);
+        for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
-        for (int m = NDC - 2; m >= 0; --m) sfx[m] = fmaxf(sfx[m + 1], fabsf(old[m]));
+            for (int m = 0; m < NDC; ++m) old[ch][m] = rnext[ch][m];
+        if (call + 1 < l.calls) fetch(a, l, call + 1);
+        sfx[NDC - 1] = absn([&](int ch) { return old[ch][NDC - 1]; });
+#pragma unroll
+        for (int m = NDC - 2; m >= 0; --m) sfx[m] = fmaxf(sfx[m + 1], absn([&](int ch) { return old[ch][m]; }));
         wmax = cmax[0];
 #pragma unroll
         for (int i = 1; i < AGC_Q - 1; ++i) wmax = fmaxf(wmax, cmax[i]);
         pmax = 0.0f;
-        ring_out = a.s.ring + (size_t)((a.ring_phase + call) % AGC_Q) * NDC * l.C + l.c;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch)
+            ring_out[ch] = ring_of(a, ch) + (size_t)((a.ring_phase + call) % AGC_Q) * NDC * l.C + l.c;
     }
 
-    // sample m of the call
-    __device__ __forceinline__ float step(int m, float x, const BackLane& l, const uhsdr_agc_plan& A)
+    // sample m of the call, x[ch] in place
+    __device__ __forceinline__ void stepn(int m, float (&x)[NCH], const BackLane& l, const uhsdr_agc_plan& A)
     {
         // ---- AudioAgc_RunAgcWdsp, audio_agc.c:349-595 ----
         if (!agc_on)
         {
-            x = x * A.fixed_gain;
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch) x[ch] = x[ch] * A.fixed_gain;
         }
         else
         {
-            const float out_sample = m ? old[m - 1] : leave_last;
-            const float abs_out = fabsf(out_sample);
-            if (l.live) ring_out[(size_t)m * l.C] = x;
+            float out_sample[NCH];
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch) out_sample[ch] = m ? old[ch][m - 1] : leave_last[ch];
+            const float abs_out = absn([&](int ch) { return out_sample[ch]; });
+            if (l.live)
+            {
+#pragma unroll
+                for (int ch = 0; ch < NCH; ++ch) ring_out[ch][(size_t)m * l.C] = x[ch];
+            }
             fast_bavg = A.fast_backmult * abs_out + A.onemfast_backmult * fast_bavg;
             hang_bavg = A.hang_backmult * abs_out + A.onemhang_backmult * hang_bavg;
-            pmax = fmaxf(pmax, fabsf(x));
+            pmax = fmaxf(pmax, absn([&](int ch) { return x[ch]; }));
             const float ring_max = fmaxf(fmaxf(pmax, wmax), sfx[m]);
             if (hang_counter > 0) --hang_counter;
             // the 5-state attack / decay / hang machine (audio_agc.c:436-551), as
@@ -694,20 +793,32 @@ struct AgcStage
             float vo = log10f_fast(A.inv_max_input * volts);
             if (vo > 0.0f) vo = 0.0f;
             const float mult = (A.out_target - A.slope_constant * vo) / volts;
-            x = out_sample * mult;
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch) x[ch] = out_sample[ch] * mult;
         }
         if (agc_on && A.remove_dc)                      // mode 5 returns first (audio_agc.c:354-365)
         {
-            const float w = (float)((double)x + (double)wold * 0.9999);
-            x = w - wold;
-            wold = w;
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch)
+            {
+                const float w = (float)((double)x[ch] + (double)wold[ch] * 0.9999);
+                x[ch] = w - wold[ch];
+                wold[ch] = w;
+            }
         }
-        return x;
+    }
+
+    __device__ __forceinline__ float step(int m, float x, const BackLane& l, const uhsdr_agc_plan& A)
+    {
+        float v[NCH] = { x };
+        stepn(m, v, l, A);
+        return v[0];
     }
 
     __device__ __forceinline__ void end()
     {
-        leave_last = old[NDC - 1];
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) leave_last[ch] = old[ch][NDC - 1];
 #pragma unroll
         for (int i = 0; i + 1 < AGC_Q - 1; ++i) cmax[i] = cmax[i + 1];
         cmax[AGC_Q - 2] = pmax;
@@ -721,10 +832,15 @@ struct AgcStage
         a.s.agc[2 * C + c] = save_volts;
         a.s.agc[3 * C + c] = fast_bavg;
         a.s.agc[4 * C + c] = hang_bavg;
-        a.s.agc[5 * C + c] = wold;
+        a.s.agc[5 * C + c] = wold[0];
 #pragma unroll
         for (int i = 0; i < AGC_Q - 1; ++i) a.s.agc[(6 + i) * C + c] = cmax[i];
-        a.s.agc[(5 + AGC_Q) * C + c] = leave_last;
+        a.s.agc[(5 + AGC_Q) * C + c] = leave_last[0];
+        if (NCH == 2)
+        {
+            a.s.agc[(6 + AGC_Q) * C + c] = wold[NCH - 1];
+            a.s.agc[(7 + AGC_Q) * C + c] = leave_last[NCH - 1];
+        }
         a.s.agci[0 * C + c] = hang_counter;
         a.s.agci[1 * C + c] = decay_type;
         a.s.agci[2 * C + c] = state;
@@ -900,8 +1016,10 @@ template <int L, int DM>
 struct DemodStage
 {
     static constexpr int NDC = BLK / L;
-    static constexpr int NA = DM == DM_SAM_SB ? 24 : 1;   // allpass delay lines (sam_data.a..d)
+    static constexpr bool SB = DM == DM_SAM_SB || DM == DM_SAM_ST;   // allpass sideband selector
+    static constexpr int NA = SB ? 24 : 1;                // allpass delay lines (sam_data.a..d)
     bool fade, lsb_sb;
+    float dc27_1, dc_insert_1, y1;                        // stereo: channel 1 fade leveler, its output
     float mtauR, onem_mtauR, mtauI, onem_mtauI;
     float g1, g2, omega_min, omega_max;
     float phs, omega2, fil_out, dsI, dsQ, dc27, dc_insert;
@@ -917,11 +1035,14 @@ struct DemodStage
         mtauR = P->fade_mtauR; onem_mtauR = P->fade_onem_mtauR;
         mtauI = P->fade_mtauI; onem_mtauI = P->fade_onem_mtauI;
         g1 = P->sam_g1; g2 = P->sam_g2; omega_min = P->sam_omega_min; omega_max = P->sam_omega_max;
-        lsb_sb = P->sam_sideband == UHSDR_SAM_SIDEBAND_LSB;
+        // SAM_SIDEBAND_STEREO puts the LSB demodulation in channel 0 (audio_driver.c:2091-2094)
+        lsb_sb = P->sam_sideband == UHSDR_SAM_SIDEBAND_LSB || P->sam_sideband == UHSDR_SAM_SIDEBAND_STEREO;
         phs = a.s.sam[0 * C + cl]; omega2 = a.s.sam[1 * C + cl]; fil_out = a.s.sam[2 * C + cl];
         dsI = a.s.sam[3 * C + cl]; dsQ = a.s.sam[4 * C + cl];
         dc27 = a.s.sam[5 * C + cl]; dc_insert = a.s.sam[6 * C + cl];
-        if (DM == DM_SAM_SB)
+        dc27_1 = 0.0f; dc_insert_1 = 0.0f; y1 = 0.0f;
+        if (DM == DM_SAM_ST) { dc27_1 = a.s.sam[103 * C + cl]; dc_insert_1 = a.s.sam[104 * C + cl]; }
+        if (SB)
         {
 #pragma unroll
             for (int f = 0; f < 4; ++f)
@@ -982,7 +1103,7 @@ struct DemodStage
             const float aq = Cos * xq[m];
             const float bq = Sin * xq[m];
             const float corr0 = ai + bq, corr1 = -bi + aq;
-            if (DM == DM_SAM_SB)
+            if (SB)
             {
                 // 7-stage allpass pair per path (audio_driver.c:2059-2097)
                 ap[0][0] = dsI; ap[1][0] = bi; ap[2][0] = dsQ; ap[3][0] = aq;
@@ -1004,12 +1125,23 @@ struct DemodStage
 #pragma unroll
                     for (int f = 0; f < 4; ++f) ap[f][j] = ap[f][j - 1];
                 audio = lsb_sb ? (ai_ps + bi_ps) - (aq_ps - bq_ps) : (ai_ps - bi_ps) + (aq_ps + bq_ps);
+                if (DM == DM_SAM_ST) y1 = (ai_ps - bi_ps) + (aq_ps + bq_ps);
             }
             else
             {
                 audio = corr0;
             }
-            if (fade) audio = fade_leveler(audio, corr0);
+            if (fade)
+            {
+                audio = fade_leveler(audio, corr0);
+                if (DM == DM_SAM_ST)
+                {
+                    // AudioDriver_FadeLeveler(1, ...), audio_driver.c:1911-1923
+                    dc27_1 = mtauR * dc27_1 + onem_mtauR * y1;
+                    dc_insert_1 = mtauI * dc_insert_1 + onem_mtauI * corr0;
+                    y1 = y1 + dc_insert_1 - dc27_1;
+                }
+            }
             // PLL (audio_driver.c:2128-2147)
             const float phzerror = ul_atan2f(corr1, corr0);
             const float del_out = fil_out;
@@ -1031,7 +1163,8 @@ struct DemodStage
         a.s.sam[0 * C + c] = phs; a.s.sam[1 * C + c] = omega2; a.s.sam[2 * C + c] = fil_out;
         a.s.sam[3 * C + c] = dsI; a.s.sam[4 * C + c] = dsQ;
         a.s.sam[5 * C + c] = dc27; a.s.sam[6 * C + c] = dc_insert;
-        if (DM == DM_SAM_SB)
+        if (DM == DM_SAM_ST) { a.s.sam[103 * C + c] = dc27_1; a.s.sam[104 * C + c] = dc_insert_1; }
+        if (SB)
         {
 #pragma unroll
             for (int f = 0; f < 4; ++f)
@@ -1288,6 +1421,124 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
 }
 
 // ------------------------------------------------------------------------------------
+// rx_back_stereo: the OVI40 two-channel back end (use_stereo, audio_driver.c:2618): channel 0
+// (a_buffer[0] at the decimated rate) and channel 1 (a_buffer[1]) each through their own
+// instances of the pre-filter, scale + biquad_1, interpolator, anti-alias lattice, biquad_2 and
+// line-out scale (audio_driver.c:2475-2479, 2527-2534, 2560-2590, 2832-2837, 2860-2866), with one
+// stereo AGC between them (audio_agc.c:366-393, 575-593).  After the interpolation the channels
+// swap buffers (:2563-2576): channel 0 ends in a_buffer[1] (audio, codec left), channel 1 in
+// a_buffer[0] (audio0, codec right).  The CW decoder front end reads channel 0.  Lane == channel,
+// all state in registers (the fused schedule; no small-batch pipeline variant).
+// DM: DM_NONE (SSB stereo / IQ: both channels from rx_front in adec / adec_q, or from rx_notch)
+// or DM_SAM_ST (the SAM PLL demodulator splitting LSB / USB here).
+template <int PRE, int AA, int L, int PH, int W, int DM>
+__global__ void __launch_bounds__(BACK_CH) rx_back_stereo(BackArgs a)
+{
+    const BackLane l(a);
+    constexpr int NDC = BLK / L;
+    static_assert(L == 2 || L == 4, "4 output frames per 1 or 2 decimated samples");
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    const uhsdr_agc_plan A = P->agc;
+    BackArgs b = a;                                      // channel 1: instances [1], input a_buffer[1]
+    b.adec = a.adec_q;
+    b.s.bq1 = a.s.bq1_1; b.s.bq2 = a.s.bq2_1; b.s.interp = a.s.interp1;
+    DemodStage<L, DM> dm;
+    InStage<L> in0, in1;
+    LatticeStage<PRE> pre0, pre1;
+    AgcStage<L, W, 2> ag;
+    AudioStage<L, PH, DM> au0, au1;
+    LatticeStage<AA> aa0, aa1;
+    OutputStage ou0, ou1;
+    if (DM) { dm.load(a, l); dm.fetch(a, l, 0); }
+    else { in0.fetch(a, l, 0); in1.fetch(b, l, 0); }
+    pre0.load(l, P->pre_k, P->pre_v, a.s.pre);
+    pre1.load(l, P->pre_k, P->pre_v, a.s.pre1);
+    ag.load(a, l, A);
+    ag.fetch(a, l, 0);
+    au0.load(a, l);
+    au1.load(b, l);
+    au1.cw = false;                                      // CwDecode_RxProcessor reads a_buffer[0] only
+    aa0.load(l, P->aa_k, P->aa_v, a.s.aa);
+    aa1.load(l, P->aa_k, P->aa_v, a.s.aa1);
+    ou0.load(a, l);
+    ou1.load(b, l);
+    for (int call = 0; call < l.calls; ++call)
+    {
+        float x0[NDC], x1[NDC];
+        if (DM)
+        {
+            dm.begin(a, l, call);
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) { x0[m] = dm.step(m); x1[m] = dm.y1; }
+        }
+        else
+        {
+            in0.begin(a, l, call, x0);
+            in1.begin(b, l, call, x1);
+        }
+        ag.begin(a, l, call);
+        float y0[BLK], y1[BLK];
+#pragma unroll
+        for (int m = 0; m < NDC; ++m)
+        {
+            float v[2] = { pre0.step(x0[m]), pre1.step(x1[m]) };
+            ag.stepn(m, v, l, A);
+            float u0[L], u1[L];
+            au0.step(v[0], u0);
+            au1.step(v[1], u1);
+#pragma unroll
+            for (int j = 0; j < L; ++j)
+            {
+                y0[m * L + j] = ou0.step(aa0.step(u0[j]));
+                y1[m * L + j] = ou1.step(aa1.step(u1[j]));
+            }
+        }
+        if (a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK)
+        {
+#pragma unroll
+            for (int n = 0; n < BLK; ++n)
+            {
+                const int fr = call * BLK + n;
+                if (fr >= a.beep_n0 && fr < a.beep_n1)
+                {
+                    const float t = beep_tone(a, fr);
+                    y1[n] += t;                          // softdds_addSingleToneToTwobuffers(a_buffer[0], [1])
+                    y0[n] += t;
+                }
+            }
+        }
+        if (l.live)
+        {
+            const size_t row = (size_t)l.c * a.N + call * BLK;
+#pragma unroll
+            for (int n0 = 0; n0 < BLK; n0 += 4)
+            {
+                if (a.audio) *(float4*)(a.audio + row + n0) = make_float4(y0[n0], y0[n0 + 1], y0[n0 + 2], y0[n0 + 3]);
+                if (a.audio0) *(float4*)(a.audio0 + row + n0) = make_float4(y1[n0], y1[n0 + 1], y1[n0 + 2], y1[n0 + 3]);
+                if (a.dst)
+                {
+                    // dst.l = a_buffer[1] (channel 0), dst.r = a_buffer[0] (channel 1), :2911-2923
+                    *(int4*)(a.dst + row + n0) = make_int4(to_dma(y0[n0]), to_dma(y1[n0]), to_dma(y0[n0 + 1]), to_dma(y1[n0 + 1]));
+                    *(int4*)(a.dst + row + n0 + 2) = make_int4(to_dma(y0[n0 + 2]), to_dma(y1[n0 + 2]), to_dma(y0[n0 + 3]), to_dma(y1[n0 + 3]));
+                }
+            }
+        }
+        ag.end();
+        au0.end(a, l, call);
+    }
+    if (DM) dm.store(a, l);
+    pre0.store(l, a.s.pre);
+    pre1.store(l, a.s.pre1);
+    ag.store(a, l);
+    au0.store(a, l);
+    au1.store(b, l);
+    aa0.store(l, a.s.aa);
+    aa1.store(l, a.s.aa1);
+    ou0.store(a, l);
+    ou1.store(b, l);
+}
+
+// ------------------------------------------------------------------------------------
 // rx_notch: the LMS auto notch (AudioDriver_NotchFilter, audio_driver.c:1746-1763, called from
 // RxProcessor_DemodAudioPostprocessing :2443-2456 when DSP_NOTCH_ENABLE is set), in place on the
 // decimated audio a_buffer[0] between the demodulator and the IIR pre-filter.  Lane == channel:
@@ -1329,12 +1580,19 @@ __global__ void __launch_bounds__(BACK_CH) rx_notch(BackArgs a)
     const float mu = P->notch_mu;
     for (int call = 0; call < l.calls; ++call)
     {
-        float x[NDC];
+        float x[NDC], x1[NDC];
         if (DM)
         {
             dm.begin(a, l, call);
 #pragma unroll
-            for (int m = 0; m < NDC; ++m) x[m] = dm.step(m);
+            for (int m = 0; m < NDC; ++m) { x[m] = dm.step(m); x1[m] = dm.y1; }
+            if (DM == DM_SAM_ST && l.live)
+            {
+                // SAM stereo: channel 1 (a_buffer[1]) continues un-notched to rx_back_stereo
+                float* d1 = const_cast<float*>(a.adec_q) + (size_t)l.c * a.Nd + call * NDC;
+#pragma unroll
+                for (int m = 0; m < NDC; m += 4) *(float4*)(d1 + m) = make_float4(x1[m], x1[m + 1], x1[m + 2], x1[m + 3]);
+            }
         }
         else
             in.begin(a, l, call, x);
@@ -1622,13 +1880,14 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
 typedef void (*front_fn)(FrontArgs);
 typedef void (*back_fn)(BackArgs);
 
-struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; front_fn fn_fma; };
+struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; front_fn fn_fma; int st; };
 struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; };
 
 // R = FIR outputs per lane: 16 for large batches (more MACs per window load), 8 for small
 // batches (twice the waves in flight).  fn: reference MAC order (bit-exact); fn_fma: fused MACs
 // (UHSDR_PRECISION_FMA)
-#define FRONT_V(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false>, R, rx_front<t1, t2, m, df, R, true> }
+#define FRONT_V(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false>, R, rx_front<t1, t2, m, df, R, true>, 0 }
+#define FRONT_ST(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false, true>, R, rx_front<t1, t2, m, df, R, true, true>, 1 }
 static const FrontVariant kFront[] = {
     FRONT_V(89, 43, 4, false, 16), FRONT_V(89, 43, 4, false, 8),     // wide SSB/CW  (P48-54)
     FRONT_V(89, 4, 2, false, 16), FRONT_V(89, 4, 2, false, 8),       // 24 ksps SSB   (P55-65)
@@ -1636,8 +1895,13 @@ static const FrontVariant kFront[] = {
     FRONT_V(89, 0, 4, true, 16), FRONT_V(89, 0, 4, true, 8),         // AM / SAM, 12 ksps (P66-82)
     FRONT_V(89, 0, 2, true, 16), FRONT_V(89, 0, 2, true, 8),         // AM / SAM, 24 ksps (P83-86)
     FRONT_V(89, 0, 1, false, 16), FRONT_V(89, 0, 1, false, 8),       // FM, 48 ksps Hilbert pair (P1-3)
+    // OVI40 stereo (DEMOD_SSBSTEREO / DEMOD_IQ with use_stereo): two channels out
+    FRONT_ST(89, 43, 4, false, 16), FRONT_ST(89, 43, 4, false, 8),
+    FRONT_ST(89, 4, 2, false, 16), FRONT_ST(89, 4, 2, false, 8),
+    FRONT_ST(83, 199, 4, true, 16), FRONT_ST(83, 199, 4, true, 8),
 };
 #undef FRONT_V
+#undef FRONT_ST
 
 #define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm> }
 static const BackVariant kBack[] = {
@@ -1657,6 +1921,17 @@ static const BackVariant kBack[] = {
 static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6>, nullptr };
 #undef BACK_V
 
+// OVI40 stereo back ends (rx_back_stereo): SSB stereo / IQ families, and SAM stereo
+#define BACK_ST(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back_stereo<pre, aa, L, ph, w, dm>, rx_back_stereo<pre, aa, L, ph, w, dm> }
+static const BackVariant kBackStereo[] = {
+    BACK_ST(10, 6, 4, 1, 49, DM_NONE), BACK_ST(10, 0, 4, 4, 49, DM_NONE), BACK_ST(0, 0, 2, 8, 97, DM_NONE),
+    BACK_ST(0, 6, 2, 2, 97, DM_NONE), BACK_ST(10, 0, 2, 8, 97, DM_NONE), BACK_ST(8, 0, 2, 8, 97, DM_NONE),
+    BACK_ST(8, 6, 2, 2, 97, DM_NONE),
+    BACK_ST(10, 0, 4, 4, 49, DM_SAM_ST), BACK_ST(10, 6, 4, 1, 49, DM_SAM_ST), BACK_ST(10, 0, 2, 8, 97, DM_SAM_ST),
+    BACK_ST(8, 0, 2, 8, 97, DM_SAM_ST), BACK_ST(8, 6, 2, 2, 97, DM_SAM_ST),
+};
+#undef BACK_ST
+
 // LMS auto notch (+ the AM / SAM demodulator ahead of it): decimation L, demodulator DM
 struct NotchVariant { int L, dm; back_fn fn; };
 static const NotchVariant kNotch[] = {
@@ -1664,13 +1939,15 @@ static const NotchVariant kNotch[] = {
     { 4, DM_AM, rx_notch<4, DM_AM> }, { 2, DM_AM, rx_notch<2, DM_AM> },
     { 4, DM_SAM, rx_notch<4, DM_SAM> }, { 2, DM_SAM, rx_notch<2, DM_SAM> },
     { 4, DM_SAM_SB, rx_notch<4, DM_SAM_SB> }, { 2, DM_SAM_SB, rx_notch<2, DM_SAM_SB> },
+    { 4, DM_SAM_ST, rx_notch<4, DM_SAM_ST> }, { 2, DM_SAM_ST, rx_notch<2, DM_SAM_ST> },
 };
 
 static int plan_dm(const uhsdr_rx_plan& p)
 {
     if (p.dmod_mode == UHSDR_DEMOD_FM) return DM_FM;
     if (p.dmod_mode == UHSDR_DEMOD_AM) return DM_AM;
-    if (p.dmod_mode == UHSDR_DEMOD_SAM) return p.sam_sideband == UHSDR_SAM_SIDEBAND_BOTH ? DM_SAM : DM_SAM_SB;
+    if (p.dmod_mode == UHSDR_DEMOD_SAM)
+        return p.sam_sideband == UHSDR_SAM_SIDEBAND_BOTH ? DM_SAM : p.stereo == 3 ? DM_SAM_ST : DM_SAM_SB;
     return DM_NONE;
 }
 
@@ -1687,9 +1964,10 @@ static const FrontVariant* find_front(const uhsdr_rx_plan& p, long long C = 0, i
     const int t2 = p.use_decimated_iq ? p.hilbert_taps : p.dec_taps;
     const char* env = getenv("UHSDR_FRONT_R");
     const int want = env ? atoi(env) : 8;
+    const int st = p.stereo == 1 || p.stereo == 2;       // SAM stereo splits in the demodulator
     const FrontVariant* best = nullptr;
     for (const FrontVariant& v : kFront)
-        if (v.t1 == t1 && v.t2 == t2 && v.m == p.decimation_rate && v.decim_first == p.use_decimated_iq)
+        if (v.t1 == t1 && v.t2 == t2 && v.m == p.decimation_rate && v.decim_first == p.use_decimated_iq && v.st == st)
         {
             if (N && (N % v.R || front_frames(N, v.R) / v.R < 4)) continue;   // >= 4 lanes per channel
             if (!best || (v.R == want && best->R != want)) best = &v;
@@ -1710,6 +1988,14 @@ static const BackVariant* find_back(const uhsdr_rx_plan& p)
 {
     if (p.dmod_mode == UHSDR_DEMOD_FM) return p.sq_stages == 6 ? &kBackFm : nullptr;
     const int dm = p.notch_enabled ? DM_NONE : plan_dm(p);
+    if (p.stereo)
+    {
+        for (const BackVariant& v : kBackStereo)
+            if (v.pre == p.pre_stages && v.aa == p.aa_stages && v.L == p.interp_L && v.ph == p.interp_phase &&
+                v.w == p.agc.attack_buffsize && v.dm == dm)
+                return &v;
+        return nullptr;
+    }
     for (const BackVariant& v : kBack)
         if (v.pre == p.pre_stages && v.aa == p.aa_stages && v.L == p.interp_L && v.ph == p.interp_phase &&
             v.w == p.agc.attack_buffsize && v.dm == dm)
@@ -1816,17 +2102,18 @@ static int front_window_pitch(const uhsdr_rx_s* h)
 {
     const int N = h->Nf, R = h->fv->R, M = h->plan.decimation_rate;
     const bool df = h->plan.use_decimated_iq;
+    const bool pair2 = df || h->fv->st;                  // pass 2 is a FIR pair over {x0, x1}
     const int nb = N / R, cpw = FRONT_WAVE / nb;
     const int n2 = df ? N / M : N;
     int need = 2 * (h->T1 - 1 + N + FRONT_TAIL);
-    const int need2 = h->T2 ? (df ? 2 : 1) * (h->T2 - 1 + n2 + FRONT_TAIL) : 0;
+    const int need2 = h->T2 ? (pair2 ? 2 : 1) * (h->T2 - 1 + n2 + FRONT_TAIL) : 0;
     need = ((need > need2 ? need : need2) + 3) & ~3;
     const int rd = R / M;
     int best = need, best_cost = 1 << 30;
     for (int lw = need; lw < need + 64; lw += 4)
     {
         int cost = window_conflicts(lw, nb, cpw, 2 * R, 2 * R, 4);
-        if (h->T2) cost += window_conflicts(lw, nb, cpw, 2 * R, df ? 2 * rd : R, 4);
+        if (h->T2) cost += window_conflicts(lw, nb, cpw, 2 * R, df ? 2 * rd : pair2 ? 2 * R : R, 4);
         if (cost < best_cost) { best_cost = cost; best = lw; }
     }
     return best;
@@ -1909,8 +2196,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     if (N % BLK) { uhsdr_set_error("frames_per_call %d not a multiple of %d", N, BLK); return UHSDR_LENGTH_ERROR; }
     *out = nullptr;
     uhsdr_rx_s* h = (uhsdr_rx_s*)calloc(1, sizeof(uhsdr_rx_s));
-    uhsdr_status st = uhsdr_rx_plan_build(cfg, &h->plan);
-    if (st != UHSDR_OK) { free(h); return st; }
+    uhsdr_status bst = uhsdr_rx_plan_build(cfg, &h->plan);
+    if (bst != UHSDR_OK) { free(h); return bst; }
     const uhsdr_rx_plan& p = h->plan;
     h->fv = find_front(p, C, N);
     h->bv = find_back(p);
@@ -1946,9 +2233,14 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const size_t o_teta = take((size_t)3 * C), o_osc = take(4);
     const size_t o_pre = take((size_t)10 * C), o_aa = take((size_t)10 * C), o_bq1 = take((size_t)16 * C);
     const size_t o_bq2 = take((size_t)4 * C), o_ip = take((size_t)15 * C), o_ring = take(W > 0 ? (size_t)(W - 1) * C : 0);
-    const size_t o_agc = take((size_t)(6 + AGC_Q) * C), o_agci = take((size_t)3 * C);
+    const size_t o_agc = take((size_t)(8 + AGC_Q) * C), o_agci = take((size_t)3 * C);
     const bool am = plan_dm(p) != DM_NONE;             // AM / SAM / FM demodulator state
-    const size_t o_sam = take(am ? (size_t)(7 + 96) * C : 0), o_adq = take(am ? (size_t)C * h->Nd : 0);
+    const bool st = p.stereo != 0;                      // second audio channel
+    const size_t o_sam = take(am ? (size_t)(7 + 96 + 2) * C : 0), o_adq = take(am || st ? (size_t)C * h->Nd : 0);
+    const size_t o_ring1 = take(st && W > 0 ? (size_t)(W - 1) * C : 0);
+    const size_t o_pre1 = take(st ? (size_t)10 * C : 0), o_aa1 = take(st ? (size_t)10 * C : 0);
+    const size_t o_bq1_1 = take(st ? (size_t)16 * C : 0), o_bq2_1 = take(st ? (size_t)4 * C : 0);
+    const size_t o_ip1 = take(st ? (size_t)15 * C : 0);
     const size_t o_notch = take(h->nv ? (size_t)(2 * NOTCH_TAPS + 2 + NOTCH_DELAY) * C : 0);
     const bool cw = p.cw_enabled && p.decimation_rate == 4;
     const size_t o_cw = take(cw ? (size_t)5 * C : 0);
@@ -1970,12 +2262,16 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->bs.sam = am ? A + o_sam : nullptr;
     h->bs.cw = cw ? A + o_cw : nullptr;
     h->bs.notch = h->nv ? A + o_notch : nullptr;
+    h->bs.ring1 = st ? A + o_ring1 : nullptr;
+    h->bs.pre1 = st ? A + o_pre1 : nullptr; h->bs.aa1 = st ? A + o_aa1 : nullptr;
+    h->bs.bq1_1 = st ? A + o_bq1_1 : nullptr; h->bs.bq2_1 = st ? A + o_bq2_1 : nullptr;
+    h->bs.interp1 = st ? A + o_ip1 : nullptr;
     {
         // blocks per call: one completes at the end of every ceil(blocksize / NDC)-th call
         const int ndc = BLK / p.decimation_rate, cpb = (p.cw_blocksize + ndc - 1) / ndc;
         h->cw_bmax = cw ? (N / BLK + cpb - 1) / cpb : 0;
     }
-    h->adec_q = am ? A + o_adq : nullptr;
+    h->adec_q = am || st ? A + o_adq : nullptr;
     {
         // pass 1: the Hilbert / low-pass pair (Hilbert-first and FM), or the I and Q decimators
         // (DECIMATE_RX_I / _Q: the same table for SSB, the path's I and Q tables for AM / SAM);
@@ -1989,7 +2285,11 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
             if (h->T2) pair_taps(t2 + 2 * TAPS2_MAX, p.hilbert_i, p.hilbert_q, p.hilbert_taps);
         }
         else
+        {
             pair_taps(t2, p.hilbert_i, p.hilbert_q, p.hilbert_taps);
+            // stereo Hilbert-first: DECIMATE_RX_I / _Q (the same table) as a pair
+            if (h->fv->st) pair_taps(t2 + 2 * TAPS2_MAX, p.dec, p.dec, p.dec_taps);
+        }
         if (hipMemcpy(h->d_taps2, t2, sizeof t2, hipMemcpyHostToDevice) != hipSuccess)
         {
             uhsdr_set_error("tap upload failed");
@@ -2038,7 +2338,29 @@ extern "C" uhsdr_status uhsdr_rx_set_stream(uhsdr_rx_handle h, void* stream)
     return UHSDR_OK;
 }
 
+static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, float* audio0, int32_t* dst);
+
 extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, int32_t* dst)
+{
+    return rx_process(h, iq, audio, nullptr, dst);
+}
+
+extern "C" uhsdr_status uhsdr_rx_process_stereo(uhsdr_rx_handle h, const int32_t* iq, float* audio, float* audio0,
+                                                int32_t* dst)
+{
+    return rx_process(h, iq, audio, audio0, dst);
+}
+
+// demodulator of rx_front's Hilbert pair (FRONT_COMB_*)
+static int front_comb_of(const uhsdr_rx_plan& p)
+{
+    if (p.stereo == 1) return FRONT_COMB_SSB_ST;
+    if (p.stereo == 2) return FRONT_COMB_IQ_ST;
+    if (p.dmod_mode == UHSDR_DEMOD_IQ) return FRONT_COMB_I;
+    return p.lsb ? FRONT_COMB_LSB : FRONT_COMB_USB;
+}
+
+static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, float* audio0, int32_t* dst)
 {
     if (!h || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
     if (h->timing && h->nev >= h->nev_cap) time_harvest(h);
@@ -2068,6 +2390,7 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
         fa.lw = h->lw;
         fa.taps2a = h->d_taps2;
         fa.taps2b = h->d_taps2 + 2 * TAPS2_MAX;
+        fa.comb = front_comb_of(h->plan);
         hipLaunchKernelGGL(h->precision == UHSDR_PRECISION_FMA ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw), dim3(FRONT_WAVE), lds, h->stream, fa);
         HIPCHK(hipGetLastError());
         h->front_launches += 1;
@@ -2079,6 +2402,7 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
     ba.adec = adec;
     ba.adec_q = adec_q;
     ba.audio = audio;
+    ba.audio0 = h->plan.stereo ? audio0 : nullptr;
     ba.dst = (int2*)dst;
     ba.s = h->bs;
     ba.C = h->C; ba.N = h->N; ba.Nd = h->Nd;
@@ -2126,7 +2450,7 @@ extern "C" uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, f
         hipLaunchKernelGGL(h->nv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
         HIPCHK(hipGetLastError());
     }
-    if (h->back_fused)
+    if (h->back_fused || h->plan.stereo)
         hipLaunchKernelGGL(h->bv->fused, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
     else
         hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH),

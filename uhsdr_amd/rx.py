@@ -59,6 +59,18 @@ class RxChain:
             C.c_void_p(audio.data_ptr() if audio is not None else 0),
             C.c_void_p(dst.data_ptr() if dst is not None else 0)), "uhsdr_rx_process")
 
+    def process_stereo(self, iq, audio=None, audio0=None, dst=None) -> None:
+        """OVI40 two-channel modes: audio = a_buffer[1] (channel 0), audio0 = a_buffer[0] (channel 1)."""
+        self._shape_ok(iq, (2,))
+        for t, last in ((audio, ()), (audio0, ()), (dst, (2,))):
+            if t is not None:
+                self._shape_ok(t, last)
+                if not t.is_contiguous():
+                    raise ValueError("buffers must be contiguous")
+        ptr = lambda t: C.c_void_p(t.data_ptr() if t is not None else 0)  # noqa: E731
+        _abi.check(self.lib.uhsdr_rx_process_stereo(self.handle, ptr(iq), ptr(audio), ptr(audio0), ptr(dst)),
+                   "uhsdr_rx_process_stereo")
+
     def process_host(self, iq: np.ndarray):
         """Host numpy in/out: returns (audio [C][N] f32, dst [C][N][2] int32)."""
         iq = np.ascontiguousarray(iq, dtype=np.int32)

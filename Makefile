@@ -65,3 +65,13 @@ clean:
 	rm -rf $(OBJDIR) uhsdr_amd/lib oracle/build examples/build
 
 .PHONY: all ref clean
+
+# compile-time variants of libuhsdr_amd.so for A/B measurement (bench.py with UHSDR_LIB=<path>):
+#   make variant VTAG=w3 VFLAGS=-DUHSDR_FUSED_WAVES=3
+VARIANT_DIR := uhsdr_amd/lib/variants
+variant: $(HOST_OBJS) $(filter-out $(OBJDIR)/uhsdr_rx.o,$(HIP_OBJS))
+	mkdir -p $(VARIANT_DIR) $(OBJDIR)/v_$(VTAG)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c uhsdr_amd/csrc/uhsdr_rx.hip -o $(OBJDIR)/v_$(VTAG)/uhsdr_rx.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(VARIANT_DIR)/libuhsdr_amd_$(VTAG).so $(HOST_OBJS) $(OBJDIR)/v_$(VTAG)/uhsdr_rx.o $(filter-out $(OBJDIR)/uhsdr_rx.o,$(HIP_OBJS)) -lm
+
+.PHONY: variant

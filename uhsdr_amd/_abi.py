@@ -227,7 +227,8 @@ def load(path: str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # UHSDR_LIB: an alternative build of the same library (A/B measurements of compile variants)
+    p = path or os.environ.get("UHSDR_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise RuntimeError(f"{p} not built: run `make` (or __graft_entry__.build())")
     lib = C.CDLL(p)

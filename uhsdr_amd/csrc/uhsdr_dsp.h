@@ -167,6 +167,23 @@ constexpr int FRONT_TAIL = 24;
 
 // LDS accesses of one wave are processed in order; the fences only stop the compiler from
 // moving a lane's LDS access across a hand-off between lanes of the same wave.
+// A wave-uniform value held in a VGPR: a VOP2 with an SGPR operand issues at half the rate of
+// one with VGPR operands, and gfx9's one-SGPR-per-VALU-instruction limit plus a
+// full SGPR file otherwise cost v_readlane refills of spilled SGPRs.  The asm keeps the compiler
+// from folding the value back into an SGPR.
+__device__ __forceinline__ float to_vgpr(float x)
+{
+    float r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void to_vgpr(float (&x)[N])
+{
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = to_vgpr(x[i]);
+}
+
 __device__ __forceinline__ void wave_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

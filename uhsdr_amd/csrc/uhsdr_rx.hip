@@ -210,6 +210,8 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
 
     // One wave per channel group.  The I/Q frames and the stage-1 history rows are issued at
     // entry; the stage-2 rows are issued before the stage-1 FIR, so their latency hides behind it.
+    // (A persistent variant that prefetched the next group's frames and rows into registers
+    // doubled the VGPRs and halved the waves per SIMD: 0.67 vs 0.59 ms at 1M x 64.)
     const int grp = blockIdx.x;
     int4 raw[R / 2];
     vf4 hA[HQ1], hB[HQ1];
@@ -502,6 +504,11 @@ __device__ __forceinline__ int to_dma(float f)
 }
 
 #define BACK_CH 64
+// rx_back_fused: waves per SIMD the register allocation targets (2: 256 VGPRs, no scratch; 3
+// spills to scratch and measured 0.265 vs 0.217 ms at 1M x 64)
+#ifndef UHSDR_FUSED_WAVES
+#define UHSDR_FUSED_WAVES 2
+#endif
 
 // demodulator kinds of rx_back (DM): the SSB/CW/DIGI sum I +- Q happens in rx_front
 enum { DM_NONE = 0, DM_AM = 1, DM_SAM = 2, DM_SAM_SB = 3 /* SAM with the allpass sideband selector */,
@@ -573,11 +580,13 @@ struct InStage
 
     __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
     {
-        const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
+        // uniform row base (SGPRs) + the lane's 32-bit offset: no 64-bit per-lane address to keep
+        const float* src = a.adec + call * NDC;
+        const unsigned off = (unsigned)l.cl * (unsigned)a.Nd;
 #pragma unroll
         for (int m = 0; m < NDC; m += 4)
         {
-            const float4 v = *(const float4*)(src + m);
+            const float4 v = *(const float4*)(src + m + off);
             xnext[m] = v.x; xnext[m + 1] = v.y; xnext[m + 2] = v.z; xnext[m + 3] = v.w;
         }
     }
@@ -633,7 +642,8 @@ struct AgcStage
     // The AGC plan values live in the caller's local copy of P->agc, passed to step() (uniform
     // -> SGPRs; reading them through P inside the loop would reload them every sample since the
     // state stores may alias, and a struct member copy of it defeats SROA and lands in scratch).
-    bool agc_on;
+    bool agc_on, dc;                                     // mode != 5; DC removal (AM / SAM)
+    bool dc_sel;                                         // DC removal applied by select, not a branch
     float volts, save_volts, fast_bavg, hang_bavg, wold[NCH];
     float cmax[AGC_Q - 1];                               // maxima of calls k-Q+1 .. k-1 (oldest first)
     float leave_last[NCH];                               // last sample of call k-Q-1
@@ -648,6 +658,8 @@ struct AgcStage
     {
         const int C = l.C, cl = l.cl;
         agc_on = A.mode != 5;
+        dc = A.remove_dc != 0;
+        dc_sel = false;
         volts = a.s.agc[1 * C + cl];
         save_volts = a.s.agc[2 * C + cl];
         fast_bavg = a.s.agc[3 * C + cl];
@@ -675,9 +687,9 @@ struct AgcStage
 #pragma unroll
             for (int ch = 0; ch < NCH; ++ch)
             {
-                const float* rs = ring_of(a, ch) + (size_t)slot * NDC * l.C + l.cl;
+                const float* rs = ring_of(a, ch) + (size_t)slot * NDC * l.C;
 #pragma unroll
-                for (int m = 0; m < NDC; ++m) rnext[ch][m] = rs[(size_t)m * l.C];
+                for (int m = 0; m < NDC; ++m) rnext[ch][m] = rs[(size_t)m * l.C + (unsigned)l.cl];
             }
         }
     }
@@ -710,10 +722,13 @@ struct AgcStage
         pmax = 0.0f;
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch)
-            ring_out[ch] = ring_of(a, ch) + (size_t)((a.ring_phase + call) % AGC_Q) * NDC * l.C + l.c;
+            ring_out[ch] = ring_of(a, ch) + (size_t)((a.ring_phase + call) % AGC_Q) * NDC * l.C;
     }
 
-    // sample m of the call, x[ch] in place
+    // sample m of the call, x[ch] in place.  Branch-free: the per-lane state machine is a set of
+    // selects, and the ring store is unconditional (a lane past the last channel computes exactly
+    // what channel C-1 computes from the clamped loads, so it stores the same value to the same
+    // address), so a whole call of the fused back end is one basic block.
     __device__ __forceinline__ void stepn(int m, float (&x)[NCH], const BackLane& l, const uhsdr_agc_plan& A)
     {
         // ---- AudioAgc_RunAgcWdsp, audio_agc.c:349-595 ----
@@ -728,75 +743,66 @@ struct AgcStage
 #pragma unroll
             for (int ch = 0; ch < NCH; ++ch) out_sample[ch] = m ? old[ch][m - 1] : leave_last[ch];
             const float abs_out = absn([&](int ch) { return out_sample[ch]; });
-            if (l.live)
-            {
 #pragma unroll
-                for (int ch = 0; ch < NCH; ++ch) ring_out[ch][(size_t)m * l.C] = x[ch];
-            }
+            for (int ch = 0; ch < NCH; ++ch) ring_out[ch][(size_t)m * l.C + (unsigned)l.cl] = x[ch];
             fast_bavg = A.fast_backmult * abs_out + A.onemfast_backmult * fast_bavg;
             hang_bavg = A.hang_backmult * abs_out + A.onemhang_backmult * hang_bavg;
             pmax = fmaxf(pmax, absn([&](int ch) { return x[ch]; }));
             const float ring_max = fmaxf(fmaxf(pmax, wmax), sfx[m]);
-            if (hang_counter > 0) --hang_counter;
-            // the 5-state attack / decay / hang machine (audio_agc.c:436-551), as
-            // selects: mu = the multiplier the taken branch applies (selects between values,
-            // not between fields of A, which would pin A in scratch memory)
-            const float attack_mult = A.attack_mult, decay_mult = A.decay_mult;
-            const float fast_decay_mult = A.fast_decay_mult, hang_decay_mult = A.hang_decay_mult;
-            const int hang_counter_init = A.hang_counter_init;
+            hang_counter = hang_counter > 0 ? hang_counter - 1 : hang_counter;
+            // the 5-state attack / decay / hang machine (audio_agc.c:436-551): every case is
+            // evaluated and the lane's state selects; mu = the multiplier the taken branch applies
             const float rv = ring_max - volts;
             const bool atk = ring_max >= volts;
-            float mu = 0.0f;
-            bool upd = false, save = false;
-            int ns = state;
-            if (state == 0)
-            {
-                const bool fast = volts > A.pop_ratio * fast_bavg;
-                const bool hang = A.hang_enable && (hang_bavg > A.hang_level);
-                ns = atk ? 0 : fast ? 1 : hang ? 2 : 3;
-                upd = atk || fast || !hang;
-                mu = atk ? attack_mult : fast ? fast_decay_mult : decay_mult;
-                if (!atk && !fast)
-                {
-                    hang_counter = hang ? hang_counter_init : hang_counter;
-                    decay_type = hang ? 1 : 0;
-                }
-            }
-            else if (state == 1)
-            {
-                const bool fd = volts > save_volts;
-                const bool hc = hang_counter > 0;
-                ns = atk ? 0 : fd ? 1 : hc ? 2 : (decay_type == 0) ? 3 : 4;
-                upd = atk || fd || !hc;
-                mu = atk ? attack_mult : fd ? fast_decay_mult
-                                               : (decay_type == 0) ? decay_mult : hang_decay_mult;
-            }
-            else if (state == 2)
-            {
-                const bool hz = hang_counter == 0;
-                ns = atk ? 0 : hz ? 4 : 2;
-                upd = atk || hz;
-                save = atk;
-                mu = atk ? attack_mult : hang_decay_mult;
-            }
-            else
-            {
-                ns = atk ? 0 : state;
-                upd = true;
-                save = atk;
-                mu = atk ? attack_mult : (state == 3) ? decay_mult : hang_decay_mult;
-            }
-            state = ns;
-            if (save) save_volts = volts;
-            if (upd) volts += rv * mu;
-            if (volts < A.min_volts) volts = A.min_volts;
+            // bools combine with & and | (no short-circuit), so the compiler emits selects, not
+            // exec-masked branches
+            const bool s0 = state == 0, s1 = state == 1, s2 = state == 2, s34 = !(s0 | s1 | s2);
+            const bool fast = volts > A.pop_ratio * fast_bavg;                    // case 0
+            const bool hang = (A.hang_enable != 0) & (hang_bavg > A.hang_level);
+            const bool fd = volts > save_volts;                                   // case 1
+            const bool hc = hang_counter > 0;
+            const bool dt0 = decay_type == 0;
+            const bool hz = hang_counter == 0;                                    // case 2
+            // without attack
+            const int ns0 = fast ? 1 : hang ? 2 : 3;
+            const int ns1 = fd ? 1 : hc ? 2 : dt0 ? 3 : 4;
+            const int ns2 = hz ? 4 : 2;
+            const int nsn = s0 ? ns0 : s1 ? ns1 : s2 ? ns2 : state;
+            const bool updn = (s0 & (fast | !hang)) | (s1 & (fd | !hc)) | (s2 & hz) | s34;
+            const float dm = A.decay_mult, fdm = A.fast_decay_mult, hdm = A.hang_decay_mult;
+            const float mu0 = fast ? fdm : dm;
+            const float mu1 = fd ? fdm : dt0 ? dm : hdm;
+            const float mu3 = state == 3 ? dm : hdm;
+            const float mun = s0 ? mu0 : s1 ? mu1 : s2 ? hdm : mu3;
+            const bool s0_decay = s0 & !atk & !fast;                              // case 0, no attack, slow
+            hang_counter = (s0_decay & hang) ? A.hang_counter_init : hang_counter;
+            decay_type = s0_decay ? (hang ? 1 : 0) : decay_type;
+            state = atk ? 0 : nsn;
+            const bool save = atk & !s0 & !s1;
+            save_volts = save ? volts : save_volts;
+            const float mu = atk ? A.attack_mult : mun;
+            const bool upd = atk | updn;
+            const float nv = volts + rv * mu;
+            volts = upd ? nv : volts;
+            volts = (volts < A.min_volts) ? A.min_volts : volts;
             float vo = log10f_fast(A.inv_max_input * volts);
-            if (vo > 0.0f) vo = 0.0f;
+            vo = (vo > 0.0f) ? 0.0f : vo;
             const float mult = (A.out_target - A.slope_constant * vo) / volts;
 #pragma unroll
             for (int ch = 0; ch < NCH; ++ch) x[ch] = out_sample[ch] * mult;
         }
-        if (agc_on && A.remove_dc)                      // mode 5 returns first (audio_agc.c:354-365)
+        if (agc_on && dc_sel)
+        {
+            // the same as a select (no branch): bodies that must not split their basic block
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch)
+            {
+                const float w = (float)((double)x[ch] + (double)wold[ch] * 0.9999);
+                x[ch] = dc ? w - wold[ch] : x[ch];
+                wold[ch] = dc ? w : wold[ch];
+            }
+        }
+        else if (agc_on && dc)                          // mode 5 returns first (audio_agc.c:354-365)
         {
 #pragma unroll
             for (int ch = 0; ch < NCH; ++ch)
@@ -815,7 +821,7 @@ struct AgcStage
         return v[0];
     }
 
-    __device__ __forceinline__ void end()
+    __device__ __forceinline__ void end(const BackLane& l)
     {
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) leave_last[ch] = old[ch][NDC - 1];
@@ -890,6 +896,12 @@ struct AudioStage
     // one decimated sample in, L samples at 48 ksps out (out[j], j = 0..L-1)
     __device__ __forceinline__ void step(float x, float (&out)[L])
     {
+        interp(step_dec(x), out);
+    }
+
+    // the decimated-rate part: scale, biquad_1, CW decoder front end
+    __device__ __forceinline__ float step_dec(float x)
+    {
         x = x * scale;
 #pragma unroll
         for (int st = 0; st < 4; ++st)
@@ -905,7 +917,12 @@ struct AudioStage
             }
             ++cw_count;
         }
-        // polyphase interpolator: output j uses phase L-1-j (arm_fir_interpolate_f32.c:482-575)
+        return x;
+    }
+
+    // polyphase interpolator: output j uses phase L-1-j (arm_fir_interpolate_f32.c:482-575)
+    __device__ __forceinline__ void interp(float x, float (&out)[L])
+    {
         float win[PH];
 #pragma unroll
         for (int t = 0; t < PH - 1; ++t) win[t] = ip[t];
@@ -952,12 +969,23 @@ struct AudioStage
 
     __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l)
     {
+        store_dec(a, l);
+        store_interp(a, l);
+    }
+
+    __device__ __forceinline__ void store_interp(const BackArgs& a, const BackLane& l)
+    {
+        if (!l.live) return;
+#pragma unroll
+        for (int i = 0; i < PH - 1; ++i) a.s.interp[i * l.C + l.c] = ip[i];
+    }
+
+    __device__ __forceinline__ void store_dec(const BackArgs& a, const BackLane& l)
+    {
         if (!l.live) return;
         const int C = l.C, c = l.c;
 #pragma unroll
         for (int i = 0; i < 16; ++i) a.s.bq1[i * C + c] = bq1[i];
-#pragma unroll
-        for (int i = 0; i < PH - 1; ++i) a.s.interp[i * C + c] = ip[i];
         if (cw)
         {
             a.s.cw[c] = g1; a.s.cw[C + c] = g2; a.s.cw[2 * C + c] = cw_old;
@@ -1053,13 +1081,14 @@ struct DemodStage
 
     __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
     {
-        const float* si = a.adec + (size_t)l.cl * a.Nd + call * NDC;
-        const float* sq = a.adec_q + (size_t)l.cl * a.Nd + call * NDC;
+        const float* si = a.adec + call * NDC;
+        const float* sq = a.adec_q + call * NDC;
+        const unsigned off = (unsigned)l.cl * (unsigned)a.Nd;
 #pragma unroll
         for (int m = 0; m < NDC; m += 4)
         {
-            const float4 v = *(const float4*)(si + m);
-            const float4 w = *(const float4*)(sq + m);
+            const float4 v = *(const float4*)(si + m + off);
+            const float4 w = *(const float4*)(sq + m + off);
             inext[m] = v.x; inext[m + 1] = v.y; inext[m + 2] = v.z; inext[m + 3] = v.w;
             qnext[m] = w.x; qnext[m + 1] = w.y; qnext[m + 2] = w.z; qnext[m + 3] = w.w;
         }
@@ -1248,7 +1277,7 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
         s.begin(a, l, call);
 #pragma unroll
         for (int m = 0; m < NDC; ++m) ao[m * BACK_CH] = s.step(m, pi[m * BACK_CH], l, A);
-        s.end();
+        s.end(l);
     BACK_ROLE_END
     s.store(a, l);
 }
@@ -1347,8 +1376,54 @@ __global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
 // all state in registers -- no LDS, no barriers, no pipeline fill / drain.  With enough
 // channels to keep every SIMD busy this beats the wave pipeline, whose only purpose is to
 // shorten the per-call critical path when channels are few.
-template <int PRE, int AA, int L, int PH, int W, int DM>
-__global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
+// pitch of a channel's row in the fused back end's LDS output staging (odd: conflict-free)
+constexpr int FUSED_YPITCH = BLK + 1;
+
+// a call's 32 output frames of the wave's 64 channels from LDS to HBM: lane (g, j) = (lane / 8,
+// lane % 8) takes frames 4j..4j+3 of channels 8k + g, so one store instruction covers 8 rows
+__device__ __forceinline__ void fused_store_call(const BackArgs& a, const BackLane& l, int call, const float* ys)
+{
+    wave_sync();                                         // the wave's rows are complete
+    const int g = l.lane >> 3, j = l.lane & 7;
+    const bool beep = a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK;
+    const int c0 = blockIdx.x * BACK_CH;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+    {
+        const int cc = 8 * k + g;
+        const float* r = ys + cc * FUSED_YPITCH + 4 * j;
+        float y[4] = { r[0], r[1], r[2], r[3] };
+        if (beep)
+        {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+            {
+                const int fr = call * BLK + 4 * j + i;
+                if (fr >= a.beep_n0 && fr < a.beep_n1) y[i] += beep_tone(a, fr);
+            }
+        }
+        const int c = c0 + cc;
+        if (c >= a.C) continue;
+        // uniform base of rows c0 + 8k.. (SGPRs) + the lane's 32-bit offset
+        const size_t rb = (size_t)(c0 + 8 * k) * a.N + call * BLK;
+        const unsigned off = (unsigned)g * (unsigned)a.N + 4 * j;
+        if (a.audio) *(float4*)(a.audio + rb + off) = make_float4(y[0], y[1], y[2], y[3]);
+        if (a.dst)
+        {
+            int2* dd = a.dst + rb + off;
+            const int d0 = to_dma(y[0]), d1 = to_dma(y[1]), d2 = to_dma(y[2]), d3 = to_dma(y[3]);
+            *(int4*)(dd) = make_int4(d0, d0, d1, d1);
+            *(int4*)(dd + 2) = make_int4(d2, d2, d3, d3);
+        }
+    }
+    wave_sync();                                         // rows read before the next call writes
+}
+
+// AGC_ON (mode != 5) and CW (decoder front end) are launch constants, made compile-time so the
+// per-sample code carries no uniform branches; the AGC's DC removal is on for AM / SAM (compile-
+// time for the demodulating bodies, a select behind rx_notch)
+template <int PRE, int AA, int L, int PH, int W, int DM, bool AGC_ON, bool CW>
+__device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys)
 {
     const BackLane l(a);
     constexpr int NDC = BLK / L;
@@ -1370,6 +1445,17 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
     au.load(a, l);
     aa.load(l, P->aa_k, P->aa_v, a.s.aa);
     ou.load(a, l);
+    // coefficients of the per-sample recursions into VGPRs (full-rate VOP2, no SGPR spills:
+    // v_readlane refills 699 -> 104 per kernel, 0.220 -> 0.211 ms at 1M x 64)
+    if (PRE > 0) { to_vgpr(pre.k); to_vgpr(pre.v); }
+    if (AA > 0) { to_vgpr(aa.k); to_vgpr(aa.v); }
+    to_vgpr(ou.b2);
+    ou.lo = to_vgpr(ou.lo);
+    to_vgpr(au.b1);
+    ag.agc_on = AGC_ON;
+    if (DM != DM_NONE) ag.dc = true;
+    else ag.dc_sel = true;
+    au.cw = CW;
     for (int call = 0; call < l.calls; ++call)
     {
         float xin[NDC];
@@ -1382,34 +1468,21 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
         else
             in.begin(a, l, call, xin);
         ag.begin(a, l, call);
-        // the call's 32 output frames are stored in one burst at its end: interleaved with the
-        // chain's arithmetic, the partial-line stores of 64 rows get evicted from L2 before
-        // their lines fill, doubling the HBM write bytes
-        float y[BLK];
+        // The call's 32 output frames go to LDS (row per channel, 33-float pitch: conflict-free)
+        // and leave in one burst at its end, each store instruction writing 8 whole 128-byte
+        // rows: holding them in registers costs 32 VGPRs of occupancy, and storing them as they
+        // come leaves partial lines that L2 evicts before they fill (twice the HBM write bytes).
+        float* yl = ys + l.lane * FUSED_YPITCH;
 #pragma unroll
         for (int m = 0; m < NDC; ++m)
         {
             float u[L];
             au.step(ag.step(m, pre.step(xin[m]), l, A), u);
 #pragma unroll
-            for (int j = 0; j < L; ++j) y[m * L + j] = ou.step(aa.step(u[j]));
+            for (int j = 0; j < L; ++j) yl[m * L + j] = ou.step(aa.step(u[j]));
         }
-        if (a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK)
-        {
-#pragma unroll
-            for (int n = 0; n < BLK; ++n)
-            {
-                const int fr = call * BLK + n;
-                if (fr >= a.beep_n0 && fr < a.beep_n1) y[n] += beep_tone(a, fr);
-            }
-        }
-#pragma unroll
-        for (int n0 = 0; n0 < BLK; n0 += 4)
-        {
-            const float y4[4] = { y[n0], y[n0 + 1], y[n0 + 2], y[n0 + 3] };
-            back_store4(a, l, call, n0, y4);
-        }
-        ag.end();
+        fused_store_call(a, l, call, ys);
+        ag.end(l);
         au.end(a, l, call);
     }
     if (DM) dm.store(a, l);
@@ -1418,6 +1491,25 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_fused(BackArgs a)
     au.store(a, l);
     aa.store(l, a.s.aa);
     ou.store(a, l);
+}
+
+// runs the body with the launch's AGC / CW flags as template arguments
+template <int PRE, int AA, int L, int PH, int W, int DM, bool CW>
+__device__ __forceinline__ void back_fused_agc(const BackArgs& a, float* ys)
+{
+    if (a.plan->agc.mode == 5) back_fused_body<PRE, AA, L, PH, W, DM, false, CW>(a, ys);
+    else back_fused_body<PRE, AA, L, PH, W, DM, true, CW>(a, ys);
+}
+
+template <int PRE, int AA, int L, int PH, int W, int DM>
+__global__ void __launch_bounds__(BACK_CH) __attribute__((amdgpu_waves_per_eu(DM == DM_SAM_SB ? 1 : UHSDR_FUSED_WAVES))) rx_back_fused(BackArgs a)
+{
+    __shared__ float ys[BACK_CH * FUSED_YPITCH];
+    if constexpr (L == 4)
+    {
+        if (a.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM, true>(a, ys); return; }
+    }
+    back_fused_agc<PRE, AA, L, PH, W, DM, false>(a, ys);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1523,7 +1615,7 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_stereo(BackArgs a)
                 }
             }
         }
-        ag.end();
+        ag.end(l);
         au0.end(a, l, call);
     }
     if (DM) dm.store(a, l);
@@ -1888,6 +1980,19 @@ struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; };
 // (UHSDR_PRECISION_FMA)
 #define FRONT_V(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false>, R, rx_front<t1, t2, m, df, R, true>, 0 }
 #define FRONT_ST(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false, true>, R, rx_front<t1, t2, m, df, R, true, true>, 1 }
+struct NotchVariant { int L, dm; back_fn fn; };
+#ifdef UHSDR_ISA_P48
+// tools/isa_stats.sh: only the P48 SSB instances, so one kernel's ISA compiles in seconds
+static const FrontVariant kFront[] = { FRONT_V(89, 43, 4, false, 8) };
+#define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm> }
+static const BackVariant kBack[] = { BACK_V(10, 6, 4, 1, 49, DM_NONE) };
+static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, nullptr, nullptr };
+static const BackVariant kBackStereo[] = { { 10, 6, 4, 1, 49, DM_NONE, nullptr, nullptr } };
+static const NotchVariant kNotch[] = { { 4, DM_NONE, nullptr } };
+#undef BACK_V
+#undef FRONT_V
+#undef FRONT_ST
+#else
 static const FrontVariant kFront[] = {
     FRONT_V(89, 43, 4, false, 16), FRONT_V(89, 43, 4, false, 8),     // wide SSB/CW  (P48-54)
     FRONT_V(89, 4, 2, false, 16), FRONT_V(89, 4, 2, false, 8),       // 24 ksps SSB   (P55-65)
@@ -1933,7 +2038,6 @@ static const BackVariant kBackStereo[] = {
 #undef BACK_ST
 
 // LMS auto notch (+ the AM / SAM demodulator ahead of it): decimation L, demodulator DM
-struct NotchVariant { int L, dm; back_fn fn; };
 static const NotchVariant kNotch[] = {
     { 4, DM_NONE, rx_notch<4, DM_NONE> }, { 2, DM_NONE, rx_notch<2, DM_NONE> },
     { 4, DM_AM, rx_notch<4, DM_AM> }, { 2, DM_AM, rx_notch<2, DM_AM> },
@@ -1941,6 +2045,8 @@ static const NotchVariant kNotch[] = {
     { 4, DM_SAM_SB, rx_notch<4, DM_SAM_SB> }, { 2, DM_SAM_SB, rx_notch<2, DM_SAM_SB> },
     { 4, DM_SAM_ST, rx_notch<4, DM_SAM_ST> }, { 2, DM_SAM_ST, rx_notch<2, DM_SAM_ST> },
 };
+
+#endif
 
 static int plan_dm(const uhsdr_rx_plan& p)
 {
@@ -2008,6 +2114,7 @@ static const BackVariant* find_back(const uhsdr_rx_plan& p)
 
 constexpr int TAPS2_MAX = (UHSDR_MAX_FIR_TAPS + 7) & ~7;   // taps per pair table
 constexpr int BACK_FUSED_MIN_CHANNELS = 131072;   // measured crossover (64-frame calls)
+enum { BACK_PIPE = 0, BACK_FUSED = 1 };
 
 struct uhsdr_rx_s
 {
@@ -2018,7 +2125,7 @@ struct uhsdr_rx_s
     const NotchVariant* nv;  // LMS auto notch kernel (null: notch off)
     int C, N, Nd, Nf;        // Nf: frames per front launch (N split into N / Nf launches)
     int lw;                  // front LDS window pitch (floats)
-    int back_fused;          // rx_back_fused (large batches) instead of the wave pipeline
+    int back_mode;           // BACK_PIPE (rx_back) or BACK_FUSED (rx_back_fused)
     int precision;           // UHSDR_PRECISION_EXACT / _FMA (front FIR MACs)
     int T1, T2;
     hipStream_t stream;
@@ -2221,8 +2328,14 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         // Back end: the wave pipeline shortens the per-call critical path, which is what bounds
         // small batches; from BACK_FUSED_MIN_CHANNELS on (>= 4 waves per SIMD of 64 channels)
         // the fused kernel wins.  UHSDR_BACK_FUSED=0/1 forces either (tests, benchmarking).
-        const char* env = getenv("UHSDR_BACK_FUSED");
-        h->back_fused = h->bv->fused && (env ? atoi(env) != 0 : C >= BACK_FUSED_MIN_CHANNELS);
+        // Measured and dropped: the fused kernel split in two at the interpolator (decimated-rate
+        // stages / 48 ksps stages, half the registers each): 0.225 vs 0.211 ms at 1M x 64, and
+        // slower on C3 / C5 too -- more waves did not raise the VALU issue rate.
+        const char* envf = getenv("UHSDR_BACK_FUSED");
+        int mode = C >= BACK_FUSED_MIN_CHANNELS ? BACK_FUSED : BACK_PIPE;
+        if (envf) mode = atoi(envf) ? BACK_FUSED : BACK_PIPE;
+        if (mode == BACK_FUSED && !h->bv->fused) mode = BACK_PIPE;
+        h->back_mode = mode;
     }
 
     size_t fl = 0;
@@ -2450,7 +2563,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         hipLaunchKernelGGL(h->nv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
         HIPCHK(hipGetLastError());
     }
-    if (h->back_fused || h->plan.stereo)
+    if (h->back_mode == BACK_FUSED || h->plan.stereo)
         hipLaunchKernelGGL(h->bv->fused, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
     else
         hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH),

@@ -274,6 +274,33 @@ uhsdr_status uhsdr_rx_set_precision(uhsdr_rx_handle h, int32_t precision);
 int32_t      uhsdr_rx_get_precision(uhsdr_rx_handle h);   /* -1 for a null handle */
 uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h);
 
+/* ---- status side outputs: the RX chain's signals to the control plane ----
+ * ADC clip indicators (audio_driver.c:2660-2676): per channel, the sticky flags ads.adc_clip /
+ * ads.adc_half_clip / ads.adc_quarter_clip, set when |I| >> 16 of any frame exceeds
+ * ADC_CLIP_WARN_THRESHOLD (4096, audio_driver.h:81) / its half / its quarter -- the S-meter's
+ * red indicator and the auto RF-gain trigger / release.  The firmware's UI reads and clears
+ * them; here the kernels OR the bits of every frame they process into clip[c] (device memory,
+ * [C] uint32, the caller zeroes it and clears it after reading).  NULL (default) = not computed.
+ * The magnitude is taken as unsigned, so a full-scale negative sample (INT32_MIN, where the
+ * reference's abs() is undefined) counts as a clip. */
+#define UHSDR_ADC_CLIP          1
+#define UHSDR_ADC_HALF_CLIP     2
+#define UHSDR_ADC_QUARTER_CLIP  4
+uhsdr_status uhsdr_rx_set_clip_output(uhsdr_rx_handle h, uint32_t* clip);
+/* Twin-peaks I/Q fault detector (AudioDriver_RxHandleTwinpeaks, audio_driver.c:2173-2248), run
+ * per 32-frame call with automatic I/Q correction: 1000 calls of settling, then 50 calls of the
+ * Moseley & Slump phase estimate asin(teta1 / teta3), smoothed; more than 22.5 degrees requests a
+ * codec restart, the fourth consecutive one declares the fault uncorrectable.  Per channel state
+ * ts.twinpeaks_tested (hardware/uhsdr_board.h:647-651), WAIT after create / reset
+ * (src/uhsdr_main.c:339). */
+enum { UHSDR_TWINPEAKS_SAMPLING = 0, UHSDR_TWINPEAKS_DONE = 1, UHSDR_TWINPEAKS_WAIT = 2,
+       UHSDR_TWINPEAKS_UNCORRECTABLE = 3, UHSDR_TWINPEAKS_CODEC_RESTART = 4 };
+/* copies the C states (int32) to `state` (device memory), ordered on the handle's stream */
+uhsdr_status uhsdr_rx_twinpeaks_state(uhsdr_rx_handle h, int32_t* state);
+/* the UI's acknowledgement after it restarted the codec (ui_driver.c:7422-7426): every channel in
+ * CODEC_RESTART goes back to WAIT; ordered on the handle's stream */
+uhsdr_status uhsdr_rx_twinpeaks_rearm(uhsdr_rx_handle h);
+
 /* ---- device memory for plain-C hosts (no HIP headers needed) ---- */
 void*        uhsdr_device_alloc(uint64_t bytes);             /* NULL on failure */
 void         uhsdr_device_free(void* p);

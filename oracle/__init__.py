@@ -32,6 +32,7 @@ def load():
         lib.uo_rx_process_batch2.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         lib.uo_rx_key_beep.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        lib.uo_rx_status.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         lib.uo_rx_bench.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                                     C.c_void_p, C.c_int, C.c_int, C.c_double, C.POINTER(C.c_double)]
         lib.uo_rx_bench.restype = C.c_longlong
@@ -66,6 +67,15 @@ class OracleRx:
     def key_beep(self, calls: int) -> None:
         """AudioManagement_KeyBeep on every channel: the next `calls` calls get the beep."""
         self.lib.uo_rx_key_beep(self.states, self.channels, calls)
+
+    def status(self, rearm: bool = False):
+        """(clip flags [C], twinpeaks state [C]): reads and clears the clip flags; rearm = the UI's
+        codec restart acknowledgement (CODEC_RESTART -> WAIT)."""
+        clip = np.empty(self.channels, np.int32)
+        tp = np.empty(self.channels, np.int32)
+        self.lib.uo_rx_status(self.states, self.channels, clip.ctypes.data_as(C.c_void_p),
+                              tp.ctypes.data_as(C.c_void_p), int(rearm))
+        return clip, tp
 
     def process(self, iq: np.ndarray, threads: int = 1):
         a1, _, dst = self.process2(iq, threads)

@@ -25,6 +25,9 @@
  *   out_a0=<file>  f32 adb.a_buffer[0] after each call (the second channel in stereo)
  *   out_clip=<file> uint8 per call: ads.adc_clip | adc_half_clip << 1 | adc_quarter_clip << 2,
  *                  read and cleared after every call (the UI's role)
+ *   out_tp=<file>  uint8 per call: ts.twinpeaks_tested after the call (AudioDriver_RxHandleTwinpeaks)
+ *   uiperiod=P     the UI loop's codec restart handling (ui_driver.c:7422-7426: CODEC_RESTART ->
+ *                  WAIT) runs after every P-th call (default 1)
  *   tx=1           transmit: in= holds codec audio frames {l,r}, out_dst= gets the IQ frames
  *                  TxProcessor_Run writes (tx_processor.c:891-1078), out_a= a_buffer[0]
  *   micmult= boost= comp= txfilter= txbass= txtreble= txpwr= txgi= txgq= txphase=
@@ -323,6 +326,10 @@ int main(int argc, char** argv)
     }
     const char* out_a0 = arg(argc, argv, "out_a0", NULL);
     const char* out_clip = arg(argc, argv, "out_clip", NULL);
+    const char* out_tp = arg(argc, argv, "out_tp", NULL);
+    const long uiperiod = iarg(argc, argv, "uiperiod", 1);
+    uint8_t* tps = out_tp ? calloc(n / block, 1) : NULL;
+    ts.twinpeaks_tested = TWINPEAKS_WAIT;                  /* src/uhsdr_main.c:339 */
     float* a0s = out_a0 ? calloc(n, sizeof(float)) : NULL;
     uint8_t* clips = out_clip ? calloc(n / block, 1) : NULL;
     const char* out_cw = arg(argc, argv, "out_cw", NULL);        /* Goertzel energy per CW block */
@@ -373,6 +380,9 @@ int main(int argc, char** argv)
             clips[call] = (uint8_t)((ads.adc_clip ? 1 : 0) | (ads.adc_half_clip ? 2 : 0) | (ads.adc_quarter_clip ? 4 : 0));
             ads.adc_clip = ads.adc_half_clip = ads.adc_quarter_clip = 0;
         }
+        if (tps) tps[call] = ts.twinpeaks_tested;
+        if ((call + 1) % uiperiod == 0 && ts.twinpeaks_tested == TWINPEAKS_CODEC_RESTART)
+            ts.twinpeaks_tested = TWINPEAKS_WAIT;          /* ui_driver.c:7422-7426, after Codec_RestartI2S */
         if (cw_signal) cw_signal[off / block] = ads.CW_signal;
         if (spec && (off + block) % (ring / 2 * zd) == 0)  /* the ring holds ring/2 new samples */
             ref_spec_snapshot(stream + 2 * ((off + block) / zd - ring / 2));
@@ -403,6 +413,7 @@ int main(int argc, char** argv)
     if (out_dst) { f = fopen(out_dst, "wb"); fwrite(dst, sizeof(AudioSample_t), n, f); fclose(f); }
     if (a0s) { f = fopen(out_a0, "wb"); fwrite(a0s, sizeof(float), n, f); fclose(f); free(a0s); }
     if (clips) { f = fopen(out_clip, "wb"); fwrite(clips, 1, n / block, f); fclose(f); free(clips); }
+    if (tps) { f = fopen(out_tp, "wb"); fwrite(tps, 1, n / block, f); fclose(f); free(tps); }
     free(iq); free(dst); free(a1);
     return 0;
 }

@@ -30,6 +30,58 @@ void uo_rx_state_init(const uhsdr_rx_plan* p, uo_rx_state* s)
     s->in_index = p->agc.in_index0;
     s->fm_squelched = 1;       /* AudioDriver_FM_Rx_Init: "we start squelched" (audio_driver.c:475) */
     s->cw_old = 0.001f;        /* static float32_t old_siglevel = 0.001 (cw_decoder.c:189) */
+    s->tp_state = UHSDR_TWINPEAKS_WAIT;   /* ts.twinpeaks_tested at boot, src/uhsdr_main.c:339 */
+}
+
+void uo_rx_status(uo_rx_state* states, int C, int32_t* clip, int32_t* twinpeaks, int rearm)
+{
+    for (int c = 0; c < C; c++)
+    {
+        uo_rx_state* s = &states[c];
+        if (clip) clip[c] = s->clip;
+        s->clip = 0;
+        if (twinpeaks) twinpeaks[c] = s->tp_state;
+        if (rearm && s->tp_state == UHSDR_TWINPEAKS_CODEC_RESTART) s->tp_state = UHSDR_TWINPEAKS_WAIT;
+    }
+}
+
+/* AudioDriver_RxHandleTwinpeaks (audio_driver.c:2173-2248), once per call after the auto I/Q
+   statistics, on this call's low-passed teta1 / teta3 */
+static void twinpeaks(uo_rx_state* s, float teta1, float teta3)
+{
+    if (s->tp_state == UHSDR_TWINPEAKS_WAIT) s->tp_counter++;
+    if (s->tp_counter > 1000)
+    {
+        s->tp_state = UHSDR_TWINPEAKS_SAMPLING;
+        s->tp_counter = 0;
+        s->tp_phase = 0.0;
+        s->tp_runs = 0;
+    }
+    if (teta3 != 0.0 && s->tp_state == UHSDR_TWINPEAKS_SAMPLING)
+    {
+        const float cur = asinf(teta1 / teta3);
+        if (s->tp_runs == 0) s->tp_phase = cur;
+        else s->tp_phase = 0.05 * cur + 0.95 * s->tp_phase;
+        s->tp_runs++;
+        if (s->tp_runs == 50)
+        {
+            if (fabsf(s->tp_phase) > (M_PI / 8.0))
+            {
+                s->tp_state = UHSDR_TWINPEAKS_CODEC_RESTART;
+                s->tp_restarts++;
+                if (s->tp_restarts >= 4)
+                {
+                    s->tp_state = UHSDR_TWINPEAKS_UNCORRECTABLE;
+                    s->tp_restarts = 0;
+                }
+            }
+            else
+            {
+                s->tp_state = UHSDR_TWINPEAKS_DONE;
+                s->tp_restarts = 0;
+            }
+        }
+    }
 }
 
 /* CwDecode_RxProcessor (cw_decoder.c:383-397) and CW_Decode_exe steps 1-5 (:182-316) with the
@@ -604,6 +656,14 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
     const int n = BLK;
     for (int i = 0; i < n; i++)
     {
+        /* ADC clip indicators on the I sample, |l| >> IQ_BIT_SHIFT against ADC_CLIP_WARN_THRESHOLD
+           = 4096 and its quarter / half (audio_driver.c:2660-2676, audio_driver.h:81); the
+           magnitude is taken unsigned, so a full-scale negative sample counts as a clip */
+        const uint32_t v = (uint32_t)iq[2 * i];
+        const uint32_t level = ((v & 0x80000000u) ? 0u - v : v) >> 16;
+        if (level > 4096 / 4) s->clip |= UHSDR_ADC_QUARTER_CLIP;
+        if (level > 4096 / 2) s->clip |= UHSDR_ADC_HALF_CLIP;
+        if (level > 4096) s->clip |= UHSDR_ADC_CLIP;
         ib[i] = iq[2 * i];
         qb[i] = iq[2 * i + 1];
     }
@@ -637,6 +697,7 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
         float help = (t2 * t2);
         if (help > 0.0) help = (t3 * t3 - t1 * t1) / help;
         const float M_c2 = (help > 0.0) ? sqrtf(help) : 1.0;
+        twinpeaks(s, t1, t3);
         s->teta1_old = t1;
         s->teta2_old = t2;
         s->teta3_old = t3;

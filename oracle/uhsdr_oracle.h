@@ -73,6 +73,12 @@ typedef struct uo_rx_state
     /* key beep: ts.beep_timing as calls left, ads.beep.acc */
     int32_t beep_left;
     uint32_t beep_acc;
+    /* side outputs: ads.adc_clip / adc_half_clip / adc_quarter_clip as UHSDR_ADC_* bits, sticky
+       until read (audio_driver.c:2660-2676); ts.twinpeaks_tested and AudioDriver_RxHandleTwinpeaks'
+       statics twinpeaks_counter, codec_restarts, phase_IQ, phase_IQ_runs (:2173-2248) */
+    int32_t clip;
+    int32_t tp_state, tp_counter, tp_restarts, tp_runs;
+    float tp_phase;
 } uo_rx_state;
 
 size_t uo_rx_state_size(void);
@@ -85,6 +91,9 @@ int uo_rx_process2(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, in
                    int32_t* dst);
 /* AudioManagement_KeyBeep on C channel states: the next `calls` calls get the beep tone */
 void uo_rx_key_beep(uo_rx_state* states, int C, int calls);
+/* the UI's side of the status outputs: read and clear the clip flags, read ts.twinpeaks_tested,
+   and (rearm != 0) the codec restart acknowledgement CODEC_RESTART -> WAIT (ui_driver.c:7422-7426) */
+void uo_rx_status(uo_rx_state* states, int C, int32_t* clip, int32_t* twinpeaks, int rearm);
 /* C channels, channel-major buffers, `threads` POSIX threads (0 = 1) */
 long long uo_rx_bench(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int pool, int n,
                       float* a1, int32_t* dst, int threads, int pin, double budget_s, double* elapsed);

@@ -15,7 +15,9 @@ freq_shift.c / CMSIS-DSP compiled for x86 by ``oracle/ref/Makefile`` -- once per
 
 plus tests/golden/filter_paths.json (FilterPathInfo[], audio_filter.c:147-922, as raw
 float bits), the TX / spectrum / CW fixtures (tx_*, spec_*, cw_*.npz) and
-tests/golden/cmsis_vectors.npz (CMSIS-DSP f32 call sequences, dump=cmsis, oracle/ref/ref_cmsis.c).  Only runs where /root/reference exists (build container); the fixtures
+tests/golden/cmsis_vectors.npz (CMSIS-DSP f32 call sequences, dump=cmsis, oracle/ref/ref_cmsis.c),
+and the status fixtures (st_*.npz: per-call ADC clip flags and twin-peaks state over >130k
+frames; the input is regenerated from uhsdr_amd.synth and checked by its crc32).  Only runs where /root/reference exists (build container); the fixtures
 are committed and the GPU box never needs the reference.
 
     python tests/golden/make_golden.py [--only NAME]
@@ -203,6 +205,42 @@ CW_CONFIGS = {
 CW_FRAMES = 8192
 
 
+# Status side outputs (ADC clip flags, twin-peaks detector): name -> (uhsdr_ref args, frames).
+# Input synth.status_iq (regenerated by the tests; its crc32 is stored), 5 channels with I/Q phase
+# errors 0 / 12 / 30 / 60 / 89 degrees, auto I/Q on; the UI acknowledges codec restarts every
+# `uiperiod` calls.  Long enough for four restart cycles (1001 + 50 calls each) -> UNCORRECTABLE.
+STATUS_CONFIGS = {
+    "p48_usb_tp": ({"mode": 0, "path": 48, "iq_auto": 1, "uiperiod": 8}, 4400 * 32),
+    "p35_lsb_tp": ({"mode": 1, "path": 35, "iq_auto": 1, "uiperiod": 4}, 1152 * 32),
+    "p70_am_tp": ({"mode": 3, "path": 70, "iq_auto": 1, "uiperiod": 16}, 2176 * 32),
+}
+STATUS_NCH = 5
+
+
+def make_status(name: str):
+    import zlib
+    args, nfr = STATUS_CONFIGS[name]
+    iq = synth.status_iq(np.arange(STATUS_NCH), 0, nfr)
+    calls = nfr // 32
+    tp = np.empty((STATUS_NCH, calls), np.uint8)
+    clip = np.empty((STATUS_NCH, calls), np.uint8)
+    a1 = np.empty((STATUS_NCH, nfr), np.float32)
+    for c in range(STATUS_NCH):
+        with tempfile.TemporaryDirectory() as td:
+            fin, fa, ft, fc = (os.path.join(td, x) for x in ("in.bin", "a.bin", "t.bin", "c.bin"))
+            iq[c].astype(np.int32).tofile(fin)
+            cmd = [REF, f"in={fin}", f"n={nfr}", f"out_a={fa}", f"out_tp={ft}", f"out_clip={fc}"]
+            subprocess.run(cmd + [f"{k}={v}" for k, v in args.items()], check=True)
+            a1[c] = np.fromfile(fa, dtype=np.float32)
+            tp[c] = np.fromfile(ft, dtype=np.uint8)
+            clip[c] = np.fromfile(fc, dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, f"st_{name}.npz"), tp=tp, clip=clip, a1_head=a1[:, :2048],
+                        a1_tail=a1[:, -2048:], frames=nfr, iq_crc32=zlib.crc32(np.ascontiguousarray(iq).tobytes()),
+                        args=json.dumps(args))
+    final = [int(x) for x in tp[:, -1]]
+    print(f"st_{name:12s} calls={calls} final twinpeaks={final} clip calls={[(clip[c] != 0).sum() for c in range(STATUS_NCH)]}")
+
+
 def make_cw(name: str):
     args, sig = CW_CONFIGS[name]
     sig = dict(sig)
@@ -343,12 +381,19 @@ def main():
     if a.only == "cmsis":
         make_cmsis()
         return
+    if a.only in STATUS_CONFIGS:
+        make_status(a.only)
+        return
     make_cmsis()
     paths = subprocess.run([REF, "dump=paths"], check=True, capture_output=True, text=True).stdout
     with open(os.path.join(HERE, "filter_paths.json"), "w") as f:
         json.dump(json.loads(paths), f, separators=(",", ":"))
     tx_tables()
     spectrum_tables()
+    for name in STATUS_CONFIGS:
+        if a.only and name != a.only:
+            continue
+        make_status(name)
     for name in CW_CONFIGS:
         if a.only and name != a.only:
             continue

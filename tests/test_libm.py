@@ -26,3 +26,10 @@ def test_atan2f_matches_glibc(tmp_path):
     r = subprocess.run([_build(tmp_path), "atan2", "2000000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout
     assert " 0 of " in r.stdout
+
+
+def test_asinf_matches_glibc(tmp_path):
+    """The twin-peaks detector's asinf (audio_driver.c:2211); exhaustive run in libm_pin.txt."""
+    r = subprocess.run([_build(tmp_path), "asin", "127"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout
+    assert " 0 of " in r.stdout

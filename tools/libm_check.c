@@ -1,6 +1,7 @@
 /* Pins uhsdr_amd/csrc/uhsdr_libm.h against the host's libm (glibc).
  *   libm_check sincos <stride>   every stride-th float in [0, 2*pi] and (-2*pi, 0)
  *   libm_check atan2 <count>     random + structured operand pairs
+ *   libm_check asin <stride>     every stride-th float in [-1, 1] (and NaN operands past it)
  * Prints mismatches (first 10) and a summary line; exit status 1 on any mismatch. */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -34,6 +35,23 @@ int main(int argc, char** argv)
                 }
             }
         printf("sincosf: %ld of %ld arguments differ\n", bad, n);
+    }
+    else if (!strcmp(argv[1], "asin"))
+    {
+        const long stride = atol(argv[2]);
+        const uint32_t hi = ul_asuint(1.0f) + 16;
+        for (int sgn = 0; sgn < 2; ++sgn)
+            for (uint64_t u = 0; u <= hi; u += (u + stride > hi && u < hi) ? 1 : stride)
+            {
+                const float y = ul_asfloat((uint32_t)u | (sgn ? 0x80000000u : 0));
+                const float r0 = asinf(y), r1 = ul_asinf(y);
+                ++n;
+                if (ul_asuint(r0) != ul_asuint(r1) && !(isnan(r0) && isnan(r1)))
+                {
+                    if (bad++ < 10) printf("asinf(%a): glibc %a, ours %a\n", y, r0, r1);
+                }
+            }
+        printf("asinf: %ld of %ld arguments differ\n", bad, n);
     }
     else
     {

@@ -3,11 +3,13 @@
 The product is ``uhsdr_amd/lib/libuhsdr_amd.so`` (C ABI: ``include/uhsdr.h``).  This
 package is the thin host-side mirror used by tests and the benchmark.
 """
-from ._abi import (RxConfig, RxPlan, build_plan, config_from_ref_args, default_config, load,  # noqa: F401
+from ._abi import (RxConfig, RxPlan, build_plan, plan_supported, config_from_ref_args, default_config, load,  # noqa: F401
                    DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI,
                    DEMOD_SSBSTEREO, DEMOD_IQ, SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB,
                    SAM_SIDEBAND_STEREO, DSP_NOTCH_ENABLE,
-                   PRECISION_EXACT, PRECISION_FMA,
+                   PRECISION_EXACT, PRECISION_FMA, ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP,
+                   TWINPEAKS_SAMPLING, TWINPEAKS_DONE, TWINPEAKS_WAIT, TWINPEAKS_UNCORRECTABLE,
+                   TWINPEAKS_CODEC_RESTART,
                    TxConfig, TxPlan, build_tx_plan, default_tx_config, tx_config_from_ref_args,
                    SpectrumConfig, SpectrumPlan, build_spectrum_plan, default_spectrum_config,
                    spectrum_config_from_ref_args)

@@ -28,6 +28,8 @@ DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI, DEMOD
 SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB, SAM_SIDEBAND_STEREO = range(4)
 DSP_NOTCH_ENABLE, DSP_MNOTCH_ENABLE, DSP_MPEAK_ENABLE = 0x04, 0x10, 0x20
 PRECISION_EXACT, PRECISION_FMA = 0, 1          # uhsdr_rx_set_precision
+ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP = 1, 2, 4   # uhsdr_rx_set_clip_output bits
+TWINPEAKS_SAMPLING, TWINPEAKS_DONE, TWINPEAKS_WAIT, TWINPEAKS_UNCORRECTABLE, TWINPEAKS_CODEC_RESTART = range(5)
 
 
 class RxConfig(C.Structure):
@@ -181,6 +183,9 @@ SIGNATURES = {
     "uhsdr_rx_cw_blocks_max": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_cw_blocks_last": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_key_beep": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_rx_set_clip_output": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "uhsdr_rx_twinpeaks_state": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "uhsdr_rx_twinpeaks_rearm": (C.c_int, [C.c_void_p]),
     "uhsdr_device_alloc": (C.c_void_p, [C.c_uint64]),
     "uhsdr_device_free": (None, [C.c_void_p]),
     "uhsdr_copy_to_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
@@ -272,6 +277,11 @@ def build_plan(cfg: RxConfig) -> RxPlan:
     return plan
 
 
+def plan_supported(plan: RxPlan) -> bool:
+    """uhsdr_rx_plan_supported: the device has a kernel instantiation for this plan's family."""
+    return bool(load().uhsdr_rx_plan_supported(C.byref(plan)))
+
+
 # uhsdr_ref key=value names (tests/golden) -> RxConfig fields
 REF_ARG_MAP = {
     "mode": "dmod_mode", "path": "filter_path", "iqmode": "iq_freq_mode", "iq_auto": "iq_auto_correction",
@@ -285,7 +295,7 @@ REF_ARG_MAP = {
     "beepfreq": "beep_frequency", "beeploud": "beep_loudness", "stereo": "stereo_enable",
 }
 # uhsdr_ref run-time controls that are calls, not configuration (tests drive them through the ABI)
-REF_RUNTIME_ARGS = {"beep"}
+REF_RUNTIME_ARGS = {"beep", "uiperiod"}
 
 
 def config_from_ref_args(args: dict) -> RxConfig:

@@ -213,4 +213,42 @@ UHSDR_LIBM_FN float ul_atan2f(float y, float x)
     }
 }
 
+/* ---- asinf (glibc sysdeps/ieee754/flt-32/e_asinf.c: fdlibm binary32 with a degree-4 minimax
+ *      polynomial; the twin-peaks I/Q phase detector, audio_driver.c:2211) ---- */
+UHSDR_LIBM_FN float ul_asinf(float x)
+{
+    const float one = 1.0f, pio2_hi = 1.57079637050628662109375f, pio2_lo = -4.37113900018624283e-8f,
+                pio4_hi = 0.785398185253143310546875f,
+                p0 = 1.666675248e-1f, p1 = 7.495297643e-2f, p2 = 4.547037598e-2f, p3 = 2.417951451e-2f,
+                p4 = 4.216630880e-2f;
+    const int32_t hx = (int32_t)ul_asuint(x);
+    const int32_t ix = hx & 0x7fffffff;
+    float t, w, p, q, c, r, s;
+    if (ix == 0x3f800000) return x * pio2_hi + x * pio2_lo;       /* asin(+-1) = +-pi/2 */
+    if (ix > 0x3f800000) return (x - x) / (x - x);                /* |x| > 1: NaN */
+    if (ix < 0x3f000000)                                          /* |x| < 0.5 */
+    {
+        if (ix < 0x32000000) return x;                            /* |x| < 2^-27 */
+        t = x * x;
+        w = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+        return x + x * w;
+    }
+    w = one - fabsf(x);                                           /* 1 > |x| >= 0.5 */
+    t = w * 0.5f;
+    p = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+    s = sqrtf(t);
+    if (ix >= 0x3F79999A)                                         /* |x| > 0.975 */
+        t = pio2_hi - (2.0f * (s + s * p) - pio2_lo);
+    else
+    {
+        w = ul_asfloat(ul_asuint(s) & 0xfffff000u);
+        c = (t - w * w) / (s + w);
+        r = p;
+        p = 2.0f * s * r - (pio2_lo - 2.0f * c);
+        q = pio4_hi - 2.0f * w;
+        t = pio4_hi - (p - q);
+    }
+    return hx > 0 ? t : -t;
+}
+
 #endif /* UHSDR_LIBM_H */

@@ -45,6 +45,8 @@ struct FrontArgs
     float* hist2_i;          // [C][HS2] stage-2 history (audio decimator, or Hilbert I)
     float* hist2_q;          // [C][HS2] (decimate-first paths: Hilbert Q)
     float* teta;             // [3][C] auto I/Q correction low-pass state
+    int* tp;                 // [5][C] twin-peaks detector: state, counter, restarts, runs, phase (f32 bits)
+    unsigned* clip;          // optional [C]: ADC clip flags OR-ed in (uhsdr_rx_set_clip_output)
     const float* osc_in;     // [2] oscillator {I, Q} at the start of this launch (shared by all channels)
     float* osc_out;          // [2] written by workgroup 0
     float* adec;             // decimated output of this launch; row stride ldd
@@ -114,6 +116,55 @@ __device__ __forceinline__ void freq_shift_block(float (&ib)[R], float (&qb)[R],
             ib[j] = (it * oq) + (qt * oi);
         }
     }
+}
+
+// AudioDriver_RxHandleTwinpeaks (audio_driver.c:2173-2248) for one channel and one call, on the
+// call's low-passed teta1 / teta3.  st: ts.twinpeaks_tested; cnt, rst, runs, ph: the function's
+// statics twinpeaks_counter, codec_restarts, phase_IQ_runs, phase_IQ.  The smoothing and the
+// threshold are double arithmetic as in the reference (0.05, 0.95 and M_PI/8.0 are doubles).
+__device__ __forceinline__ void twinpeaks_step(float t1, float t3, int& st, int& cnt, int& rst, int& runs, float& ph)
+{
+    if (st == UHSDR_TWINPEAKS_WAIT) ++cnt;
+    if (cnt > 1000)
+    {
+        st = UHSDR_TWINPEAKS_SAMPLING;
+        cnt = 0; ph = 0.0f; runs = 0;
+    }
+    if (t3 != 0.0f && st == UHSDR_TWINPEAKS_SAMPLING)
+    {
+        const float cur = ul_asinf(t1 / t3);
+        ph = runs == 0 ? cur : (float)(0.05 * (double)cur + 0.95 * (double)ph);
+        if (++runs == 50)
+        {
+            if ((double)fabsf(ph) > (M_PI / 8.0))
+            {
+                st = UHSDR_TWINPEAKS_CODEC_RESTART;
+                if (++rst >= 4) { st = UHSDR_TWINPEAKS_UNCORRECTABLE; rst = 0; }
+            }
+            else
+            {
+                st = UHSDR_TWINPEAKS_DONE;
+                rst = 0;
+            }
+        }
+    }
+}
+
+// ADC clip indicators of R frames (audio_driver.c:2660-2676): |I| >> IQ_BIT_SHIFT against
+// ADC_CLIP_WARN_THRESHOLD (4096) and its half / quarter, magnitude taken unsigned
+template <int R>
+__device__ __forceinline__ unsigned clip_flags(const int4 (&raw)[R / 2])
+{
+    unsigned lv = 0;
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+    {
+        const int v = (j & 1) ? raw[j / 2].z : raw[j / 2].x;
+        const unsigned m = (unsigned)(v < 0 ? -(long long)v : (long long)v) >> 16;
+        lv = lv > m ? lv : m;
+    }
+    return (lv > 4096u / 4 ? (unsigned)UHSDR_ADC_QUARTER_CLIP : 0u) | (lv > 4096u / 2 ? (unsigned)UHSDR_ADC_HALF_CLIP : 0u) |
+           (lv > 4096u ? (unsigned)UHSDR_ADC_CLIP : 0u);
 }
 
 // R consecutive frames n0.. of one channel: int32 -> f32 x 2^-16 (audio_driver.c:2660-2685),
@@ -225,6 +276,11 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
         front_load_row<T1>(a.hist1_i, cl, b, nb, hA);
         front_load_row<T1>(a.hist1_q, cl, b, nb, hB);
     }
+    if (a.clip)
+    {
+        const unsigned f = clip_flags<R>(raw);
+        if (f && live) atomicOr(a.clip + c, f);
+    }
     if (in.shift == 2 && lane == 0)
     {
         // FreqShift_Approx (freq_shift.c:57-101): the oscillator does not depend on the data,
@@ -278,6 +334,8 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
                 const int cc = grp * CPW + gg;
                 if (cc >= C) continue;
                 float o1 = a.teta[cc], o2 = a.teta[C + cc], o3 = a.teta[2 * C + cc];
+                int tst = a.tp[cc], tcnt = a.tp[C + cc], trst = a.tp[2 * C + cc], truns = a.tp[3 * C + cc];
+                float tph = __int_as_float(a.tp[4 * C + cc]);
                 for (int bb = 0; bb < nblk32; ++bb)
                 {
                     const int e = gg * nblk32 + bb;
@@ -289,11 +347,14 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
                     float help = (t2 * t2);
                     if (help > 0.0f) help = (t3 * t3 - t1 * t1) / help;
                     const float M_c2 = (help > 0.0f) ? sqrtf(help) : 1.0f;
+                    twinpeaks_step(t1, t3, tst, tcnt, trst, truns, tph);
                     m1[e] = M_c1;
                     m2[e] = M_c2;
                     o1 = t1; o2 = t2; o3 = t3;
                 }
                 a.teta[cc] = o1; a.teta[C + cc] = o2; a.teta[2 * C + cc] = o3;
+                a.tp[cc] = tst; a.tp[C + cc] = tcnt; a.tp[2 * C + cc] = trst; a.tp[3 * C + cc] = truns;
+                a.tp[4 * C + cc] = __float_as_int(tph);
             }
         }
         wave_sync();
@@ -2131,6 +2192,8 @@ struct uhsdr_rx_s
     hipStream_t stream;
     // front state
     float *hist1_i, *hist1_q, *hist2_i, *hist2_q, *teta, *osc, *adec, *adec_q;
+    int* tp;                 // [5][C] twin-peaks detector state
+    unsigned* clip;          // user output (uhsdr_rx_set_clip_output)
     float* d_taps2;          // FIR pair tables: [2][2 * TAPS2_MAX] (pass 1, pass 2)
     // back state
     BackState bs;
@@ -2267,6 +2330,8 @@ extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
     // oscillator starts at {I=0, Q=1} (freq_shift.c:48-49); both ping-pong copies
     const float osc0[4] = { 0.0f, 1.0f, 0.0f, 1.0f };
     HIPCHK(hipMemcpyAsync(h->osc, osc0, sizeof osc0, hipMemcpyHostToDevice, h->stream));
+    // ts.twinpeaks_tested = TWINPEAKS_WAIT at boot (src/uhsdr_main.c:339); the statics start at 0
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->tp, UHSDR_TWINPEAKS_WAIT, (size_t)h->C, h->stream));
     if (h->bs.cw)
     {
         // old_siglevel starts at 0.001 (function static, cw_decoder.c:189)
@@ -2343,7 +2408,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const size_t hs1 = (h->T1 - 1 + 3) & ~3, hs2 = (h->T2 - 1 + 3) & ~3;   // padded history rows
     const size_t o_h1i = take((size_t)C * hs1), o_h1q = take((size_t)C * hs1);
     const size_t o_h2i = take((size_t)C * hs2), o_h2q = take((size_t)C * hs2);
-    const size_t o_teta = take((size_t)3 * C), o_osc = take(4);
+    const size_t o_teta = take((size_t)3 * C), o_osc = take(4), o_tp = take((size_t)5 * C);
     const size_t o_pre = take((size_t)10 * C), o_aa = take((size_t)10 * C), o_bq1 = take((size_t)16 * C);
     const size_t o_bq2 = take((size_t)4 * C), o_ip = take((size_t)15 * C), o_ring = take(W > 0 ? (size_t)(W - 1) * C : 0);
     const size_t o_agc = take((size_t)(8 + AGC_Q) * C), o_agci = take((size_t)3 * C);
@@ -2369,7 +2434,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     }
     float* A = (float*)h->arena;
     h->hist1_i = A + o_h1i; h->hist1_q = A + o_h1q; h->hist2_i = A + o_h2i; h->hist2_q = A + o_h2q;
-    h->teta = A + o_teta; h->osc = A + o_osc;
+    h->teta = A + o_teta; h->osc = A + o_osc; h->tp = (int*)(A + o_tp);
     h->bs.pre = A + o_pre; h->bs.aa = A + o_aa; h->bs.bq1 = A + o_bq1; h->bs.bq2 = A + o_bq2;
     h->bs.interp = A + o_ip; h->bs.ring = A + o_ring; h->bs.agc = A + o_agc; h->bs.agci = (int*)(A + o_agci);
     h->bs.sam = am ? A + o_sam : nullptr;
@@ -2427,6 +2492,34 @@ extern "C" uhsdr_status uhsdr_rx_set_cw_outputs(uhsdr_rx_handle h, uint8_t* sign
     if (!h) return UHSDR_ARGUMENT_ERROR;
     h->cw_signal = signal;
     h->cw_energy = energy;
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_rx_set_clip_output(uhsdr_rx_handle h, uint32_t* clip)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    h->clip = clip;
+    return UHSDR_OK;
+}
+
+__global__ void twinpeaks_rearm(int* st, int C)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < C && st[c] == UHSDR_TWINPEAKS_CODEC_RESTART) st[c] = UHSDR_TWINPEAKS_WAIT;
+}
+
+extern "C" uhsdr_status uhsdr_rx_twinpeaks_state(uhsdr_rx_handle h, int32_t* state)
+{
+    if (!h || !state) return UHSDR_ARGUMENT_ERROR;
+    HIPCHK(hipMemcpyAsync(state, h->tp, sizeof(int32_t) * (size_t)h->C, hipMemcpyDeviceToDevice, h->stream));
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_rx_twinpeaks_rearm(uhsdr_rx_handle h)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    hipLaunchKernelGGL(twinpeaks_rearm, dim3((h->C + 255) / 256), dim3(256), 0, h->stream, h->tp, h->C);
+    HIPCHK(hipGetLastError());
     return UHSDR_OK;
 }
 
@@ -2495,6 +2588,8 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         fa.iq = (const int2*)iq + f0;
         fa.hist1_i = h->hist1_i; fa.hist1_q = h->hist1_q; fa.hist2_i = h->hist2_i; fa.hist2_q = h->hist2_q;
         fa.teta = h->teta;
+        fa.tp = h->tp;
+        fa.clip = h->clip;
         fa.osc_in = h->osc + 2 * (h->front_launches & 1);     // ping-pong: read one copy, write the other
         fa.osc_out = h->osc + 2 * ((h->front_launches + 1) & 1);
         fa.adec = adec + f0 / h->plan.decimation_rate;

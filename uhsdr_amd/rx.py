@@ -102,6 +102,26 @@ class RxChain:
     def cw_blocks_last(self) -> int:
         return self.lib.uhsdr_rx_cw_blocks_last(self.handle)
 
+    def set_clip_output(self, clip=None) -> None:
+        """ADC clip flags (ads.adc_clip / _half_clip / _quarter_clip as ADC_* bits): the kernels OR
+        the bits of every frame into clip, uint32 [C] on the device; the caller reads and clears it
+        (the UI's role).  None stops the computation."""
+        if clip is not None and (tuple(clip.shape) != (self.channels,) or clip.element_size() != 4):
+            raise ValueError("clip must be a 4-byte integer tensor [C]")
+        self._clip = clip
+        _abi.check(self.lib.uhsdr_rx_set_clip_output(self.handle, C.c_void_p(clip.data_ptr() if clip is not None else 0)),
+                   "uhsdr_rx_set_clip_output")
+
+    def twinpeaks_state(self, out) -> None:
+        """ts.twinpeaks_tested of every channel into out (int32 [C] on the device), stream-ordered."""
+        if tuple(out.shape) != (self.channels,) or out.element_size() != 4:
+            raise ValueError("out must be a 4-byte integer tensor [C]")
+        _abi.check(self.lib.uhsdr_rx_twinpeaks_state(self.handle, C.c_void_p(out.data_ptr())), "uhsdr_rx_twinpeaks_state")
+
+    def twinpeaks_rearm(self) -> None:
+        """The UI's acknowledgement after a codec restart: CODEC_RESTART -> WAIT on every channel."""
+        _abi.check(self.lib.uhsdr_rx_twinpeaks_rearm(self.handle), "uhsdr_rx_twinpeaks_rearm")
+
     def key_beep(self, calls: int) -> None:
         """AudioManagement_KeyBeep for every channel: the beep tone is added to the next `calls`
         32-frame calls (uhsdr_rx_key_beep)."""

@@ -169,6 +169,35 @@ def fm_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, carrier
     return _frames(i_sig, q_sig)
 
 
+STATUS_PHASE_DEG = (0.0, 12.0, 30.0, 60.0, 89.0)
+
+
+def status_iq(channels, start: int, nframes: int, noise_sigma: float = 30.0, burst_every: int = 3000,
+              burst_len: int = 256):
+    """Status side outputs (ADC clip flags, twin-peaks detector; audio_driver.c:2660-2676,
+    2173-2248): the two-tone SSB signal of ``ssb_iq`` with an I/Q phase error of
+    STATUS_PHASE_DEG[channel % 5] degrees on Q (Q = A sin(theta + phi); the Moseley & Slump
+    estimate asin(teta1 / teta3) sees -phi), and every `burst_every` frames a `burst_len`-frame
+    burst at 1.5 + (channel*7 + k) % 6 times the level, so |I| crosses the quarter / half / full
+    ADC clip thresholds (1024 / 2048 / 4096 LSB16) on different calls per channel.  Peak stays
+    below 32767 (no full-scale samples)."""
+    channels = np.asarray(channels, dtype=np.int64)
+    f1, f2, a1, a2, p1, p2 = channel_params(channels, "ssb2tone")
+    phi = np.deg2rad(np.array(STATUS_PHASE_DEG)[channels % len(STATUS_PHASE_DEG)])[:, None]
+    n = np.arange(start, start + nframes, dtype=np.float64)[None, :]
+    k = (np.arange(start, start + nframes) // burst_every)[None, :]
+    inb = (np.arange(start, start + nframes) % burst_every) < burst_len
+    gain = np.where(inb[None, :], 1.5 + ((channels[:, None] * 7 + k) % 6), 1.0)
+    ph1 = 2.0 * np.pi * (12000.0 + f1[:, None]) / FS * n + p1[:, None]
+    ph2 = 2.0 * np.pi * (12000.0 + f2[:, None]) / FS * n + p2[:, None]
+    i_sig = gain * (a1[:, None] * np.cos(ph1) + a2[:, None] * np.cos(ph2))
+    q_sig = gain * (a1[:, None] * np.sin(ph1 + phi) + a2[:, None] * np.sin(ph2 + phi))
+    if noise_sigma > 0:
+        ni, nq = _noise(channels, start, nframes, noise_sigma)
+        i_sig, q_sig = i_sig + ni, q_sig + nq
+    return _frames(i_sig, q_sig)
+
+
 def tx_audio(channels, start: int, nframes: int, kind: str = "ssb2tone", noise_sigma: float = 10.0):
     """C4 SSB-TX input: the codec's microphone frames (AudioSample_t {int32 l, r}, the sample in
     both channels as (int16) value << 16) carrying a per-channel two-tone audio signal."""

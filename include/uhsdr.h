@@ -340,7 +340,9 @@ typedef struct uhsdr_tx_config
     float   phase_balance;        /* ads.iq_phase_balance_tx[trans] */
     int32_t fm_deviation_5k;      /* FLAGS2_FM_MODE_DEVIATION_5KHZ: FM transmit deviation 5 kHz (else 2.5) */
     int32_t fm_subaudible_tone;   /* ts.fm_subaudible_tone_gen_select: index into fm_subaudible_tone_table, 0 = off */
-    int32_t reserved[14];
+    int32_t fm_tone_burst_mode;   /* ts.fm_tone_burst_mode: 0 off, 1 1750 Hz, 2 2135 Hz (fm_tone_burst_freq,
+                                     audio_management.c:328), sent while uhsdr_tx_set_tone_burst is on */
+    int32_t reserved[13];
 } uhsdr_tx_config;
 
 typedef struct uhsdr_tx_plan
@@ -373,7 +375,12 @@ typedef struct uhsdr_tx_plan
     uint32_t fm_sub_step;         /* softdds_stepForSampleRate(tone, 48000) (softdds.c:26-32) */
     float   fm_sub_scale;         /* FM_SUBAUDIBLE_TONE_AMPLITUDE_SCALING * fm_mod_mult */
     int16_t dds_table[1024];      /* DDS_TABLE, softdds/dds_table.c */
-    int32_t reserved[32];
+    /* softdds tones: TUNE (AudioManagement_SetSidetoneForDemodMode, audio_management.c:377-404:
+       SSB_TUNE_FREQ 750 Hz, two-tone + 1950 Hz) and the FM tone burst (LoadToneBurstMode :339-349) */
+    uint32_t tune_step[2];
+    uint32_t tone_burst_step;
+    float   tone_burst_scale;     /* FM_TONE_BURST_AMPLITUDE_SCALING * fm_mod_mult */
+    int32_t reserved[28];
 } uhsdr_tx_plan;
 
 typedef struct uhsdr_tx_s* uhsdr_tx_handle;
@@ -391,6 +398,18 @@ uhsdr_status uhsdr_tx_destroy(uhsdr_tx_handle h);
 /* TxProcessor_PrepareRun (tx_processor.c:63-66): clear the ALC look-ahead delay line only,
    the first time back to TX; all other TX state carries on */
 uhsdr_status uhsdr_tx_prepare_run(uhsdr_tx_handle h);
+/* TUNE (ts.tune with ts.tune_tone_mode): from the next uhsdr_tx_process on, the transmitter's audio
+   is the softdds tone instead of the codec input (TxProcessor_AudioBufferFill, tx_processor.c:344-347;
+   softdds_runIQ into one buffer keeps the quadrature sample), the TX filters and the post-filter
+   gain are skipped (:444-447, :179), the ALC runs.  Entering and leaving TUNE reconfigures the
+   tone generator with its phase reset (AudioManagement_SetSidetoneForDemodMode, as
+   RadioManagement_SwitchTxRx does, radio_management.c:1035).  Common to all channels. */
+enum { UHSDR_TUNE_OFF = 0, UHSDR_TUNE_SINGLE = 1, UHSDR_TUNE_TWO = 2 };
+uhsdr_status uhsdr_tx_set_tune(uhsdr_tx_handle h, int32_t tune);
+/* FM tone burst ("whistle-up", ads.fm_conf.tone_burst_active, tx_processor.c:555-564): while on,
+   the fm_tone_burst_mode tone replaces the sub-audible tone in the FM modulator.  No effect for
+   SSB or with fm_tone_burst_mode 0. */
+uhsdr_status uhsdr_tx_set_tone_burst(uhsdr_tx_handle h, int32_t active);
 int32_t      uhsdr_sizeof_tx_config(void);
 int32_t      uhsdr_sizeof_tx_plan(void);
 

@@ -40,6 +40,8 @@ def load():
                                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         lib.uo_tx_state_size.restype = C.c_size_t
         lib.uo_tx_state_init.argtypes = [C.c_void_p, C.c_void_p]
+        lib.uo_tx_set_tune.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        lib.uo_tx_set_tone_burst.argtypes = [C.c_void_p, C.c_int, C.c_int]
         lib.uo_tx_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                             C.c_void_p, C.c_void_p, C.c_int]
         lib.uo_spec_state_size.restype = C.c_size_t
@@ -128,6 +130,12 @@ class OracleTx:
         self.states = (C.c_char * (self.ssize * channels))()
         for c in range(channels):
             self.lib.uo_tx_state_init(C.byref(plan), C.byref(self.states, c * self.ssize))
+
+    def set_tune(self, tune: int) -> None:
+        self.lib.uo_tx_set_tune(self.states, self.channels, int(tune))
+
+    def set_tone_burst(self, active: bool) -> None:
+        self.lib.uo_tx_set_tone_burst(self.states, self.channels, int(bool(active)))
 
     def process(self, audio: np.ndarray, threads: int = 1):
         """audio: int32 [C][n][2] codec frames -> (iq int32 [C][n][2], a0 f32 [C][n])"""

@@ -31,6 +31,10 @@
  *   tx=1           transmit: in= holds codec audio frames {l,r}, out_dst= gets the IQ frames
  *                  TxProcessor_Run writes (tx_processor.c:891-1078), out_a= a_buffer[0]
  *   micmult= boost= comp= txfilter= txbass= txtreble= txpwr= txgi= txgq= txphase=
+ *   tune=t0:K:M    TUNE on calls t0 .. t0+K-1, M = 1 single tone, 2 two-tone (ts.tune, ts.tune_tone_mode,
+ *                  AudioManagement_SetSidetoneForDemodMode on entry and exit, as RadioManagement does)
+ *   burst=t0:K     FM tone burst on calls t0 .. t0+K-1 (ads.fm_conf.tone_burst_active)
+ *   burstmode=     ts.fm_tone_burst_mode (0 off, 1 1750 Hz, 2 2135 Hz)
  *   dump=setup     print the configured chain (coefficients as raw bits) as JSON
  *   dump=paths     print FilterPathInfo[] (audio_filter.c:147-922) as JSON
  */
@@ -289,6 +293,7 @@ int main(int argc, char** argv)
     ts.alc_tx_postfilt_gain = ALC_POSTFILT_GAIN_DEFAULT;
     ts.tx_filter = iarg(argc, argv, "txfilter", 0);
     ts.fm_subaudible_tone_gen_select = iarg(argc, argv, "subtone", 0);   /* FM_SUBAUDIBLE_TONE_OFF */
+    ts.fm_tone_burst_mode = iarg(argc, argv, "burstmode", 0);           /* FM_TONE_BURST_OFF */
     ts.dsp.tx_bass_gain = iarg(argc, argv, "txbass", 4);
     ts.dsp.tx_treble_gain = iarg(argc, argv, "txtreble", 4);
     ts.tx_power_factor = farg(argc, argv, "txpwr", 0.5f);
@@ -352,8 +357,23 @@ int main(int argc, char** argv)
         ts.txrx_mode = TRX_MODE_TX;
         AudioSample_t ablk[IQ_BLOCK_SIZE], side[IQ_BLOCK_SIZE];
         IqSample_t oblk[IQ_BLOCK_SIZE];
+        long tune0 = -1, tunen = 0, tunem = 1, burst0 = -1, burstn = 0;
+        {
+            const char* t = arg(argc, argv, "tune", NULL);
+            if (t && sscanf(t, "%ld:%ld:%ld", &tune0, &tunen, &tunem) != 3) { fprintf(stderr, "tune=t0:K:M\n"); return 2; }
+            const char* b = arg(argc, argv, "burst", NULL);
+            if (b && sscanf(b, "%ld:%ld", &burst0, &burstn) != 2) { fprintf(stderr, "burst=t0:K\n"); return 2; }
+        }
         for (long off = 0; off < n; off += block)
         {
+            const long call = off / block;
+            if (call == tune0 || (tune0 >= 0 && call == tune0 + tunen))
+            {
+                ts.tune = call == tune0;
+                ts.tune_tone_mode = tunem == 2 ? TUNE_TONE_TWO : TUNE_TONE_SINGLE;
+                AudioManagement_SetSidetoneForDemodMode(ts.dmod_mode, ts.tune);
+            }
+            ads.fm_conf.tone_burst_active = burst0 >= 0 && call >= burst0 && call < burst0 + burstn;
             memcpy(ablk, iq + off, sizeof(AudioSample_t) * block);
             AudioDriver_I2SCallback(ablk, oblk, side, block);
             memcpy(dst + off, oblk, sizeof(IqSample_t) * block);

@@ -1073,22 +1073,64 @@ static int32_t to_int32(float f)     /* float -> int32 as x86 cvttss2si (out of 
     return (f > -2147483904.0f && f < 2147483648.0f) ? (int32_t)f : INT32_MIN;
 }
 
+void uo_tx_set_tune(uo_tx_state* states, int C, int tune)
+{
+    for (int c = 0; c < C; c++)     /* AudioManagement_SetSidetoneForDemodMode: configRunIQ, smooth 0 */
+    {
+        states[c].tune = tune;
+        states[c].tune_acc[0] = states[c].tune_acc[1] = 0;
+    }
+}
+
+void uo_tx_set_tone_burst(uo_tx_state* states, int C, int active)
+{
+    for (int c = 0; c < C; c++) states[c].burst = active;
+}
+
+/* softdds_nextSampleIndex (softdds.h:37-44) */
+static uint32_t dds_next(uint32_t* acc, uint32_t step)
+{
+    const uint32_t k = (*acc >> 22) % 1024;
+    *acc += step;
+    return k;
+}
+
 /* one TxProcessor_Run call (SSB voice) on BLK frames */
 static void tx_call(const uhsdr_tx_plan* p, uo_tx_state* s, const int32_t* audio, int32_t* iq, float* a0)
 {
     const int n = BLK;
     float a[BLK], ib[BLK], qb[BLK], valbuf[BLK];
     /* TxProcessor_AudioBufferFill (tx_processor.c:339-405) */
-    for (int i = 0; i < n; i++) a[i] = (p->audio_source == UHSDR_TX_AUDIO_LINEIN_R) ? audio[2 * i + 1] : audio[2 * i];
-    if (p->apply_in_gain)
-        for (int i = 0; i < n; i++) a[i] = a[i] * p->in_gain;
-    /* TxProcessor_FilterAudio (:416-429) */
-    if (p->run_lattice) iir_lattice(p->lat_k, p->lat_v, p->lat_stages, s->lat, a, a, n);
-    if (p->run_biquad) biquad_df1(p->biquad, 3, s->bq, a, n);
+    if (s->tune)
+    {
+        /* softdds_runIQ(a, a, n) (softdds.c:152-163): genIQSingleTone / genIQTwoTone write I then Q
+           to the same sample, so the quadrature value remains */
+        for (int i = 0; i < n; i++)
+        {
+            const uint32_t k0 = dds_next(&s->tune_acc[0], p->tune_step[0]);
+            if (s->tune == 1)
+                a[i] = p->dds_table[(k0 + 768) % 1024];
+            else
+            {
+                const uint32_t k1 = dds_next(&s->tune_acc[1], p->tune_step[1]);
+                a[i] = ((int32_t)p->dds_table[(k0 + 768) % 1024] + (int32_t)p->dds_table[(k1 + 768) % 1024]) / 2;
+            }
+        }
+    }
+    else
+    {
+        for (int i = 0; i < n; i++) a[i] = (p->audio_source == UHSDR_TX_AUDIO_LINEIN_R) ? audio[2 * i + 1] : audio[2 * i];
+        if (p->apply_in_gain)
+            for (int i = 0; i < n; i++) a[i] = a[i] * p->in_gain;
+        /* TxProcessor_FilterAudio (:416-429), skipped in TUNE (:444) */
+        if (p->run_lattice) iir_lattice(p->lat_k, p->lat_v, p->lat_stages, s->lat, a, a, n);
+        if (p->run_biquad) biquad_df1(p->biquad, 3, s->bq, a, n);
+    }
     /* TxProcessor_VoiceCompressor (:173-242) */
     if (p->comp_on)
     {
-        for (int i = 0; i < n; i++) a[i] = a[i] * p->postfilt_gain;
+        if (!s->tune)
+            for (int i = 0; i < n; i++) a[i] = a[i] * p->postfilt_gain;
         for (int i = 0; i < n; i++)
         {
             const float alc_var = fabsf(a[i] * s->alc_val) / 30000 - 1.0;        /* ALC_KNEE */
@@ -1124,13 +1166,16 @@ static void tx_call(const uhsdr_tx_plan* p, uo_tx_state* s, const int32_t* audio
             s->fm_hpf_a = x;
             a1[i] = s->fm_hpf_b;
         }
-        if (p->fm_sub_on)                                                  /* softdds_addSingleTone */
+        if (p->fm_sub_on && !s->burst)                                     /* softdds_addSingleTone */
             for (int i = 0; i < n; i++)
             {
                 const uint32_t k = (s->fm_sub_acc >> 22) % 1024;
                 s->fm_sub_acc += p->fm_sub_step;
                 a1[i] += (float)p->dds_table[k] * p->fm_sub_scale;
             }
+        if (s->burst)                                                      /* tone burst, :561-564 */
+            for (int i = 0; i < n; i++)
+                a1[i] += (float)p->dds_table[dds_next(&s->burst_acc, p->tone_burst_step)] * p->tone_burst_scale;
         float* ip = p->fm_swap ? qb : ib;
         float* qp = p->fm_swap ? ib : qb;
         for (int i = 0; i < n; i++)

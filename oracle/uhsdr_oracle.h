@@ -119,12 +119,19 @@ typedef struct uo_tx_state
     /* TxProcessor_FM statics (tx_processor.c:536-537) and the sub-audible tone softdds */
     float fm_hpf_a, fm_hpf_b;
     uint32_t fm_accum, fm_sub_acc;
+    /* softdds tones: ts.tune / tune_tone_mode with dbldds[0..1] (softdds.c:19), FM tone burst
+       (ads.fm_conf.tone_burst_active, tone_burst_dds) */
+    int32_t tune, burst;
+    uint32_t tune_acc[2], burst_acc;
 } uo_tx_state;
 
 size_t uo_tx_state_size(void);
 void uo_tx_state_init(const uhsdr_tx_plan* p, uo_tx_state* s);
 int uo_tx_process_batch(const uhsdr_tx_plan* p, uo_tx_state* states, int C, const int32_t* audio, int n,
                         int32_t* iq, float* a0, int threads);
+/* TUNE on / off (0 off, 1 single tone, 2 two-tone) and the FM tone burst, on C channel states */
+void uo_tx_set_tune(uo_tx_state* states, int C, int tune);
+void uo_tx_set_tone_burst(uo_tx_state* states, int C, int active);
 
 /* spectrum display: producer ring + UiSpectrum_RedrawSpectrum states 0-3
    (audio_driver.c:1811-1851, ui_spectrum.c:1350-1446) */

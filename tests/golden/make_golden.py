@@ -137,6 +137,14 @@ TX_CONFIGS = {
     "fm_subtone": {"mode": 5, "path": 1, "iqmode": 4, "subtone": 10},
     "fm_m6k_subtone": {"mode": 5, "path": 1, "iqmode": 2, "subtone": 33, "fm5k": 1, "comp": 3},
     "fm_p6k_iqadj": {"mode": 5, "path": 1, "iqmode": 1, "txgi": 0.97, "txgq": 1.02, "txphase": 0.02},
+    # TUNE tones (softdds_runIQ into the voice chain) and the FM tone burst; events on call indices
+    # that are multiples of 8 so 256-frame device calls can switch them between launches
+    "usb_tune": {"mode": 0, "path": 48, "tune": "8:40:1"},
+    "lsb_tune2": {"mode": 1, "path": 48, "comp": 5, "tune": "16:32:2"},
+    "usb_tune_comp_off": {"mode": 0, "path": 48, "comp": -1, "tune": "0:64:1"},
+    "fm_tune2": {"mode": 5, "path": 1, "iqmode": 4, "tune": "8:24:2"},
+    "fm_burst": {"mode": 5, "path": 1, "iqmode": 4, "subtone": 10, "burstmode": 1, "burst": "16:24"},
+    "fm_burst2_5k": {"mode": 5, "path": 1, "iqmode": 3, "fm5k": 1, "burstmode": 2, "burst": "8:16"},
 }
 
 

@@ -24,6 +24,37 @@ def load_tx(path):
             "setup": json.loads(str(d["setup"])), "args": json.loads(str(d["args"]))}
 
 
+def tx_events(args):
+    """uhsdr_ref's run-time TX controls -> {call: [(what, value)]}: tune=t0:K:M (TUNE mode M on calls
+    t0 .. t0+K-1), burst=t0:K (FM tone burst)"""
+    ev = {}
+    if "tune" in args:
+        t0, k, m = (int(x) for x in str(args["tune"]).split(":"))
+        ev.setdefault(t0, []).append(("tune", m))
+        ev.setdefault(t0 + k, []).append(("tune", 0))
+    if "burst" in args:
+        b0, k = (int(x) for x in str(args["burst"]).split(":"))
+        ev.setdefault(b0, []).append(("burst", 1))
+        ev.setdefault(b0 + k, []).append(("burst", 0))
+    return ev
+
+
+def drive_tx(chain, process, audio, frames, args):
+    """Feed audio [C][n][2] in calls of `frames`, applying the run-time events between calls
+    (chain: set_tune / set_tone_burst); process(block) -> (iq, a0)."""
+    ev = tx_events(args)
+    cpl = frames // 32
+    assert all(c % cpl == 0 for c in ev), "events must fall on call boundaries"
+    iqs, a0s = [], []
+    for off in range(0, audio.shape[1], frames):
+        for what, v in ev.get(off // 32, []):
+            (chain.set_tune if what == "tune" else chain.set_tone_burst)(v)
+        iq, a0 = process(np.ascontiguousarray(audio[:, off:off + frames]))
+        iqs.append(iq)
+        a0s.append(a0)
+    return np.concatenate(iqs, axis=1), np.concatenate(a0s, axis=1)
+
+
 def fb(arr, n):
     return np.frombuffer(bytes(arr), dtype=np.uint32)[:n]
 
@@ -48,6 +79,7 @@ def test_tx_plan_matches_reference_setup(path):
 def test_tx_oracle_matches_reference(path):
     g = load_tx(path)
     plan = U.build_tx_plan(U.tx_config_from_ref_args(g["args"]))
-    iq, a0 = oracle.OracleTx(plan, g["audio"].shape[0]).process(g["audio"])
+    o = oracle.OracleTx(plan, g["audio"].shape[0])
+    iq, a0 = drive_tx(o, o.process, g["audio"], 256, g["args"])
     np.testing.assert_array_equal(a0.view(np.uint32), g["a0"].view(np.uint32))
     np.testing.assert_array_equal(iq, g["iq"])

@@ -10,6 +10,7 @@ from ._abi import (RxConfig, RxPlan, build_plan, plan_supported, config_from_ref
                    PRECISION_EXACT, PRECISION_FMA, ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP,
                    TWINPEAKS_SAMPLING, TWINPEAKS_DONE, TWINPEAKS_WAIT, TWINPEAKS_UNCORRECTABLE,
                    TWINPEAKS_CODEC_RESTART,
+                   TUNE_OFF, TUNE_SINGLE, TUNE_TWO,
                    TxConfig, TxPlan, build_tx_plan, default_tx_config, tx_config_from_ref_args,
                    SpectrumConfig, SpectrumPlan, build_spectrum_plan, default_spectrum_config,
                    spectrum_config_from_ref_args)

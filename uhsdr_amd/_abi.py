@@ -104,7 +104,8 @@ class TxConfig(C.Structure):
         ("alc_postfilt_gain", C.c_int32), ("tx_filter", C.c_int32), ("bass_gain", C.c_int32),
         ("treble_gain", C.c_int32), ("filter_disable", C.c_int32), ("power_factor", C.c_float),
         ("gain_i", C.c_float), ("gain_q", C.c_float), ("phase_balance", C.c_float),
-        ("fm_deviation_5k", C.c_int32), ("fm_subaudible_tone", C.c_int32), ("reserved", C.c_int32 * 14),
+        ("fm_deviation_5k", C.c_int32), ("fm_subaudible_tone", C.c_int32), ("fm_tone_burst_mode", C.c_int32),
+        ("reserved", C.c_int32 * 13),
     ]
 
 
@@ -120,7 +121,8 @@ class TxPlan(C.Structure):
         ("final_q_gain", C.c_float), ("phase_balance", C.c_float),
         ("fm", C.c_int32), ("fm_mod_mult", C.c_float), ("fm_word", C.c_uint32), ("fm_swap", C.c_int32),
         ("fm_sub_on", C.c_int32), ("fm_sub_step", C.c_uint32), ("fm_sub_scale", C.c_float),
-        ("dds_table", C.c_int16 * 1024), ("reserved", C.c_int32 * 32),
+        ("dds_table", C.c_int16 * 1024), ("tune_step", C.c_uint32 * 2), ("tone_burst_step", C.c_uint32),
+        ("tone_burst_scale", C.c_float), ("reserved", C.c_int32 * 28),
     ]
 
 
@@ -198,6 +200,8 @@ SIGNATURES = {
     "uhsdr_tx_get_plan": (C.c_int, [C.c_void_p, C.POINTER(TxPlan)]),
     "uhsdr_tx_destroy": (C.c_int, [C.c_void_p]),
     "uhsdr_tx_prepare_run": (C.c_int, [C.c_void_p]),
+    "uhsdr_tx_set_tune": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_tx_set_tone_burst": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_fir_create": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                    C.POINTER(C.c_void_p)]),
     "uhsdr_fir_reset": (C.c_int, [C.c_void_p]),
@@ -307,8 +311,9 @@ TX_ARG_MAP = {
     "mode": "dmod_mode", "iqmode": "iq_freq_mode", "micmult": "mic_gain_mult", "boost": "mic_boost",
     "comp": "comp_level", "txfilter": "tx_filter", "txbass": "bass_gain", "txtreble": "treble_gain",
     "txpwr": "power_factor", "txgi": "gain_i", "txgq": "gain_q", "txphase": "phase_balance",
-    "fm5k": "fm_deviation_5k", "subtone": "fm_subaudible_tone",
+    "fm5k": "fm_deviation_5k", "subtone": "fm_subaudible_tone", "burstmode": "fm_tone_burst_mode",
 }
+TUNE_OFF, TUNE_SINGLE, TUNE_TWO = range(3)      # uhsdr_tx_set_tune
 
 
 def default_tx_config(**overrides) -> TxConfig:

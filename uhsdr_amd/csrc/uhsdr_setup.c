@@ -570,6 +570,11 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
         uhsdr_set_error("FM transmit needs the I/Q frequency translation");
         return UHSDR_UNSUPPORTED;
     }
+    if (cfg->fm_tone_burst_mode < 0 || cfg->fm_tone_burst_mode > 2)   /* FM_TONE_BURST_MAX, audio_driver.h:440 */
+    {
+        uhsdr_set_error("fm_tone_burst_mode %d outside 0..2", cfg->fm_tone_burst_mode);
+        return UHSDR_ARGUMENT_ERROR;
+    }
     if (fm && (cfg->fm_subaudible_tone < 0 || cfg->fm_subaudible_tone >= uhsdr_fm_subaudible_count))
     {
         uhsdr_set_error("fm_subaudible_tone %d outside 0..%d", cfg->fm_subaudible_tone, uhsdr_fm_subaudible_count - 1);
@@ -679,7 +684,15 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
         p->fm_sub_step = (uint32_t)(freq64_shifted / IQ_SAMPLE_RATE);
         const float fm_mod_mult = p->fm_mod_mult;
         p->fm_sub_scale = 0.00045 * fm_mod_mult;              /* FM_SUBAUDIBLE_TONE_AMPLITUDE_SCALING */
+        /* tone burst: fm_tone_burst_freq[] = { 0, 1750, 2135 } (audio_management.c:328),
+           FM_TONE_BURST_AMPLITUDE_SCALING = FM_MOD_SCALING / 4266.0 (tx_processor.c:519) */
+        static const uint32_t burst_hz[3] = { 0, 1750, 2135 };
+        p->tone_burst_step = softdds_step((float)burst_hz[cfg->fm_tone_burst_mode], IQ_SAMPLE_RATE);
+        p->tone_burst_scale = (16 / 4266.0) * fm_mod_mult;
     }
+    /* TUNE tones of the voice modes: SSB_TUNE_FREQ (hardware/uhsdr_board.h:114) and + 1200 Hz */
+    p->tune_step[0] = softdds_step(750.0f, IQ_SAMPLE_RATE);
+    p->tune_step[1] = softdds_step(750.0f + 1200, IQ_SAMPLE_RATE);
     return UHSDR_OK;
 }
 

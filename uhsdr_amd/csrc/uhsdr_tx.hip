@@ -43,7 +43,22 @@ struct TxVoiceArgs
     int2* iq;               // FM: DAC frames [C][N] written here (no tx_iq)
     int C, N;
     int delay_phase;        // alc_delay_inbuf / 32 before this launch
+    // softdds tones common to all channels (accumulators at frame 0 of this launch):
+    // tune 0 off, 1 single (dbldds[0]), 2 two-tone (dbldds[0] + [1]); burst: FM tone burst on
+    int tune, burst;
+    uint32_t tune_acc0, tune_acc1, burst_acc;
 };
+
+// softdds_runIQ(a, a, n) (softdds.c:152-163): with both outputs in one buffer the quadrature
+// sample, written second, stays -- DDS_TABLE[k + 768] single, or the two-tone integer mean
+__device__ __forceinline__ float tune_tone(const TxVoiceArgs& a, const uhsdr_tx_plan* __restrict__ P, int n)
+{
+    const uint32_t k0 = ((a.tune_acc0 + (uint32_t)n * P->tune_step[0]) >> 22) % 1024u;
+    const int q0 = P->dds_table[(k0 + 768u) % 1024u];
+    if (a.tune == 1) return (float)q0;
+    const uint32_t k1 = ((a.tune_acc1 + (uint32_t)n * P->tune_step[1]) >> 22) % 1024u;
+    return (float)((q0 + (int)P->dds_table[(k1 + 768u) % 1024u]) / 2);
+}
 
 __device__ __forceinline__ int tx_to_int32(float f)
 {
@@ -73,7 +88,10 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
     for (int i = 0; i < 12; ++i) bq[i] = a.bq[i * C + cl];
     float alc_val = a.alc[cl];
     const bool right = P->audio_source == UHSDR_TX_AUDIO_LINEIN_R;
-    const bool apply_gain = P->apply_in_gain, run_lat = P->run_lattice, run_bq = P->run_biquad, comp = P->comp_on;
+    // TUNE: the tone replaces the input, no gain, no filters, no post-filter gain (tx_processor.c:344,444,179)
+    const bool tune = a.tune != 0;
+    const bool apply_gain = P->apply_in_gain && !tune, run_lat = P->run_lattice && !tune, run_bq = P->run_biquad && !tune;
+    const bool comp = P->comp_on;
     const float in_gain = P->in_gain, post = P->postfilt_gain, decay = P->alc_decay, gscale = P->alc_gain_scaling;
     const int calls = a.N / BLK;
     float hpf_a = 0.0f, hpf_b = 0.0f;
@@ -93,6 +111,11 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
             const int4 v = src[j];
             x[2 * j] = (float)(right ? v.y : v.x);
             x[2 * j + 1] = (float)(right ? v.w : v.z);
+        }
+        if (tune)
+        {
+#pragma unroll
+            for (int m = 0; m < BLK; ++m) x[m] = tune_tone(a, P, k * BLK + m);
         }
         const int slot_in = (a.delay_phase + k + 1) % TX_DELAY_SLOTS;   // alc_delay_inbuf after += 32
         const int slot_out = (a.delay_phase + k + 2) % TX_DELAY_SLOTS;  // alc_delay_outbuf
@@ -123,7 +146,7 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
 #pragma unroll
             for (int m = 0; m < BLK; ++m)
             {
-                const float v = x[m] * post;
+                const float v = tune ? x[m] : x[m] * post;
                 // ALC (tx_processor.c:197-221)
                 const float alc_var = (float)((double)(fabsf(v * alc_val) / 30000) - 1.0);
                 if (alc_var < 0)
@@ -155,7 +178,10 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
         if constexpr (FM)
         {
             const int16_t* __restrict__ dds = P->dds_table;
-            const bool sub = P->fm_sub_on, swap = P->fm_swap;
+            // the sub-audible tone pauses during a tone burst (tx_processor.c:555-564)
+            const bool sub = P->fm_sub_on && !a.burst, swap = P->fm_swap;
+            const bool burst = a.burst != 0;
+            const float burst_scale = P->tone_burst_scale;
             const float mult = P->fm_mod_mult, sub_scale = P->fm_sub_scale;
             const uint32_t word = P->fm_word, step = P->fm_sub_step;
             const float gi = P->final_i_gain, gq = P->final_q_gain, ph = P->phase_balance;
@@ -173,6 +199,11 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
                     const uint32_t idx = (sub_acc >> 22) % 1024u;
                     sub_acc += step;
                     a1 += (float)dds[idx] * sub_scale;
+                }
+                if (burst)
+                {
+                    const uint32_t idx = ((a.burst_acc + (uint32_t)(k * BLK + m) * P->tone_burst_step) >> 22) % 1024u;
+                    a1 += (float)dds[idx] * burst_scale;
                 }
                 // fm_mod_accum += word + a1 * FM_MOD_SCALING * mult; as on x86, the float sum is
                 // truncated through a 64-bit integer (cvttss2si) into the uint32 accumulator
@@ -349,6 +380,8 @@ struct uhsdr_tx_s
     void* arena;
     size_t arena_bytes;
     long long calls_done, iq_launches;
+    int tune, burst;                 // uhsdr_tx_set_tune / _set_tone_burst
+    uint32_t tune_acc[2], burst_acc; // softdds accumulators (dbldds[0..1], tone_burst_dds) at the next frame
 };
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { uhsdr_set_error("%s: %s", #x, hipGetErrorString(e_)); return UHSDR_DEVICE_ERROR; } } while (0)
@@ -378,8 +411,28 @@ extern "C" uhsdr_status uhsdr_tx_reset(uhsdr_tx_handle h)
     HIPCHK(hipMemcpyAsync(h->osc, osc0, sizeof osc0, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     free(ones);
+    // TxProcessor_Init -> AudioManagement_LoadToneBurstMode: tone burst DDS from phase 0
+    h->burst_acc = 0;
+    h->tune_acc[0] = h->tune_acc[1] = 0;
     h->calls_done = 0;
     h->iq_launches = 0;
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_tx_set_tune(uhsdr_tx_handle h, int32_t tune)
+{
+    if (!h || tune < UHSDR_TUNE_OFF || tune > UHSDR_TUNE_TWO) { uhsdr_set_error("bad argument"); return UHSDR_ARGUMENT_ERROR; }
+    // AudioManagement_SetSidetoneForDemodMode -> softdds_configRunIQ(freq, rate, smooth = 0): both
+    // accumulators restart at 0, on entering and on leaving TUNE (audio_management.c:377-404)
+    h->tune = tune;
+    h->tune_acc[0] = h->tune_acc[1] = 0;
+    return UHSDR_OK;
+}
+
+extern "C" uhsdr_status uhsdr_tx_set_tone_burst(uhsdr_tx_handle h, int32_t active)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    h->burst = active != 0;    // the tone burst DDS keeps its phase between bursts
     return UHSDR_OK;
 }
 
@@ -460,6 +513,17 @@ extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio
     va.fm = h->fm; va.iq = (int2*)iq;
     va.C = h->C; va.N = h->N;
     va.delay_phase = (int)(h->calls_done % TX_DELAY_SLOTS);
+    va.tune = h->tune;
+    va.tune_acc0 = h->tune_acc[0];
+    va.tune_acc1 = h->tune_acc[1];
+    va.burst = h->plan.fm && h->burst;
+    va.burst_acc = h->burst_acc;
+    if (h->tune)
+    {
+        h->tune_acc[0] += (uint32_t)h->N * h->plan.tune_step[0];
+        if (h->tune == 2) h->tune_acc[1] += (uint32_t)h->N * h->plan.tune_step[1];
+    }
+    if (va.burst) h->burst_acc += (uint32_t)h->N * h->plan.tone_burst_step;
     if (h->plan.fm)
     {
         // FM: the modulator is sequential per channel and finishes in tx_voice

@@ -39,6 +39,14 @@ class TxChain:
         _abi.check(self.lib.uhsdr_tx_process(self.handle, C.c_void_p(audio.data_ptr()), C.c_void_p(iq.data_ptr()),
                                              C.c_void_p(a0.data_ptr() if a0 is not None else 0)), "uhsdr_tx_process")
 
+    def set_tune(self, tune: int) -> None:
+        """TUNE for the following calls: TUNE_OFF, TUNE_SINGLE (750 Hz) or TUNE_TWO (750 + 1950 Hz)."""
+        _abi.check(self.lib.uhsdr_tx_set_tune(self.handle, int(tune)), "uhsdr_tx_set_tune")
+
+    def set_tone_burst(self, active: bool) -> None:
+        """FM tone burst (whistle-up) on / off for the following calls."""
+        _abi.check(self.lib.uhsdr_tx_set_tone_burst(self.handle, int(bool(active))), "uhsdr_tx_set_tone_burst")
+
     def close(self) -> None:
         if self.handle:
             self.lib.uhsdr_tx_destroy(self.handle)

@@ -17,7 +17,8 @@ meta = {}
 for f in sorted(glob.glob(os.path.join(base, "p*", "pmc_counter_collection.csv"))):
     for row in csv.DictReader(open(f)):
         name = row["Kernel_Name"]
-        for k in ("rx_front", "rx_back_dec", "rx_back_out", "rx_back", "rx_fm", "tx_voice", "tx_iq", "spectrum_frames", "spectrum_accumulate"):
+        for k in ("rx_front", "rx_back_dec", "rx_back_out", "rx_back", "rx_fm", "rx_notch", "tx_voice", "tx_iq", "spectrum_frames",
+                  "spectrum_accumulate", "spectrum_zoom", "fir_batch"):
             if k in name:
                 break
         else:

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Per-role timing of the pipelined back end (rx_back) from a UHSDR_TRACE build
+(make variant VTAG=trace VFLAGS=-DUHSDR_TRACE): shader-clock cycles each role spends on its
+call per pipeline step, and waiting at the step's barrier.  Usage:
+    UHSDR_LIB=uhsdr_amd/lib/variants/libuhsdr_amd_trace.so python tools/trace_back.py [C] [N]"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import uhsdr_amd as U
+    from uhsdr_amd import synth
+    Cn = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    os.environ["UHSDR_BACK_FUSED"] = "0"
+    chain = U.RxChain(U.default_config(), channels=Cn, frames=N)
+    x = synth.ssb_iq_torch(0, Cn, 0, N, "cuda")
+    audio = torch.empty((Cn, N), dtype=torch.float32, device="cuda")
+    for _ in range(5):
+        chain.process(x, audio)
+    torch.cuda.synchronize()
+    lib = U.load()
+    buf = np.zeros((64, 8, 40, 3), np.uint64)
+    lib.uhsdr_trace_read.argtypes = [C.c_void_p]
+    assert lib.uhsdr_trace_read(buf.ctypes.data_as(C.c_void_p)) == 0
+    calls = N // 32
+    roles = 5
+    its = calls + roles - 1
+    t = buf[:, :roles, :its, :].astype(np.int64)
+    t0 = t[:, :, 0, 0].min(axis=1)[:, None, None]
+    work = (t[:, :, :, 1] - t[:, :, :, 0])
+    wait = (t[:, :, :, 2] - t[:, :, :, 1])
+    names = ["pre", "agc", "audio", "aa", "output"]
+    print(f"C={Cn} N={N}: per-step cycles (median over workgroups), work / barrier wait")
+    for it in range(its):
+        row = " ".join(f"{names[r]:>6} {int(np.median(work[:, r, it])):6d}/{int(np.median(wait[:, r, it])):6d}" for r in range(roles))
+        print(f"step {it:2d}: {row}")
+    total = int(np.median(t[:, 0, its - 1, 2] - t[:, 0, 0, 0]))
+    print(f"total cycles (median WG): {total}")
+
+
+if __name__ == "__main__":
+    main()

@@ -191,7 +191,20 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier for LDS hand-offs between the waves of a pipeline: the writers' LDS
+// operations complete (lgkmcnt(0)), then s_barrier.  __syncthreads() would also wait for every
+// outstanding global load and store of the wave (its workgroup-scope fence emits vmcnt(0)): the
+// next call's prefetched inputs and this call's output stores would then cost a full HBM round
+// trip per pipeline step.  Only LDS data crosses waves here; global data stays wave-private.
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 constexpr int FRONT_WAVE = 64;
+#define FRONT_WAVE_L 64
 
 // history rows: HS = T-1 rounded up to 4 floats; lane b of a channel loads float4s b, b+nb, ...
 __host__ __device__ constexpr int hist_stride(int T) { return (T - 1 + 3) & ~3; }
@@ -307,6 +320,135 @@ __device__ __forceinline__ void front_fill2(float* W, float* row0, float* row1, 
             *(vf4*)(row0 + ro + 4 * q) = vf4{ p0.x, p0.z, p1.x, p1.z };
             if (!DUP) *(vf4*)(row1 + ro + 4 * q) = vf4{ p0.y, p0.w, p1.y, p1.w };
         }
+    }
+}
+
+// ---- group-coalesced history rows ----
+// The CPW channels of a front wave own consecutive rows [c0, c0 + CPW) of a [C][HS] history array:
+// one contiguous region of CPW * HS floats.  Lane l moves its float4s l, l + 64, ... of that region,
+// so every wave instruction reads or writes whole 1 KB runs (the per-channel lane map would touch
+// CPW partial 128-byte lines per instruction).  Float4 q of the region is channel q / (HS/4) at
+// offset 4 * (q % (HS/4)) of its row.  HQ = hist_q(T) float4s per lane are prefetched; a wave with
+// more than 64 * HQ float4s (fewer than 8 lanes per channel) loads the rest when it fills.
+template <int T, int HQM>
+__device__ __forceinline__ void group_load_rows(const float* row, int c0, int nlive, int lane, vf4 (&buf)[HQM])
+{
+    constexpr int hs4 = hist_stride(T) / 4, HQ = hist_q(T);
+    const vf4* h = (const vf4*)(row + (size_t)c0 * (hs4 * 4));
+    const int qmax = nlive * hs4 - 1;                    // loads clamped to the live channels' rows
+#pragma unroll
+    for (int i = 0; i < HQ; ++i)
+    {
+        const int q = lane + FRONT_WAVE_L * i;
+        buf[i] = h[q < qmax ? q : qmax];
+    }
+}
+
+// pass window of a FIR pair (interleaved {x0[n], x1[n]}): the history part from the two rows
+template <int T, int HQM>
+__device__ __forceinline__ void group_fill_rows2(float* smem, int LW, const float* row0, const float* row1, int c0,
+                                                 int cpw, int nlive, int lane, const vf4 (&buf0)[HQM], const vf4 (&buf1)[HQM])
+{
+    constexpr int hs4 = hist_stride(T) / 4, HQ = hist_q(T);
+    const int nq = cpw * hs4;
+#pragma unroll
+    for (int i = 0; i < HQ; ++i)
+    {
+        const int q = lane + FRONT_WAVE_L * i;
+        if (q < nq)
+        {
+            float* d = smem + (q / hs4) * LW + 8 * (q % hs4);
+            const vf4 x = buf0[i], y = buf1[i];
+            *(vf4*)d = vf4{ x.x, y.x, x.y, y.y };
+            *(vf4*)(d + 4) = vf4{ x.z, y.z, x.w, y.w };
+        }
+    }
+    const vf4* h0 = (const vf4*)(row0 + (size_t)c0 * (hs4 * 4));
+    const vf4* h1 = (const vf4*)(row1 + (size_t)c0 * (hs4 * 4));
+    const int qmax = nlive * hs4 - 1;
+    for (int q = lane + FRONT_WAVE_L * HQ; q < nq; q += FRONT_WAVE_L)
+    {
+        const int qs = q < qmax ? q : qmax;
+        const vf4 x = h0[qs], y = h1[qs];
+        float* d = smem + (q / hs4) * LW + 8 * (q % hs4);
+        *(vf4*)d = vf4{ x.x, y.x, x.y, y.y };
+        *(vf4*)(d + 4) = vf4{ x.z, y.z, x.w, y.w };
+    }
+}
+
+// the next call's history rows (window samples nnew .. nnew + T - 2 of each channel) back to HBM,
+// de-interleaved; DUP: one row only
+template <int T, bool DUP = false>
+__device__ __forceinline__ void group_store_rows2(const float* smem, int LW, float* row0, float* row1, int c0, int nlive,
+                                                  int lane, int nnew)
+{
+    constexpr int hs4 = hist_stride(T) / 4;
+    vf4* h0 = (vf4*)(row0 + (size_t)c0 * (hs4 * 4));
+    vf4* h1 = (vf4*)(row1 + (size_t)c0 * (hs4 * 4));
+    for (int q = lane; q < nlive * hs4; q += FRONT_WAVE_L)
+    {
+        const float* sp = smem + (q / hs4) * LW + 2 * (nnew + 4 * (q % hs4));
+        const vf4 p0 = *(const vf4*)sp, p1 = *(const vf4*)(sp + 4);
+        h0[q] = vf4{ p0.x, p0.z, p1.x, p1.z };
+        if (!DUP) h1[q] = vf4{ p0.y, p0.w, p1.y, p1.w };
+    }
+}
+
+// scalar window (the audio decimator): history part, and the write-back
+template <int T, int HQM>
+__device__ __forceinline__ void group_fill_rows(float* smem, int LW, const float* row, int c0, int cpw, int nlive,
+                                                int lane, const vf4 (&buf)[HQM])
+{
+    constexpr int hs4 = hist_stride(T) / 4, HQ = hist_q(T);
+    const int nq = cpw * hs4;
+#pragma unroll
+    for (int i = 0; i < HQ; ++i)
+    {
+        const int q = lane + FRONT_WAVE_L * i;
+        if (q < nq) *(vf4*)(smem + (q / hs4) * LW + 4 * (q % hs4)) = buf[i];
+    }
+    const vf4* h = (const vf4*)(row + (size_t)c0 * (hs4 * 4));
+    const int qmax = nlive * hs4 - 1;
+    for (int q = lane + FRONT_WAVE_L * HQ; q < nq; q += FRONT_WAVE_L)
+        *(vf4*)(smem + (q / hs4) * LW + 4 * (q % hs4)) = h[q < qmax ? q : qmax];
+}
+
+template <int T>
+__device__ __forceinline__ void group_store_rows(const float* smem, int LW, float* row, int c0, int nlive, int lane, int nnew)
+{
+    constexpr int hs4 = hist_stride(T) / 4;
+    vf4* h = (vf4*)(row + (size_t)c0 * (hs4 * 4));
+    for (int q = lane; q < nlive * hs4; q += FRONT_WAVE_L)
+        h[q] = *(const vf4*)(smem + (q / hs4) * LW + nnew + 4 * (q % hs4));
+}
+
+// new samples and the zero tail of one channel's window (the lane's own NV values)
+__device__ __forceinline__ void window_new2(float* W, int T, bool act, int b, int nb, const v2f* vals, int NV)
+{
+    const int nnew = nb * NV;
+    if (act)
+    {
+        float* d = W + 2 * (T - 1 + b * NV);
+        if (((T - 1) & 1) == 0)                           // 16-byte aligned: two pairs per store
+            for (int j = 0; j < NV; j += 2)
+                *(vf4*)(d + 2 * j) = vf4{ vals[j].x, vals[j].y, vals[j + 1].x, vals[j + 1].y };
+        else
+            for (int j = 0; j < NV; ++j) *(v2f*)(d + 2 * j) = vals[j];
+        for (int t = b; t < FRONT_TAIL; t += nb) *(v2f*)(W + 2 * (T - 1 + nnew + t)) = v2f{ 0.0f, 0.0f };
+    }
+}
+
+__device__ __forceinline__ void window_new(float* W, int T, bool act, int b, int nb, const float* vals, int NV)
+{
+    const int nnew = nb * NV;
+    if (act)
+    {
+        float* d = W + T - 1 + b * NV;
+        if (((T - 1 + b * NV) & 3) == 0 && (NV & 3) == 0)
+            for (int j = 0; j < NV; j += 4) *(vf4*)(d + j) = vf4{ vals[j], vals[j + 1], vals[j + 2], vals[j + 3] };
+        else
+            for (int j = 0; j < NV; ++j) d[j] = vals[j];
+        for (int t = b; t < FRONT_TAIL; t += nb) W[T - 1 + nnew + t] = 0.0f;
     }
 }
 

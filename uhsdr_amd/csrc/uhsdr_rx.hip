@@ -66,9 +66,23 @@ enum { FRONT_COMB_USB = 0,       // I + Q                      (USB, CW/DIGI upp
        FRONT_COMB_SSB_ST = 3,    // {I + Q, I - Q}             (DEMOD_SSBSTEREO, use_stereo)
        FRONT_COMB_IQ_ST = 4 };   // {I, Q}                     (DEMOD_IQ, use_stereo)
 
-__device__ __forceinline__ float front_comb(int comb, v2f h)
+// the Hilbert pair's combination into a_buffer[0] for the mono families (audio_driver.c:2755-2790):
+// I + Q (USB), I - Q (LSB, as I + (-Q): the same binary32 result), I (IQ mono); one wave-uniform
+// branch per block instead of one per sample
+template <int R>
+__device__ __forceinline__ void front_comb_block(int comb, const v2f (&h)[R], float (&o)[R])
 {
-    return comb == FRONT_COMB_I ? h.x : comb == FRONT_COMB_LSB ? (h.x - h.y) : (h.x + h.y);
+    if (comb == FRONT_COMB_I)
+    {
+#pragma unroll
+        for (int r = 0; r < R; ++r) o[r] = h[r].x;
+    }
+    else
+    {
+        const float sg = comb == FRONT_COMB_LSB ? -1.0f : 1.0f;
+#pragma unroll
+        for (int r = 0; r < R; ++r) o[r] = h[r].x + h[r].y * sg;
+    }
 }
 __device__ __forceinline__ v2f front_comb2(int comb, v2f h)
 {
@@ -237,6 +251,8 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
     const int lane = threadIdx.x;
     const int nb = N / R;                            // lanes per channel (>= 4)
     const int CPW = FRONT_WAVE / nb;                 // channels per wave (one channel group)
+    // (Measured and dropped: four independent waves per workgroup, 0.617 vs 0.600 ms at 1M x 64.)
+    const int grp = blockIdx.x;
     int g, b;
     front_lane(lane, nb, 2 * R, g, b);               // lane map for the pair window (2R floats per lane)
     const bool act = g < CPW;
@@ -262,19 +278,23 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
     // One wave per channel group.  The I/Q frames and the stage-1 history rows are issued at
     // entry; the stage-2 rows are issued before the stage-1 FIR, so their latency hides behind it.
     // (A persistent variant that prefetched the next group's frames and rows into registers
-    // doubled the VGPRs and halved the waves per SIMD: 0.67 vs 0.59 ms at 1M x 64.)
-    const int grp = blockIdx.x;
+    // doubled the VGPRs and halved the waves per SIMD: 0.67 vs 0.59 ms at 1M x 64; so did a
+    // re-measurement of it in round 2, 0.656 ms, compute-bound at 2 waves per SIMD.)
+    // History rows move group-coalesced (group_load_rows: whole 1 KB runs per wave instruction);
+    // the I/Q frames in the lane's own (channel, block) layout.
     int4 raw[R / 2];
     vf4 hA[HQ1], hB[HQ1];
     const int c = grp * CPW + g;
     const bool live = act && c < C;
     const int cl = c < C ? c : C - 1;                // loads clamped: no exec-masked load branches
+    const int c0 = grp * CPW;
+    const int nlive = C - c0 < CPW ? C - c0 : CPW;   // live channels of the group
     {
         const int4* src = (const int4*)(a.iq + (size_t)cl * a.ld + b * R);
 #pragma unroll
         for (int j = 0; j < R / 2; ++j) raw[j] = src[j];
-        front_load_row<T1>(a.hist1_i, cl, b, nb, hA);
-        front_load_row<T1>(a.hist1_q, cl, b, nb, hB);
+        group_load_rows<T1>(a.hist1_i, c0, nlive, lane, hA);
+        group_load_rows<T1>(a.hist1_q, c0, nlive, lane, hB);
     }
     if (a.clip)
     {
@@ -368,7 +388,11 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
 #pragma unroll
             for (int j = 0; j < R; ++j) x2[j] = v2f{ xi[j], xq[j] };
         }
-        front_fill2<T1>(W, a.hist1_i, a.hist1_q, c, act, live, b, nb, hA, hB, x2, R);
+        group_fill_rows2<T1>(smem, LW, a.hist1_i, a.hist1_q, c0, CPW, nlive, lane, hA, hB);
+        wave_sync();
+        window_new2(W, T1, act, b, nb, x2, R);
+        wave_sync();
+        group_store_rows2<T1>(smem, LW, a.hist1_i, a.hist1_q, c0, nlive, lane, nb * R);
 
         float o[RD];
         if constexpr (T2 == 0)
@@ -392,14 +416,18 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
         {
             // stereo: {a_buffer[0], a_buffer[1]} through the decimator pair (taps2b = {dec, dec})
             vf4 hC[HQ2], hD[HQ2];
-            front_load_row<T2>(a.hist2_i, cl, b, nb, hC);
-            front_load_row<T2>(a.hist2_q, cl, b, nb, hD);
+            group_load_rows<T2>(a.hist2_i, c0, nlive, lane, hC);
+            group_load_rows<T2>(a.hist2_q, c0, nlive, lane, hD);
             v2f h2[R], d2[RD];
             fir_block2<T1, R, 1, F>(W + 2 * b * R, tA, h2);
 #pragma unroll
             for (int r = 0; r < R; ++r) h2[r] = front_comb2(comb, h2[r]);
             wave_sync();
-            front_fill2<T2>(W, a.hist2_i, a.hist2_q, c, act, live, b, nb, hC, hD, h2, R);
+            group_fill_rows2<T2>(smem, LW, a.hist2_i, a.hist2_q, c0, CPW, nlive, lane, hC, hD);
+            wave_sync();
+            window_new2(W, T2, act, b, nb, h2, R);
+            wave_sync();
+            group_store_rows2<T2>(smem, LW, a.hist2_i, a.hist2_q, c0, nlive, lane, nb * R);
             fir_block2<T2, RD, M, F>(W + 2 * b * R, as_taps2(a.taps2b), d2);
 #pragma unroll
             for (int r = 0; r < RD; ++r) o[r] = d2[r].x;
@@ -413,26 +441,32 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
         else if constexpr (!DECIM_FIRST)
         {
             vf4 hC[HQ2];
-            front_load_row<T2>(a.hist2_i, cl, b, nb, hC);
+            group_load_rows<T2>(a.hist2_i, c0, nlive, lane, hC);
                 v2f h2[R];
             float hs[R];
             fir_block2<T1, R, 1, F>(W + 2 * b * R, tA, h2);
-            // a = I + Q (USB) or I - Q (LSB) or I (IQ mono), audio_driver.c:2755-2790
-#pragma unroll
-            for (int r = 0; r < R; ++r) hs[r] = front_comb(comb, h2[r]);
+            front_comb_block<R>(comb, h2, hs);
             wave_sync();
-            front_fill<T2>(W, a.hist2_i, c, act, live, b, nb, hC, hs, R);
+            group_fill_rows<T2>(smem, LW, a.hist2_i, c0, CPW, nlive, lane, hC);
+            wave_sync();
+            window_new(W, T2, act, b, nb, hs, R);
+            wave_sync();
+            group_store_rows<T2>(smem, LW, a.hist2_i, c0, nlive, lane, nb * R);
             fir_block<T2, RD, M, 4, F>(W + b * R, as_taps(P->dec), o);
         }
         else
         {
             vf4 hC[HQ2], hD[HQ2];
-            front_load_row<T2>(a.hist2_i, cl, b, nb, hC);
-            front_load_row<T2>(a.hist2_q, cl, b, nb, hD);
-                v2f d2[RD], h2[RD];
+            group_load_rows<T2>(a.hist2_i, c0, nlive, lane, hC);
+            group_load_rows<T2>(a.hist2_q, c0, nlive, lane, hD);
+            v2f d2[RD], h2[RD];
             fir_block2<T1, RD, M, F>(W + 2 * b * R, tA, d2);
             wave_sync();
-            front_fill2<T2>(W, a.hist2_i, a.hist2_q, c, act, live, b, nb, hC, hD, d2, RD);
+            group_fill_rows2<T2>(smem, LW, a.hist2_i, a.hist2_q, c0, CPW, nlive, lane, hC, hD);
+            wave_sync();
+            window_new2(W, T2, act, b, nb, d2, RD);
+            wave_sync();
+            group_store_rows2<T2>(smem, LW, a.hist2_i, a.hist2_q, c0, nlive, lane, nb * RD);
             fir_block2<T2, RD, 1, F>(W + 2 * b * RD, as_taps2(a.taps2b), h2);
             if constexpr (ST)
             {
@@ -452,8 +486,7 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
             }
             else
             {
-#pragma unroll
-                for (int r = 0; r < RD; ++r) o[r] = front_comb(comb, h2[r]);
+                front_comb_block<RD>(comb, h2, o);
             }
         }
         if (live)
@@ -1266,15 +1299,31 @@ struct DemodStage
 
 // ---- pipelined roles (rx_back): stage s of the wave pipeline works on call it - s in
 //      iteration it; hand-offs through double-buffered LDS, one barrier per iteration ----
+#ifdef UHSDR_TRACE
+// timing build (tools/trace_back.py): per workgroup, role and iteration the shader clock when the
+// role starts its call, ends it, and leaves the barrier
+__device__ unsigned long long g_trace[64][8][40][3];
+#define TRACE_MARK(k) do { if (l.lane == 0 && blockIdx.x < 64 && it < 40) \
+    g_trace[blockIdx.x][threadIdx.x / BACK_CH][it][k] = __builtin_readcyclecounter(); } while (0)
+extern "C" int uhsdr_trace_read(void* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), sizeof(g_trace)) == hipSuccess ? 0 : -1;
+}
+#else
+#define TRACE_MARK(k) do { } while (0)
+#endif
 #define BACK_ROLE_LOOP(ST)                                                                     \
     for (int it = 0; it < l.calls + back_roles(DM) - 1; ++it)                                  \
     {                                                                                          \
         const int call = it - (ST);                                                            \
+        TRACE_MARK(0);                                                                         \
         if (call >= 0 && call < l.calls)                                                       \
         {
 #define BACK_ROLE_END                                                                          \
         }                                                                                      \
-        __syncthreads();                                                                       \
+        TRACE_MARK(1);                                                                         \
+        lds_barrier();                                                                         \
+        TRACE_MARK(2);                                                                         \
     }
 
 template <int L, int DM>
@@ -1335,9 +1384,12 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
     BACK_ROLE_LOOP(DM ? 2 : 1)
         const float* pi = lds.pre + (call & 1) * NDC * BACK_CH + l.lane;
         float* ao = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
+        float x[NDC];
+#pragma unroll
+        for (int m = 0; m < NDC; ++m) x[m] = pi[m * BACK_CH];
         s.begin(a, l, call);
 #pragma unroll
-        for (int m = 0; m < NDC; ++m) ao[m * BACK_CH] = s.step(m, pi[m * BACK_CH], l, A);
+        for (int m = 0; m < NDC; ++m) ao[m * BACK_CH] = s.step(m, x[m], l, A);
         s.end(l);
     BACK_ROLE_END
     s.store(a, l);
@@ -1353,11 +1405,14 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
     BACK_ROLE_LOOP(DM ? 3 : 2)
         const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
         float* mo = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
+        float x[NDC];
+#pragma unroll
+        for (int m = 0; m < NDC; ++m) x[m] = ai[m * BACK_CH];
 #pragma unroll
         for (int m = 0; m < NDC; ++m)
         {
             float u[L];
-            s.step(ai[m * BACK_CH], u);
+            s.step(x[m], u);
 #pragma unroll
             for (int j = 0; j < L; ++j) mo[(m * L + j) * BACK_CH] = u[j];
         }
@@ -1377,8 +1432,14 @@ __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
     BACK_ROLE_LOOP(DM ? 4 : 3)
         const float* mi = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
         float* mo = lds.aa + (call & 1) * BLK * BACK_CH + l.lane;
-#pragma unroll 4
-        for (int n = 0; n < BLK; ++n) mo[n * BACK_CH] = s.step(mi[n * BACK_CH]);
+        // the call's inputs in one batch of LDS reads, then the recursion: a single wave issues
+        // one VALU instruction per ~4 cycles, so a read waited on per sample would add its whole
+        // latency to every sample of the step
+        float x[BLK];
+#pragma unroll
+        for (int n = 0; n < BLK; ++n) x[n] = mi[n * BACK_CH];
+#pragma unroll
+        for (int n = 0; n < BLK; ++n) mo[n * BACK_CH] = s.step(x[n]);
     BACK_ROLE_END
     s.store(l, a.s.aa);
 }
@@ -1391,18 +1452,25 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
     s.load(a, l);
     BACK_ROLE_LOOP(DM ? 5 : 4)
         const float* mi = lds.aa + (call & 1) * BLK * BACK_CH + l.lane;
-#pragma unroll 2
+        float y[BLK];
+#pragma unroll
+        for (int n = 0; n < BLK; ++n) y[n] = mi[n * BACK_CH];      // one batch of LDS reads
+#pragma unroll
+        for (int n = 0; n < BLK; ++n) y[n] = s.step(y[n]);
+        if (a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK)   // key beep in this call
+        {
+#pragma unroll
+            for (int n = 0; n < BLK; ++n)
+            {
+                const int fr = call * BLK + n;
+                if (fr >= a.beep_n0 && fr < a.beep_n1) y[n] += beep_tone(a, fr);
+            }
+        }
+#pragma unroll
         for (int n0 = 0; n0 < BLK; n0 += 4)
         {
-            float y[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-            {
-                y[j] = s.step(mi[(n0 + j) * BACK_CH]);
-                const int fr = call * BLK + n0 + j;
-                if (fr >= a.beep_n0 && fr < a.beep_n1) y[j] += beep_tone(a, fr);
-            }
-            back_store4(a, l, call, n0, y);
+            const float y4[4] = { y[n0], y[n0 + 1], y[n0 + 2], y[n0 + 3] };
+            back_store4(a, l, call, n0, y4);
         }
     BACK_ROLE_END
     s.store(a, l);
@@ -1954,7 +2022,7 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                 }
                 act[(it & 1) * BACK_CH + lane] = squelched ? 0.0f : 1.0f;
             }
-            __syncthreads();
+            lds_barrier();
         }
         if (live)
         {
@@ -2017,7 +2085,7 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                     }
                 }
             }
-            __syncthreads();
+            lds_barrier();
         }
         if (live)
         {
@@ -2599,7 +2667,8 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         fa.taps2a = h->d_taps2;
         fa.taps2b = h->d_taps2 + 2 * TAPS2_MAX;
         fa.comb = front_comb_of(h->plan);
-        hipLaunchKernelGGL(h->precision == UHSDR_PRECISION_FMA ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw), dim3(FRONT_WAVE), lds, h->stream, fa);
+        hipLaunchKernelGGL(h->precision == UHSDR_PRECISION_FMA ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw),
+                           dim3(FRONT_WAVE), lds, h->stream, fa);
         HIPCHK(hipGetLastError());
         h->front_launches += 1;
     }

@@ -15,7 +15,7 @@
  * beside them.
  *
  * Errors: CMSIS processing functions return void.  A device failure (or an fftLen other than
- * 256 / 512 / 1024 in arm_cfft_f32) leaves pDst untouched and is reported by
+ * 16, 32, ..., 4096 in arm_cfft_f32) leaves pDst untouched and is reported by
  * uhsdr_cmsis_last_status() / uhsdr_last_error() (libuhsdr_amd.so).
  */
 #ifndef UHSDR_CMSIS_H
@@ -108,8 +108,11 @@ void arm_biquad_cascade_df1_init_f32(arm_biquad_casd_df1_inst_f32* S, uint8_t nu
 void arm_biquad_cascade_df1_f32(const arm_biquad_casd_df1_inst_f32* S, float32_t* pSrc, float32_t* pDst,
                                 uint32_t blockSize);
 
-/* arm_math.h:2141-2147 -- replaces arm_cfft_f32 (TransformFunctions/arm_cfft_f32.c:574-628);
-   fftLen 256, 512, 1024 (the lengths the firmware's spectrum display uses) */
+/* arm_math.h:2141-2147 -- replaces arm_cfft_f32 (TransformFunctions/arm_cfft_f32.c:574-628) for
+   every length CMSIS dispatches, 16 ... 4096.  256 / 512 / 1024 (the firmware's spectrum display)
+   run the one-wave transform of the spectrum kernels on the library's own copies of the CMSIS
+   tables; the other lengths run on the instance's pTwiddle / pBitRevTable (arm_const_structs.c),
+   which must be set as CMSIS sets them. */
 typedef struct
 {
     uint16_t fftLen;

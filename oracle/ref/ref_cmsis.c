@@ -186,11 +186,24 @@ static void cfft_wrapper(int L, float* p1, int ifft, int bitrev)
     }
 }
 
+const arm_cfft_instance_f32* ref_cfft_instance(int L);
+
 static void cfft_case(const char* name, int L, int ifft, int bitrev)
 {
-    char p[128];
-    snprintf(p, sizeof p, "{\"fftLen\": %d, \"ifftFlag\": %d, \"bitReverseFlag\": %d}", L, ifft, bitrev);
+    char p[160];
+    const arm_cfft_instance_f32* S = ref_cfft_instance(L);
+    snprintf(p, sizeof p, "{\"fftLen\": %d, \"ifftFlag\": %d, \"bitReverseFlag\": %d, \"bitRevLength\": %d}", L, ifft,
+             bitrev, S->bitRevLength);
     case_begin(name, p);
+    {
+        /* the instance's own tables (arm_const_structs.c / arm_common_tables.c): twiddleCoef_L
+           (L complex values; the radix-8 stages index up to 7(L/8-1)) and the bit-reversal byte-offset table, stored as floats (exact) */
+        float* tab = malloc(sizeof(float) * (S->bitRevLength + 1));
+        for (int i = 0; i < S->bitRevLength; ++i) tab[i] = (float)S->pBitRevTable[i];
+        put(name, "twiddle", S->pTwiddle, 2 * (size_t)L);
+        put(name, "bitrev", tab, S->bitRevLength);
+        free(tab);
+    }
     float* x = frand(2 * (size_t)L, 1.0f);
     float* y = malloc(sizeof(float) * 2 * L);
     memcpy(y, x, sizeof(float) * 2 * L);
@@ -242,6 +255,18 @@ int ref_cmsis_dump(const char* dir)
     cfft_case("cfft_1024_nobitrev", 1024, 0, 0);
     cfft_case("icfft_256", 256, 1, 1);
     cfft_case("icfft_1024", 1024, 1, 1);
+    cfft_case("cfft_16", 16, 0, 1);
+    cfft_case("cfft_32", 32, 0, 1);
+    cfft_case("cfft_64", 64, 0, 1);
+    cfft_case("cfft_128", 128, 0, 1);
+    cfft_case("cfft_2048", 2048, 0, 1);
+    cfft_case("cfft_4096", 4096, 0, 1);
+    cfft_case("icfft_16", 16, 1, 1);
+    cfft_case("icfft_128", 128, 1, 1);
+    cfft_case("icfft_2048", 2048, 1, 1);
+    cfft_case("icfft_4096", 4096, 1, 1);
+    cfft_case("cfft_64_nobitrev", 64, 0, 0);
+    cfft_case("cfft_2048_nobitrev", 2048, 0, 0);
     mag_case("mag_1000", 1000);
     printf("}\n");
     return 0;

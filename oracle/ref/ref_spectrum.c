@@ -39,14 +39,21 @@ void arm_radix8_butterfly_f32(float32_t* pSrc, uint16_t fftLen, const float32_t*
 
 static const arm_cfft_instance_f32* instance(int L)
 {
-    switch (L)
+    switch (L)          /* CMSIS arm_const_structs.c: every length arm_cfft_f32 dispatches */
     {
+    case 16: return &arm_cfft_sR_f32_len16;
+    case 32: return &arm_cfft_sR_f32_len32;
+    case 64: return &arm_cfft_sR_f32_len64;
+    case 128: return &arm_cfft_sR_f32_len128;
     case 256: return &arm_cfft_sR_f32_len256;
     case 512: return &arm_cfft_sR_f32_len512;
     case 1024: return &arm_cfft_sR_f32_len1024;
+    case 2048: return &arm_cfft_sR_f32_len2048;
+    case 4096: return &arm_cfft_sR_f32_len4096;
     default: return NULL;
     }
 }
+const arm_cfft_instance_f32* ref_cfft_instance(int L) { return instance(L); }
 
 /* ring length in floats: the firmware's FFT_RingBuffer holds FFT_IQ_BUFF_LEN = 1024 floats
    (audio_driver.h:62-67 with USE_FFT_1024), so a 1024-point frame is assembled from two
@@ -88,16 +95,15 @@ static void bitreverse(float* p, uint16_t len, const uint16_t* tab)
         }
 }
 
-/* the length switch and optional bit reversal of arm_cfft_f32 (arm_cfft_f32.c:594-614) for L
-   in {256, 512, 1024} */
+/* the length switch and optional bit reversal of arm_cfft_f32 (arm_cfft_f32.c:594-614) */
 void ref_cfft_stages(int L, float* p, int bitrev)
 {
     const arm_cfft_instance_f32* S = instance(L);
     switch (L)
     {
-    case 1024: arm_cfft_radix8by2_f32((arm_cfft_instance_f32*)S, p); break;
-    case 256: arm_cfft_radix8by4_f32((arm_cfft_instance_f32*)S, p); break;
-    case 512: arm_radix8_butterfly_f32(p, L, (float32_t*)S->pTwiddle, 1); break;
+    case 16: case 128: case 1024: arm_cfft_radix8by2_f32((arm_cfft_instance_f32*)S, p); break;
+    case 32: case 256: case 2048: arm_cfft_radix8by4_f32((arm_cfft_instance_f32*)S, p); break;
+    case 64: case 512: case 4096: arm_radix8_butterfly_f32(p, L, (float32_t*)S->pTwiddle, 1); break;
     }
     if (bitrev) bitreverse(p, S->bitRevLength, S->pBitRevTable);
 }

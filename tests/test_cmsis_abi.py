@@ -60,3 +60,29 @@ def test_init_functions_follow_cmsis_rules():
     assert lib.arm_fir_interpolate_init_f32(C.byref(I), 3, 8, cmsis._fp(c), cmsis._fp(st2), 4) == -2
     assert lib.arm_fir_interpolate_init_f32(C.byref(I), 4, 8, cmsis._fp(c), cmsis._fp(st2), 4) == 0
     assert I.phaseLength == 2 and not st2[:5].any()
+
+
+def test_cfft_vectors_cover_every_cmsis_length():
+    """tests/golden/cmsis_vectors.npz holds arm_cfft_f32 sequences of the reference build for every
+    length arm_cfft_f32.c:594-611 dispatches, with the instance tables; each output is the DFT
+    of its input (float64 check of the fixture itself, tolerance of binary32 rounding)."""
+    import json
+    import os
+    import numpy as np
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cmsis_vectors.npz"))
+    man = json.loads(str(d["manifest"]))
+    lens = set()
+    for case, m in man.items():
+        if not case.startswith(("cfft_", "icfft_")):
+            continue
+        p = m["params"]
+        L = p["fftLen"]
+        lens.add(L)
+        assert d[f"{case}.twiddle"].size == 2 * L and d[f"{case}.bitrev"].size == p["bitRevLength"]
+        if not p["bitReverseFlag"]:
+            continue
+        x = d[f"{case}.src"].astype(np.float64).view(np.complex128)
+        y = d[f"{case}.dst"].astype(np.float64).view(np.complex128)
+        ref = np.fft.ifft(x) if p["ifftFlag"] else np.fft.fft(x)
+        assert np.abs(y - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max()), case
+    assert lens == {16, 32, 64, 128, 256, 512, 1024, 2048, 4096}

@@ -182,13 +182,21 @@ class BiquadDf1(_Inst):
         return self._run(self.lib.arm_biquad_cascade_df1_f32, x, len(x))
 
 
-def cfft(x: np.ndarray, ifft: bool = False, bitrev: bool = True) -> np.ndarray:
-    """arm_cfft_f32 on a copy of x (interleaved complex float32, 2L values); the instance carries
-    only fftLen (the shim uses its own copies of the CMSIS tables)."""
+def cfft(x: np.ndarray, ifft: bool = False, bitrev: bool = True, twiddle=None, bitrev_table=None) -> np.ndarray:
+    """arm_cfft_f32 on a copy of x (interleaved complex float32, 2L values).  The instance carries
+    fftLen and, when given, the CMSIS tables of arm_cfft_sR_f32_lenL (twiddleCoef_L as float32,
+    the bit-reversal byte offsets as uint16): lengths other than 256 / 512 / 1024 run on them."""
     lib = load()
     p = np.array(x, np.float32, copy=True)
     S = arm_cfft_instance_f32()
     S.fftLen = len(p) // 2
+    if twiddle is not None:
+        tw = np.ascontiguousarray(twiddle, np.float32)
+        S.pTwiddle = _fp(tw)
+    if bitrev_table is not None:
+        rv = np.ascontiguousarray(bitrev_table, np.uint16)
+        S.pBitRevTable = rv.ctypes.data_as(C.POINTER(C.c_uint16))
+        S.bitRevLength = len(rv)
     lib.arm_cfft_f32(C.byref(S), _fp(p), 1 if ifft else 0, 1 if bitrev else 0)
     _check(lib)
     return p

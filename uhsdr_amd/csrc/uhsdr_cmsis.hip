@@ -154,6 +154,219 @@ __global__ void __launch_bounds__(64) shim_cfft(float* __restrict__ p1, const uh
 }
 
 // ---- per-thread device context ----
+
+// ---- arm_cfft_f32 for the lengths the spectrum kernels do not specialise (16, 32, 64, 128, 2048,
+//      4096), on the instance's own tables: one workgroup, the frame in LDS, one thread per
+//      butterfly of a stage (the butterflies of a stage touch disjoint points), the binary32
+//      sequence of CMSIS's arm_cfft_radix8by2_f32 / _by4_f32 (arm_cfft_f32.c:207-557) and
+//      arm_radix8_butterfly_f32 (arm_cfft_radix8_f32.c:130-282) per butterfly ----
+__device__ __forceinline__ void gcf_radix8(float* x, int base, int stride, const float* __restrict__ tw, int tstep)
+{
+    const float C81 = 0.70710678118f;
+    float re[8], im[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) { re[k] = x[2 * (base + k * stride)]; im[k] = x[2 * (base + k * stride) + 1]; }
+    float sr[4], dr[4], si[4], di[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+    {
+        sr[k] = re[k] + re[k + 4]; dr[k] = re[k] - re[k + 4];
+        si[k] = im[k] + im[k + 4]; di[k] = im[k] - im[k + 4];
+    }
+    float Xr[8], Xi[8];
+    const float a = sr[0] - sr[2], b = sr[0] + sr[2], cc = sr[1] - sr[3], d = sr[1] + sr[3];
+    const float ai = si[0] - si[2], bi = si[0] + si[2], ci = si[1] - si[3], dd = si[1] + si[3];
+    Xr[0] = b + d;   Xi[0] = bi + dd;
+    Xr[4] = b - d;   Xi[4] = bi - dd;
+    Xr[2] = a + ci;  Xi[2] = ai - cc;
+    Xr[6] = a - ci;  Xi[6] = ai + cc;
+    const float u = (dr[1] - dr[3]) * C81, v = (dr[1] + dr[3]) * C81;
+    const float ui = (di[1] - di[3]) * C81, vi = (di[1] + di[3]) * C81;
+    const float e0 = dr[0] - u, e1 = dr[0] + u, f0 = dr[2] - v, f1 = dr[2] + v;
+    const float g0 = di[0] - ui, g1 = di[0] + ui, h0 = di[2] - vi, h1 = di[2] + vi;
+    Xr[1] = e1 + h1; Xi[1] = g1 - f1;
+    Xr[7] = e1 - h1; Xi[7] = g1 + f1;
+    Xr[5] = e0 + h0; Xi[5] = g0 - f0;
+    Xr[3] = e0 - h0; Xi[3] = g0 + f0;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+    {
+        float yr = Xr[k], yi = Xi[k];
+        if (tstep && k)
+        {
+            const float c = tw[2 * k * tstep], s = tw[2 * k * tstep + 1];
+            const float p1 = c * Xr[k], p2 = s * Xi[k], p3 = c * Xi[k], p4 = s * Xr[k];
+            yr = p1 + p2;
+            yi = p3 - p4;
+        }
+        x[2 * (base + k * stride)] = yr;
+        x[2 * (base + k * stride) + 1] = yi;
+    }
+}
+
+// radix-8 stages over `parts` sub-arrays of n points each, twiddle modifier tm
+__device__ __forceinline__ void gcf_stages(float* x, int parts, int n, const float* __restrict__ tw, int tm)
+{
+    for (int span = n; span >= 8; span >>= 3, tm <<= 3)
+    {
+        const int stride = span >> 3, nbf = n / 8;
+        for (int t = threadIdx.x; t < parts * nbf; t += blockDim.x)
+        {
+            const int part = t / nbf, r = t % nbf, j = r % stride, g = j + (r / stride) * span;
+            gcf_radix8(x + 2 * part * n, g, stride, tw, j * tm);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(SHIM_THREADS) shim_cfft_generic(float* __restrict__ p1, const float* __restrict__ tw,
+                                                                  const uint16_t* __restrict__ perm, int L, int ifft)
+{
+    extern __shared__ float x[];                      // 2L floats
+    for (int i = threadIdx.x; i < L; i += blockDim.x)
+    {
+        const float2 v = ((const float2*)p1)[i];
+        x[2 * i] = v.x;
+        x[2 * i + 1] = ifft ? -v.y : v.y;             // conjugate input (arm_cfft_f32.c:583-592)
+    }
+    __syncthreads();
+    const bool by2 = L == 16 || L == 128 || L == 1024 || L == 8192;
+    const bool by4 = L == 32 || L == 256 || L == 2048;
+    if (by2)
+    {
+        // arm_cfft_radix8by2_f32 (arm_cfft_f32.c:207-317)
+        const int H = L / 2, Q = L / 4;
+        for (int a = threadIdx.x; a < Q; a += blockDim.x)
+        {
+            float* q1 = x + 2 * a;
+            float* q3 = x + 2 * (a + Q);
+            float* q2 = x + 2 * (a + H);
+            float* q4 = x + 2 * (a + H + Q);
+            const float t2r = q1[0] - q2[0], t2i = q1[1] - q2[1];
+            const float t4r = q4[0] - q3[0], t4i = q4[1] - q3[1];
+            q1[0] = q1[0] + q2[0];
+            q1[1] = q1[1] + q2[1];
+            q3[0] = q3[0] + q4[0];
+            q3[1] = q3[1] + q4[1];
+            const float c = tw[2 * a], s = tw[2 * a + 1];
+            {
+                const float m0 = t2r * c, m1 = t2i * s, m2 = t2i * c, m3 = t2r * s;
+                q2[0] = m0 + m1;
+                q2[1] = m2 - m3;
+            }
+            {
+                const float m0 = t4r * s, m1 = t4i * c, m2 = t4i * s, m3 = t4r * c;
+                q4[0] = m0 - m1;
+                q4[1] = m2 + m3;
+            }
+        }
+        __syncthreads();
+        gcf_stages(x, 2, H, tw, 2);
+    }
+    else if (by4)
+    {
+        // arm_cfft_radix8by4_f32 (arm_cfft_f32.c:319-557): top rows t = 0 .. Q/2, bottom rows
+        // Q - t for t = 1 .. Q/2 - 1 with the mirrored twiddles of t
+        const int Q = L / 4;
+        float* c1 = x;
+        float* c2 = x + 2 * Q;
+        float* c3 = x + 4 * Q;
+        float* c4 = x + 6 * Q;
+        for (int w = threadIdx.x; w < Q; w += blockDim.x)
+        {
+            if (w <= Q / 2)
+            {
+                const int t = w;
+                float* q1 = c1 + 2 * t;
+                float* q2 = c2 + 2 * t;
+                float* q3 = c3 + 2 * t;
+                float* q4 = c4 + 2 * t;
+                const float s13r = q1[0] + q3[0], d13r = q1[0] - q3[0];
+                const float s13i = q1[1] + q3[1], d13i = q1[1] - q3[1];
+                const float t2r = d13r + q2[1] - q4[1], t2i = d13i - q2[0] + q4[0];
+                const float t3r = s13r - q2[0] - q4[0], t3i = s13i - q2[1] - q4[1];
+                const float t4r = d13r - q2[1] + q4[1], t4i = d13i + q2[0] - q4[0];
+                q1[0] = s13r + q2[0] + q4[0];
+                q1[1] = s13i + q2[1] + q4[1];
+                if (t == 0)
+                {
+                    q2[0] = t2r; q2[1] = t2i;
+                    q3[0] = t3r; q3[1] = t3i;
+                    q4[0] = t4r; q4[1] = t4i;
+                }
+                else
+                {
+                    const float* tt[3] = { tw + 2 * t, tw + 4 * t, tw + 6 * t };
+                    float* qq[3] = { q2, q3, q4 };
+                    const float xr[3] = { t2r, t3r, t4r }, xi[3] = { t2i, t3i, t4i };
+#pragma unroll
+                    for (int k = 0; k < 3; ++k)
+                    {
+                        const float c = tt[k][0], s = tt[k][1];
+                        const float m0 = xr[k] * c, m1 = xi[k] * s, m2 = xi[k] * c, m3 = xr[k] * s;
+                        qq[k][0] = m0 + m1;
+                        qq[k][1] = m2 - m3;
+                    }
+                }
+            }
+            else
+            {
+                const int t = Q - w, b = w;            // w = Q - t for t = 1 .. Q/2 - 1
+                float* q1 = c1 + 2 * b;
+                float* q2 = c2 + 2 * b;
+                float* q3 = c3 + 2 * b;
+                float* q4 = c4 + 2 * b;
+                const float s13r = q1[0] + q3[0], d13r = q1[0] - q3[0];
+                const float s13i = q1[1] + q3[1], d13i = q1[1] - q3[1];
+                const float u2r = q2[1] - q4[1] + d13r;
+                const float u2i = q1[1] - q3[1] - q2[0] + q4[0];
+                const float u3r = s13r - q2[0] - q4[0];
+                const float u3i = s13i - q2[1] - q4[1];
+                const float u4r = q2[1] - q4[1] - d13r;
+                const float u4i = q4[0] - q2[0] - d13i;
+                q1[1] = s13i + q2[1] + q4[1];
+                q1[0] = s13r + q2[0] + q4[0];
+                {
+                    const float c = tw[2 * t], s = tw[2 * t + 1];
+                    const float m0 = u2i * s, m1 = u2r * c, m2 = u2r * s, m3 = u2i * c;
+                    q2[1] = m0 - m1;
+                    q2[0] = m2 + m3;
+                }
+                {
+                    const float c = tw[4 * t], s = tw[4 * t + 1];
+                    const float m0 = -u3i * c, m1 = u3r * s, m2 = u3r * c, m3 = u3i * s;
+                    q3[1] = m0 - m1;
+                    q3[0] = m3 - m2;
+                }
+                {
+                    const float c = tw[6 * t], s = tw[6 * t + 1];
+                    const float m0 = u4i * s, m1 = u4r * c, m2 = u4r * s, m3 = u4i * c;
+                    q4[1] = m0 - m1;
+                    q4[0] = m2 + m3;
+                }
+            }
+        }
+        __syncthreads();
+        gcf_stages(x, 4, Q, tw, 4);
+    }
+    else
+        gcf_stages(x, 1, L, tw, 1);                   // arm_radix8_butterfly_f32(p1, L, pTwiddle, 1)
+    // bit reversal as the permutation the reference's swap sequence composes (host-built, perm null
+    // without bitReverseFlag): point i of the output is point perm[i] of the transform
+    const float invL = 1.0f / (float)L;
+    for (int i = threadIdx.x; i < L; i += blockDim.x)
+    {
+        const int src = perm ? perm[i] : i;
+        float re = x[2 * src], im = x[2 * src + 1];
+        if (ifft)
+        {
+            re = re * invL;                           // arm_cfft_f32.c:617-628
+            im = -im * invL;
+        }
+        ((float2*)p1)[i] = make_float2(re, im);
+    }
+}
+
 struct ShimCtx
 {
     hipStream_t stream = nullptr;
@@ -283,6 +496,47 @@ int cfft_run(float* p1, int ifft, int bitrev)
     hipError_t e = hipMemcpyAsync(d, p1, sizeof(float) * 2 * L, hipMemcpyHostToDevice, c.stream);
     if (e != hipSuccess) return fail(UHSDR_DEVICE_ERROR, "arm_cfft_f32 upload", e);
     hipLaunchKernelGGL(shim_cfft<L>, dim3(1), dim3(64), 0, c.stream, d, c.plans[idx], ifft, bitrev);
+    if ((e = hipGetLastError()) != hipSuccess || !finish(p1, d, 2 * L)) return fail(UHSDR_DEVICE_ERROR, "arm_cfft_f32", e);
+    return 0;
+}
+
+// the other CMSIS lengths: the instance's twiddle (twiddleCoef_L: L complex;
+// the first radix-8 stage reads up to index 7 (L/8 - 1)) and bit-reversal tables go up with
+// the frame (CMSIS keeps them in the caller's arm_cfft_sR_f32_lenL instance)
+int cfft_run_generic(const arm_cfft_instance_f32* S, float* p1, int ifft, int bitrev)
+{
+    const int L = S->fftLen;
+    if (!S->pTwiddle || (bitrev && !S->pBitRevTable))
+        return fail(UHSDR_ARGUMENT_ERROR, "arm_cfft_f32: instance without twiddle / bit-reversal tables", hipSuccess);
+    const size_t ntw = 2 * (size_t)L, nperm = bitrev ? ((size_t)L + 1) / 2 : 0;   // uint16 pairs per float
+    float* d = scratch(2 * (size_t)L + ntw + nperm);
+    if (!d) return fail(UHSDR_DEVICE_ERROR, "arm_cfft_f32 scratch", hipGetLastError());
+    float* dtw = d + 2 * L;
+    uint16_t* dperm = bitrev ? (uint16_t*)(dtw + ntw) : nullptr;
+    hipError_t e = hipMemcpyAsync(d, p1, sizeof(float) * 2 * L, hipMemcpyHostToDevice, t_ctx.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dtw, S->pTwiddle, sizeof(float) * ntw, hipMemcpyHostToDevice, t_ctx.stream);
+    if (e == hipSuccess && bitrev)
+    {
+        // arm_bitreversal_32 (arm_bitreversal2.S:136-180): (len + 1) >> 2 iterations of two swaps of
+        // the complex values at the table's byte offsets, in order -- cycles of the permutation
+        // share points between swaps, so the sequence is composed here into one gather
+        uint16_t* perm = (uint16_t*)malloc(sizeof(uint16_t) * L);
+        if (!perm) return fail(UHSDR_DEVICE_ERROR, "arm_cfft_f32 table", hipSuccess);
+        for (int i = 0; i < L; ++i) perm[i] = (uint16_t)i;
+        const int it = (S->bitRevLength + 1) >> 2;
+        for (int k = 0; k < 2 * it && 2 * k + 1 < S->bitRevLength; ++k)
+        {
+            const int ia = S->pBitRevTable[2 * k] >> 3, ib = S->pBitRevTable[2 * k + 1] >> 3;
+            if (ia >= L || ib >= L) { free(perm); return fail(UHSDR_ARGUMENT_ERROR, "arm_cfft_f32: bit-reversal table", hipSuccess); }
+            const uint16_t t = perm[ia]; perm[ia] = perm[ib]; perm[ib] = t;
+        }
+        e = hipMemcpyAsync(dperm, perm, sizeof(uint16_t) * L, hipMemcpyHostToDevice, t_ctx.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(t_ctx.stream);
+        free(perm);
+    }
+    if (e != hipSuccess) return fail(UHSDR_DEVICE_ERROR, "arm_cfft_f32 upload", e);
+    hipLaunchKernelGGL(shim_cfft_generic, dim3(1), dim3(SHIM_THREADS), sizeof(float) * 2 * L, t_ctx.stream, d, dtw, dperm,
+                       L, ifft);
     if ((e = hipGetLastError()) != hipSuccess || !finish(p1, d, 2 * L)) return fail(UHSDR_DEVICE_ERROR, "arm_cfft_f32", e);
     return 0;
 }
@@ -432,7 +686,8 @@ void arm_cfft_f32(const arm_cfft_instance_f32* S, float32_t* p1, uint8_t ifftFla
     case 256: cfft_run<256>(p1, ifft, bitrev); break;
     case 512: cfft_run<512>(p1, ifft, bitrev); break;
     case 1024: cfft_run<1024>(p1, ifft, bitrev); break;
-    default: fail(UHSDR_UNSUPPORTED, "arm_cfft_f32: fftLen not 256 / 512 / 1024", hipSuccess); break;
+    case 16: case 32: case 64: case 128: case 2048: case 4096: cfft_run_generic(S, p1, ifft, bitrev); break;
+    default: fail(UHSDR_UNSUPPORTED, "arm_cfft_f32: fftLen not 16 / 32 / ... / 4096", hipSuccess); break;
     }
 }
 

@@ -236,9 +236,12 @@ def main():
     ap.add_argument("--no-northstar", action="store_true", help="skip the 1M-channel north-star leg")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL gather leg (N > 1)")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--pipelined", action="store_true",
-                    help="overlap call k+1's rx_front with call k's rx_back (uhsdr_rx_set_pipelined); "
-                         "measured no faster on MI355X, so off by default")
+    ap.add_argument("--serial", action="store_true",
+                    help="run rx_front and rx_back of a call back to back on one stream instead of the "
+                         "default pipelined mode (uhsdr_rx_set_pipelined: call k+1's rx_front overlaps "
+                         "call k's rx_back); the 1M-channel north-star leg always runs serial (both "
+                         "kernels fill the chip there)")
+    ap.add_argument("--pipelined", action="store_true", help="(default; kept for old command lines)")
     ap.add_argument("--precision", default="exact", choices=["exact", "fma"],
                     help="FIR MACs: exact (bit-identical to the reference) or fma (1e-5 normwise)")
     ap.add_argument("--pool", type=int, default=8, help="distinct input blocks cycled through")
@@ -262,8 +265,9 @@ def main():
     wl = WORKLOADS[args.workload]
     C = args.channels or wl["channels"]
     N = args.frames or wl["frames"]
+    pipelined = not args.serial and args.workload != "northstar"
     elapsed, ktimes, plan, ok, _ = timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, args.steps,
-                                             args.warmup, max(1, args.pool), args.dst, args.pipelined, prec)
+                                             args.warmup, max(1, args.pool), args.dst, pipelined, prec)
 
     gather = None
     if world > 1 and not args.no_gather:
@@ -277,7 +281,7 @@ def main():
     def north_star_leg(precision):
         nw = WORKLOADS["northstar"]
         n_el, n_kt, n_plan, n_ok, _ = timed_run(U, synth, shard, torch, dist, dev, 1, 0, nw["channels"], nw["frames"],
-                                                NS_STEPS, 10, 3, False, args.pipelined, precision)
+                                                NS_STEPS, 10, 3, False, False, precision)
         n_ab = algorithmic_bytes(n_plan, nw["channels"], nw["frames"], False)
         n_roof, n_kms = roofline_of(n_ab, n_kt, pmc_traffic("northstar" if precision == U.PRECISION_EXACT
                                                             else "northstar_fma"))
@@ -322,7 +326,7 @@ def main():
                    "channels_per_gpu": C, "frames_per_call": N, "filter_path": int(plan.filter_path),
                    "parallelism": f"channel-sharded x{world}, no data-path collective",
                    "outputs": "f32 audio" + (" + int32 codec frames" if args.dst else ""),
-                   "pipelined": args.pipelined, "precision": args.precision},
+                   "pipelined": pipelined, "precision": args.precision},
         "roofline": roofline,
         "chain": {"device_ms_per_step": round(chain_dev_ms, 5),
                   "kernel_ms": {k: round(v, 5) for k, v in kms.items()},

@@ -506,6 +506,61 @@ __device__ __forceinline__ float lattice_step(float x, float (&g)[S > 0 ? S : 1]
     return acc;
 }
 
+// The same sample on packed f32 (v_pk_mul_f32 / v_pk_add_f32): every product and sum is the
+// reference's binary32 operation on the same operands, two independent ones per instruction.
+// Stages are taken in pairs (i, i+1): both k*g products of a pair up front (old states), the
+// f chain as scalar subtracts, then {f_i k_i, f_i+1 k_i+1} + {g_i, g_i+1} -> {gn_i, gn_i+1} and
+// {gn_i v_i, gn_i+1 v_i+1} for the output sum, which is added in the reference's order.  The state
+// shifts by one stage per sample (g_i <- gn_i+1), so the pairing alternates with the sample's
+// parity PAR: pairs (0,1),(2,3)... on even samples, stage 0 alone then (1,2),(3,4)... on odd
+// ones -- each sample's pairs are then exactly the register pairs the previous sample produced,
+// and no moves are needed to form them.  Results are bit-identical for either parity.
+template <int S, int PAR>
+__device__ __forceinline__ float lattice_step_pk(float x, float (&g)[S > 0 ? S : 1], const float* k, const float* v)
+{
+    if constexpr (S < 3) return lattice_step<S>(x, g, k, v);
+    else
+    {
+        float gn[S], q[S];
+        float f = x;
+        int i = 0;
+        if (PAR)
+        {
+            f = f - (k[0] * g[0]);
+            gn[0] = (f * k[0]) + g[0];
+            q[0] = gn[0] * v[0];
+            i = 1;
+        }
+#pragma unroll
+        for (; i + 1 < S; i += 2)
+        {
+            const v2f gp = v2f{ g[i], g[i + 1] }, kp = v2f{ k[i], k[i + 1] };
+            const v2f kg = kp * gp;
+            const float f0 = f - kg.x;
+            const float f1 = f0 - kg.y;
+            const v2f gnp = (v2f{ f0, f1 } * kp) + gp;
+            const v2f qp = gnp * v2f{ v[i], v[i + 1] };
+            gn[i] = gnp.x; gn[i + 1] = gnp.y;
+            q[i] = qp.x; q[i + 1] = qp.y;
+            f = f1;
+        }
+        if (i < S)
+        {
+            f = f - (k[i] * g[i]);
+            gn[i] = (f * k[i]) + g[i];
+            q[i] = gn[i] * v[i];
+        }
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < S; ++j) acc += q[j];
+        acc += (f * v[S]);
+#pragma unroll
+        for (int j = 0; j + 1 < S; ++j) g[j] = gn[j + 1];
+        g[S - 1] = f;
+        return acc;
+    }
+}
+
 // arm_biquad_cascade_df1_f32 (.../arm_biquad_cascade_df1_f32.c:349-418), one stage
 __device__ __forceinline__ float biquad_step(float x, float& x1, float& x2, float& y1, float& y2, const float* c)
 {

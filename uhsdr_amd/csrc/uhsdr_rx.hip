@@ -28,6 +28,7 @@
 // (tests/test_gpu_parity.py).
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
@@ -620,6 +621,10 @@ __host__ __device__ constexpr int back_roles(int dm) { return dm == DM_FM ? 2 : 
 //   output   biquad_2 -> line-out scale -> f32 / int32 stores  (48 ksps)
 // Splitting the serial chain shortens the critical path per call, which is what bounds small
 // batches (one wave per SIMD).  Large batches use rx_back_fused (all stages in one wave).
+// the wave pipeline splits the AGC after its recursion when there is no demod role (whose
+// hand-off buffer then carries the volts) and no DC removal (AM / SAM, also behind rx_notch)
+__host__ __device__ constexpr bool back_agc_split(int dm) { return dm == 0; }
+
 struct BackLds
 {
     float* dem;   // [2][NDC][64]  demod -> pre
@@ -711,9 +716,11 @@ struct LatticeStage
         for (int i = 0; i < S; ++i) g[i] = st[i * l.C + l.cl];
     }
 
-    __device__ __forceinline__ float step(float x)
+    // par: the sample's position parity in an unrolled loop (a compile-time constant there), which
+    // only selects the register pairing of the packed form
+    __device__ __forceinline__ float step(float x, int par = 0)
     {
-        if constexpr (S > 0) return lattice_step<S>(x, g, k, v);
+        if constexpr (S > 0) return (par & 1) ? lattice_step_pk<S, 1>(x, g, k, v) : lattice_step_pk<S, 0>(x, g, k, v);
         return x;
     }
 
@@ -823,7 +830,25 @@ struct AgcStage
     // selects, and the ring store is unconditional (a lane past the last channel computes exactly
     // what channel C-1 computes from the clamped loads, so it stores the same value to the same
     // address), so a whole call of the fused back end is one basic block.
+    // the gain the reference applies after the state update (audio_agc.c:553-560): not part of
+    // the recursion, so the wave pipeline runs it in the next role
+    __device__ __forceinline__ static float gain(float volts, const uhsdr_agc_plan& A)
+    {
+        float vo = log10f_fast(A.inv_max_input * volts);
+        vo = (vo > 0.0f) ? 0.0f : vo;
+        return (A.out_target - A.slope_constant * vo) / volts;
+    }
+
     __device__ __forceinline__ void stepn(int m, float (&x)[NCH], const BackLane& l, const uhsdr_agc_plan& A)
+    {
+        float v;
+        stepn_t<true>(m, x, l, A, v);
+    }
+
+    // TAIL false (no DC removal): x <- the delayed sample, vout <- volts; the caller applies
+    // gain(vout) when agc_on
+    template <bool TAIL>
+    __device__ __forceinline__ void stepn_t(int m, float (&x)[NCH], const BackLane& l, const uhsdr_agc_plan& A, float& vout)
     {
         // ---- AudioAgc_RunAgcWdsp, audio_agc.c:349-595 ----
         if (!agc_on)
@@ -879,12 +904,20 @@ struct AgcStage
             const float nv = volts + rv * mu;
             volts = upd ? nv : volts;
             volts = (volts < A.min_volts) ? A.min_volts : volts;
-            float vo = log10f_fast(A.inv_max_input * volts);
-            vo = (vo > 0.0f) ? 0.0f : vo;
-            const float mult = (A.out_target - A.slope_constant * vo) / volts;
+            if (TAIL)
+            {
+                const float mult = gain(volts, A);
 #pragma unroll
-            for (int ch = 0; ch < NCH; ++ch) x[ch] = out_sample[ch] * mult;
+                for (int ch = 0; ch < NCH; ++ch) x[ch] = out_sample[ch] * mult;
+            }
+            else
+            {
+#pragma unroll
+                for (int ch = 0; ch < NCH; ++ch) x[ch] = out_sample[ch];
+                vout = volts;
+            }
         }
+        if (!TAIL) return;
         if (agc_on && dc_sel)
         {
             // the same as a select (no branch): bodies that must not split their basic block
@@ -1366,7 +1399,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
             in.begin(a, l, call, xin);
         float* po = lds.pre + (call & 1) * NDC * BACK_CH + l.lane;
 #pragma unroll
-        for (int m = 0; m < NDC; ++m) po[m * BACK_CH] = s.step(xin[m]);
+        for (int m = 0; m < NDC; ++m) po[m * BACK_CH] = s.step(xin[m], m);
     BACK_ROLE_END
     s.store(l, a.s.pre);
 }
@@ -1388,26 +1421,54 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
 #pragma unroll
         for (int m = 0; m < NDC; ++m) x[m] = pi[m * BACK_CH];
         s.begin(a, l, call);
+        if (back_agc_split(DM) && !A.remove_dc)
+        {
+            // volts to the audio role through the demod role's (unused) hand-off buffer
+            float* vo = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
 #pragma unroll
-        for (int m = 0; m < NDC; ++m) ao[m * BACK_CH] = s.step(m, x[m], l, A);
+            for (int m = 0; m < NDC; ++m)
+            {
+                float xv[1] = { x[m] }, v = 0.0f;
+                s.template stepn_t<false>(m, xv, l, A, v);
+                ao[m * BACK_CH] = xv[0];
+                vo[m * BACK_CH] = v;
+            }
+        }
+        else
+        {
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) ao[m * BACK_CH] = s.step(m, x[m], l, A);
+        }
         s.end(l);
     BACK_ROLE_END
     s.store(a, l);
 }
 
-template <int L, int PH, int DM>
+template <int L, int PH, int W, int DM>
 __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     AudioStage<L, PH, DM> s;
     s.load(a, l);
+    const uhsdr_agc_plan A = a.plan->agc;
+    const bool agc_on = A.mode != 5;
     BACK_ROLE_LOOP(DM ? 3 : 2)
         const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
         float* mo = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
         float x[NDC];
 #pragma unroll
         for (int m = 0; m < NDC; ++m) x[m] = ai[m * BACK_CH];
+        if (back_agc_split(DM) && agc_on && !A.remove_dc)
+        {
+            // the AGC role's gain step (AgcStage::gain) on its delayed samples
+            const float* vi = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
+            float v[NDC];
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) v[m] = vi[m * BACK_CH];
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) x[m] = x[m] * AgcStage<L, W, 1>::gain(v[m], A);
+        }
 #pragma unroll
         for (int m = 0; m < NDC; ++m)
         {
@@ -1439,7 +1500,7 @@ __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
 #pragma unroll
         for (int n = 0; n < BLK; ++n) x[n] = mi[n * BACK_CH];
 #pragma unroll
-        for (int n = 0; n < BLK; ++n) mo[n * BACK_CH] = s.step(x[n]);
+        for (int n = 0; n < BLK; ++n) mo[n * BACK_CH] = s.step(x[n], n);
     BACK_ROLE_END
     s.store(l, a.s.aa);
 }
@@ -1485,6 +1546,10 @@ __global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const BackLds lds = back_lds_carve<BLK / L>(smem);
+    // raised issue priority: with the pipelined mode's rx_front of the next call sharing these
+    // CUs, the pipeline's per-call critical path keeps the SIMDs' issue slots first (C2 pipelined
+    // 25.5 -> 26.5-27.1 Gsamples/s; no effect when the kernels run back to back)
+    __builtin_amdgcn_s_setprio(3);
     // readfirstlane makes the role provably wave-uniform (scalar branches)
     const int role = __builtin_amdgcn_readfirstlane(threadIdx.x / BACK_CH) - (DM ? 1 : 0);
     if (role < 0)
@@ -1494,7 +1559,7 @@ __global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
     else if (role == 1)
         rx_back_agc<L, W, DM>(a, lds);
     else if (role == 2)
-        rx_back_audio<L, PH, DM>(a, lds);
+        rx_back_audio<L, PH, W, DM>(a, lds);
     else if (role == 3)
         rx_back_aa<AA, DM>(a, lds);
     else
@@ -1606,9 +1671,9 @@ __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys)
         for (int m = 0; m < NDC; ++m)
         {
             float u[L];
-            au.step(ag.step(m, pre.step(xin[m]), l, A), u);
+            au.step(ag.step(m, pre.step(xin[m], m), l, A), u);
 #pragma unroll
-            for (int j = 0; j < L; ++j) yl[m * L + j] = ou.step(aa.step(u[j]));
+            for (int j = 0; j < L; ++j) yl[m * L + j] = ou.step(aa.step(u[j], j));
         }
         fused_store_call(a, l, call, ys);
         ag.end(l);
@@ -2297,7 +2362,13 @@ struct uhsdr_rx_s
 
 static const char* kKernelNames[2] = { "rx_front", "rx_back" };
 
-static hipStream_t back_stream(const uhsdr_rx_s* h) { return h->pipelined ? h->side : h->stream; }
+#ifdef UHSDR_ANYORDER
+static constexpr bool kAnyOrder = true;
+#else
+static constexpr bool kAnyOrder = false;
+#endif
+static bool side_mode(const uhsdr_rx_s* h) { return h->pipelined && !kAnyOrder; }
+static hipStream_t back_stream(const uhsdr_rx_s* h) { return side_mode(h) ? h->side : h->stream; }
 
 static void time_mark(uhsdr_rx_s* h, int k, int which)
 {
@@ -2644,7 +2715,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
     const int par = h->pipelined ? (int)(h->calls_issued & 1) : 0;
     float* adec = par ? h->adec2 : h->adec;
     float* adec_q = par ? h->adec_q2 : h->adec_q;
-    if (h->pipelined) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[par], 0));
+    if (side_mode(h)) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[par], 0));
     h->calls_issued += 1;
     time_mark(h, 0, 0);
     const int cpw = FRONT_WAVE / (h->Nf / h->fv->R);
@@ -2667,6 +2738,10 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         fa.taps2a = h->d_taps2;
         fa.taps2b = h->d_taps2 + 2 * TAPS2_MAX;
         fa.comb = front_comb_of(h->plan);
+        if (h->pipelined && kAnyOrder && f0 == 0)
+            hipExtLaunchKernelGGL(h->precision == UHSDR_PRECISION_FMA ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw),
+                                  dim3(FRONT_WAVE), lds, h->stream, nullptr, nullptr, hipExtAnyOrderLaunch, fa);
+        else
         hipLaunchKernelGGL(h->precision == UHSDR_PRECISION_FMA ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw),
                            dim3(FRONT_WAVE), lds, h->stream, fa);
         HIPCHK(hipGetLastError());
@@ -2716,7 +2791,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         h->cw_blocks_last = blocks;
     }
     const hipStream_t bst = back_stream(h);
-    if (h->pipelined)
+    if (side_mode(h))
     {
         HIPCHK(hipEventRecord(h->ev_front, h->stream));
         HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
@@ -2734,7 +2809,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
                            back_lds(h), bst, ba);
     HIPCHK(hipGetLastError());
     time_mark(h, 1, 1);
-    if (h->pipelined) HIPCHK(hipEventRecord(h->ev_back[par], bst));
+    if (side_mode(h)) HIPCHK(hipEventRecord(h->ev_back[par], bst));
     if (h->tsample) h->nev++;
     h->tsample = 0;
     h->dec_samples += h->Nd;
@@ -2797,7 +2872,7 @@ extern "C" int32_t uhsdr_rx_get_precision(uhsdr_rx_handle h) { return h ? h->pre
 extern "C" uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
-    if (h->pipelined)
+    if (side_mode(h))
     {
         HIPCHK(hipEventRecord(h->ev_join, h->side));
         HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));

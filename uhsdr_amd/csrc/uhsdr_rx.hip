@@ -28,7 +28,6 @@
 // (tests/test_gpu_parity.py).
 
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
@@ -2310,6 +2309,10 @@ constexpr int TAPS2_MAX = (UHSDR_MAX_FIR_TAPS + 7) & ~7;   // taps per pair tabl
 constexpr int BACK_FUSED_MIN_CHANNELS = 131072;   // measured crossover (64-frame calls)
 enum { BACK_PIPE = 0, BACK_FUSED = 1 };
 
+// pipelined mode: hand-off buffers in rotation, so rx_front can run up to two calls ahead of
+// rx_back and the side stream's wait on it is already satisfied when rx_back gets there
+constexpr int PIPE_BUFS = 3;
+
 struct uhsdr_rx_s
 {
     uhsdr_rx_plan plan;
@@ -2342,13 +2345,13 @@ struct uhsdr_rx_s
     long long calls_done;
     long long front_launches; // oscillator ping-pong parity
     // pipelined mode (uhsdr_rx_set_pipelined): rx_back on a side stream, decimated hand-off
-    // double-buffered so the next call's rx_front overlaps this call's rx_back
+    // rotated over PIPE_BUFS buffers so the next calls' rx_front overlaps this call's rx_back
     int pipelined;
     hipStream_t side;
-    hipEvent_t ev_front, ev_join, ev_back[2];
+    hipEvent_t ev_front, ev_join, ev_back[PIPE_BUFS];
     hipEvent_t ev_switch;    // uhsdr_rx_set_stream: new stream after the old one's work
-    float *adec2, *adec_q2;  // second hand-off buffer pair
-    long long calls_issued;  // process() calls (hand-off buffer parity)
+    float *adecp[PIPE_BUFS - 1], *adec_qp[PIPE_BUFS - 1];  // the pipelined mode's other hand-off buffers
+    long long calls_issued;  // process() calls (hand-off buffer index)
     // per-kernel timing (uhsdr_rx_enable_timing)
     int timing;               // 0 off, else every timing-th call is bracketed
     int tsample;              // the call being enqueued is a timed one
@@ -2362,12 +2365,7 @@ struct uhsdr_rx_s
 
 static const char* kKernelNames[2] = { "rx_front", "rx_back" };
 
-#ifdef UHSDR_ANYORDER
-static constexpr bool kAnyOrder = true;
-#else
-static constexpr bool kAnyOrder = false;
-#endif
-static bool side_mode(const uhsdr_rx_s* h) { return h->pipelined && !kAnyOrder; }
+static bool side_mode(const uhsdr_rx_s* h) { return h->pipelined; }
 static hipStream_t back_stream(const uhsdr_rx_s* h) { return side_mode(h) ? h->side : h->stream; }
 
 static void time_mark(uhsdr_rx_s* h, int k, int which)
@@ -2710,11 +2708,11 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
     if (!h || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
     if (h->timing && h->nev >= h->nev_cap) time_harvest(h);
     h->tsample = h->timing && (h->tcalls++ % h->timing) == 0;
-    // hand-off buffers of this call; pipelined: alternate, and wait until the rx_back that
-    // read this pair two calls ago has finished
-    const int par = h->pipelined ? (int)(h->calls_issued & 1) : 0;
-    float* adec = par ? h->adec2 : h->adec;
-    float* adec_q = par ? h->adec_q2 : h->adec_q;
+    // hand-off buffers of this call; pipelined: rotate, and wait until the rx_back that read
+    // this buffer PIPE_BUFS calls ago has finished
+    const int par = h->pipelined ? (int)(h->calls_issued % PIPE_BUFS) : 0;
+    float* adec = par ? h->adecp[par - 1] : h->adec;
+    float* adec_q = par ? h->adec_qp[par - 1] : h->adec_q;
     if (side_mode(h)) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[par], 0));
     h->calls_issued += 1;
     time_mark(h, 0, 0);
@@ -2738,10 +2736,6 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         fa.taps2a = h->d_taps2;
         fa.taps2b = h->d_taps2 + 2 * TAPS2_MAX;
         fa.comb = front_comb_of(h->plan);
-        if (h->pipelined && kAnyOrder && f0 == 0)
-            hipExtLaunchKernelGGL(h->precision == UHSDR_PRECISION_FMA ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw),
-                                  dim3(FRONT_WAVE), lds, h->stream, nullptr, nullptr, hipExtAnyOrderLaunch, fa);
-        else
         hipLaunchKernelGGL(h->precision == UHSDR_PRECISION_FMA ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw),
                            dim3(FRONT_WAVE), lds, h->stream, fa);
         HIPCHK(hipGetLastError());
@@ -2889,13 +2883,16 @@ extern "C" uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable
         HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&h->ev_front, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < PIPE_BUFS; ++i)
         {
             HIPCHK(hipEventCreateWithFlags(&h->ev_back[i], hipEventDisableTiming));
             HIPCHK(hipEventRecord(h->ev_back[i], h->side));
         }
-        HIPCHK(hipMalloc((void**)&h->adec2, sizeof(float) * nd));
-        if (h->adec_q) HIPCHK(hipMalloc((void**)&h->adec_q2, sizeof(float) * nd));
+        for (int i = 0; i < PIPE_BUFS - 1; ++i)
+        {
+            HIPCHK(hipMalloc((void**)&h->adecp[i], sizeof(float) * nd));
+            if (h->adec_q) HIPCHK(hipMalloc((void**)&h->adec_qp[i], sizeof(float) * nd));
+        }
     }
     if (h->timing) time_harvest(h);
     // leaving the mode: the side stream's work completes before the handle stream goes on
@@ -2982,11 +2979,13 @@ extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
     {
         (void)hipEventDestroy(h->ev_front);
         (void)hipEventDestroy(h->ev_join);
-        (void)hipEventDestroy(h->ev_back[0]);
-        (void)hipEventDestroy(h->ev_back[1]);
+        for (int i = 0; i < PIPE_BUFS; ++i) (void)hipEventDestroy(h->ev_back[i]);
         (void)hipStreamDestroy(h->side);
-        (void)hipFree(h->adec2);
-        if (h->adec_q2) (void)hipFree(h->adec_q2);
+        for (int i = 0; i < PIPE_BUFS - 1; ++i)
+        {
+            (void)hipFree(h->adecp[i]);
+            if (h->adec_qp[i]) (void)hipFree(h->adec_qp[i]);
+        }
     }
     if (h->ev)
     {

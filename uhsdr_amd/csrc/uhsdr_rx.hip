@@ -631,10 +631,11 @@ struct BackLds
     float* agc;   // [2][NDC][64]  agc -> audio
     float* mid;   // [2][BLK][64]  audio -> aa
     float* aa;    // [2][BLK][64]  aa -> output
+    float* prep;  // [3][2][NDC][64]  pre -> agc: window maximum, fast / hang averages
 };
 
 // floats of the hand-off buffers (host: back_lds)
-__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (3 * ndc + 2 * BLK); }
+__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (6 * ndc + 2 * BLK); }
 
 template <int NDC>
 __device__ __forceinline__ BackLds back_lds_carve(float* smem)
@@ -645,6 +646,7 @@ __device__ __forceinline__ BackLds back_lds_carve(float* smem)
     l.agc = l.aa + 2 * BLK * BACK_CH;
     l.pre = l.agc + 2 * NDC * BACK_CH;
     l.dem = l.pre + 2 * NDC * BACK_CH;
+    l.prep = l.dem + 2 * NDC * BACK_CH;
     return l;
 }
 
@@ -838,6 +840,63 @@ struct AgcStage
         return (A.out_target - A.slope_constant * vo) / volts;
     }
 
+    // the gain state's update from the window maximum and the two averages of the delayed
+    // magnitude (audio_agc.c:431-551)
+    __device__ __forceinline__ void recur(float ring_max, float fast_bavg, float hang_bavg, const uhsdr_agc_plan& A)
+    {
+        hang_counter = hang_counter > 0 ? hang_counter - 1 : hang_counter;
+        // the 5-state attack / decay / hang machine (audio_agc.c:436-551): every case is
+        // evaluated and the lane's state selects; mu = the multiplier the taken branch applies
+        const float rv = ring_max - volts;
+        const bool atk = ring_max >= volts;
+        // bools combine with & and | (no short-circuit), so the compiler emits selects, not
+        // exec-masked branches
+        const bool s0 = state == 0, s1 = state == 1, s2 = state == 2, s34 = !(s0 | s1 | s2);
+        const bool fast = volts > A.pop_ratio * fast_bavg;                    // case 0
+        const bool hang = (A.hang_enable != 0) & (hang_bavg > A.hang_level);
+        const bool fd = volts > save_volts;                                   // case 1
+        const bool hc = hang_counter > 0;
+        const bool dt0 = decay_type == 0;
+        const bool hz = hang_counter == 0;                                    // case 2
+        // without attack
+        const int ns0 = fast ? 1 : hang ? 2 : 3;
+        const int ns1 = fd ? 1 : hc ? 2 : dt0 ? 3 : 4;
+        const int ns2 = hz ? 4 : 2;
+        const int nsn = s0 ? ns0 : s1 ? ns1 : s2 ? ns2 : state;
+        const bool updn = (s0 & (fast | !hang)) | (s1 & (fd | !hc)) | (s2 & hz) | s34;
+        const float dm = A.decay_mult, fdm = A.fast_decay_mult, hdm = A.hang_decay_mult;
+        const float mu0 = fast ? fdm : dm;
+        const float mu1 = fd ? fdm : dt0 ? dm : hdm;
+        const float mu3 = state == 3 ? dm : hdm;
+        const float mun = s0 ? mu0 : s1 ? mu1 : s2 ? hdm : mu3;
+        const bool s0_decay = s0 & !atk & !fast;                              // case 0, no attack, slow
+        hang_counter = (s0_decay & hang) ? A.hang_counter_init : hang_counter;
+        decay_type = s0_decay ? (hang ? 1 : 0) : decay_type;
+        state = atk ? 0 : nsn;
+        const bool save = atk & !s0 & !s1;
+        save_volts = save ? volts : save_volts;
+        const float mu = atk ? A.attack_mult : mun;
+        const bool upd = atk | updn;
+        const float nv = volts + rv * mu;
+        volts = upd ? nv : volts;
+        volts = (volts < A.min_volts) ? A.min_volts : volts;
+    }
+
+    // NCH == 1: the part of a sample that does not depend on the gain state -- the ring store,
+    // the window maximum and both averages of the delayed magnitude (audio_agc.c:397-430).  The
+    // wave pipeline runs it in the pre role and recur() in the AGC role; out is the delayed sample.
+    struct Prep { float out, rmax, fb, hb; };
+    __device__ __forceinline__ Prep prep(int m, float x, const BackLane& l, const uhsdr_agc_plan& A)
+    {
+        const float out = m ? old[0][m - 1] : leave_last[0];
+        const float abs_out = fabsf(out);
+        ring_out[0][(size_t)m * l.C + (unsigned)l.cl] = x;
+        fast_bavg = A.fast_backmult * abs_out + A.onemfast_backmult * fast_bavg;
+        hang_bavg = A.hang_backmult * abs_out + A.onemhang_backmult * hang_bavg;
+        pmax = fmaxf(pmax, fabsf(x));
+        return Prep{ out, fmaxf(fmaxf(pmax, wmax), sfx[m]), fast_bavg, hang_bavg };
+    }
+
     __device__ __forceinline__ void stepn(int m, float (&x)[NCH], const BackLane& l, const uhsdr_agc_plan& A)
     {
         float v;
@@ -867,42 +926,7 @@ struct AgcStage
             hang_bavg = A.hang_backmult * abs_out + A.onemhang_backmult * hang_bavg;
             pmax = fmaxf(pmax, absn([&](int ch) { return x[ch]; }));
             const float ring_max = fmaxf(fmaxf(pmax, wmax), sfx[m]);
-            hang_counter = hang_counter > 0 ? hang_counter - 1 : hang_counter;
-            // the 5-state attack / decay / hang machine (audio_agc.c:436-551): every case is
-            // evaluated and the lane's state selects; mu = the multiplier the taken branch applies
-            const float rv = ring_max - volts;
-            const bool atk = ring_max >= volts;
-            // bools combine with & and | (no short-circuit), so the compiler emits selects, not
-            // exec-masked branches
-            const bool s0 = state == 0, s1 = state == 1, s2 = state == 2, s34 = !(s0 | s1 | s2);
-            const bool fast = volts > A.pop_ratio * fast_bavg;                    // case 0
-            const bool hang = (A.hang_enable != 0) & (hang_bavg > A.hang_level);
-            const bool fd = volts > save_volts;                                   // case 1
-            const bool hc = hang_counter > 0;
-            const bool dt0 = decay_type == 0;
-            const bool hz = hang_counter == 0;                                    // case 2
-            // without attack
-            const int ns0 = fast ? 1 : hang ? 2 : 3;
-            const int ns1 = fd ? 1 : hc ? 2 : dt0 ? 3 : 4;
-            const int ns2 = hz ? 4 : 2;
-            const int nsn = s0 ? ns0 : s1 ? ns1 : s2 ? ns2 : state;
-            const bool updn = (s0 & (fast | !hang)) | (s1 & (fd | !hc)) | (s2 & hz) | s34;
-            const float dm = A.decay_mult, fdm = A.fast_decay_mult, hdm = A.hang_decay_mult;
-            const float mu0 = fast ? fdm : dm;
-            const float mu1 = fd ? fdm : dt0 ? dm : hdm;
-            const float mu3 = state == 3 ? dm : hdm;
-            const float mun = s0 ? mu0 : s1 ? mu1 : s2 ? hdm : mu3;
-            const bool s0_decay = s0 & !atk & !fast;                              // case 0, no attack, slow
-            hang_counter = (s0_decay & hang) ? A.hang_counter_init : hang_counter;
-            decay_type = s0_decay ? (hang ? 1 : 0) : decay_type;
-            state = atk ? 0 : nsn;
-            const bool save = atk & !s0 & !s1;
-            save_volts = save ? volts : save_volts;
-            const float mu = atk ? A.attack_mult : mun;
-            const bool upd = atk | updn;
-            const float nv = volts + rv * mu;
-            volts = upd ? nv : volts;
-            volts = (volts < A.min_volts) ? A.min_volts : volts;
+            recur(ring_max, fast_bavg, hang_bavg, A);
             if (TAIL)
             {
                 const float mult = gain(volts, A);
@@ -956,12 +980,20 @@ struct AgcStage
         cmax[AGC_Q - 2] = pmax;
     }
 
-    __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l)
+    // which[0]: the prep() side (ring, averages, DC state), which[1]: the recur() side
+    __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l, const bool (&which)[2] = { true, true })
     {
         if (!l.live) return;
         const int C = l.C, c = l.c;
-        a.s.agc[1 * C + c] = volts;
-        a.s.agc[2 * C + c] = save_volts;
+        if (which[1])
+        {
+            a.s.agc[1 * C + c] = volts;
+            a.s.agc[2 * C + c] = save_volts;
+            a.s.agci[0 * C + c] = hang_counter;
+            a.s.agci[1 * C + c] = decay_type;
+            a.s.agci[2 * C + c] = state;
+        }
+        if (!which[0]) return;
         a.s.agc[3 * C + c] = fast_bavg;
         a.s.agc[4 * C + c] = hang_bavg;
         a.s.agc[5 * C + c] = wold[0];
@@ -973,9 +1005,6 @@ struct AgcStage
             a.s.agc[(6 + AGC_Q) * C + c] = wold[NCH - 1];
             a.s.agc[(7 + AGC_Q) * C + c] = leave_last[NCH - 1];
         }
-        a.s.agci[0 * C + c] = hang_counter;
-        a.s.agci[1 * C + c] = decay_type;
-        a.s.agci[2 * C + c] = state;
     }
 };
 
@@ -1375,8 +1404,15 @@ __device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
     s.store(a, l);
 }
 
+// the AGC's ring side (AgcStage::prep) runs in the pre role, its recursion in the AGC role and
+// its gain in the audio role: SSB / CW / DIGI with the AGC on and no DC removal
+__device__ __forceinline__ bool back_agc_prep_in_pre(int dm, const uhsdr_agc_plan& A)
+{
+    return back_agc_split(dm) && !A.remove_dc && A.mode != 5;
+}
+
 // IIR lattice pre-filter; input: rx_front's decimated I +- Q (SSB) or the demod role's output
-template <int PRE, int L, int DM>
+template <int PRE, int L, int W, int DM>
 __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
@@ -1386,6 +1422,14 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
     LatticeStage<PRE> s;
     s.load(l, P->pre_k, P->pre_v, a.s.pre);
     if (!DM) in.fetch(a, l, 0);
+    const uhsdr_agc_plan A = P->agc;
+    const bool prep = back_agc_prep_in_pre(DM, A);
+    AgcStage<L, W> ag;
+    if (prep)
+    {
+        ag.load(a, l, A);
+        ag.fetch(a, l, 0);
+    }
     BACK_ROLE_LOOP(DM ? 1 : 0)
         float xin[NDC];
         if (DM)
@@ -1397,10 +1441,35 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
         else
             in.begin(a, l, call, xin);
         float* po = lds.pre + (call & 1) * NDC * BACK_CH + l.lane;
+        if (prep)
+        {
+            // to the AGC role: the delayed sample, window maximum and both averages
+            float* pr = lds.prep + (call & 1) * NDC * BACK_CH + l.lane;
+            float* pf = pr + 2 * NDC * BACK_CH;
+            float* ph = pf + 2 * NDC * BACK_CH;
+            float y[NDC];
 #pragma unroll
-        for (int m = 0; m < NDC; ++m) po[m * BACK_CH] = s.step(xin[m], m);
+            for (int m = 0; m < NDC; ++m) y[m] = s.step(xin[m], m);
+            ag.begin(a, l, call);
+#pragma unroll
+            for (int m = 0; m < NDC; ++m)
+            {
+                const auto q = ag.prep(m, y[m], l, A);
+                po[m * BACK_CH] = q.out;
+                pr[m * BACK_CH] = q.rmax;
+                pf[m * BACK_CH] = q.fb;
+                ph[m * BACK_CH] = q.hb;
+            }
+            ag.end(l);
+        }
+        else
+        {
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) po[m * BACK_CH] = s.step(xin[m], m);
+        }
     BACK_ROLE_END
     s.store(l, a.s.pre);
+    if (prep) ag.store(a, l, { true, false });
 }
 
 template <int L, int W, int DM>
@@ -1412,13 +1481,34 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
     const uhsdr_agc_plan A = P->agc;
     AgcStage<L, W> s;
     s.load(a, l, A);
-    s.fetch(a, l, 0);
+    const bool prep = back_agc_prep_in_pre(DM, A);
+    if (!prep) s.fetch(a, l, 0);
     BACK_ROLE_LOOP(DM ? 2 : 1)
         const float* pi = lds.pre + (call & 1) * NDC * BACK_CH + l.lane;
         float* ao = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
         float x[NDC];
 #pragma unroll
         for (int m = 0; m < NDC; ++m) x[m] = pi[m * BACK_CH];
+        if (prep)
+        {
+            // the recursion on the pre role's values; volts on to the audio role
+            const float* pr = lds.prep + (call & 1) * NDC * BACK_CH + l.lane;
+            const float* pf = pr + 2 * NDC * BACK_CH;
+            const float* ph = pf + 2 * NDC * BACK_CH;
+            float r[NDC], fb[NDC], hb[NDC];
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) { r[m] = pr[m * BACK_CH]; fb[m] = pf[m * BACK_CH]; hb[m] = ph[m * BACK_CH]; }
+            float* vo = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m)
+            {
+                s.recur(r[m], fb[m], hb[m], A);
+                ao[m * BACK_CH] = x[m];
+                vo[m * BACK_CH] = s.volts;
+            }
+        }
+        else
+        {
         s.begin(a, l, call);
         if (back_agc_split(DM) && !A.remove_dc)
         {
@@ -1439,8 +1529,9 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
             for (int m = 0; m < NDC; ++m) ao[m * BACK_CH] = s.step(m, x[m], l, A);
         }
         s.end(l);
+        }
     BACK_ROLE_END
-    s.store(a, l);
+    s.store(a, l, { !prep, true });
 }
 
 template <int L, int PH, int W, int DM>
@@ -1554,7 +1645,7 @@ __global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
     if (role < 0)
         rx_back_demod<L, DM>(a, lds);
     else if (role == 0)
-        rx_back_pre<PRE, L, DM>(a, lds);
+        rx_back_pre<PRE, L, W, DM>(a, lds);
     else if (role == 1)
         rx_back_agc<L, W, DM>(a, lds);
     else if (role == 2)

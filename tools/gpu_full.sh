@@ -20,9 +20,9 @@ cat gpurun_out/bench_${tag}.json
 step "rocprof kernel trace c2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2_${tag} -o prof --output-format csv -- python bench.py --steps 200 --warmup 20 --no-cpu --no-northstar > gpurun_out/prof_c2_${tag}.log 2>&1 || { tail -20 gpurun_out/prof_c2_${tag}.log; exit 1; }
 step "rocprof kernel trace northstar"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ns_${tag} -o prof --output-format csv -- python bench.py --workload northstar --steps 20 --warmup 3 --no-cpu > gpurun_out/prof_ns_${tag}.log 2>&1 || { tail -20 gpurun_out/prof_ns_${tag}.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ns_${tag} -o prof --output-format csv -- python bench.py --workload northstar --steps 100 --warmup 10 --no-cpu > gpurun_out/prof_ns_${tag}.log 2>&1 || { tail -20 gpurun_out/prof_ns_${tag}.log; exit 1; }
 step "rocprof kernel trace northstar fma"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_nsfma_${tag} -o prof --output-format csv -- python bench.py --workload northstar --precision fma --steps 20 --warmup 3 --no-cpu > gpurun_out/prof_nsfma_${tag}.log 2>&1 || { tail -20 gpurun_out/prof_nsfma_${tag}.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_nsfma_${tag} -o prof --output-format csv -- python bench.py --workload northstar --precision fma --steps 100 --warmup 10 --no-cpu > gpurun_out/prof_nsfma_${tag}.log 2>&1 || { tail -20 gpurun_out/prof_nsfma_${tag}.log; exit 1; }
 step "pmc northstar"
 bash tools/gpu_pmc.sh ns_${tag} --workload northstar --steps 5 --warmup 2 || exit 1
 step "pmc northstar fma"

@@ -702,7 +702,12 @@ struct InStage
 // ---- IIR lattice (arm_iir_lattice_f32): the pre-filter on a_buffer[0] at the decimated rate
 //      (IIR_PreFilter, audio_driver.c:2473-2482) or the anti-alias filter at 48 ksps
 //      (IIR_AntiAlias, :2581-2590); state [S][C] in `st` ----
-template <int S>
+// PK: the packed form (lattice_step_pk); the fused back end keeps the scalar one, where the
+// packed form's extra live pairs cost SGPR spills and scratch at no gain (it is not issue-bound)
+#ifndef UHSDR_FUSED_PK
+#define UHSDR_FUSED_PK false
+#endif
+template <int S, bool PK = true>
 struct LatticeStage
 {
     float k[S > 0 ? S : 1], v[S + 1], g[S > 0 ? S : 1];
@@ -721,7 +726,8 @@ struct LatticeStage
     // only selects the register pairing of the packed form
     __device__ __forceinline__ float step(float x, int par = 0)
     {
-        if constexpr (S > 0) return (par & 1) ? lattice_step_pk<S, 1>(x, g, k, v) : lattice_step_pk<S, 0>(x, g, k, v);
+        if constexpr (S > 0 && PK) return (par & 1) ? lattice_step_pk<S, 1>(x, g, k, v) : lattice_step_pk<S, 0>(x, g, k, v);
+        if constexpr (S > 0 && !PK) return lattice_step<S>(x, g, k, v);
         return x;
     }
 
@@ -1716,10 +1722,10 @@ __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys)
     const uhsdr_agc_plan A = P->agc;
     DemodStage<L, DM> dm;
     InStage<L> in;
-    LatticeStage<PRE> pre;
+    LatticeStage<PRE, UHSDR_FUSED_PK> pre;
     AgcStage<L, W> ag;
     AudioStage<L, PH, DM> au;
-    LatticeStage<AA> aa;
+    LatticeStage<AA, UHSDR_FUSED_PK> aa;
     OutputStage ou;
     if (DM) { dm.load(a, l); dm.fetch(a, l, 0); }
     else in.fetch(a, l, 0);

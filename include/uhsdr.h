@@ -247,7 +247,7 @@ uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h);
 uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h);
 
 /* Pipelined mode (off by default).  On: rx_back runs on a private side stream and the
-   decimated hand-off is double-buffered, so call k+1's rx_front overlaps call k's rx_back —
+   decimated hand-off rotates over three buffers, so rx_front runs up to two calls ahead of rx_back —
    the streaming throughput of back-to-back ISR calls is max(front, back) instead of the sum.
    Results are identical; only their completion point moves: the audio / dst / CW outputs of
    a call are complete after uhsdr_rx_synchronize(), or for work enqueued on the handle's

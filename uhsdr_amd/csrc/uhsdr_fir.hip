@@ -52,41 +52,10 @@ struct FirArgs
     int cp;              // LDS floats of the padded tap copy
 };
 
+// the tiles of one channel group from its LDS windows Wb (4 channels from c0)
 template <bool MFMA>
-__global__ void __launch_bounds__(256) fir_batch(FirArgs a)
+__device__ __forceinline__ void fir_group(const FirArgs& a, const float* Wb, const float* cp, int c0, int lane)
 {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int H = a.T - 1, n = H + a.B;
-    float* cp = sm;                                   // cp[16 + k] = c[k], zeros around
-    for (int i = threadIdx.x; i < a.cp; i += blockDim.x)
-        cp[i] = (i >= 16 && i < 16 + a.T) ? a.taps[i - 16] : 0.0f;
-    float* Wb = sm + a.cp + (size_t)w * FIR_CPW * a.lw;
-    const int c0 = (blockIdx.x * nw + w) * FIR_CPW;
-    // windows: carried samples + this call's block + zero tail
-#pragma unroll
-    for (int j = 0; j < FIR_CPW; ++j)
-    {
-        const int c = c0 + j;
-        const int cl = c < a.C ? c : a.C - 1;         // loads clamped: no exec-masked load branches
-        const float* h = a.hist + (size_t)cl * H;
-        const float* s = a.src + (size_t)cl * a.B;
-        float* W = Wb + j * a.lw;
-        for (int i = lane; i < n + FIR_TAIL; i += 64)
-            W[fpad(i)] = i < H ? h[i] : (i < n ? s[i - H] : 0.0f);
-    }
-    __syncthreads();                                  // taps (whole workgroup) and windows ready
-    // the next call's carried samples: the window's last T-1
-#pragma unroll
-    for (int j = 0; j < FIR_CPW; ++j)
-    {
-        const int c = c0 + j;
-        if (c < a.C)
-        {
-            const float* W = Wb + j * a.lw;
-            for (int i = lane; i < H; i += 64) a.hist[(size_t)c * H + i] = W[fpad(i + a.B)];
-        }
-    }
     const int r = lane & 15, kq = lane >> 4;
     for (int t = 0; t < a.B / FIR_TILE; ++t)
     {
@@ -190,11 +159,122 @@ __global__ void __launch_bounds__(256) fir_batch(FirArgs a)
     }
 }
 
+// One group per wave, windows filled straight from HBM (EXACT: VALU-bound, the fill hides behind
+// the other waves; the persistent form's prefetch registers cost it 20 %)
+template <bool MFMA>
+__global__ void __launch_bounds__(256) fir_batch_direct(FirArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int H = a.T - 1, n = H + a.B;
+    float* cp = sm;
+    for (int i = threadIdx.x; i < a.cp; i += blockDim.x)
+        cp[i] = (i >= 16 && i < 16 + a.T) ? a.taps[i - 16] : 0.0f;
+    float* Wb = sm + a.cp + (size_t)w * FIR_CPW * a.lw;
+    const int c0 = (blockIdx.x * nw + w) * FIR_CPW;
+#pragma unroll
+    for (int j = 0; j < FIR_CPW; ++j)
+    {
+        const int c = c0 + j;
+        const int cl = c < a.C ? c : a.C - 1;
+        const float* h = a.hist + (size_t)cl * H;
+        const float* s = a.src + (size_t)cl * a.B;
+        float* W = Wb + j * a.lw;
+        for (int i = lane; i < n + FIR_TAIL; i += 64)
+            W[fpad(i)] = i < H ? h[i] : (i < n ? s[i - H] : 0.0f);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FIR_CPW; ++j)
+    {
+        const int c = c0 + j;
+        if (c < a.C)
+        {
+            const float* W = Wb + j * a.lw;
+            for (int i = lane; i < H; i += 64) a.hist[(size_t)c * H + i] = W[fpad(i + a.B)];
+        }
+    }
+    fir_group<MFMA>(a, Wb, cp, c0, lane);
+}
+
+// floats of a channel's window each lane carries in registers between groups (n <= 64 * FIR_NPL)
+constexpr int FIR_NPL = 16;
+
+// Persistent: each wave walks channel groups g = wave, wave + waves in grid, ...  The next
+// group's window (carried samples + block) is loaded into registers while the current group's
+// tiles run from LDS, then written into the wave's LDS windows -- the HBM latency of the fill
+// hides behind the MFMA (or VALU) chain instead of stalling the wave between groups.
+template <bool MFMA>
+__global__ void __launch_bounds__(256) fir_batch(FirArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int H = a.T - 1, n = H + a.B;
+    float* cp = sm;                                   // cp[16 + k] = c[k], zeros around
+    for (int i = threadIdx.x; i < a.cp; i += blockDim.x)
+        cp[i] = (i >= 16 && i < 16 + a.T) ? a.taps[i - 16] : 0.0f;
+    float* Wb = sm + a.cp + (size_t)w * FIR_CPW * a.lw;
+    // windows: [carried samples | block | zero tail]; the tail is written once
+#pragma unroll
+    for (int j = 0; j < FIR_CPW; ++j)
+        for (int i = n + lane; i < n + FIR_TAIL; i += 64) Wb[j * a.lw + fpad(i)] = 0.0f;
+    __syncthreads();                                  // taps (whole workgroup) ready
+    const int ng = (a.C + FIR_CPW - 1) / FIR_CPW;
+    const int nwt = gridDim.x * nw;
+    float pf[FIR_CPW][FIR_NPL];
+    auto fetch = [&](int g) {
+#pragma unroll
+        for (int j = 0; j < FIR_CPW; ++j)
+        {
+            const int c = g * FIR_CPW + j;
+            const int cl = c < a.C ? c : a.C - 1;     // loads clamped: no exec-masked load branches
+            const float* h = a.hist + (size_t)cl * H;
+            const float* s = a.src + (size_t)cl * a.B;
+#pragma unroll
+            for (int k = 0; k < FIR_NPL; ++k)
+            {
+                const int i = lane + 64 * k;
+                const int is = i - H < a.B ? i - H : a.B - 1;
+                pf[j][k] = *(i < H ? h + i : s + is);
+            }
+        }
+    };
+    int g = blockIdx.x * nw + w;
+    if (g < ng) fetch(g);
+    for (; g < ng; g += nwt)
+    {
+        wave_sync();                                  // every lane is done with the last group's windows
+#pragma unroll
+        for (int j = 0; j < FIR_CPW; ++j)
+#pragma unroll
+            for (int k = 0; k < FIR_NPL; ++k)
+            {
+                const int i = lane + 64 * k;
+                if (i < n) Wb[j * a.lw + fpad(i)] = pf[j][k];
+            }
+        wave_sync();
+        if (g + nwt < ng) fetch(g + nwt);             // in flight while this group computes
+        const int c0 = g * FIR_CPW;
+        // the next call's carried samples: the window's last T-1
+#pragma unroll
+        for (int j = 0; j < FIR_CPW; ++j)
+        {
+            const int c = c0 + j;
+            if (c < a.C)
+            {
+                const float* W = Wb + j * a.lw;
+                for (int i = lane; i < H; i += 64) a.hist[(size_t)c * H + i] = W[fpad(i + a.B)];
+            }
+        }
+        fir_group<MFMA>(a, Wb, cp, c0, lane);
+    }
+}
+
 } // namespace
 
 struct uhsdr_fir_s
 {
-    int C, B, T, K, mode, lw, cp, waves;
+    int C, B, T, K, mode, lw, cp, waves, grid;
     hipStream_t stream;
     float* taps;
     float* hist;
@@ -248,11 +328,29 @@ extern "C" uhsdr_status uhsdr_fir_create(const float* coeffs, int32_t num_taps, 
     h->cp = (h->K + 16 + 16 + 3) & ~3;
     h->waves = 4;
     while (h->waves > 1 && fir_lds(h, h->waves) > 64 * 1024) h->waves /= 2;
-    if (fir_lds(h, h->waves) > 64 * 1024)
+    if (fir_lds(h, h->waves) > 64 * 1024 || num_taps - 1 + block_size > 64 * FIR_NPL)
     {
         free(h);
-        uhsdr_set_error("num_taps + block_size too long for LDS");
+        uhsdr_set_error("num_taps - 1 + block_size above %d", 64 * FIR_NPL);
         return UHSDR_LENGTH_ERROR;
+    }
+    {
+        // persistent grid: as many workgroups as the CUs hold at once (LDS-limited), each wave
+        // walking channel groups
+        int dev = 0, cus = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+            cus = prop.multiProcessorCount;
+        const size_t lds = fir_lds(h, h->waves);
+        int per_cu = (int)((160 * 1024) / lds);
+        const int thread_cap = 2048 / (64 * h->waves);
+        if (per_cu > thread_cap) per_cu = thread_cap;
+        if (per_cu < 1) per_cu = 1;
+        const int groups = (num_channels + FIR_CPW - 1) / FIR_CPW;
+        const int need = (groups + h->waves - 1) / h->waves;
+        // MFMA: persistent (C5 0.69 -> 0.40 ms per call); EXACT: fir_batch_direct, one
+        // group per wave (0.99 ms; 1.20 in the persistent form)
+        h->grid = (mode == UHSDR_FIR_MFMA && need > cus * per_cu) ? cus * per_cu : need;
     }
     if (hipMalloc((void**)&h->taps, sizeof(float) * num_taps) != hipSuccess ||
         hipMalloc((void**)&h->hist, sizeof(float) * (size_t)num_channels * (num_taps > 1 ? num_taps - 1 : 1)) != hipSuccess ||
@@ -272,12 +370,11 @@ extern "C" uhsdr_status uhsdr_fir_process(uhsdr_fir_handle h, const float* src, 
     FirArgs a;
     a.taps = h->taps; a.hist = h->hist; a.src = src; a.dst = dst;
     a.C = h->C; a.B = h->B; a.T = h->T; a.K = h->K; a.lw = h->lw; a.cp = h->cp;
-    const int per_block = h->waves * FIR_CPW;
-    const dim3 grid((h->C + per_block - 1) / per_block), block(64 * h->waves);
+    const dim3 grid(h->grid), block(64 * h->waves);
     if (h->mode == UHSDR_FIR_MFMA)
         hipLaunchKernelGGL(fir_batch<true>, grid, block, fir_lds(h, h->waves), h->stream, a);
     else
-        hipLaunchKernelGGL(fir_batch<false>, grid, block, fir_lds(h, h->waves), h->stream, a);
+        hipLaunchKernelGGL(fir_batch_direct<false>, grid, block, fir_lds(h, h->waves), h->stream, a);
     HIPCHK(hipGetLastError());
     return UHSDR_OK;
 }

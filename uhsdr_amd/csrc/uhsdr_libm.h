@@ -115,6 +115,12 @@ UHSDR_LIBM_FN void ul_sincosf(float y, float* sinp, float* cosp)
 }
 
 /* ---- atanf / atan2f (fdlibm binary32) ---- */
+/* Both are written branch-free on the main path: in a wave, lanes whose arguments fall in
+ * different reduction intervals would otherwise run every interval's division one after the
+ * other.  Each interval of fdlibm's reduction is a quotient num / den of the same operations,
+ * so the interval selects num, den and the atanhi / atanlo pair, one division runs, and the
+ * special cases (tiny, huge, NaN) select their results at the end -- the same binary32
+ * operations on the same operands as the branches (pinned against glibc, tests/test_libm.py). */
 UHSDR_LIBM_FN float ul_atanf(float x)
 {
     const float atanhi[4] = { 4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f };
@@ -124,38 +130,28 @@ UHSDR_LIBM_FN float ul_atanf(float x)
                            4.9768779427e-02f, -3.6531571299e-02f, 1.6285819933e-02f };
     const uint32_t hx = ul_asuint(x);
     const uint32_t ix = hx & 0x7fffffff;
-    int id;
-    if (ix >= 0x4c000000)                               /* |x| >= 2^25 */
-    {
-        if (ix > 0x7f800000) return x + x;              /* NaN */
-        return (hx >> 31) ? -atanhi[3] - atanlo[3] : atanhi[3] + atanlo[3];
-    }
-    if (ix < 0x3ee00000)                                /* |x| < 0.4375 */
-    {
-        if (ix < 0x31000000) return x;                  /* |x| < 2^-29 */
-        id = -1;
-    }
-    else
-    {
-        x = fabsf(x);
-        if (ix < 0x3f980000)                            /* |x| < 1.1875 */
-        {
-            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }   /* 7/16 <= |x| < 11/16 */
-            else { id = 1; x = (x - 1.0f) / (x + 1.0f); }                          /* 11/16 <= |x| < 19/16 */
-        }
-        else
-        {
-            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }   /* |x| < 2.4375 */
-            else { id = 3; x = -1.0f / x; }                                         /* 2.4375 <= |x| < 2^25 */
-        }
-    }
-    const float z = x * x;
+    const float ax = fabsf(x);
+    /* |x| < 7/16: no reduction; 7/16 <= |x| < 11/16: (2|x| - 1) / (2 + |x|); < 19/16:
+       (|x| - 1) / (|x| + 1); < 2.4375: (|x| - 1.5) / (1 + 1.5|x|); above: -1 / |x| */
+    const int small = ix < 0x3ee00000, lo2 = ix < 0x3f980000, i0 = ix < 0x3f300000, i2 = ix < 0x401c0000;
+    const float n0 = 2.0f * ax - 1.0f, d0 = 2.0f + ax;
+    const float n1 = ax - 1.0f, d1 = ax + 1.0f;
+    const float n2 = ax - 1.5f, d2 = 1.0f + 1.5f * ax;
+    const float num = lo2 ? (i0 ? n0 : n1) : (i2 ? n2 : -1.0f);
+    const float den = lo2 ? (i0 ? d0 : d1) : (i2 ? d2 : ax);
+    const float hi = lo2 ? (i0 ? atanhi[0] : atanhi[1]) : (i2 ? atanhi[2] : atanhi[3]);
+    const float lo = lo2 ? (i0 ? atanlo[0] : atanlo[1]) : (i2 ? atanlo[2] : atanlo[3]);
+    const float xr = small ? x : num / den;
+    const float z = xr * xr;
     const float w = z * z;
     const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
     const float s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
-    if (id < 0) return x - x * (s1 + s2);
-    const float zz = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
-    return (hx >> 31) ? -zz : zz;
+    const float zz = hi - ((xr * (s1 + s2) - lo) - xr);
+    float r = small ? xr - xr * (s1 + s2) : ((hx >> 31) ? -zz : zz);
+    r = (ix < 0x31000000) ? x : r;                                      /* |x| < 2^-29 */
+    const float huge = (hx >> 31) ? -atanhi[3] - atanlo[3] : atanhi[3] + atanlo[3];
+    r = (ix >= 0x4c000000) ? ((ix > 0x7f800000) ? x + x : huge) : r;   /* |x| >= 2^25, NaN */
+    return r;
 }
 
 UHSDR_LIBM_FN float ul_atan2f(float y, float x)
@@ -164,9 +160,10 @@ UHSDR_LIBM_FN float ul_atan2f(float y, float x)
                 pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
     const int32_t hx = (int32_t)ul_asuint(x), hy = (int32_t)ul_asuint(y);
     const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);      /* 2*sign(x) + sign(y) */
+    /* rare operands (NaN, x = 1, zeros, infinities): wave-uniformly skipped when no lane has one */
     if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;   /* NaN */
     if (hx == 0x3f800000) return ul_atanf(y);               /* x = 1.0 */
-    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);      /* 2*sign(x) + sign(y) */
     if (iy == 0)
     {
         switch (m)
@@ -200,17 +197,13 @@ UHSDR_LIBM_FN float ul_atan2f(float y, float x)
     }
     if (iy == 0x7f800000) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
     const int32_t k = (iy - ix) >> 23;
-    float z;
-    if (k > 26) z = pi_o_2 + 0.5f * pi_lo;                 /* |y/x| > 2^26 */
-    else if (hx < 0 && k < -26) z = 0.0f;                   /* |y|/x < -2^26 */
-    else z = ul_atanf(fabsf(y / x));
-    switch (m)
-    {
-    case 0: return z;
-    case 1: return ul_asfloat(ul_asuint(z) ^ 0x80000000u);
-    case 2: return pi - (z - pi_lo);
-    default: return (z - pi_lo) - pi;
-    }
+    float z = ul_atanf(fabsf(y / x));
+    z = (hx < 0 && k < -26) ? 0.0f : z;                     /* |y|/x < -2^26 */
+    z = (k > 26) ? pi_o_2 + 0.5f * pi_lo : z;               /* |y/x| > 2^26 */
+    const float zm = z - pi_lo;
+    const float r2 = pi - zm, r3 = zm - pi;
+    const float r1 = ul_asfloat(ul_asuint(z) ^ 0x80000000u);
+    return (m & 2) ? ((m & 1) ? r3 : r2) : ((m & 1) ? r1 : z);
 }
 
 /* ---- asinf (glibc sysdeps/ieee754/flt-32/e_asinf.c: fdlibm binary32 with a degree-4 minimax

@@ -2134,7 +2134,9 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                         out[m * BACK_CH] = o;
                         q_prev = xq[m];
                         i_prev = xi[m];
-                        const float sqo = lattice_step<SQ>(angle, g, sk, sv);   // squelch HPF (:1594)
+                        // squelch HPF (:1594); the packed lattice, pairing by the sample's parity
+                        const float sqo = (m & 1) ? lattice_step_pk<SQ, 1>(angle, g, sk, sv)
+                                                  : lattice_step_pk<SQ, 0>(angle, g, sk, sv);
                         if (m == 0) sq0 = sqo;
                     }
                     sql_avg = (float)(((1 - 0.005) * (double)sql_avg) + (0.005 * (double)sqrtf(fabsf(sq0))));
@@ -2276,7 +2278,7 @@ struct NotchVariant { int L, dm; back_fn fn; };
 static const FrontVariant kFront[] = { FRONT_V(89, 43, 4, false, 8) };
 #define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm> }
 static const BackVariant kBack[] = { BACK_V(10, 6, 4, 1, 49, DM_NONE) };
-static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, nullptr, nullptr };
+static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6>, nullptr };
 static const BackVariant kBackStereo[] = { { 10, 6, 4, 1, 49, DM_NONE, nullptr, nullptr } };
 static const NotchVariant kNotch[] = { { 4, DM_NONE, nullptr } };
 #undef BACK_V

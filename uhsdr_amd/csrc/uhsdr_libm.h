@@ -67,7 +67,7 @@ static inline const ul_sincos_t* ul_sincosf_table(int k)
     return &t[k];
 }
 
-/* sincosf.h sincosf_poly (FMA build) */
+/* sincosf.h sincosf_poly (FMA build); the quadrant swap as selects */
 UHSDR_LIBM_FN void ul_sincosf_poly(double x, double x2, const ul_sincos_t* p, int n, float* sinp, float* cosp)
 {
     const double x4 = x2 * x2;
@@ -81,37 +81,35 @@ UHSDR_LIBM_FN void ul_sincosf_poly(double x, double x2, const ul_sincos_t* p, in
     const double c = fma(x4, p->c2, c1);
     const float rs = (float)fma(x5, s1, s);
     const float rc = (float)fma(x6, c2, c);
-    if (n & 1) { *sinp = rc; *cosp = rs; }   /* quadrant swap */
-    else { *sinp = rs; *cosp = rc; }
+    *sinp = (n & 1) ? rc : rs;                       /* quadrant swap */
+    *cosp = (n & 1) ? rs : rc;
 }
 
 /* s_sincosf.c for |y| < 120 (callers guarantee the range; the Payne-Hanek branch for huge
-   arguments is not needed by the PLL) */
+   arguments is not needed by the PLL).  Branch-free: for |y| < pi/4 the reduction yields
+   n = 0, x - 0*pi/2 = x (exact) and sign +1, i.e. exactly the small branch's polynomial call,
+   so one path serves both and a wave's lanes never split between them; |y| < 2^-12 selects
+   (y, 1) at the end.  The quadrant's table is chosen by selects on its coefficients. */
 UHSDR_LIBM_FN void ul_sincosf(float y, float* sinp, float* cosp)
 {
     double x = y;
-    const ul_sincos_t* p = ul_sincosf_table(0);
-    if (ul_abstop12(y) < ul_abstop12(0x1.921fb6p-1f))        /* pio4f */
-    {
-        const double x2 = x * x;
-        if (ul_abstop12(y) < ul_abstop12(0x1p-12f))
-        {
-            *sinp = y;
-            *cosp = 1.0f;
-            return;
-        }
-        ul_sincosf_poly(x, x2, p, 0, sinp, cosp);
-    }
-    else
-    {
-        /* reduce_fast, !TOINT_INTRINSICS */
-        const double r = x * p->hpi_inv;
-        const int n = ((int32_t)r + 0x800000) >> 24;
-        x = fma(-(double)n, p->hpi, x);
-        const double s = p->sign[n & 3];
-        if (n & 2) p = ul_sincosf_table(1);
-        ul_sincosf_poly(x * s, x * x, p, n, sinp, cosp);
-    }
+    const ul_sincos_t* p0 = ul_sincosf_table(0);
+    const ul_sincos_t* p1 = ul_sincosf_table(1);
+    /* reduce_fast, !TOINT_INTRINSICS */
+    const double r = x * p0->hpi_inv;
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    x = fma(-(double)n, p0->hpi, x);
+    const double s = (n & 1) ? ((n & 2) ? p0->sign[3] : p0->sign[1]) : ((n & 2) ? p0->sign[2] : p0->sign[0]);
+    ul_sincos_t q;
+    const int h = (n & 2) != 0;
+    q.c0 = h ? p1->c0 : p0->c0; q.c1 = h ? p1->c1 : p0->c1; q.s1 = h ? p1->s1 : p0->s1;
+    q.c2 = h ? p1->c2 : p0->c2; q.s2 = h ? p1->s2 : p0->s2; q.c3 = h ? p1->c3 : p0->c3;
+    q.s3 = h ? p1->s3 : p0->s3; q.c4 = h ? p1->c4 : p0->c4;
+    float sv, cv;
+    ul_sincosf_poly(x * s, x * x, &q, n, &sv, &cv);
+    const int tiny = ul_abstop12(y) < ul_abstop12(0x1p-12f);
+    *sinp = tiny ? y : sv;
+    *cosp = tiny ? 1.0f : cv;
 }
 
 /* ---- atanf / atan2f (fdlibm binary32) ---- */

@@ -131,7 +131,8 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
         {
             float v = x[m];
             if (apply_gain) v = v * in_gain;
-            if (run_lat) v = lattice_step<S>(v, g, lk, lv);
+            // the packed lattice (uhsdr_dsp.h), pairing by the sample's parity
+            if (run_lat) v = (m & 1) ? lattice_step_pk<S, 1>(v, g, lk, lv) : lattice_step_pk<S, 0>(v, g, lk, lv);
             if (run_bq)
             {
 #pragma unroll
@@ -149,15 +150,11 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
                 const float v = tune ? x[m] : x[m] * post;
                 // ALC (tx_processor.c:197-221)
                 const float alc_var = (float)((double)(fabsf(v * alc_val) / 30000) - 1.0);
-                if (alc_var < 0)
-                {
-                    alc_val -= alc_val * decay * alc_var;
-                }
-                else
-                {
-                    alc_val = (float)((double)alc_val - (double)alc_val * 0.1 * (double)alc_var);
-                    if ((double)alc_val < 0.001) alc_val = 0.001f;
-                }
+                // both branches evaluated and selected: lanes of a wave no longer split
+                const float dec = alc_val - alc_val * decay * alc_var;
+                float att = (float)((double)alc_val - (double)alc_val * 0.1 * (double)alc_var);
+                att = ((double)att < 0.001) ? 0.001f : att;
+                alc_val = (alc_var < 0) ? dec : att;
                 if (alc_val > 1) alc_val = 1;
                 if (live) dw[(size_t)m * C] = v;                        // into the delay buffer
                 x[m] = dly[m] * (alc_val * gscale);                     // delayed audio x ALC gain

@@ -57,6 +57,7 @@ struct FrontArgs
     int lw;                  // LDS window pitch per channel (floats, multiple of 4; host picks it
                              // for conflict-free ds_read_b128, front_window_pitch)
     int comb;                // demodulator of the Hilbert pair (audio_driver.c:2755-2790, FRONT_COMB_*)
+    float* fm_prev;          // FM: [2][C] the last {I, Q} of the previous launch (rx_fm's i_prev, q_prev)
 };
 
 // what rx_front makes of the Hilbert pair (I', Q'): a_buffer[0] (and a_buffer[1] in stereo)
@@ -266,6 +267,7 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
     float* m1 = aux;
     float* m2 = aux + CPW * nblk32;
     float* osc = aux + (P->iq_auto_correction ? 2 * CPW * nblk32 : 0);
+    float* fmx = osc + ((P->freq_shift_hz != 0 && P->shift_kind == 2) ? 2 * N : 0);   // [64][2]
 
     InputStage in;
     in.gi = P->iq_gain_i; in.gq = P->iq_gain_q; in.ph = P->iq_phase_balance;
@@ -403,13 +405,50 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
             // The demodulator in rx_back / rx_fm takes both I and Q.
                 v2f d2[RD];
             fir_block2<T1, RD, M, F>(W + 2 * b * R, tA, d2);
-#pragma unroll
-            for (int r = 0; r < RD; ++r) o[r] = d2[r].x;
-            if (live)
+            if constexpr (M == 1)
             {
-                float* dst = a.adec_q + (size_t)c * a.ldd + b * RD;
+                // FM (the only undecimated pair): the discriminator's angle per sample
+                // (AudioDriver_DemodFM, audio_driver.c:1588-1592) is not recursive, so it runs
+                // here on the time-parallel lanes and rx_fm receives the angle in adec.  Each
+                // sample needs the one before: in the lane, from the lane holding block b-1 of
+                // the channel (LDS exchange), or for block 0 the previous launch's last sample.
+                // No translation: the reference skips the demodulator and keeps its state (:1548).
+                const bool translate = P->freq_shift_hz != 0;
+                if (act)
+                {
+                    fmx[2 * (g * nb + b)] = d2[RD - 1].x;
+                    fmx[2 * (g * nb + b) + 1] = d2[RD - 1].y;
+                }
+                wave_sync();
+                const int pb = 2 * (g * nb + (b > 0 ? b - 1 : 0));
+                const float li = fmx[pb], lq = fmx[pb + 1];
+                const float si = a.fm_prev[cl], sq = a.fm_prev[C + cl];
+                float ip = b > 0 ? li : si, qp = b > 0 ? lq : sq;
 #pragma unroll
-                for (int r = 0; r < RD; ++r) dst[r] = d2[r].y;
+                for (int r = 0; r < RD; ++r)
+                {
+                    const float xi = d2[r].x, xq = d2[r].y;
+                    const float y = (ip * xq) - (xi * qp);
+                    const float x = (ip * xi) + (xq * qp);
+                    o[r] = translate ? ul_atan2f(y, x) : 0.0f;
+                    ip = xi; qp = xq;
+                }
+                if (translate && live && b == nb - 1)
+                {
+                    a.fm_prev[c] = d2[RD - 1].x;
+                    a.fm_prev[C + c] = d2[RD - 1].y;
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int r = 0; r < RD; ++r) o[r] = d2[r].x;
+                if (live)
+                {
+                    float* dst = a.adec_q + (size_t)c * a.ldd + b * RD;
+#pragma unroll
+                    for (int r = 0; r < RD; ++r) dst[r] = d2[r].y;
+                }
             }
         }
         else if constexpr (!DECIM_FIRST && ST)
@@ -2064,7 +2103,7 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
         for (int i = 0; i <= SQ; ++i) sv[i] = P->sq_v[i];
 #pragma unroll
         for (int i = 0; i < SQ; ++i) g[i] = S[(7 + i) * C + cl];
-        float i_prev = S[0 * C + cl], q_prev = S[1 * C + cl], lpf_prev = S[2 * C + cl];
+        float lpf_prev = S[2 * C + cl];                   // fields 0, 1 (i_prev, q_prev): rx_front's
         float hpf_a = S[3 * C + cl], hpf_b = S[4 * C + cl], sql_avg = S[5 * C + cl];
         bool squelched = S[6 * C + cl] == 0.0f;          // field 6 = "open": zeroed state starts squelched (:475)
         const int thr = P->fm_sql_threshold;
@@ -2076,17 +2115,15 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
         int tdet = tone_en ? (int)S[20 * C + cl] : 0;
         bool detected = tone_en && S[21 * C + cl] != 0.0f;
         const bool translate = P->freq_shift_hz != 0;   // no translation: the demod bails out (:1548)
-        float inext[BLK], qnext[BLK];
+        // the discriminator's angle per sample, computed by rx_front (audio_driver.c:1588-1592)
+        float inext[BLK];
         auto fetch = [&](int call) {
             const float* si = a.adec + (size_t)cl * a.Nd + call * BLK;
-            const float* sq = a.adec_q + (size_t)cl * a.Nd + call * BLK;
 #pragma unroll
             for (int m = 0; m < BLK; m += 4)
             {
                 const float4 v = *(const float4*)(si + m);
-                const float4 w = *(const float4*)(sq + m);
                 inext[m] = v.x; inext[m + 1] = v.y; inext[m + 2] = v.z; inext[m + 3] = v.w;
-                qnext[m] = w.x; qnext[m + 1] = w.y; qnext[m + 2] = w.z; qnext[m + 3] = w.w;
             }
         };
         fetch(0);
@@ -2094,9 +2131,9 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
         {
             if (it < calls)
             {
-                float xi[BLK], xq[BLK];
+                float xa[BLK];
 #pragma unroll
-                for (int m = 0; m < BLK; ++m) { xi[m] = inext[m]; xq[m] = qnext[m]; }
+                for (int m = 0; m < BLK; ++m) xa[m] = inext[m];
                 if (it + 1 < calls) fetch(it + 1);
                 float* out = dem + (it & 1) * BLK * BACK_CH + lane;
                 if (translate)
@@ -2107,9 +2144,7 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
 #pragma unroll 4
                     for (int m = 0; m < BLK; ++m)
                     {
-                        const float y = (i_prev * xq[m]) - (xi[m] * q_prev);
-                        const float x = (i_prev * xi[m]) + (xq[m] * q_prev);
-                        const float angle = ul_atan2f(y, x);
+                        const float angle = xa[m];
                         const float aa = (float)((double)lpf_prev + (0.05 * (double)(angle - lpf_prev)));
                         lpf_prev = aa;
                         if (tone_en)
@@ -2132,8 +2167,6 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                             o = bb;
                         }
                         out[m * BACK_CH] = o;
-                        q_prev = xq[m];
-                        i_prev = xi[m];
                         // squelch HPF (:1594); the packed lattice, pairing by the sample's parity
                         const float sqo = (m & 1) ? lattice_step_pk<SQ, 1>(angle, g, sk, sv)
                                                   : lattice_step_pk<SQ, 0>(angle, g, sk, sv);
@@ -2189,7 +2222,7 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
         }
         if (live)
         {
-            S[0 * C + c] = i_prev; S[1 * C + c] = q_prev; S[2 * C + c] = lpf_prev;
+            S[2 * C + c] = lpf_prev;
             S[3 * C + c] = hpf_a; S[4 * C + c] = hpf_b; S[5 * C + c] = sql_avg;
             S[6 * C + c] = squelched ? 0.0f : 1.0f;
 #pragma unroll
@@ -2544,6 +2577,7 @@ static size_t front_lds(const uhsdr_rx_s* h)
     size_t f = (size_t)cpw * h->lw;
     if (h->plan.iq_auto_correction) f += 2 * cpw * (N / BLK);
     if (h->plan.freq_shift_hz != 0 && h->plan.shift_kind == 2) f += 2 * N;
+    f += 2 * FRONT_WAVE;                                 // FM: per-lane last {I, Q} exchange
     return f * sizeof(float);
 }
 
@@ -2835,6 +2869,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         fa.taps2a = h->d_taps2;
         fa.taps2b = h->d_taps2 + 2 * TAPS2_MAX;
         fa.comb = front_comb_of(h->plan);
+        fa.fm_prev = h->bs.sam;                          // FM: fields 0, 1 of rx_fm's state
         hipLaunchKernelGGL(h->precision == UHSDR_PRECISION_FMA ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw),
                            dim3(FRONT_WAVE), lds, h->stream, fa);
         HIPCHK(hipGetLastError());

@@ -334,7 +334,10 @@ def main():
                   "s_live_bytes_per_channel": ab["s_live_bytes"],
                   "hbm_frac": round(chain_gbs / HBM_PEAK_GBS, 4),
                   "note": "C2 (4096 channels) is latency-bound: one lane per channel for the recursive "
-                          "stages leaves most of the 256 CUs idle; see DESIGN.md and north_star"},
+                          "stages leaves most of the 256 CUs idle; see DESIGN.md and north_star"
+                          + ("; pipelined: rx_front of the next call overlaps rx_back, so the kernels' "
+                             "event times (and device_ms_per_step, their sum) exceed ms_per_step"
+                             if pipelined else "")},
         "outputs_finite": ok,
     }
     if ns:

@@ -326,7 +326,15 @@ extern "C" uhsdr_status uhsdr_fir_create(const float* coeffs, int32_t num_taps, 
     h->stream = (hipStream_t)stream;
     h->lw = (fpad(num_taps - 1 + block_size + FIR_TAIL) + 4) & ~3;
     h->cp = (h->K + 16 + 16 + 3) & ~3;
-    h->waves = 4;
+    {
+        // waves per workgroup: EXACT 2 (one group per wave, more resident waves per CU: C5
+        // 513-tap 1.048 -> 0.927 ms per call), MFMA 4 (persistent; 0.395 ms vs 0.497 at 2);
+        // benchmarking knob UHSDR_FIR_WAVES = 1, 2 or 4
+        const char* env = getenv("UHSDR_FIR_WAVES");
+        const int wv = env ? atoi(env) : mode == UHSDR_FIR_MFMA ? 4 : 2;
+        h->waves = 4;
+        if (wv == 1 || wv == 2 || wv == 4) h->waves = wv;
+    }
     while (h->waves > 1 && fir_lds(h, h->waves) > 64 * 1024) h->waves /= 2;
     if (fir_lds(h, h->waves) > 64 * 1024 || num_taps - 1 + block_size > 64 * FIR_NPL)
     {

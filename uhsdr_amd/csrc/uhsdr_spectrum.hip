@@ -28,7 +28,10 @@
 
 namespace {
 
-constexpr int SPEC_WAVES = 4;
+#ifndef UHSDR_SPEC_WAVES
+#define UHSDR_SPEC_WAVES 4
+#endif
+constexpr int SPEC_WAVES = UHSDR_SPEC_WAVES;   // waves (channels) per workgroup
 
 struct SpecArgs
 {

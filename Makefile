@@ -68,10 +68,18 @@ clean:
 
 # compile-time variants of libuhsdr_amd.so for A/B measurement (bench.py with UHSDR_LIB=<path>):
 #   make variant VTAG=w3 VFLAGS=-DUHSDR_FUSED_WAVES=3
+# every HIP source is rebuilt with VFLAGS into its own object directory, so a flag read by any
+# source takes effect (-DUHSDR_ISA_P48 builds only the P48 receive kernels: quick A/B builds)
 VARIANT_DIR := uhsdr_amd/lib/variants
-variant: $(HOST_OBJS) $(filter-out $(OBJDIR)/uhsdr_rx.o,$(HIP_OBJS))
-	mkdir -p $(VARIANT_DIR) $(OBJDIR)/v_$(VTAG)
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c uhsdr_amd/csrc/uhsdr_rx.hip -o $(OBJDIR)/v_$(VTAG)/uhsdr_rx.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(VARIANT_DIR)/libuhsdr_amd_$(VTAG).so $(HOST_OBJS) $(OBJDIR)/v_$(VTAG)/uhsdr_rx.o $(filter-out $(OBJDIR)/uhsdr_rx.o,$(HIP_OBJS)) -lm
+VOBJDIR = $(OBJDIR)/v_$(VTAG)
+VHIP_OBJS = $(patsubst uhsdr_amd/csrc/%.hip,$(VOBJDIR)/%.o,$(HIP_SRCS))
+$(OBJDIR)/v_%/.dir:
+	mkdir -p $(dir $@) && touch $@
+.PRECIOUS: $(OBJDIR)/v_%/.dir
+$(VOBJDIR)/%.o: uhsdr_amd/csrc/%.hip $(HDRS) | $(VOBJDIR)/.dir
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $< -o $@
+variant: $(HOST_OBJS) $(VHIP_OBJS)
+	mkdir -p $(VARIANT_DIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(VARIANT_DIR)/libuhsdr_amd_$(VTAG).so $(HOST_OBJS) $(VHIP_OBJS) -lm
 
 .PHONY: variant

@@ -68,7 +68,8 @@ def algorithmic_bytes(plan, C: int, N: int, write_dst: bool):
     back = C * (4 * Nd + out_b * N + 2 * 4 * back_state + ring)
     chain = C * ((8 + out_b) * N + 2 * 4 * (fir_hist + back_state) + ring)
     s_live = 4 * (fir_hist + back_state + (AGC_Q * (BLK // M) if plan.agc.mode != 5 else 0))
-    return {"rx_front": front, "rx_back": back, "chain": chain, "s_live_bytes": s_live}
+    # rx_chain (one kernel per call, the hand-off in LDS) moves exactly the chain's bytes
+    return {"rx_front": front, "rx_back": back, "rx_chain": chain, "chain": chain, "s_live_bytes": s_live}
 
 
 BLK = 32
@@ -130,14 +131,21 @@ def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
                       f"(affinity mask has {cpus} CPUs), channels split evenly; host CPU: {model}"}
 
 
+SCHEDULES = {"auto": None, "pipe": 1, "fused": 2, "chain": 3}   # uhsdr_rx_set_schedule
+SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain"}
+
+
 def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, pool, want_dst, pipelined=False,
-              precision=0):
+              precision=0, schedule=None, front_block=0):
     """W untimed + K timed steps of one RxChain on this rank; returns (max-rank seconds,
     per-kernel (total ms, launches) from HIP events on the library's stream, plan, finite)."""
     cfg = U.default_config()
     stream = torch.cuda.current_stream(dev)
-    chain = U.RxChain(cfg, channels=C, frames=N, stream=stream.cuda_stream)
+    chain = U.RxChain(cfg, channels=C, frames=N, stream=stream.cuda_stream, schedule=schedule)
     chain.set_precision(precision)
+    if front_block:
+        chain.set_front_block(front_block)
+    sched = SCHEDULE_NAMES.get(chain.schedule, str(chain.schedule))
     if pipelined:
         chain.set_pipelined(True)        # call k+1's rx_front overlaps call k's rx_back
     plan = chain.plan
@@ -177,7 +185,7 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     ok = bool(torch.isfinite(audio).all().item())
     chain.close()
     del inputs
-    return float(t.item()), ktimes, plan, ok, audio
+    return float(t.item()), ktimes, plan, ok, sched
 
 
 def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup):
@@ -241,10 +249,16 @@ def main():
                          "default pipelined mode (uhsdr_rx_set_pipelined: call k+1's rx_front overlaps "
                          "call k's rx_back); the 1M-channel north-star leg always runs serial (both "
                          "kernels fill the chip there)")
-    ap.add_argument("--pipelined", action="store_true", help="(default; kept for old command lines)")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="pipelined mode even on the north-star workload (default on for the others)")
     ap.add_argument("--precision", default="exact", choices=["exact", "fma"],
                     help="FIR MACs: exact (bit-identical to the reference) or fma (1e-5 normwise)")
     ap.add_argument("--pool", type=int, default=8, help="distinct input blocks cycled through")
+    ap.add_argument("--schedule", default="auto", choices=sorted(SCHEDULES),
+                    help="kernel schedule of a call (uhsdr_rx_set_schedule); auto: the library's choice "
+                         "(rx_chain from 131072 channels on, else rx_front + the back-end wave pipeline)")
+    ap.add_argument("--front-block", type=int, default=0, choices=[0, 8, 16],
+                    help="FIR outputs per lane of rx_front (uhsdr_rx_set_front_block; 0: the library default)")
     args = ap.parse_args()
 
     import torch
@@ -265,9 +279,10 @@ def main():
     wl = WORKLOADS[args.workload]
     C = args.channels or wl["channels"]
     N = args.frames or wl["frames"]
-    pipelined = not args.serial and args.workload != "northstar"
-    elapsed, ktimes, plan, ok, _ = timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, args.steps,
-                                             args.warmup, max(1, args.pool), args.dst, pipelined, prec)
+    pipelined = args.pipelined or (not args.serial and args.workload != "northstar")
+    elapsed, ktimes, plan, ok, sched = timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, args.steps,
+                                                 args.warmup, max(1, args.pool), args.dst, pipelined, prec,
+                                                 SCHEDULES[args.schedule], args.front_block)
 
     gather = None
     if world > 1 and not args.no_gather:
@@ -280,8 +295,8 @@ def main():
 
     def north_star_leg(precision):
         nw = WORKLOADS["northstar"]
-        n_el, n_kt, n_plan, n_ok, _ = timed_run(U, synth, shard, torch, dist, dev, 1, 0, nw["channels"], nw["frames"],
-                                                NS_STEPS, 10, 3, False, False, precision)
+        n_el, n_kt, n_plan, n_ok, n_sched = timed_run(U, synth, shard, torch, dist, dev, 1, 0, nw["channels"],
+                                                      nw["frames"], NS_STEPS, 10, 3, False, False, precision)
         n_ab = algorithmic_bytes(n_plan, nw["channels"], nw["frames"], False)
         n_roof, n_kms = roofline_of(n_ab, n_kt, pmc_traffic("northstar" if precision == U.PRECISION_EXACT
                                                             else "northstar_fma"))
@@ -291,7 +306,7 @@ def main():
                 "kernel_ms": {k: round(v, 5) for k, v in n_kms.items()},
                 "chain_hbm_frac": round(n_ab["chain"] / (n_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "alg_bytes_per_sample": round(n_ab["chain"] / (nw["channels"] * nw["frames"]), 2),
-                "outputs_finite": n_ok}
+                "schedule": n_sched, "outputs_finite": n_ok}
 
     ns = None
     if world == 1 and not args.no_northstar and args.workload != "northstar" and not (args.channels or args.frames):
@@ -326,7 +341,7 @@ def main():
                    "channels_per_gpu": C, "frames_per_call": N, "filter_path": int(plan.filter_path),
                    "parallelism": f"channel-sharded x{world}, no data-path collective",
                    "outputs": "f32 audio" + (" + int32 codec frames" if args.dst else ""),
-                   "pipelined": pipelined, "precision": args.precision},
+                   "pipelined": pipelined, "precision": args.precision, "schedule": sched},
         "roofline": roofline,
         "chain": {"device_ms_per_step": round(chain_dev_ms, 5),
                   "kernel_ms": {k: round(v, 5) for k, v in kms.items()},

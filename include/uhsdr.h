@@ -274,6 +274,27 @@ uhsdr_status uhsdr_rx_set_precision(uhsdr_rx_handle h, int32_t precision);
 int32_t      uhsdr_rx_get_precision(uhsdr_rx_handle h);   /* -1 for a null handle */
 uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h);
 
+/* Kernel schedule of a call (a launch-shape choice: outputs are bit-identical under every one).
+ *   AUTO        (default) CHAIN where supported from 131072 channels on, else SPLIT_FUSED from
+ *               131072 channels on, else SPLIT_PIPE
+ *   SPLIT_PIPE  rx_front, then rx_back: one wave per back-end stage, a pipeline over 32-frame
+ *               calls (short per-call critical path: small batches)
+ *   SPLIT_FUSED rx_front, then rx_back_fused: every back-end stage in one wave per 64 channels
+ *   CHAIN       rx_chain: one kernel, each wave runs the front passes of its 64 channels and then
+ *               their back end, the decimated hand-off kept in LDS (large batches).  SSB / CW /
+ *               DIGI mono paths (no notch, no stereo, not AM / SAM / FM) with one front pass per
+ *               call; elsewhere UHSDR_UNSUPPORTED.
+ * Stereo, AM / SAM / FM and the LMS notch have their own back-end kernels and ignore SPLIT_*.
+ * Returns UHSDR_UNSUPPORTED (handle unchanged) for a schedule the handle's path cannot run.
+ * Takes effect from the next uhsdr_rx_process; get returns the resolved schedule. */
+enum { UHSDR_SCHEDULE_AUTO = 0, UHSDR_SCHEDULE_SPLIT_PIPE = 1, UHSDR_SCHEDULE_SPLIT_FUSED = 2,
+       UHSDR_SCHEDULE_CHAIN = 3 };
+uhsdr_status uhsdr_rx_set_schedule(uhsdr_rx_handle h, int32_t schedule);
+int32_t      uhsdr_rx_get_schedule(uhsdr_rx_handle h);    /* -1 for a null handle */
+/* FIR outputs per lane of the front passes: 8 (default: more waves per batch) or 16 (fewer LDS
+   window reads per MAC); UHSDR_UNSUPPORTED when the call size does not admit it.  Bit-identical. */
+uhsdr_status uhsdr_rx_set_front_block(uhsdr_rx_handle h, int32_t outputs_per_lane);
+
 /* ---- status side outputs: the RX chain's signals to the control plane ----
  * ADC clip indicators (audio_driver.c:2660-2676): per channel, the sticky flags ads.adc_clip /
  * ads.adc_half_clip / ads.adc_quarter_clip, set when |I| >> 16 of any frame exceeds
@@ -554,7 +575,8 @@ const char*  uhsdr_version(void);
 int32_t      uhsdr_sizeof_config(void);
 int32_t      uhsdr_sizeof_plan(void);
 const char*  uhsdr_last_error(void);
-/* number of kernels one uhsdr_rx_process call enqueues */
+/* number of kernel slots uhsdr_rx_kernel_times reports: rx_front, rx_back (any back-end kernel),
+   rx_chain; a call enqueues rx_front + rx_back, or rx_chain alone */
 int32_t      uhsdr_rx_kernel_count(uhsdr_rx_handle h);
 /* Per-kernel device timing: while enabled (enable = k > 0), every k-th uhsdr_rx_process call
    (the 1st, (k+1)-th, ...) brackets each kernel with hipEvents on the stream it runs on; k = 1

@@ -29,9 +29,15 @@ def cuda():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(params=["pipe", "fused"])
+SCHEDULES = {"pipe": 1, "fused": 2, "chain": 3}   # uhsdr_rx_set_schedule values
+
+
+@pytest.fixture(params=["pipe", "fused", "chain"])
 def back(request, monkeypatch):
-    """Both back-end kernels: the wave pipeline (rx_back, small batches) and the fused
-    one-wave-per-64-channels kernel (rx_back_fused, large batches), forced per handle."""
-    monkeypatch.setenv("UHSDR_BACK_FUSED", "1" if request.param == "fused" else "0")
+    """Every kernel schedule of a call: the back-end wave pipeline (rx_back, small batches), the
+    fused one-wave-per-64-channels back end (rx_back_fused), and the one-kernel rx_chain (front
+    passes + fused back end per wave, large batches), forced on every RxChain the test makes.
+    rx_chain covers the SSB / CW / DIGI mono paths; elsewhere its handles keep the AUTO choice."""
+    from uhsdr_amd import rx
+    monkeypatch.setattr(rx, "DEFAULT_SCHEDULE", SCHEDULES[request.param])
     return request.param

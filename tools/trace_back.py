@@ -19,8 +19,7 @@ def main():
     from uhsdr_amd import synth
     Cn = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-    os.environ["UHSDR_BACK_FUSED"] = "0"
-    chain = U.RxChain(U.default_config(), channels=Cn, frames=N)
+    chain = U.RxChain(U.default_config(), channels=Cn, frames=N, schedule=U.SCHEDULE_SPLIT_PIPE)
     x = synth.ssb_iq_torch(0, Cn, 0, N, "cuda")
     audio = torch.empty((Cn, N), dtype=torch.float32, device="cuda")
     for _ in range(5):

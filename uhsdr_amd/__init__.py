@@ -7,7 +7,8 @@ from ._abi import (RxConfig, RxPlan, build_plan, plan_supported, config_from_ref
                    DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI,
                    DEMOD_SSBSTEREO, DEMOD_IQ, SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB,
                    SAM_SIDEBAND_STEREO, DSP_NOTCH_ENABLE,
-                   PRECISION_EXACT, PRECISION_FMA, ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP,
+                   PRECISION_EXACT, PRECISION_FMA,
+                   SCHEDULE_AUTO, SCHEDULE_SPLIT_PIPE, SCHEDULE_SPLIT_FUSED, SCHEDULE_CHAIN, ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP,
                    TWINPEAKS_SAMPLING, TWINPEAKS_DONE, TWINPEAKS_WAIT, TWINPEAKS_UNCORRECTABLE,
                    TWINPEAKS_CODEC_RESTART,
                    TUNE_OFF, TUNE_SINGLE, TUNE_TWO,

@@ -28,6 +28,7 @@ DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI, DEMOD
 SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB, SAM_SIDEBAND_STEREO = range(4)
 DSP_NOTCH_ENABLE, DSP_MNOTCH_ENABLE, DSP_MPEAK_ENABLE = 0x04, 0x10, 0x20
 PRECISION_EXACT, PRECISION_FMA = 0, 1          # uhsdr_rx_set_precision
+SCHEDULE_AUTO, SCHEDULE_SPLIT_PIPE, SCHEDULE_SPLIT_FUSED, SCHEDULE_CHAIN = range(4)   # uhsdr_rx_set_schedule
 ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP = 1, 2, 4   # uhsdr_rx_set_clip_output bits
 TWINPEAKS_SAMPLING, TWINPEAKS_DONE, TWINPEAKS_WAIT, TWINPEAKS_UNCORRECTABLE, TWINPEAKS_CODEC_RESTART = range(5)
 
@@ -181,6 +182,9 @@ SIGNATURES = {
     "uhsdr_rx_join": (C.c_int, [C.c_void_p]),
     "uhsdr_rx_set_precision": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_rx_get_precision": (C.c_int32, [C.c_void_p]),
+    "uhsdr_rx_set_schedule": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_rx_get_schedule": (C.c_int32, [C.c_void_p]),
+    "uhsdr_rx_set_front_block": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_rx_set_cw_outputs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "uhsdr_rx_cw_blocks_max": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_cw_blocks_last": (C.c_int32, [C.c_void_p]),

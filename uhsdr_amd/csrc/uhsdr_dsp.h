@@ -26,8 +26,8 @@ typedef float vf4 __attribute__((ext_vector_type(4)));
 // of T % 8: the register window (WA samples, a multiple of 8) slides by 8 samples per chunk and
 // the next 8 samples (two ds_read_b128) and taps are fetched before the current MACs, so the
 // live set stays at R accumulators + one window; the chunk loop is unrolled by the window's
-// rotation period, which turns the slide into register renaming.  Reads run up to 22 samples
-// past the last one used (zeroed).
+// rotation period, which turns the slide into register renaming.  Reads run up to FRONT_TAIL
+// samples past the last one used.
 // LDS load of V (4 or 2) consecutive floats into w[j..j+V)
 template <int V, int N>
 __device__ __forceinline__ void lds_vec(const float* p, float (&w)[N], int j)
@@ -162,8 +162,10 @@ __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&
     }
 }
 
-// samples zeroed after the end of a window (fir_block over-read, see above)
-constexpr int FRONT_TAIL = 24;
+// samples after the end of a window that the register-window FIRs read (never use): the last
+// chunk's next-8 prefetch runs -R + 8*floor(T/8) + WA - T + 1 samples past the data, at most 8
+// for every (T, R, M) instantiated here; zeroed all the same
+constexpr int FRONT_TAIL = 8;
 
 // LDS accesses of one wave are processed in order; the fences only stop the compiler from
 // moving a lane's LDS access across a hand-off between lanes of the same wave.

@@ -243,17 +243,18 @@ __device__ __forceinline__ void convert_block(const int4 (&raw)[R / 2], const In
 // ST: use_stereo (DEMOD_SSBSTEREO / DEMOD_IQ): both channels of the pair continue -- through a
 // decimator pair (DECIMATE_RX_I / _Q, audio_driver.c:2792-2801) on the Hilbert-first paths --
 // into adec (a_buffer[0]) and adec_q (a_buffer[1])
-template <int T1, int T2, int M, bool DECIM_FIRST, int R, bool F, bool ST = false>
-__global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
+// The pass of one channel group `grp` (CPW channels) by one wave over its LDS region `smem`.
+// Its decimated output o[RD] (lane: channel g of the group, block b) goes to `sink(live, c, g, b,
+// o)`: rx_front's sink stores it to adec in HBM, rx_chain's keeps it in LDS for the back end.
+template <int T1, int T2, int M, bool DECIM_FIRST, int R, bool F, bool ST, typename Sink>
+__device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, float* smem, Sink&& sink)
 {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     const int N = a.N, C = a.C;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & (FRONT_WAVE - 1);
     const int nb = N / R;                            // lanes per channel (>= 4)
     const int CPW = FRONT_WAVE / nb;                 // channels per wave (one channel group)
     // (Measured and dropped: four independent waves per workgroup, 0.617 vs 0.600 ms at 1M x 64.)
-    const int grp = blockIdx.x;
     int g, b;
     front_lane(lane, nb, 2 * R, g, b);               // lane map for the pair window (2R floats per lane)
     const bool act = g < CPW;
@@ -322,7 +323,7 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
                 vq = gn * vq; vi = gn * vi;
             }
         }
-        if (blockIdx.x == 0) { a.osc_out[0] = vi; a.osc_out[1] = vq; }
+        if (grp == 0) { a.osc_out[0] = vi; a.osc_out[1] = vq; }
     }
 
     {
@@ -528,8 +529,19 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
                 front_comb_block<RD>(comb, h2, o);
             }
         }
-        if (live)
+        sink(live, c, g, b, o);
+    }
+}
+
+template <int T1, int T2, int M, bool DECIM_FIRST, int R, bool F, bool ST = false>
+__global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int RD = R / M;
+    front_body<T1, T2, M, DECIM_FIRST, R, F, ST>(a, blockIdx.x, smem,
+        [&](bool live, int c, int, int b, const float (&o)[RD])
         {
+            if (!live) return;
             float* dst = a.adec + (size_t)c * a.ldd + b * RD;
             if (RD % 4 == 0)
             {
@@ -541,8 +553,7 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
 #pragma unroll
                 for (int r = 0; r < RD; ++r) dst[r] = o[r];
             }
-        }
-    }
+        });
 }
 
 // ------------------------------------------------------------------------------------
@@ -694,10 +705,12 @@ struct BackLane
 {
     int lane, c, cl, C, calls;
     bool live;
-    __device__ __forceinline__ explicit BackLane(const BackArgs& a)
+    __device__ __forceinline__ explicit BackLane(const BackArgs& a) : BackLane(a, blockIdx.x) {}
+    // channel group grp (channels 64 grp ..): rx_chain's waves name their group themselves
+    __device__ __forceinline__ BackLane(const BackArgs& a, int grp)
     {
         lane = threadIdx.x & (BACK_CH - 1);
-        c = blockIdx.x * BACK_CH + lane;
+        c = grp * BACK_CH + lane;
         live = c < a.C;
         cl = live ? c : a.C - 1;
         C = a.C;
@@ -711,14 +724,27 @@ struct BackLane
 // wave; the fused kernel (rx_back_fused) runs all of them per sample in one wave.
 
 // ---- input stage (SSB / CW / DIGI): rx_front's decimated I +- Q, fetched one call ahead ----
-template <int L>
+// LDS_IN (rx_chain): the decimated samples come from the wave's own LDS hand-off `lds`,
+// [sample][lane] with row pitch CHAIN_ADP, instead of adec in HBM
+constexpr int CHAIN_ADP = BACK_CH + 4;
+template <int L, bool LDS_IN = false>
 struct InStage
 {
     static constexpr int NDC = BLK / L;
     float xnext[NDC];
+    const float* lds;
 
     __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
     {
+        if constexpr (LDS_IN)
+        {
+            // a lane past the last channel reads channel C-1's column (the clamped-load rule: it
+            // then stores exactly what that channel stores to the same ring address)
+            const int col = l.cl - (l.c - l.lane);
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) xnext[m] = lds[(call * NDC + m) * CHAIN_ADP + col];
+            return;
+        }
         // uniform row base (SGPRs) + the lane's 32-bit offset: no 64-bit per-lane address to keep
         const float* src = a.adec + call * NDC;
         const unsigned off = (unsigned)l.cl * (unsigned)a.Nd;
@@ -1715,7 +1741,7 @@ __device__ __forceinline__ void fused_store_call(const BackArgs& a, const BackLa
     wave_sync();                                         // the wave's rows are complete
     const int g = l.lane >> 3, j = l.lane & 7;
     const bool beep = a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK;
-    const int c0 = blockIdx.x * BACK_CH;
+    const int c0 = l.c - l.lane;
 #pragma unroll
     for (int k = 0; k < 8; ++k)
     {
@@ -1751,16 +1777,19 @@ __device__ __forceinline__ void fused_store_call(const BackArgs& a, const BackLa
 // AGC_ON (mode != 5) and CW (decoder front end) are launch constants, made compile-time so the
 // per-sample code carries no uniform branches; the AGC's DC removal is on for AM / SAM (compile-
 // time for the demodulating bodies, a select behind rx_notch)
-template <int PRE, int AA, int L, int PH, int W, int DM, bool AGC_ON, bool CW>
-__device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys)
+// LDS_IN (rx_chain): channel group grp, input from the wave's LDS hand-off adl
+template <int PRE, int AA, int L, int PH, int W, int DM, bool AGC_ON, bool CW, bool LDS_IN = false>
+__device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys, int grp, const float* adl = nullptr)
 {
-    const BackLane l(a);
+    const BackLane l(a, grp);
     constexpr int NDC = BLK / L;
     static_assert(L == 2 || L == 4, "4 output frames per 1 or 2 decimated samples");
+    static_assert(!LDS_IN || DM == DM_NONE, "rx_chain: SSB / CW / DIGI back ends only");
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     const uhsdr_agc_plan A = P->agc;
     DemodStage<L, DM> dm;
-    InStage<L> in;
+    InStage<L, LDS_IN> in;
+    in.lds = adl;
     LatticeStage<PRE, UHSDR_FUSED_PK> pre;
     AgcStage<L, W> ag;
     AudioStage<L, PH, DM> au;
@@ -1823,11 +1852,11 @@ __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys)
 }
 
 // runs the body with the launch's AGC / CW flags as template arguments
-template <int PRE, int AA, int L, int PH, int W, int DM, bool CW>
-__device__ __forceinline__ void back_fused_agc(const BackArgs& a, float* ys)
+template <int PRE, int AA, int L, int PH, int W, int DM, bool CW, bool LDS_IN = false>
+__device__ __forceinline__ void back_fused_agc(const BackArgs& a, float* ys, int grp, const float* adl = nullptr)
 {
-    if (a.plan->agc.mode == 5) back_fused_body<PRE, AA, L, PH, W, DM, false, CW>(a, ys);
-    else back_fused_body<PRE, AA, L, PH, W, DM, true, CW>(a, ys);
+    if (a.plan->agc.mode == 5) back_fused_body<PRE, AA, L, PH, W, DM, false, CW, LDS_IN>(a, ys, grp, adl);
+    else back_fused_body<PRE, AA, L, PH, W, DM, true, CW, LDS_IN>(a, ys, grp, adl);
 }
 
 template <int PRE, int AA, int L, int PH, int W, int DM>
@@ -1836,9 +1865,47 @@ __global__ void __launch_bounds__(BACK_CH) __attribute__((amdgpu_waves_per_eu(DM
     __shared__ float ys[BACK_CH * FUSED_YPITCH];
     if constexpr (L == 4)
     {
-        if (a.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM, true>(a, ys); return; }
+        if (a.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM, true>(a, ys, blockIdx.x); return; }
     }
-    back_fused_agc<PRE, AA, L, PH, W, DM, false>(a, ys);
+    back_fused_agc<PRE, AA, L, PH, W, DM, false>(a, ys, blockIdx.x);
+}
+
+// ------------------------------------------------------------------------------------
+// rx_chain: the whole call in one kernel for large batches (SSB / CW / DIGI, mono).  One wave
+// owns 64 channels: it runs rx_front's pass over them CPW channels at a time (64 / CPW passes,
+// the decimated output of each kept in LDS, [sample][channel] with pitch CHAIN_ADP), then
+// rx_back_fused's per-sample recursions with lane == channel, reading that LDS instead of adec.
+// The decimated hand-off never reaches HBM and there is no kernel boundary; since every wave
+// alternates a FIR phase (VALU + HBM stream) and a recursion phase (dependent VALU chains),
+// waves in different phases share a SIMD and its HBM stream.  The register budget is the back
+// end's (2 waves per SIMD); the front window and the back's output staging share one LDS region.
+template <int T1, int T2, int M, bool DF, int R, bool F, int PRE, int AA, int L, int PH, int W>
+__global__ void __launch_bounds__(FRONT_WAVE) __attribute__((amdgpu_waves_per_eu(UHSDR_FUSED_WAVES)))
+rx_chain(FrontArgs fa, BackArgs ba, int front_floats)
+{
+    static_assert(M == L, "decimation and interpolation rates agree");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int RD = R / M;
+    float* adl = smem + front_floats;                  // [N / M][CHAIN_ADP]
+    const int nb = fa.N / R, cpw = FRONT_WAVE / nb, passes = BACK_CH / cpw;
+    const int grp = blockIdx.x;
+    for (int p = 0; p < passes; ++p)
+    {
+        if ((grp * passes + p) * cpw >= fa.C) break;   // past the last channel (wave-uniform)
+        front_body<T1, T2, M, DF, R, F, false>(fa, grp * passes + p, smem,
+            [&](bool, int, int g, int b, const float (&o)[RD])
+            {
+                float* d = adl + p * cpw + g;
+#pragma unroll
+                for (int r = 0; r < RD; ++r) d[(b * RD + r) * CHAIN_ADP] = o[r];
+            });
+        wave_sync();                                   // the window region is reused by the next pass
+    }
+    if constexpr (L == 4)
+    {
+        if (ba.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM_NONE, true, true>(ba, smem, grp, adl); return; }
+    }
+    back_fused_agc<PRE, AA, L, PH, W, DM_NONE, false, true>(ba, smem, grp, adl);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2297,8 +2364,13 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
 typedef void (*front_fn)(FrontArgs);
 typedef void (*back_fn)(BackArgs);
 
+typedef void (*chain_fn)(FrontArgs, BackArgs, int);
 struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; front_fn fn_fma; int st; };
 struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; };
+// rx_chain instances: a front family (t1, t2, m, decim_first, R = 8) with a DM_NONE back end
+struct ChainVariant { int t1, t2, m, decim_first, R, pre, aa, L, ph, w; chain_fn fn, fn_fma; };
+#define CHAIN_V(t1, t2, m, df, pre, aa, ph, w) { t1, t2, m, df, 8, pre, aa, m, ph, w, \
+    rx_chain<t1, t2, m, df, 8, false, pre, aa, m, ph, w>, rx_chain<t1, t2, m, df, 8, true, pre, aa, m, ph, w> }
 
 // R = FIR outputs per lane: 16 for large batches (more MACs per window load), 8 for small
 // batches (twice the waves in flight).  fn: reference MAC order (bit-exact); fn_fma: fused MACs
@@ -2314,6 +2386,7 @@ static const BackVariant kBack[] = { BACK_V(10, 6, 4, 1, 49, DM_NONE) };
 static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6>, nullptr };
 static const BackVariant kBackStereo[] = { { 10, 6, 4, 1, 49, DM_NONE, nullptr, nullptr } };
 static const NotchVariant kNotch[] = { { 4, DM_NONE, nullptr } };
+static const ChainVariant kChain[] = { CHAIN_V(89, 43, 4, false, 10, 6, 1, 49) };
 #undef BACK_V
 #undef FRONT_V
 #undef FRONT_ST
@@ -2371,7 +2444,21 @@ static const NotchVariant kNotch[] = {
     { 4, DM_SAM_ST, rx_notch<4, DM_SAM_ST> }, { 2, DM_SAM_ST, rx_notch<2, DM_SAM_ST> },
 };
 
+// one front pass + back end per wave: the SSB / CW / DIGI families of kFront x kBack (DM_NONE)
+static const ChainVariant kChain[] = {
+    CHAIN_V(89, 43, 4, false, 10, 6, 1, 49),             // wide SSB, 12 ksps (P48 ...)
+    CHAIN_V(89, 43, 4, false, 10, 0, 4, 49),
+    CHAIN_V(83, 199, 4, true, 10, 6, 1, 49),             // narrow SSB / CW, 12 ksps
+    CHAIN_V(83, 199, 4, true, 10, 0, 4, 49),
+    CHAIN_V(89, 4, 2, false, 0, 0, 8, 97),               // 24 ksps SSB
+    CHAIN_V(89, 4, 2, false, 0, 6, 2, 97),
+    CHAIN_V(89, 4, 2, false, 10, 0, 8, 97),
+    CHAIN_V(89, 4, 2, false, 8, 0, 8, 97),
+    CHAIN_V(89, 4, 2, false, 8, 6, 2, 97),
+};
+
 #endif
+#undef CHAIN_V
 
 static int plan_dm(const uhsdr_rx_plan& p)
 {
@@ -2385,25 +2472,35 @@ static int plan_dm(const uhsdr_rx_plan& p)
 // frames handled by one front launch: one wave covers a channel's launch block
 static int front_frames(int N, int R) { return N < FRONT_WAVE * R ? N : FRONT_WAVE * R; }
 
-// C, N == 0: support query.  R = 8 by default: more waves per batch, and its 8+ lanes per
-// channel prefetch whole history rows; UHSDR_FRONT_R=16 selects the 16-output blocks
-// (benchmarking knob).
-static const FrontVariant* find_front(const uhsdr_rx_plan& p, long long C = 0, int N = 0)
+// N == 0: support query.  want: outputs per lane, 8 by default (more waves per batch, and its
+// 8+ lanes per channel prefetch whole history rows) or 16 (uhsdr_rx_set_front_block); strict:
+// only that R, else the nearest the call size admits.
+static const FrontVariant* find_front(const uhsdr_rx_plan& p, int N = 0, int want = 8, bool strict = false)
 {
-    (void)C;
     const int t1 = p.use_decimated_iq ? p.dec_taps : p.hilbert_taps;
     const int t2 = p.use_decimated_iq ? p.hilbert_taps : p.dec_taps;
-    const char* env = getenv("UHSDR_FRONT_R");
-    const int want = env ? atoi(env) : 8;
     const int st = p.stereo == 1 || p.stereo == 2;       // SAM stereo splits in the demodulator
     const FrontVariant* best = nullptr;
     for (const FrontVariant& v : kFront)
         if (v.t1 == t1 && v.t2 == t2 && v.m == p.decimation_rate && v.decim_first == p.use_decimated_iq && v.st == st)
         {
             if (N && (N % v.R || front_frames(N, v.R) / v.R < 4)) continue;   // >= 4 lanes per channel
+            if (strict && v.R != want) continue;
             if (!best || (v.R == want && best->R != want)) best = &v;
         }
     return best;
+}
+
+static const ChainVariant* find_chain(const uhsdr_rx_plan& p, const BackVariant* bv)
+{
+    if (!bv || bv->dm != DM_NONE || p.stereo || p.notch_enabled || p.dmod_mode == UHSDR_DEMOD_FM) return nullptr;
+    const int t1 = p.use_decimated_iq ? p.dec_taps : p.hilbert_taps;
+    const int t2 = p.use_decimated_iq ? p.hilbert_taps : p.dec_taps;
+    for (const ChainVariant& v : kChain)
+        if (v.t1 == t1 && v.t2 == t2 && v.m == p.decimation_rate && v.decim_first == p.use_decimated_iq &&
+            v.pre == bv->pre && v.aa == bv->aa && v.L == bv->L && v.ph == bv->ph && v.w == bv->w)
+            return &v;
+    return nullptr;
 }
 
 static const NotchVariant* find_notch(const uhsdr_rx_plan& p)
@@ -2439,7 +2536,6 @@ static const BackVariant* find_back(const uhsdr_rx_plan& p)
 
 constexpr int TAPS2_MAX = (UHSDR_MAX_FIR_TAPS + 7) & ~7;   // taps per pair table
 constexpr int BACK_FUSED_MIN_CHANNELS = 131072;   // measured crossover (64-frame calls)
-enum { BACK_PIPE = 0, BACK_FUSED = 1 };
 
 // pipelined mode: hand-off buffers in rotation, so rx_front can run up to two calls ahead of
 // rx_back and the side stream's wait on it is already satisfied when rx_back gets there
@@ -2452,9 +2548,10 @@ struct uhsdr_rx_s
     const FrontVariant* fv;
     const BackVariant* bv;
     const NotchVariant* nv;  // LMS auto notch kernel (null: notch off)
+    const ChainVariant* cv;  // rx_chain instance of the path (null: none)
     int C, N, Nd, Nf;        // Nf: frames per front launch (N split into N / Nf launches)
     int lw;                  // front LDS window pitch (floats)
-    int back_mode;           // BACK_PIPE (rx_back) or BACK_FUSED (rx_back_fused)
+    int schedule;            // resolved UHSDR_SCHEDULE_SPLIT_PIPE / _SPLIT_FUSED / _CHAIN
     int precision;           // UHSDR_PRECISION_EXACT / _FMA (front FIR MACs)
     int T1, T2;
     hipStream_t stream;
@@ -2490,12 +2587,15 @@ struct uhsdr_rx_s
     long long tcalls;         // calls since timing was enabled
     int nev;
     int nev_cap;
-    hipEvent_t* ev;          // [cap][2 kernels][start, stop]
-    float total_ms[2];
-    int launches[2];
+    hipEvent_t* ev;          // [cap][NKERN kernels][start, stop]
+    uint8_t* evmask;         // [cap] kernels recorded in each timed call
+    float total_ms[3];
+    int launches[3];
 };
 
-static const char* kKernelNames[2] = { "rx_front", "rx_back" };
+// kernel slots of the timing API: a call runs rx_front + rx_back (any back-end kernel) or rx_chain
+enum { K_FRONT = 0, K_BACK = 1, K_CHAIN = 2, NKERN = 3 };
+static const char* kKernelNames[NKERN] = { "rx_front", "rx_back", "rx_chain" };
 
 static bool side_mode(const uhsdr_rx_s* h) { return h->pipelined; }
 static hipStream_t back_stream(const uhsdr_rx_s* h) { return side_mode(h) ? h->side : h->stream; }
@@ -2503,7 +2603,8 @@ static hipStream_t back_stream(const uhsdr_rx_s* h) { return side_mode(h) ? h->s
 static void time_mark(uhsdr_rx_s* h, int k, int which)
 {
     if (!h->tsample) return;
-    (void)hipEventRecord(h->ev[(size_t)h->nev * 4 + 2 * k + which], k ? back_stream(h) : h->stream);
+    (void)hipEventRecord(h->ev[((size_t)h->nev * NKERN + k) * 2 + which], k == K_BACK ? back_stream(h) : h->stream);
+    if (which) h->evmask[h->nev] |= (uint8_t)(1u << k);
 }
 
 // every call enqueued so far, on both streams, has finished
@@ -2519,10 +2620,11 @@ static void time_harvest(uhsdr_rx_s* h)
     if (!h->nev) return;
     (void)sync_all(h);
     for (int i = 0; i < h->nev; ++i)
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < NKERN; ++k)
         {
             float ms = 0.0f;
-            if (hipEventElapsedTime(&ms, h->ev[(size_t)i * 4 + 2 * k], h->ev[(size_t)i * 4 + 2 * k + 1]) == hipSuccess)
+            const size_t e = ((size_t)i * NKERN + k) * 2;
+            if ((h->evmask[i] >> k & 1) && hipEventElapsedTime(&ms, h->ev[e], h->ev[e + 1]) == hipSuccess)
             {
                 h->total_ms[k] += ms;
                 h->launches[k] += 1;
@@ -2537,6 +2639,19 @@ static void time_harvest(uhsdr_rx_s* h)
 // a multiple of 4 floats, chosen among 16 candidates for the fewest ds_read bank conflicts
 // Pass 1 is always a FIR pair over an interleaved window (2 floats per sample); pass 2 is the
 // scalar audio decimator (Hilbert-first paths) or the Hilbert pair (decimate-first paths).
+static size_t front_lds_extra(const uhsdr_rx_s* h);
+constexpr size_t LDS_PER_CU = 160 * 1024;           // MI355X_MICROARCH.md §LDS
+
+// waves per CU a kernel's register allocation allows (MI355X_MICROARCH.md §Register files:
+// granule 8, 512 VGPRs + AGPRs per lane per SIMD, at most 8 waves per SIMD)
+static int kernel_waves_per_cu(const void* fn)
+{
+    hipFuncAttributes at;
+    if (hipFuncGetAttributes(&at, fn) != hipSuccess || at.numRegs <= 0) return 16;
+    const int alloc = (at.numRegs + 7) & ~7;
+    const int w = 512 / alloc;
+    return 4 * (w > 8 ? 8 : w);
+}
 static int front_window_pitch(const uhsdr_rx_s* h)
 {
     const int N = h->Nf, R = h->fv->R, M = h->plan.decimation_rate;
@@ -2548,12 +2663,21 @@ static int front_window_pitch(const uhsdr_rx_s* h)
     const int need2 = h->T2 ? (pair2 ? 2 : 1) * (h->T2 - 1 + n2 + FRONT_TAIL) : 0;
     need = ((need > need2 ? need : need2) + 3) & ~3;
     const int rd = R / M;
-    int best = need, best_cost = 1 << 30;
+    // the front is occupancy-sensitive (LDS per wave sets its waves per CU): the fewest window-read
+    // conflicts among the pitches that keep the most waves per CU
+    const size_t extra = front_lds_extra(h);
+    const int vgpr_waves = kernel_waves_per_cu((const void*)h->fv->fn);
+    int best = need, best_cost = 1 << 30, best_waves = 0;
     for (int lw = need; lw < need + 64; lw += 4)
     {
         int cost = window_conflicts(lw, nb, cpw, 2 * R, 2 * R, 4);
         if (h->T2) cost += window_conflicts(lw, nb, cpw, 2 * R, df ? 2 * rd : pair2 ? 2 * R : R, 4);
-        if (cost < best_cost) { best_cost = cost; best = lw; }
+        int waves = (int)(LDS_PER_CU / (sizeof(float) * ((size_t)cpw * lw + extra)));
+        waves = waves > vgpr_waves ? vgpr_waves : waves;
+#ifdef UHSDR_PITCH_CONFLICTS_ONLY
+        waves = 0;
+#endif
+        if (waves > best_waves || (waves == best_waves && cost < best_cost)) { best_cost = cost; best = lw; best_waves = waves; }
     }
     return best;
 }
@@ -2570,15 +2694,82 @@ static void pair_taps(float* dst, const float* c0, const float* c1, int T)
 }
 
 // LDS of one front workgroup (one wave): must match the carve-up in rx_front
+// floats after the windows: auto-IQ factors, oscillator trajectory, FM exchange
+static size_t front_lds_extra(const uhsdr_rx_s* h)
+{
+    const int N = h->Nf;
+    const int cpw = FRONT_WAVE / (N / h->fv->R);
+    size_t f = 0;
+    if (h->plan.iq_auto_correction) f += 2 * cpw * (N / BLK);
+    if (h->plan.freq_shift_hz != 0 && h->plan.shift_kind == 2) f += 2 * N;
+    if (h->fv->m == 1) f += 2 * FRONT_WAVE;              // FM: per-lane last {I, Q} exchange
+    return f;
+}
+
 static size_t front_lds(const uhsdr_rx_s* h)
 {
     const int N = h->Nf;
     const int cpw = FRONT_WAVE / (N / h->fv->R);
-    size_t f = (size_t)cpw * h->lw;
-    if (h->plan.iq_auto_correction) f += 2 * cpw * (N / BLK);
-    if (h->plan.freq_shift_hz != 0 && h->plan.shift_kind == 2) f += 2 * N;
-    f += 2 * FRONT_WAVE;                                 // FM: per-lane last {I, Q} exchange
+    size_t f = (size_t)cpw * h->lw + front_lds_extra(h);
+#ifdef UHSDR_FRONT_LDS_MIN
+    // experiment builds: a floor on the front's LDS per wave (caps its waves per CU)
+    if (f * sizeof(float) < (size_t)UHSDR_FRONT_LDS_MIN) return UHSDR_FRONT_LDS_MIN;
+#endif
     return f * sizeof(float);
+}
+
+// rx_chain's LDS: the front region (also the back end's output staging) + the decimated hand-off
+static size_t chain_front_floats(const uhsdr_rx_s* h)
+{
+    const size_t f = front_lds(h) / sizeof(float), ys = (size_t)BACK_CH * FUSED_YPITCH;
+    return ((f > ys ? f : ys) + 3) & ~(size_t)3;
+}
+static size_t chain_lds(const uhsdr_rx_s* h)
+{
+    return sizeof(float) * (chain_front_floats(h) + (size_t)h->Nd * CHAIN_ADP);
+}
+
+// front variant with R outputs per lane for the handle's call size (strict: exactly R)
+static uhsdr_status configure_front(uhsdr_rx_s* h, int R, bool strict)
+{
+    const FrontVariant* fv = find_front(h->plan, h->N, R, strict);
+    if (!fv) { uhsdr_set_error("no front kernel with %d outputs per lane for %d-frame calls", R, h->N); return UHSDR_UNSUPPORTED; }
+    const FrontVariant* old = h->fv;
+    const int oNf = h->Nf, olw = h->lw;
+    h->fv = fv;
+    h->T1 = fv->t1; h->T2 = fv->t2;
+    h->Nf = front_frames(h->N, fv->R);
+    h->lw = front_window_pitch(h);
+    uhsdr_status st = UHSDR_OK;
+    if (h->N % h->Nf) { uhsdr_set_error("frames_per_call %d not a multiple of %d", h->N, h->Nf); st = UHSDR_LENGTH_ERROR; }
+    else if (front_lds(h) > 64 * 1024) { uhsdr_set_error("frames_per_call too long for LDS"); st = UHSDR_LENGTH_ERROR; }
+    if (st != UHSDR_OK && old) { h->fv = old; h->T1 = old->t1; h->T2 = old->t2; h->Nf = oNf; h->lw = olw; }
+    return st;
+}
+
+// can the handle run rx_chain: a chain instance, one front pass per call, LDS within a workgroup's
+static bool chain_ok(const uhsdr_rx_s* h)
+{
+    return h->cv && h->fv->R == h->cv->R && h->Nf == h->N && chain_lds(h) <= 64 * 1024;
+}
+
+// AUTO: large batches run one kernel (rx_chain) where the path has one, else the fused back end;
+// small ones the back-end wave pipeline (measured crossover BACK_FUSED_MIN_CHANNELS).
+// Measured and dropped: the fused back end split in two at the interpolator (decimated-rate stages
+// / 48 ksps stages, half the registers each): 0.225 vs 0.211 ms at 1M x 64, and slower on C3 / C5
+// too -- more waves did not raise the VALU issue rate.
+static int resolve_schedule(const uhsdr_rx_s* h, int want)
+{
+    if (want == UHSDR_SCHEDULE_AUTO)
+    {
+        if (h->C < BACK_FUSED_MIN_CHANNELS) return UHSDR_SCHEDULE_SPLIT_PIPE;
+        if (chain_ok(h)) return UHSDR_SCHEDULE_CHAIN;
+        return h->bv->fused ? UHSDR_SCHEDULE_SPLIT_FUSED : UHSDR_SCHEDULE_SPLIT_PIPE;
+    }
+    if (want == UHSDR_SCHEDULE_CHAIN) return chain_ok(h) ? want : -1;
+    if (want == UHSDR_SCHEDULE_SPLIT_FUSED) return h->bv->fused ? want : -1;
+    if (want == UHSDR_SCHEDULE_SPLIT_PIPE) return want;
+    return -1;
 }
 
 static size_t back_lds(const uhsdr_rx_s* h)
@@ -2641,9 +2832,10 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     uhsdr_status bst = uhsdr_rx_plan_build(cfg, &h->plan);
     if (bst != UHSDR_OK) { free(h); return bst; }
     const uhsdr_rx_plan& p = h->plan;
-    h->fv = find_front(p, C, N);
+    h->fv = find_front(p, N);
     h->bv = find_back(p);
     h->nv = find_notch(p);
+    h->cv = find_chain(p, h->bv);
     if (!uhsdr_rx_mode_supported(&p) || !h->fv || !h->bv || (p.notch_enabled && !h->nv))
     {
         free(h);
@@ -2653,25 +2845,14 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     }
     h->C = C; h->N = N; h->Nd = N / p.decimation_rate;
     h->stream = (hipStream_t)stream;
-    h->T1 = h->fv->t1; h->T2 = h->fv->t2;
-    h->Nf = front_frames(N, h->fv->R);
-    h->lw = front_window_pitch(h);
-    if (N % h->Nf) { free(h); uhsdr_set_error("frames_per_call %d not a multiple of %d", N, h->Nf); return UHSDR_LENGTH_ERROR; }
-    if (front_lds(h) > 64 * 1024) { free(h); uhsdr_set_error("frames_per_call too long for LDS"); return UHSDR_LENGTH_ERROR; }
-    const int W = h->bv->w;
     {
-        // Back end: the wave pipeline shortens the per-call critical path, which is what bounds
-        // small batches; from BACK_FUSED_MIN_CHANNELS on (>= 4 waves per SIMD of 64 channels)
-        // the fused kernel wins.  UHSDR_BACK_FUSED=0/1 forces either (tests, benchmarking).
-        // Measured and dropped: the fused kernel split in two at the interpolator (decimated-rate
-        // stages / 48 ksps stages, half the registers each): 0.225 vs 0.211 ms at 1M x 64, and
-        // slower on C3 / C5 too -- more waves did not raise the VALU issue rate.
-        const char* envf = getenv("UHSDR_BACK_FUSED");
-        int mode = C >= BACK_FUSED_MIN_CHANNELS ? BACK_FUSED : BACK_PIPE;
-        if (envf) mode = atoi(envf) ? BACK_FUSED : BACK_PIPE;
-        if (mode == BACK_FUSED && !h->bv->fused) mode = BACK_PIPE;
-        h->back_mode = mode;
+        const int R = h->fv->R;
+        h->fv = nullptr;
+        const uhsdr_status fs = configure_front(h, R, true);
+        if (fs != UHSDR_OK) { free(h); return fs; }
     }
+    const int W = h->bv->w;
+    h->schedule = resolve_schedule(h, UHSDR_SCHEDULE_AUTO);
 
     size_t fl = 0;
     auto take = [&](size_t n) { size_t o = fl; fl += (n + 63) & ~(size_t)63; return o; };
@@ -2836,47 +3017,33 @@ static int front_comb_of(const uhsdr_rx_plan& p)
     return p.lsb ? FRONT_COMB_LSB : FRONT_COMB_USB;
 }
 
-static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, float* audio0, int32_t* dst)
+// rx_front's arguments for the launch covering frames f0 .. f0 + Nf of the call
+static FrontArgs front_args(const uhsdr_rx_s* h, const int32_t* iq, int f0, float* adec, float* adec_q)
 {
-    if (!h || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
-    if (h->timing && h->nev >= h->nev_cap) time_harvest(h);
-    h->tsample = h->timing && (h->tcalls++ % h->timing) == 0;
-    // hand-off buffers of this call; pipelined: rotate, and wait until the rx_back that read
-    // this buffer PIPE_BUFS calls ago has finished
-    const int par = h->pipelined ? (int)(h->calls_issued % PIPE_BUFS) : 0;
-    float* adec = par ? h->adecp[par - 1] : h->adec;
-    float* adec_q = par ? h->adec_qp[par - 1] : h->adec_q;
-    if (side_mode(h)) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[par], 0));
-    h->calls_issued += 1;
-    time_mark(h, 0, 0);
-    const int cpw = FRONT_WAVE / (h->Nf / h->fv->R);
-    const size_t lds = front_lds(h);
-    for (int f0 = 0; f0 < h->N; f0 += h->Nf)
-    {
-        FrontArgs fa;
-        fa.plan = h->d_plan;
-        fa.iq = (const int2*)iq + f0;
-        fa.hist1_i = h->hist1_i; fa.hist1_q = h->hist1_q; fa.hist2_i = h->hist2_i; fa.hist2_q = h->hist2_q;
-        fa.teta = h->teta;
-        fa.tp = h->tp;
-        fa.clip = h->clip;
-        fa.osc_in = h->osc + 2 * (h->front_launches & 1);     // ping-pong: read one copy, write the other
-        fa.osc_out = h->osc + 2 * ((h->front_launches + 1) & 1);
-        fa.adec = adec + f0 / h->plan.decimation_rate;
-        fa.adec_q = adec_q ? adec_q + f0 / h->plan.decimation_rate : nullptr;
-        fa.C = h->C; fa.N = h->Nf; fa.ld = h->N; fa.ldd = h->Nd;
-        fa.lw = h->lw;
-        fa.taps2a = h->d_taps2;
-        fa.taps2b = h->d_taps2 + 2 * TAPS2_MAX;
-        fa.comb = front_comb_of(h->plan);
-        fa.fm_prev = h->bs.sam;                          // FM: fields 0, 1 of rx_fm's state
-        hipLaunchKernelGGL(h->precision == UHSDR_PRECISION_FMA ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw),
-                           dim3(FRONT_WAVE), lds, h->stream, fa);
-        HIPCHK(hipGetLastError());
-        h->front_launches += 1;
-    }
-    time_mark(h, 0, 1);
+    FrontArgs fa;
+    fa.plan = h->d_plan;
+    fa.iq = (const int2*)iq + f0;
+    fa.hist1_i = h->hist1_i; fa.hist1_q = h->hist1_q; fa.hist2_i = h->hist2_i; fa.hist2_q = h->hist2_q;
+    fa.teta = h->teta;
+    fa.tp = h->tp;
+    fa.clip = h->clip;
+    fa.osc_in = h->osc + 2 * (h->front_launches & 1);     // ping-pong: read one copy, write the other
+    fa.osc_out = h->osc + 2 * ((h->front_launches + 1) & 1);
+    fa.adec = adec ? adec + f0 / h->plan.decimation_rate : nullptr;
+    fa.adec_q = adec_q ? adec_q + f0 / h->plan.decimation_rate : nullptr;
+    fa.C = h->C; fa.N = h->Nf; fa.ld = h->N; fa.ldd = h->Nd;
+    fa.lw = h->lw;
+    fa.taps2a = h->d_taps2;
+    fa.taps2b = h->d_taps2 + 2 * TAPS2_MAX;
+    fa.comb = front_comb_of(h->plan);
+    fa.fm_prev = h->bs.sam;                          // FM: fields 0, 1 of rx_fm's state
+    return fa;
+}
 
+// the back end's arguments of this call; advances the host-side per-call counters (key beep,
+// CW decoder sample counter)
+static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audio, float* audio0, int32_t* dst)
+{
     BackArgs ba;
     ba.plan = h->d_plan;
     ba.adec = adec;
@@ -2918,26 +3085,78 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         }
         h->cw_blocks_last = blocks;
     }
-    const hipStream_t bst = back_stream(h);
-    if (side_mode(h))
+    return ba;
+}
+
+static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, float* audio0, int32_t* dst)
+{
+    if (!h || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
+    if (h->timing && h->nev >= h->nev_cap) time_harvest(h);
+    h->tsample = h->timing && (h->tcalls++ % h->timing) == 0;
+    if (h->tsample) h->evmask[h->nev] = 0;
+    const bool fma = h->precision == UHSDR_PRECISION_FMA;
+    if (h->schedule == UHSDR_SCHEDULE_CHAIN)
     {
-        HIPCHK(hipEventRecord(h->ev_front, h->stream));
-        HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
-    }
-    time_mark(h, 1, 0);
-    if (h->nv)
-    {
-        hipLaunchKernelGGL(h->nv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
+        // one kernel: front passes and back end per 64 channels, the hand-off in LDS
+        // after every back end still running on the pipelined mode's side stream (state it writes)
+        if (side_mode(h))
+        {
+            HIPCHK(hipEventRecord(h->ev_join, h->side));
+            HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+        }
+        const FrontArgs fa = front_args(h, iq, 0, nullptr, nullptr);
+        const BackArgs ba = back_args(h, nullptr, nullptr, audio, audio0, dst);
+        time_mark(h, K_CHAIN, 0);
+        hipLaunchKernelGGL(fma ? h->cv->fn_fma : h->cv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(FRONT_WAVE),
+                           chain_lds(h), h->stream, fa, ba, (int)chain_front_floats(h));
         HIPCHK(hipGetLastError());
+        time_mark(h, K_CHAIN, 1);
+        h->front_launches += 1;
     }
-    if (h->back_mode == BACK_FUSED || h->plan.stereo)
-        hipLaunchKernelGGL(h->bv->fused, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
     else
-        hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH),
-                           back_lds(h), bst, ba);
-    HIPCHK(hipGetLastError());
-    time_mark(h, 1, 1);
-    if (side_mode(h)) HIPCHK(hipEventRecord(h->ev_back[par], bst));
+    {
+        // hand-off buffers of this call; pipelined: rotate, and wait until the rx_back that read
+        // this buffer PIPE_BUFS calls ago has finished
+        const int par = h->pipelined ? (int)(h->calls_issued % PIPE_BUFS) : 0;
+        float* adec = par ? h->adecp[par - 1] : h->adec;
+        float* adec_q = par ? h->adec_qp[par - 1] : h->adec_q;
+        if (side_mode(h)) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[par], 0));
+        time_mark(h, K_FRONT, 0);
+        const int cpw = FRONT_WAVE / (h->Nf / h->fv->R);
+        const size_t lds = front_lds(h);
+        for (int f0 = 0; f0 < h->N; f0 += h->Nf)
+        {
+            const FrontArgs fa = front_args(h, iq, f0, adec, adec_q);
+            hipLaunchKernelGGL(fma ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw), dim3(FRONT_WAVE), lds,
+                               h->stream, fa);
+            HIPCHK(hipGetLastError());
+            h->front_launches += 1;
+        }
+        time_mark(h, K_FRONT, 1);
+
+        const BackArgs ba = back_args(h, adec, adec_q, audio, audio0, dst);
+        const hipStream_t bst = back_stream(h);
+        if (side_mode(h))
+        {
+            HIPCHK(hipEventRecord(h->ev_front, h->stream));
+            HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
+        }
+        time_mark(h, K_BACK, 0);
+        if (h->nv)
+        {
+            hipLaunchKernelGGL(h->nv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
+            HIPCHK(hipGetLastError());
+        }
+        if (h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo)
+            hipLaunchKernelGGL(h->bv->fused, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
+        else
+            hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH),
+                               back_lds(h), bst, ba);
+        HIPCHK(hipGetLastError());
+        time_mark(h, K_BACK, 1);
+        if (side_mode(h)) HIPCHK(hipEventRecord(h->ev_back[par], bst));
+    }
+    h->calls_issued += 1;
     if (h->tsample) h->nev++;
     h->tsample = 0;
     h->dec_samples += h->Nd;
@@ -2996,6 +3215,43 @@ extern "C" uhsdr_status uhsdr_rx_set_precision(uhsdr_rx_handle h, int32_t precis
 }
 
 extern "C" int32_t uhsdr_rx_get_precision(uhsdr_rx_handle h) { return h ? h->precision : -1; }
+
+extern "C" uhsdr_status uhsdr_rx_set_schedule(uhsdr_rx_handle h, int32_t schedule)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    if (schedule < UHSDR_SCHEDULE_AUTO || schedule > UHSDR_SCHEDULE_CHAIN)
+    {
+        uhsdr_set_error("schedule %d: not a UHSDR_SCHEDULE_*", (int)schedule);
+        return UHSDR_ARGUMENT_ERROR;
+    }
+    const int s = resolve_schedule(h, schedule);
+    if (s < 0)
+    {
+        uhsdr_set_error("schedule %d not available on filter path %d with %d-frame calls", (int)schedule,
+                        (int)h->plan.filter_path, h->N);
+        return UHSDR_UNSUPPORTED;
+    }
+    h->schedule = s;
+    return UHSDR_OK;
+}
+
+extern "C" int32_t uhsdr_rx_get_schedule(uhsdr_rx_handle h) { return h ? h->schedule : -1; }
+
+extern "C" uhsdr_status uhsdr_rx_set_front_block(uhsdr_rx_handle h, int32_t outputs_per_lane)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    if (outputs_per_lane != 8 && outputs_per_lane != 16)
+    {
+        uhsdr_set_error("front block %d: 8 or 16 outputs per lane", (int)outputs_per_lane);
+        return UHSDR_ARGUMENT_ERROR;
+    }
+    const uhsdr_status st = configure_front(h, outputs_per_lane, true);
+    if (st != UHSDR_OK) return st;
+    // a CHAIN schedule needs the chain's block: fall back to the split kernels otherwise
+    if (h->schedule == UHSDR_SCHEDULE_CHAIN && !chain_ok(h))
+        h->schedule = h->bv->fused ? UHSDR_SCHEDULE_SPLIT_FUSED : UHSDR_SCHEDULE_SPLIT_PIPE;
+    return UHSDR_OK;
+}
 
 extern "C" uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h)
 {
@@ -3069,7 +3325,7 @@ extern "C" uhsdr_status uhsdr_rx_get_plan(uhsdr_rx_handle h, uhsdr_rx_plan* plan
     return UHSDR_OK;
 }
 
-extern "C" int32_t uhsdr_rx_kernel_count(uhsdr_rx_handle h) { return h ? 2 : 0; }
+extern "C" int32_t uhsdr_rx_kernel_count(uhsdr_rx_handle h) { return h ? NKERN : 0; }
 
 extern "C" uhsdr_status uhsdr_rx_enable_timing(uhsdr_rx_handle h, int32_t enable)
 {
@@ -3077,16 +3333,16 @@ extern "C" uhsdr_status uhsdr_rx_enable_timing(uhsdr_rx_handle h, int32_t enable
     if (enable && !h->ev)
     {
         h->nev_cap = 1024;
-        h->ev = (hipEvent_t*)calloc((size_t)h->nev_cap * 4, sizeof(hipEvent_t));
-        for (int i = 0; i < h->nev_cap * 4; ++i) HIPCHK(hipEventCreate(&h->ev[i]));
+        h->ev = (hipEvent_t*)calloc((size_t)h->nev_cap * NKERN * 2, sizeof(hipEvent_t));
+        h->evmask = (uint8_t*)calloc((size_t)h->nev_cap, 1);
+        for (int i = 0; i < h->nev_cap * NKERN * 2; ++i) HIPCHK(hipEventCreate(&h->ev[i]));
     }
     if (h->timing) time_harvest(h);
     h->timing = enable > 0 ? enable : 0;
     h->tsample = 0;
     h->tcalls = 0;
     h->nev = 0;
-    h->total_ms[0] = h->total_ms[1] = 0.0f;
-    h->launches[0] = h->launches[1] = 0;
+    for (int k = 0; k < NKERN; ++k) { h->total_ms[k] = 0.0f; h->launches[k] = 0; }
     return UHSDR_OK;
 }
 
@@ -3094,16 +3350,16 @@ extern "C" int32_t uhsdr_rx_kernel_times(uhsdr_rx_handle h, float* total_ms, int
 {
     if (!h) return 0;
     time_harvest(h);
-    const int n = max_kernels < 2 ? max_kernels : 2;
+    const int n = max_kernels < NKERN ? max_kernels : NKERN;
     for (int k = 0; k < n; ++k)
     {
         if (total_ms) total_ms[k] = h->total_ms[k];
         if (launches) launches[k] = h->launches[k];
     }
-    return 2;
+    return n;
 }
 
-extern "C" const char* uhsdr_rx_kernel_name(int32_t index) { return (index >= 0 && index < 2) ? kKernelNames[index] : ""; }
+extern "C" const char* uhsdr_rx_kernel_name(int32_t index) { return (index >= 0 && index < NKERN) ? kKernelNames[index] : ""; }
 
 extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
 {
@@ -3123,8 +3379,9 @@ extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
     }
     if (h->ev)
     {
-        for (int i = 0; i < h->nev_cap * 4; ++i) (void)hipEventDestroy(h->ev[i]);
+        for (int i = 0; i < h->nev_cap * NKERN * 2; ++i) (void)hipEventDestroy(h->ev[i]);
         free(h->ev);
+        free(h->evmask);
     }
     if (h->ev_switch) (void)hipEventDestroy(h->ev_switch);
     if (h->arena) (void)hipFree(h->arena);

@@ -18,9 +18,15 @@ import numpy as np
 from . import _abi
 
 
+# Schedule every new RxChain asks for (tests/conftest.py's `back` fixture sets it to cover each
+# kernel schedule); None keeps the library's AUTO choice.  A schedule the handle's path cannot run
+# leaves it on AUTO's choice.
+DEFAULT_SCHEDULE = None
+
+
 class RxChain:
     def __init__(self, config: _abi.RxConfig | None = None, channels: int = 1, frames: int = 32,
-                 stream: int | None = None, **overrides):
+                 stream: int | None = None, schedule: int | None = None, **overrides):
         self.lib = _abi.load()
         self.config = config if config is not None else _abi.default_config(**overrides)
         self.channels = int(channels)
@@ -31,6 +37,10 @@ class RxChain:
         self.handle = h
         self.plan = _abi.RxPlan()
         _abi.check(self.lib.uhsdr_rx_get_plan(h, C.byref(self.plan)), "uhsdr_rx_get_plan")
+        if schedule is not None:
+            self.set_schedule(schedule)
+        elif DEFAULT_SCHEDULE is not None:
+            self.lib.uhsdr_rx_set_schedule(h, int(DEFAULT_SCHEDULE))   # best effort (see above)
 
     def set_stream(self, stream: int) -> None:
         _abi.check(self.lib.uhsdr_rx_set_stream(self.handle, C.c_void_p(stream)), "uhsdr_rx_set_stream")
@@ -140,6 +150,20 @@ class RxChain:
     def precision(self) -> int:
         return self.lib.uhsdr_rx_get_precision(self.handle)
 
+    def set_schedule(self, schedule: int) -> None:
+        """SCHEDULE_AUTO / _SPLIT_PIPE / _SPLIT_FUSED / _CHAIN (uhsdr_rx_set_schedule): which kernels
+        run a call; outputs are identical under every one."""
+        _abi.check(self.lib.uhsdr_rx_set_schedule(self.handle, int(schedule)), "uhsdr_rx_set_schedule")
+
+    @property
+    def schedule(self) -> int:
+        """The resolved schedule (never AUTO)."""
+        return self.lib.uhsdr_rx_get_schedule(self.handle)
+
+    def set_front_block(self, outputs_per_lane: int) -> None:
+        """FIR outputs per lane of the front passes, 8 or 16 (uhsdr_rx_set_front_block)."""
+        _abi.check(self.lib.uhsdr_rx_set_front_block(self.handle, int(outputs_per_lane)), "uhsdr_rx_set_front_block")
+
     def join(self) -> None:
         _abi.check(self.lib.uhsdr_rx_join(self.handle), "uhsdr_rx_join")
 
@@ -156,7 +180,8 @@ class RxChain:
         ms = (C.c_float * 8)()
         n = (C.c_int32 * 8)()
         k = self.lib.uhsdr_rx_kernel_times(self.handle, ms, n, 8)
-        return {self.lib.uhsdr_rx_kernel_name(i).decode(): (ms[i], n[i]) for i in range(k)}
+        # kernel slots that ran (rx_front + rx_back, or rx_chain)
+        return {self.lib.uhsdr_rx_kernel_name(i).decode(): (ms[i], n[i]) for i in range(k) if n[i] > 0}
 
     def close(self) -> None:
         if self.handle:

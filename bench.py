@@ -21,7 +21,6 @@ import argparse
 import json
 import os
 import sys
-import time
 
 import numpy as np
 
@@ -155,20 +154,10 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     audio = torch.empty((C, N), dtype=torch.float32, device=dev)
     dst = torch.empty((C, N, 2), dtype=torch.int32, device=dev) if want_dst else None
     torch.cuda.synchronize(dev)
-    for s in range(warmup):
-        chain.process(inputs[s % pool], audio, dst)
-    torch.cuda.synchronize(dev)
     # throughput: K calls with nothing but the calls themselves inside the timed region
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for s in range(steps):
-        chain.process(inputs[s % pool], audio, dst)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    # (shard.timed_loop: warm-up, barrier + sync brackets, max over ranks)
+    elapsed = shard.timed_loop(lambda s: chain.process(inputs[s % pool], audio, dst),
+                               lambda: torch.cuda.synchronize(dev), steps, warmup, dist, world, dev)
     # per-kernel breakdown in a separate pass: HIP events on the library's own stream bracket
     # every kernel of every call (the records cost host time, so they never share a clock with
     # the throughput loop above)
@@ -179,13 +168,10 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     torch.cuda.synchronize(dev)
     ktimes = chain.kernel_times()
     chain.enable_timing(False)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ok = bool(torch.isfinite(audio).all().item())
     chain.close()
     del inputs
-    return float(t.item()), ktimes, plan, ok, sched
+    return elapsed, ktimes, plan, ok, sched
 
 
 def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup):
@@ -202,21 +188,9 @@ def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warm
 
     def compute(out):
         chain.process(x, out, None)
-    for s in range(warmup):
-        pipe.step(compute)
-    pipe.drain()
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    t0 = time.perf_counter()
-    for s in range(steps):
-        pipe.step(compute)
-    pipe.drain()
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = shard.gather_timed(pipe, compute, lambda: torch.cuda.synchronize(dev), steps, warmup, dist, dev)
     chain.close()
-    return float(t.item())
+    return t
 
 
 def roofline_of(ab, ktimes, traffic):

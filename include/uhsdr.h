@@ -333,20 +333,28 @@ uhsdr_status uhsdr_copy_to_host(void* dst, const void* src, uint64_t bytes);
  *   codec audio frames -> mic gain -> TX band-pass lattice -> bass/treble biquads ->
  *   ALC compressor with its 288-sample look-ahead delay -> 201-tap Hilbert pair ->
  *   FreqShift -> I/Q gain + phase -> int32 IQ frames for the DAC.
+ * AM voice (TxProcessor_AM, :715-800, dispatch :1000-1008): the same voice chain with
+ *   AM_ALC_GAIN_CORRECTION, the Hilbert pair, both sidebands plus carrier
+ *   (I - Q + 2 * AM_CARRIER_LEVEL, Q - I - 2 * AM_CARRIER_LEVEL), FreqShift.
+ * FM voice: the voice chain, pre-emphasis and the softdds modulator (:534-588).
+ * USB I/Q source (TX_AUDIO_DIGIQ, :950-961): the input frames are the I/Q itself, straight to the
+ *   final gain / phase stage (not in CW or TUNE, where the voice path runs as usual).
  * One uhsdr_tx_process call == N/32 TX-mode AudioDriver_I2SCallback invocations per channel.
  */
 #define UHSDR_TX_HILBERT_TAPS 201    /* iq_tx_wide, drivers/audio/filters/iq_tx_filter.h:22 */
 #define UHSDR_TX_DELAY 320           /* AUDIO_DELAY_BUFSIZE, audio_driver.h:516 */
 
-/* TX_AUDIO_*, hardware/uhsdr_board.h:128-131.  Modes: UHSDR_DEMOD_USB / LSB (SSB voice) and
-   UHSDR_DEMOD_FM (FM voice, needs iq_freq_mode != OFF like the reference, tx_processor.c:1009) */
-enum { UHSDR_TX_AUDIO_MIC = 0, UHSDR_TX_AUDIO_LINEIN_L = 1, UHSDR_TX_AUDIO_LINEIN_R = 2, UHSDR_TX_AUDIO_DIG = 3 };
+/* TX_AUDIO_*, hardware/uhsdr_board.h:128-132 (DIG: USB audio in place of the codec's, no bass /
+   treble; DIGIQ: USB I/Q).  Modes: UHSDR_DEMOD_USB / LSB (SSB voice), UHSDR_DEMOD_AM and
+   UHSDR_DEMOD_FM (both need iq_freq_mode != OFF like the reference, tx_processor.c:1000-1011) */
+enum { UHSDR_TX_AUDIO_MIC = 0, UHSDR_TX_AUDIO_LINEIN_L = 1, UHSDR_TX_AUDIO_LINEIN_R = 2, UHSDR_TX_AUDIO_DIG = 3,
+       UHSDR_TX_AUDIO_DIGIQ = 4 };
 
 typedef struct uhsdr_tx_config
 {
-    int32_t dmod_mode;            /* ts.dmod_mode: UHSDR_DEMOD_USB or UHSDR_DEMOD_LSB */
+    int32_t dmod_mode;            /* ts.dmod_mode: UHSDR_DEMOD_USB, _LSB, _AM or _FM */
     int32_t iq_freq_mode;         /* ts.iq_freq_mode */
-    int32_t audio_source;         /* ts.tx_audio_source: MIC, LINEIN_L, LINEIN_R */
+    int32_t audio_source;         /* ts.tx_audio_source: MIC, LINEIN_L, LINEIN_R, DIG, DIGIQ */
     int32_t mic_gain_mult;        /* ts.tx_mic_gain_mult (codec.c:313-321) */
     int32_t mic_boost;            /* ts.tx_mic_boost */
     int32_t comp_level;           /* ts.tx_comp_level: -1 off, 0..12 presets, 13 = stored values */
@@ -355,7 +363,7 @@ typedef struct uhsdr_tx_config
     int32_t tx_filter;            /* ts.tx_filter: 0/1 soprano, 2 tenor, 3 bass */
     int32_t bass_gain;            /* ts.dsp.tx_bass_gain */
     int32_t treble_gain;          /* ts.dsp.tx_treble_gain */
-    int32_t filter_disable;       /* FLAGS1_SSB_TX_FILTER_DISABLE */
+    int32_t filter_disable;       /* FLAGS1_SSB_TX_FILTER_DISABLE (SSB) / FLAGS1_AM_TX_FILTER_DISABLE (AM) */
     float   power_factor;         /* ts.tx_power_factor */
     float   gain_i, gain_q;       /* ts.tx_adj_gain_var[trans].i / .q */
     float   phase_balance;        /* ads.iq_phase_balance_tx[trans] */
@@ -401,7 +409,10 @@ typedef struct uhsdr_tx_plan
     uint32_t tune_step[2];
     uint32_t tone_burst_step;
     float   tone_burst_scale;     /* FM_TONE_BURST_AMPLITUDE_SCALING * fm_mod_mult */
-    int32_t reserved[28];
+    int32_t am;                   /* TxProcessor_AM: both sidebands + carrier after the Hilbert pair */
+    int32_t digiq;                /* TX_AUDIO_DIGIQ: the input frames are I/Q for the final stage */
+    float   digiq_i_gain, digiq_q_gain;   /* final gains with iq_gain_comp 1.0 (tx_processor.c:924) */
+    int32_t reserved[24];
 } uhsdr_tx_plan;
 
 typedef struct uhsdr_tx_s* uhsdr_tx_handle;
@@ -465,6 +476,11 @@ uhsdr_status uhsdr_fir_reset(uhsdr_fir_handle h);
 uhsdr_status uhsdr_fir_process(uhsdr_fir_handle h, const float* src, float* dst);
 uhsdr_status uhsdr_fir_synchronize(uhsdr_fir_handle h);
 uhsdr_status uhsdr_fir_destroy(uhsdr_fir_handle h);
+/* waves per workgroup of the FIR kernel: 1, 2 or 4 (default EXACT 2, MFMA 4; results do not
+ * depend on it).  UHSDR_ARGUMENT_ERROR for another value, UHSDR_LENGTH_ERROR when that
+ * many windows do not fit one workgroup's LDS (the setting is then unchanged). */
+uhsdr_status uhsdr_fir_set_waves(uhsdr_fir_handle h, int32_t waves);
+int32_t uhsdr_fir_get_waves(uhsdr_fir_handle h);
 
 typedef struct uhsdr_i2s_s* uhsdr_i2s_handle;
 

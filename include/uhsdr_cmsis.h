@@ -126,6 +126,24 @@ void arm_cfft_f32(const arm_cfft_instance_f32* S, float32_t* p1, uint8_t ifftFla
 /* arm_math.h:6312 -- replaces arm_cmplx_mag_f32 (ComplexMathFunctions/arm_cmplx_mag_f32.c) */
 void arm_cmplx_mag_f32(float32_t* pSrc, float32_t* pDst, uint32_t numSamples);
 
+/* arm_math.h:4119-4127 -- replaces arm_lms_norm_f32 (FilteringFunctions/arm_lms_norm_f32.c), the
+   firmware's LMS auto notch (AudioDriver_NotchFilter, audio_driver.c:1755; in-place: pErr may be
+   pSrc).  The coefficients in pCoeffs adapt in place; energy and x0 carry in the instance. */
+typedef struct
+{
+    uint16_t numTaps;
+    float32_t* pState;     /* numTaps + blockSize - 1 */
+    float32_t* pCoeffs;    /* numTaps */
+    float32_t mu;
+    float32_t energy;
+    float32_t x0;
+} arm_lms_norm_instance_f32;
+
+void arm_lms_norm_init_f32(arm_lms_norm_instance_f32* S, uint16_t numTaps, float32_t* pCoeffs, float32_t* pState,
+                           float32_t mu, uint32_t blockSize);
+void arm_lms_norm_f32(arm_lms_norm_instance_f32* S, float32_t* pSrc, float32_t* pRef, float32_t* pOut,
+                      float32_t* pErr, uint32_t blockSize);
+
 /* status of the last shim call on this thread: 0 ok, UHSDR_* error code (uhsdr.h) otherwise */
 int32_t uhsdr_cmsis_last_status(void);
 

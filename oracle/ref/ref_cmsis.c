@@ -18,6 +18,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 #include "arm_math.h"
 
 void ref_cfft_stages(int L, float* p, int bitrev);
@@ -213,6 +214,45 @@ static void cfft_case(const char* name, int L, int ifft, int bitrev)
     free(x); free(y);
 }
 
+/* arm_lms_norm_f32: numTaps T, blockSize B, K calls, step mu; the coefficients start from small
+   random values (the firmware keeps them across re-inits unless reset_dsp_nr), the reference
+   signal is a second LCG stream.  inplace: pErr == pSrc, as AudioDriver_NotchFilter calls it
+   (audio_driver.c:1755). */
+static void lms_case(const char* name, int T, int B, int K, float mu, int inplace)
+{
+    char p[192];
+    snprintf(p, sizeof p, "{\"numTaps\": %d, \"blockSize\": %d, \"calls\": %d, \"mu\": %.9g, \"inplace\": %d}",
+             T, B, K, mu, inplace);
+    case_begin(name, p);
+    float* c = frand(T, 0.05f);
+    float* x = frand((size_t)B * K, 1.0f);
+    float* d = frand((size_t)B * K, 1.0f);
+    for (size_t i = 0; i < (size_t)B * K; ++i) d[i] = 0.5f * d[i] + 0.5f * x[i];   /* correlated reference */
+    put(name, "coeffs0", c, T); put(name, "src", x, (size_t)B * K); put(name, "ref", d, (size_t)B * K);
+    float* y = calloc((size_t)B * K, sizeof(float));
+    float* e = calloc((size_t)B * K, sizeof(float));
+    float* st = calloc(T + B - 1, sizeof(float));
+    float* blk = malloc(sizeof(float) * B);
+    arm_lms_norm_instance_f32 S;
+    arm_lms_norm_init_f32(&S, T, c, st, mu, B);
+    for (int k = 0; k < K; ++k)
+    {
+        if (inplace)
+        {
+            memcpy(blk, x + (size_t)k * B, sizeof(float) * B);
+            arm_lms_norm_f32(&S, blk, d + (size_t)k * B, y + (size_t)k * B, blk, B);
+            memcpy(e + (size_t)k * B, blk, sizeof(float) * B);
+        }
+        else
+            arm_lms_norm_f32(&S, x + (size_t)k * B, d + (size_t)k * B, y + (size_t)k * B, e + (size_t)k * B, B);
+    }
+    const float ex[2] = { S.energy, S.x0 };
+    put(name, "out", y, (size_t)B * K); put(name, "err", e, (size_t)B * K);
+    put(name, "coeffs", c, T); put(name, "state", st, T - 1); put(name, "energy_x0", ex, 2);
+    case_end();
+    free(c); free(x); free(d); free(y); free(e); free(st); free(blk);
+}
+
 static void mag_case(const char* name, int n)
 {
     char p[64];
@@ -268,6 +308,13 @@ int ref_cmsis_dump(const char* dir)
     cfft_case("cfft_64_nobitrev", 64, 0, 0);
     cfft_case("cfft_2048_nobitrev", 2048, 0, 0);
     mag_case("mag_1000", 1000);
+    /* the auto notch's instance: 64 taps, IQ_BLOCK_SIZE 32, mu from notch_mu 5
+       (audio_driver.c:1169-1173: log10f((5 + 1) / 1500 + 1)) */
+    lms_case("lms_64x32", 64, 32, 12, log10f(((5 + 1.0) / 1500.0) + 1.0), 1);
+    lms_case("lms_64x32_sep", 64, 32, 4, 0.1f, 0);
+    lms_case("lms_13x7", 13, 7, 6, 0.05f, 0);
+    lms_case("lms_1x5", 1, 5, 3, 0.2f, 1);
+    lms_case("lms_200x3", 200, 3, 9, 0.01f, 0);
     printf("}\n");
     return 0;
 }

@@ -98,7 +98,13 @@ void Psk_Demodulator_ProcessSample(float32_t sample) { (void)sample; }
 int16_t Psk_Modulator_GenSample(void) { return 0; }
 void UhsdrHwI2s_Codec_ClearTxDmaBuffer(void) {}
 void UiDriver_Callback_AudioISR(void) {}
-void UsbdAudio_FillTxBuffer(AudioSample_t* buffer, uint32_t len) { (void)buffer; (void)len; }
+/* the USB audio the TX chain reads for ts.tx_audio_source DIG / DIGIQ (tx_processor.c:929-938):
+   the harness points this at the call's input block (ref_main.c, txsrc=) */
+const AudioSample_t* oracle_usb_tx_block;
+void UsbdAudio_FillTxBuffer(AudioSample_t* buffer, uint32_t len)
+{
+    for (uint32_t i = 0; i < len; i++) buffer[i] = oracle_usb_tx_block ? oracle_usb_tx_block[i] : (AudioSample_t){ 0, 0 };
+}
 void UsbdAudio_PutSample(int16_t sample) { (void)sample; }
 
 /* hardware / CAT / UI / digital-mode hooks of the CW keyer and decoder (cw_gen.c, cw_decoder.c):

@@ -31,6 +31,9 @@
  *   tx=1           transmit: in= holds codec audio frames {l,r}, out_dst= gets the IQ frames
  *                  TxProcessor_Run writes (tx_processor.c:891-1078), out_a= a_buffer[0]
  *   micmult= boost= comp= txfilter= txbass= txtreble= txpwr= txgi= txgq= txphase=
+ *   txsrc=         ts.tx_audio_source (0 mic, 1/2 line in L/R, 3 USB audio, 4 USB I/Q): for 3 / 4
+ *                  the USB buffer (UsbdAudio_FillTxBuffer) delivers the in= block of the call
+ *   flags1=        ts.flags1 (FLAGS1_AM_TX_FILTER_DISABLE 0x08, FLAGS1_SSB_TX_FILTER_DISABLE 0x40)
  *   tune=t0:K:M    TUNE on calls t0 .. t0+K-1, M = 1 single tone, 2 two-tone (ts.tune, ts.tune_tone_mode,
  *                  AudioManagement_SetSidetoneForDemodMode on entry and exit, as RadioManagement does)
  *   burst=t0:K     FM tone burst on calls t0 .. t0+K-1 (ads.fm_conf.tone_burst_active)
@@ -54,6 +57,7 @@
 #include <stdint.h>
 
 extern __IO TransceiverState ts;
+extern const AudioSample_t* oracle_usb_tx_block;
 extern SpectrumDisplay sd;
 extern AudioDriverState ads;
 extern AudioDriverBuffer adb;
@@ -236,7 +240,8 @@ int main(int argc, char** argv)
     ts.samp_rate = IQ_SAMPLE_RATE;
     ts.dmod_mode = mode;
     ts.rx_iq_source = RX_IQ_CODEC;
-    ts.tx_audio_source = TX_AUDIO_MIC;
+    ts.tx_audio_source = iarg(argc, argv, "txsrc", TX_AUDIO_MIC);
+    ts.flags1 = iarg(argc, argv, "flags1", 0);
     ts.iq_freq_mode = iarg(argc, argv, "iqmode", FREQ_IQ_CONV_M12KHZ);
     ts.iq_auto_correction = iarg(argc, argv, "iq_auto", 0);
     ts.rx_adj_gain_var.i = farg(argc, argv, "gain_i", 1.0f);
@@ -375,6 +380,7 @@ int main(int argc, char** argv)
             }
             ads.fm_conf.tone_burst_active = burst0 >= 0 && call >= burst0 && call < burst0 + burstn;
             memcpy(ablk, iq + off, sizeof(AudioSample_t) * block);
+            oracle_usb_tx_block = ablk;                     /* the USB sources see the same block */
             AudioDriver_I2SCallback(ablk, oblk, side, block);
             memcpy(dst + off, oblk, sizeof(IqSample_t) * block);
             memcpy(a1 + off, adb.a_buffer[0], sizeof(float) * block);

@@ -1095,11 +1095,37 @@ static uint32_t dds_next(uint32_t* acc, uint32_t step)
     return k;
 }
 
-/* one TxProcessor_Run call (SSB voice) on BLK frames */
+/* TxProcessor_IqFinalProcessing (tx_processor.c:282-330) with final gains gi / gq */
+static void tx_final(const uhsdr_tx_plan* p, float gi, float gq, float* ib, float* qb, int32_t* iq, int n)
+{
+    for (int i = 0; i < n; i++) ib[i] = ib[i] * gi;
+    for (int i = 0; i < n; i++) qb[i] = qb[i] * gq;
+    const float ph = p->phase_balance;                 /* AudioDriver_IQPhaseAdjust, audio_driver.c:1776-1801 */
+    if (ph < 0)
+        for (int i = 0; i < n; i++) { const float e = ib[i] * ph; qb[i] = qb[i] + e; }
+    else if (ph > 0)
+        for (int i = 0; i < n; i++) { const float e = qb[i] * ph; ib[i] = ib[i] + e; }
+    for (int i = 0; i < n; i++)
+    {
+        iq[2 * i] = to_int32(ib[i]);
+        iq[2 * i + 1] = to_int32(qb[i]);
+    }
+}
+
+/* one TxProcessor_Run call (voice: SSB, AM, FM; or the USB I/Q source) on BLK frames */
 static void tx_call(const uhsdr_tx_plan* p, uo_tx_state* s, const int32_t* audio, int32_t* iq, float* a0)
 {
     const int n = BLK;
     float a[BLK], ib[BLK], qb[BLK], valbuf[BLK];
+    if (p->digiq && !s->tune)
+    {
+        /* TX_AUDIO_DIGIQ (tx_processor.c:950-961): the USB frames are the I/Q; the voice chain
+           does not run, a_buffer[0] keeps its contents (a0 left unwritten) */
+        for (int i = 0; i < n; i++) { ib[i] = audio[2 * i]; qb[i] = audio[2 * i + 1]; }
+        tx_final(p, p->digiq_i_gain, p->digiq_q_gain, ib, qb, iq, n);
+        if (a0) memcpy(a0, s->a0, sizeof(float) * n);
+        return;
+    }
     /* TxProcessor_AudioBufferFill (tx_processor.c:339-405) */
     if (s->tune)
     {
@@ -1154,6 +1180,7 @@ static void tx_call(const uhsdr_tx_plan* p, uo_tx_state* s, const int32_t* audio
         memcpy(a, &s->delay[out], sizeof(float) * n);
         for (int i = 0; i < n; i++) a[i] = a[i] * valbuf[i];
     }
+    memcpy(s->a0, a, sizeof(float) * n);
     if (a0) memcpy(a0, a, sizeof(float) * n);
     if (p->fm)
     {
@@ -1191,9 +1218,18 @@ static void tx_call(const uhsdr_tx_plan* p, uo_tx_state* s, const int32_t* audio
     }
     else
     {
-    /* TxProcessor_SSB (:467-490): Hilbert pair, then FreqShift */
+    /* TxProcessor_SSB (:467-490) / TxProcessor_AM (:734-800): Hilbert pair, [both sidebands +
+       carrier,] then FreqShift */
     fir(p->hilbert_i, UHSDR_TX_HILBERT_TAPS, s->hil_i, a, ib, n);
     fir(p->hilbert_q, UHSDR_TX_HILBERT_TAPS, s->hil_q, a, qb, n);
+    if (p->am)
+        for (int i = 0; i < n; i++)
+        {
+            const float i_am = (ib[i] - qb[i]) + (2 * 5100);          /* AM_CARRIER_LEVEL, audio_driver.h:429 */
+            const float q_am = (qb[i] - ib[i]) - (2 * 5100);
+            ib[i] = i_am;
+            qb[i] = q_am;
+        }
     if (p->freq_shift_hz != 0)
     {
         float* ip = p->shift_up ? ib : qb;
@@ -1228,19 +1264,7 @@ static void tx_call(const uhsdr_tx_plan* p, uo_tx_state* s, const int32_t* audio
         }
     }
     }
-    /* TxProcessor_IqFinalProcessing (:282-330) */
-    for (int i = 0; i < n; i++) ib[i] = ib[i] * p->final_i_gain;
-    for (int i = 0; i < n; i++) qb[i] = qb[i] * p->final_q_gain;
-    const float ph = p->phase_balance;                 /* AudioDriver_IQPhaseAdjust, audio_driver.c:1776-1801 */
-    if (ph < 0)
-        for (int i = 0; i < n; i++) { const float e = ib[i] * ph; qb[i] = qb[i] + e; }
-    else if (ph > 0)
-        for (int i = 0; i < n; i++) { const float e = qb[i] * ph; ib[i] = ib[i] + e; }
-    for (int i = 0; i < n; i++)
-    {
-        iq[2 * i] = to_int32(ib[i]);
-        iq[2 * i + 1] = to_int32(qb[i]);
-    }
+    tx_final(p, p->final_i_gain, p->final_q_gain, ib, qb, iq, n);
 }
 
 typedef struct

@@ -106,7 +106,8 @@ int uo_rx_process_batch2(const uhsdr_rx_plan* p, uo_rx_state* states, int C, con
 int uo_rx_process_batch_cw(const uhsdr_rx_plan* p, uo_rx_state* states, int C, const int32_t* iq, int n,
                            float* a1, int32_t* dst, uint8_t* cw_signal, float* cw_energy, int bmax, int threads);
 
-/* transmit: TxProcessor_Run SSB voice path (drivers/audio/tx_processor.c:891-1078) */
+/* transmit: TxProcessor_Run voice paths (SSB, AM, FM) and the USB I/Q source
+   (drivers/audio/tx_processor.c:891-1078) */
 typedef struct uo_tx_state
 {
     float lat[UHSDR_MAX_LATTICE + 1];        /* IIR_TXFilter state */
@@ -123,6 +124,7 @@ typedef struct uo_tx_state
        (ads.fm_conf.tone_burst_active, tone_burst_dds) */
     int32_t tune, burst;
     uint32_t tune_acc[2], burst_acc;
+    float a0[32];                             /* adb.a_buffer[0] as the last voice call left it */
 } uo_tx_state;
 
 size_t uo_tx_state_size(void);

@@ -145,12 +145,30 @@ TX_CONFIGS = {
     "fm_tune2": {"mode": 5, "path": 1, "iqmode": 4, "tune": "8:24:2"},
     "fm_burst": {"mode": 5, "path": 1, "iqmode": 4, "subtone": 10, "burstmode": 1, "burst": "16:24"},
     "fm_burst2_5k": {"mode": 5, "path": 1, "iqmode": 3, "fm5k": 1, "burstmode": 2, "burst": "8:16"},
+    # AM transmit (TxProcessor_AM, tx_processor.c:715-800): the SSB voice chain with
+    # AM_ALC_GAIN_CORRECTION, Hilbert pair, both sidebands + carrier, FreqShift
+    "am": {"mode": 3, "path": 70},
+    "am_p6k_comp": {"mode": 3, "path": 70, "iqmode": 1, "comp": 8, "txphase": 0.01},
+    "am_filter_off": {"mode": 3, "path": 70, "flags1": 0x08, "txfilter": 2},
+    "am_tune": {"mode": 3, "path": 70, "iqmode": 3, "tune": "8:24:1"},
+    # FLAGS1_SSB_TX_FILTER_DISABLE (tx_processor.c:991): no TX band-pass lattice
+    "usb_filter_off": {"mode": 0, "path": 48, "flags1": 0x40},
+    # USB audio source (TX_AUDIO_DIG: gain 1, no bass / treble, tx_processor.c:374-377,445)
+    "lsb_dig": {"mode": 1, "path": 48, "txsrc": 3},
+    # USB I/Q source (TX_AUDIO_DIGIQ, :950-961): the frames are the I/Q; TUNE runs the voice path
+    "usb_digiq": {"mode": 0, "path": 48, "txsrc": 4, "txgi": 0.98, "txphase": -0.01},
+    "am_digiq_m6k": {"mode": 3, "path": 70, "txsrc": 4, "iqmode": 2, "txpwr": 0.9},
 }
+# TX_AUDIO_DIGIQ fixtures take 16-bit I/Q (the USB audio class delivers int16 samples; the final
+# stage scales by 2^16 with no headroom for the codec's left-aligned frames)
+TX_DIGIQ_INPUT = ("usb_digiq", "am_digiq_m6k")
 
 
 def make_tx(name: str):
     args = dict(TX_CONFIGS[name], tx=1)
     audio = synth.tx_audio(np.arange(NCH), 0, NFRAMES)
+    if name in TX_DIGIQ_INPUT:
+        audio = synth.ssb_iq(np.arange(NCH), 0, NFRAMES) >> 16
     a0 = np.empty((NCH, NFRAMES), np.float32)
     iq = np.empty((NCH, NFRAMES, 2), np.int32)
     for c in range(NCH):

@@ -33,7 +33,8 @@ def test_library_exports_every_declared_symbol():
 
 @pytest.mark.parametrize("name", ["arm_fir_instance_f32", "arm_fir_decimate_instance_f32",
                                   "arm_fir_interpolate_instance_f32", "arm_iir_lattice_instance_f32",
-                                  "arm_biquad_casd_df1_inst_f32", "arm_cfft_instance_f32"])
+                                  "arm_biquad_casd_df1_inst_f32", "arm_cfft_instance_f32",
+                                  "arm_lms_norm_instance_f32"])
 def test_instance_layout_matches_header(name, tmp_path):
     st = getattr(cmsis, name)
     src = tmp_path / "sz.c"
@@ -86,3 +87,44 @@ def test_cfft_vectors_cover_every_cmsis_length():
         ref = np.fft.ifft(x) if p["ifftFlag"] else np.fft.fft(x)
         assert np.abs(y - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max()), case
     assert lens == {16, 32, 64, 128, 256, 512, 1024, 2048, 4096}
+
+
+def test_lms_vectors_follow_the_nlms_recursion():
+    """The arm_lms_norm_f32 fixtures of the reference build (tests/golden/cmsis_vectors.npz,
+    lms_*) against a binary32 restatement of arm_lms_norm_f32.c:205-300 (every operation
+    rounded to float32, in the reference's order): bit-exact outputs, errors, coefficients,
+    carried window, energy and x0."""
+    import json
+    f32 = np.float32
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cmsis_vectors.npz"))
+    man = json.loads(str(d["manifest"]))
+    cases = [c for c in man if c.startswith("lms_")]
+    assert len(cases) >= 4
+    for case in cases:
+        p = man[case]["params"]
+        T, B, K, mu = p["numTaps"], p["blockSize"], p["calls"], f32(p["mu"])
+        w = d[f"{case}.coeffs0"].copy()
+        src, ref = d[f"{case}.src"], d[f"{case}.ref"]
+        win = np.zeros(T - 1, np.float32)
+        energy, x0 = f32(0), f32(0)
+        out, err = [], []
+        for k in range(K):
+            x = np.concatenate([win, src[k * B:(k + 1) * B]])
+            for n in range(B):
+                xin = x[n + T - 1]
+                energy = f32(energy - f32(x0 * x0))
+                energy = f32(energy + f32(xin * xin))
+                acc = f32(0)
+                for t in range(T):
+                    acc = f32(acc + f32(x[n + t] * w[t]))
+                e = f32(ref[k * B + n] - acc)
+                step = f32(f32(e * mu) / f32(energy + f32(0.000000119209289)))
+                w = (w + (step * x[n:n + T]).astype(np.float32)).astype(np.float32)
+                x0 = x[n]
+                out.append(acc)
+                err.append(e)
+            win = x[B:]
+        for name, got in (("out", np.array(out, np.float32)), ("err", np.array(err, np.float32)), ("coeffs", w),
+                          ("state", win), ("energy_x0", np.array([energy, x0], np.float32))):
+            want = d[f"{case}.{name}"]
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (case, name)

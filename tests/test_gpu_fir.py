@@ -75,6 +75,40 @@ def test_fir_matches_oracle_distinct_channels(cuda, mode, T, B):
         assert normwise(got, ref) < TOL
 
 
+@pytest.mark.parametrize("mode", [U.fir.EXACT, U.fir.MFMA], ids=["exact", "mfma"])
+@pytest.mark.parametrize("waves", [1, 2, 4])
+@pytest.mark.parametrize("T,B", [(513, 256), (89, 512)])
+def test_fir_waves_per_workgroup(cuda, mode, waves, T, B):
+    """uhsdr_fir_set_waves changes the launch shape only: every count gives the oracle's output
+    (EXACT bit-exact), across a call boundary and over 300 channels (several groups per
+    workgroup at 4 waves, ragged last group)."""
+    rng = np.random.default_rng(7 * T + waves)
+    C = 300
+    taps = np.load(os.path.join(GOLD, "fir513_kaiser.npy")) if T == 513 else rng.uniform(-0.3, 0.3, T).astype(np.float32)
+    x = rng.normal(0, 1000, (C, 2 * B)).astype(np.float32)
+    fir = U.FirBatch(taps, C, B, mode)
+    assert fir.waves == (4 if mode == U.fir.MFMA else 2)
+    fir.set_waves(waves)
+    assert fir.waves == waves
+    got = run(fir, x, B)
+    fir.close()
+    o = oracle.OracleFir(taps, C)
+    ref = np.concatenate([o.process(x[:, k * B:(k + 1) * B]) for k in range(2)], axis=1)
+    if mode == U.fir.EXACT:
+        np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+    else:
+        assert normwise(got, ref) < TOL
+
+
+def test_fir_set_waves_rejects(cuda):
+    fir = U.FirBatch(np.ones(9, np.float32), 4, 256)
+    for bad in (0, 3, 8, -1):
+        with pytest.raises(RuntimeError):
+            fir.set_waves(bad)
+        assert fir.waves == 2
+    fir.close()
+
+
 def test_fir_rejects_bad_block(cuda):
     with pytest.raises(RuntimeError):
         U.FirBatch(np.ones(9, np.float32), 4, 100)

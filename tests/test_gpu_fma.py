@@ -79,6 +79,70 @@ def test_fma_within_tolerance(cuda, back, name, kw, gen, C, N, tol):
         assert not np.array_equal(got.view(np.uint32), ref.view(np.uint32)), f"{name}: FMA output is bit-exact"
 
 
+def accepted_fma_cases():
+    """Every (filter path, demodulator, stereo) the library takes FMA for: the Hilbert-first
+    families (plan.use_decimated_iq false) of every live FilterPathInfo entry."""
+    import json
+    import os
+    paths = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "filter_paths.json")))
+    out = []
+    for p in paths:
+        if p["index"] == 0:
+            continue
+        for mode in range(9):
+            for st in (0, 1):
+                kw = dict(filter_path=p["index"], dmod_mode=mode, stereo_enable=st)
+                if mode == U.DEMOD_FM:
+                    kw["fm_sql_threshold"] = 0
+                try:
+                    plan = U.build_plan(U.default_config(**kw))
+                except RuntimeError:
+                    continue
+                if not U.plan_supported(plan) or plan.use_decimated_iq or (st and not plan.stereo):
+                    continue
+                out.append(kw)
+    return out
+
+
+ACCEPTED = accepted_fma_cases()
+
+
+def test_fma_accepted_set():
+    """18 wide / 24 ksps paths x {USB, LSB, DIGI, SSB stereo, IQ} mono and stereo, and FM"""
+    assert len(ACCEPTED) == 129
+
+
+@pytest.mark.parametrize("kw", ACCEPTED, ids=[f"p{k['filter_path']}_m{k['dmod_mode']}_s{k['stereo_enable']}" for k in ACCEPTED])
+def test_fma_every_accepted_path(cuda, kw):
+    """Every path x demodulator that accepts FMA, both output channels in stereo, 8 calls of
+    128 frames (past the AGC ring), within 1e-5 normwise of the oracle."""
+    import torch
+    cfg = U.default_config(**kw)
+    plan = U.build_plan(cfg)
+    C, N, calls = 64, 128, 8
+    mode = kw["dmod_mode"]
+    iq = synth.fm_iq(np.arange(C), 0, calls * N) if mode == U.DEMOD_FM else \
+        synth.ssb_iq(np.arange(C), 0, calls * N, lsb=mode == U.DEMOD_LSB)
+    chain = U.RxChain(cfg, channels=C, frames=N)
+    chain.set_precision(U.PRECISION_FMA)
+    a1 = torch.empty((C, N), dtype=torch.float32, device="cuda")
+    a0 = torch.empty((C, N), dtype=torch.float32, device="cuda")
+    g1, g0 = [], []
+    for k in range(calls):
+        chain.process_stereo(torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda(), a1, a0, None)
+        g1.append(a1.cpu().numpy())
+        g0.append(a0.cpu().numpy())
+    chain.close()
+    r1, r0, _ = oracle.OracleRx(plan, C).process2(iq, threads=8)
+    outs = [(np.concatenate(g1, axis=1), r1, "a_buffer[1]")]
+    if plan.stereo:
+        outs.append((np.concatenate(g0, axis=1), r0, "a_buffer[0]"))
+    for got, ref, what in outs:
+        assert np.isfinite(got).all()
+        err = normwise(got, ref)
+        assert err.max() <= TOL, f"{kw} {what}: normwise error {err.max():.3g} > {TOL}"
+
+
 def test_fma_toggle_back_to_exact(cuda):
     """Switching to FMA and back: the EXACT calls stay bit-identical to the oracle."""
     import torch

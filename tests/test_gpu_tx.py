@@ -17,7 +17,7 @@ def run_tx(cfg, audio, frames, args=None):
     C, n, _ = audio.shape
     chain = U.TxChain(cfg, channels=C, frames=frames)
     d_iq = torch.empty((C, frames, 2), dtype=torch.int32, device="cuda")
-    d_a0 = torch.empty((C, frames), dtype=torch.float32, device="cuda")
+    d_a0 = torch.zeros((C, frames), dtype=torch.float32, device="cuda")   # DIGIQ calls leave a_buffer[0]
 
     def process(block):
         chain.process(torch.from_numpy(block).cuda(), d_iq, d_a0)

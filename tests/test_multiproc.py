@@ -33,12 +33,18 @@ def _rank_main(rank, world, port, out_path):
     lo, hi = shard.channel_range(PER_RANK, rank)
     plan = U.build_plan(U.default_config())
     iq = synth.ssb_iq(np.arange(lo, hi), 0, FRAMES)
-    a1, _ = oracle.OracleRx(plan, hi - lo).process(iq)
-    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)           # bench.py's max-over-ranks timing
-    full = shard.gather_to_root(torch.from_numpy(a1), dist, world, rank)
+    orx = oracle.OracleRx(plan, hi - lo)
+    res = {}
+
+    def step(k):
+        res["a1"], _ = orx.process(iq)
+    # bench.py's timed region (barrier + sync brackets, max-over-ranks seconds): rank 1 sleeps,
+    # so the reduced time must cover its sleep on every rank
+    import time
+    el = shard.timed_loop(step, lambda: time.sleep(0.2 if rank == 1 else 0.0), 1, 0, dist, world, "cpu")
+    assert el >= 0.2
+    full = shard.gather_to_root(torch.from_numpy(res["a1"]), dist, world, rank)
     if rank == 0:
-        assert float(t.item()) == float(world)
         np.save(out_path, full.numpy())
     dist.barrier()
     dist.destroy_process_group()

@@ -79,6 +79,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--only", default="c3,c3spec,c3zoom,c4fm,c4tx,c5,c5fir")
+    ap.add_argument("--fir-waves", type=int, default=0, help="c5fir: waves per workgroup (1, 2, 4; 0 = the default)")
     a = ap.parse_args()
     import torch
     import uhsdr_amd as U
@@ -99,9 +100,10 @@ def main():
         ms = time_calls(lambda: spec.process(iq, None, avg), a.steps, a.warmup)
         byts = C * N * (8 + 4) + C * L * 8
         lines.append({"workload": "C3 spectrum 1024-point (Hann, CFFT, magnitude, IIR average)", "channels": C,
-                      "frames_per_call": N, "ms_per_call": round(ms, 4), "msamples_per_s": round(C * N / ms / 1e3, 1),
+                      "frames_per_call": N, "waves_per_workgroup": waves, "ms_per_call": round(ms, 4), "msamples_per_s": round(C * N / ms / 1e3, 1),
                       "alg_bytes_per_frame": round(byts / (C * N), 2),
-                      "hbm_frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4)})
+                      "hbm_frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4),
+                      "finite": bool(torch.isfinite(avg).all().item())})
         spec.close()
     if "c3zoom" in want:
         # zoom producer (spectrum_zoom) 8x + 256-point display: 8 B in per frame, the ring
@@ -118,7 +120,8 @@ def main():
         lines.append({"workload": f"C3-size zoom spectrum {D}x, {L}-point (FreqShift, zoom biquad, decimate, CFFT)",
                       "channels": C, "frames_per_call": N, "ms_per_call": round(ms, 4),
                       "msamples_per_s": round(C * N / ms / 1e3, 1), "alg_bytes_per_frame": round(byts / (C * N), 2),
-                      "hbm_frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4)})
+                      "hbm_frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4),
+                      "finite": bool(torch.isfinite(avg).all().item())})
         spec.close()
     if "c4fm" in want:
         C, N = 262144 // 8, 256
@@ -131,7 +134,8 @@ def main():
         tx = U.TxChain(channels=C, frames=N, stream=s.cuda_stream)
         audio = tiled(synth.tx_audio, C, N)
         iq = torch.empty((C, N, 2), dtype=torch.int32, device="cuda")
-        ms = time_calls(lambda: tx.process(audio, iq), a.steps, a.warmup)
+        a0 = torch.empty((C, N), dtype=torch.float32, device="cuda")
+        ms = time_calls(lambda: tx.process(audio, iq, a0), a.steps, a.warmup)
         # 8 B audio frame in, 8 B I/Q frame out, state (Hilbert 200, lattice 10, biquads 12, ALC,
         # 320-sample delay line) read + written once per call, the f32 hand-off between kernels
         state = 4 * (200 + 10 + 12 + 1 + 320)
@@ -139,7 +143,8 @@ def main():
         lines.append({"workload": "C4 per-GPU share: SSB-TX (IIR_TX_SOPRANO + biquads + ALC + 201-tap Hilbert + Fs/4)",
                       "channels": C, "frames_per_call": N, "ms_per_call": round(ms, 4),
                       "msamples_per_s": round(C * N / ms / 1e3, 1), "alg_bytes_per_frame": round(per, 2),
-                      "hbm_frac": round(C * N * per / ms / 1e6 / HBM_PEAK_GBS, 4)})
+                      "hbm_frac": round(C * N * per / ms / 1e6 / HBM_PEAK_GBS, 4),
+                      "finite": bool(torch.isfinite(a0).all().item()) and bool((iq != 0).any().item())})
         tx.close()
     if "c5" in want:
         C, N = 1048576 // 8, 256
@@ -157,21 +162,32 @@ def main():
         for mode, name in ((U.fir.EXACT, "exact, bit-identical to arm_fir_f32"),
                            (U.fir.MFMA, "MFMA v_mfma_f32_16x16x4_f32, FIR as GEMM, fused MACs")):
             fir = U.FirBatch(taps, C, N, mode, stream=s.cuda_stream)
+            if a.fir_waves:
+                fir.set_waves(a.fir_waves)
             ms = time_calls(lambda: fir.process(x, y), a.steps, a.warmup)
+            waves = fir.waves
             fir.close()
             per = 8 + 2 * 4 * (T - 1) / N                 # 4 B in + 4 B out, carried samples in + out
             K = (T + 15 + 3) & ~3
             line = {"workload": f"C5 per-GPU share: batched 513-tap FIR at 12 ksps ({name})", "channels": C,
-                    "frames_per_call": N, "ms_per_call": round(ms, 4), "msamples_per_s": round(C * N / ms / 1e3, 1),
+                    "frames_per_call": N, "waves_per_workgroup": waves, "ms_per_call": round(ms, 4), "msamples_per_s": round(C * N / ms / 1e3, 1),
                     "alg_bytes_per_frame": round(per, 2), "hbm_frac": round(C * N * per / ms / 1e6 / HBM_PEAK_GBS, 4),
-                    "alg_tflops": round(C * N * 2 * T / ms / 1e9, 1)}
+                    "alg_tflops": round(C * N * 2 * T / ms / 1e9, 1),
+                    "finite": bool(torch.isfinite(y).all().item())}
             if mode == U.fir.MFMA:
                 line["mfma_tflops_issued"] = round(C * N * 2 * K / ms / 1e9, 1)
                 line["mfma_f32_peak_tflops"] = 157.3
             lines.append(line)
+    bad = []
     for ln in lines:
         ln["data"] = "synthetic: 4096 distinct channels tiled"
         print(json.dumps(ln), flush=True)
+        if not ln.get("finite", False):
+            bad.append(ln["workload"])
+    if bad:
+        # every line's outputs must be finite (and the TX I/Q not all zero): a fast wrong kernel
+        # is not a measurement
+        sys.exit(f"non-finite outputs: {bad}")
 
 
 if __name__ == "__main__":

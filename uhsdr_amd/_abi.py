@@ -123,7 +123,8 @@ class TxPlan(C.Structure):
         ("fm", C.c_int32), ("fm_mod_mult", C.c_float), ("fm_word", C.c_uint32), ("fm_swap", C.c_int32),
         ("fm_sub_on", C.c_int32), ("fm_sub_step", C.c_uint32), ("fm_sub_scale", C.c_float),
         ("dds_table", C.c_int16 * 1024), ("tune_step", C.c_uint32 * 2), ("tone_burst_step", C.c_uint32),
-        ("tone_burst_scale", C.c_float), ("reserved", C.c_int32 * 28),
+        ("tone_burst_scale", C.c_float), ("am", C.c_int32), ("digiq", C.c_int32), ("digiq_i_gain", C.c_float),
+        ("digiq_q_gain", C.c_float), ("reserved", C.c_int32 * 24),
     ]
 
 
@@ -212,6 +213,8 @@ SIGNATURES = {
     "uhsdr_fir_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "uhsdr_fir_synchronize": (C.c_int, [C.c_void_p]),
     "uhsdr_fir_destroy": (C.c_int, [C.c_void_p]),
+    "uhsdr_fir_set_waves": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_fir_get_waves": (C.c_int32, [C.c_void_p]),
     "uhsdr_i2s_create": (C.c_int, [C.POINTER(RxConfig), C.POINTER(TxConfig), C.c_int32, C.c_void_p,
                                    C.POINTER(C.c_void_p)]),
     "uhsdr_i2s_set_txrx_mode": (C.c_int, [C.c_void_p, C.c_int32]),
@@ -316,7 +319,9 @@ TX_ARG_MAP = {
     "comp": "comp_level", "txfilter": "tx_filter", "txbass": "bass_gain", "txtreble": "treble_gain",
     "txpwr": "power_factor", "txgi": "gain_i", "txgq": "gain_q", "txphase": "phase_balance",
     "fm5k": "fm_deviation_5k", "subtone": "fm_subaudible_tone", "burstmode": "fm_tone_burst_mode",
+    "txsrc": "audio_source",
 }
+FLAGS1_AM_TX_FILTER_DISABLE, FLAGS1_SSB_TX_FILTER_DISABLE = 0x08, 0x40   # hardware/uhsdr_board.h:513,516
 TUNE_OFF, TUNE_SINGLE, TUNE_TWO = range(3)      # uhsdr_tx_set_tune
 
 
@@ -329,7 +334,11 @@ def default_tx_config(**overrides) -> TxConfig:
 
 
 def tx_config_from_ref_args(args: dict) -> TxConfig:
-    return default_tx_config(**{TX_ARG_MAP[k]: v for k, v in args.items() if k in TX_ARG_MAP})
+    kw = {TX_ARG_MAP[k]: v for k, v in args.items() if k in TX_ARG_MAP}
+    # ts.flags1: the filter-disable flag of the configured mode (tx_processor.c:991, :1003)
+    flag = FLAGS1_AM_TX_FILTER_DISABLE if args.get("mode", 0) == DEMOD_AM else FLAGS1_SSB_TX_FILTER_DISABLE
+    kw["filter_disable"] = int(bool(int(args.get("flags1", 0)) & flag))
+    return default_tx_config(**kw)
 
 
 def build_tx_plan(cfg: TxConfig) -> TxPlan:

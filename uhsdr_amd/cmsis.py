@@ -1,7 +1,7 @@
 """ctypes view of include/uhsdr_cmsis.h: the CMSIS-DSP signature shims of libuhsdr_cmsis.so.
 
 The instance structs mirror CMSIS-DSP V1.4.5 (basesw/ovi40/Drivers/CMSIS/Include/arm_math.h)
-field for field.  `Fir`, `FirDecimate`, `FirInterpolate`, `IirLattice`, `BiquadDf1` wrap one
+field for field.  `Fir`, `FirDecimate`, `FirInterpolate`, `IirLattice`, `BiquadDf1`, `LmsNorm` wrap one
 instance with its caller-owned state and coefficient arrays the way firmware code holds them
 (audio_filter.c:1084-1115), and call the shims exactly like the firmware calls CMSIS.
 """
@@ -43,6 +43,11 @@ class arm_cfft_instance_f32(C.Structure):
                 ("bitRevLength", C.c_uint16)]
 
 
+class arm_lms_norm_instance_f32(C.Structure):
+    _fields_ = [("numTaps", C.c_uint16), ("pState", FP), ("pCoeffs", FP), ("mu", C.c_float),
+                ("energy", C.c_float), ("x0", C.c_float)]
+
+
 P = C.POINTER
 SIGNATURES = {
     "arm_fir_init_f32": (None, [P(arm_fir_instance_f32), C.c_uint16, FP, FP, C.c_uint32]),
@@ -59,6 +64,8 @@ SIGNATURES = {
     "arm_biquad_cascade_df1_f32": (None, [P(arm_biquad_casd_df1_inst_f32), FP, FP, C.c_uint32]),
     "arm_cfft_f32": (None, [P(arm_cfft_instance_f32), FP, C.c_uint8, C.c_uint8]),
     "arm_cmplx_mag_f32": (None, [FP, FP, C.c_uint32]),
+    "arm_lms_norm_init_f32": (None, [P(arm_lms_norm_instance_f32), C.c_uint16, FP, FP, C.c_float, C.c_uint32]),
+    "arm_lms_norm_f32": (None, [P(arm_lms_norm_instance_f32), FP, FP, FP, FP, C.c_uint32]),
     "uhsdr_cmsis_last_status": (C.c_int32, []),
 }
 
@@ -180,6 +187,32 @@ class BiquadDf1(_Inst):
 
     def __call__(self, x):
         return self._run(self.lib.arm_biquad_cascade_df1_f32, x, len(x))
+
+
+class LmsNorm:
+    """arm_lms_norm_f32 on one instance: coefficients (adapted in place in `coeffs`), the
+    carried window `state`, energy / x0 in the struct.  in_place: pErr == pSrc, the way
+    AudioDriver_NotchFilter calls it (audio_driver.c:1755)."""
+
+    in_place = False
+
+    def __init__(self, coeffs, mu: float, block: int):
+        self.lib = load()
+        self.coeffs = np.array(coeffs, np.float32, copy=True)
+        self.state = np.zeros(len(self.coeffs) + block - 1, np.float32)
+        self.S = arm_lms_norm_instance_f32()
+        self.lib.arm_lms_norm_init_f32(C.byref(self.S), len(self.coeffs), _fp(self.coeffs), _fp(self.state),
+                                       float(mu), block)
+
+    def __call__(self, x, ref):
+        """one block: returns (out, err)"""
+        x = np.array(x, np.float32, copy=True)
+        d = np.ascontiguousarray(ref, np.float32)
+        y = np.zeros(len(x), np.float32)
+        e = x if self.in_place else np.zeros(len(x), np.float32)
+        self.lib.arm_lms_norm_f32(C.byref(self.S), _fp(x), _fp(d), _fp(y), _fp(e), len(x))
+        _check(self.lib)
+        return y, e.copy()
 
 
 def cfft(x: np.ndarray, ifft: bool = False, bitrev: bool = True, twiddle=None, bitrev_table=None) -> np.ndarray:

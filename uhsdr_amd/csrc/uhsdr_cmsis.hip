@@ -17,6 +17,9 @@
 //                                       conjugation, bit reversal and 1/L scaling
 //                                       (TransformFunctions/arm_cfft_f32.c:574-628)
 //   arm_cmplx_mag_f32                   sqrtf(re * re + im * im) (arm_cmplx_mag_f32.c:84-170)
+//   arm_lms_norm_f32                    per sample: energy -= x0 x0, += in in; y = sum_k x[n+k] w[k]
+//                                       in tap order; e = d - y; w[k] += (e mu / (energy + eps))
+//                                       x[n+k]; x0 = x[n] (arm_lms_norm_f32.c:205-300)
 // The recursive filters (lattice, biquad) are sequential in time: one lane runs the block.
 
 #include <hip/hip_runtime.h>
@@ -108,6 +111,48 @@ __global__ void __launch_bounds__(SHIM_THREADS) shim_mag(const float* __restrict
     const float re = x[2 * i], im = x[2 * i + 1];
     const float in = (re * re) + (im * im);
     y[i] = (in >= 0.0f) ? sqrtf(in) : 0.0f;      // arm_sqrt_f32 (arm_math.h:5745-5771)
+}
+
+// one wave: the dot product runs in lane 0 in tap order (the reference's sum), the coefficient
+// update is split over the lanes (each w[k] is updated independently); w lives in LDS for the
+// block.  win: [T-1 carried | B new] samples; ex: {energy, x0} in and out; w_io: coefficients in
+// and out.
+constexpr int MAX_LMS_TAPS = 8192;
+
+__global__ void __launch_bounds__(64) shim_lms_norm(const float* __restrict__ win, const float* __restrict__ ref,
+                                                    float* __restrict__ out, float* __restrict__ err,
+                                                    float* __restrict__ w_io, float* __restrict__ ex, float mu,
+                                                    int T, int B)
+{
+    __shared__ float w[MAX_LMS_TAPS];
+    __shared__ float step;
+    const int lane = threadIdx.x;
+    for (int k = lane; k < T; k += 64) w[k] = w_io[k];
+    float energy = ex[0], x0 = ex[1];
+    __syncthreads();
+    for (int n = 0; n < B; ++n)
+    {
+        const float* x = win + n;
+        if (lane == 0)
+        {
+            const float in = x[T - 1];
+            energy -= x0 * x0;
+            energy += in * in;
+            float sum = 0.0f;
+            for (int k = 0; k < T; ++k) sum += x[k] * w[k];
+            out[n] = sum;
+            const float e = ref[n] - sum;
+            err[n] = e;
+            step = (e * mu) / (energy + 0.000000119209289f);
+            x0 = x[0];
+        }
+        __syncthreads();
+        const float wf = step;
+        for (int k = lane; k < T; k += 64) w[k] += wf * x[k];
+        __syncthreads();
+    }
+    for (int k = lane; k < T; k += 64) w_io[k] = w[k];
+    if (lane == 0) { ex[0] = energy; ex[1] = x0; }
 }
 
 // one wave: p1 (interleaved complex, L points) in place
@@ -704,6 +749,53 @@ void arm_cmplx_mag_f32(float32_t* pSrc, float32_t* pDst, uint32_t numSamples)
     hipLaunchKernelGGL(shim_mag, dim3(grid(n)), dim3(SHIM_THREADS), 0, t_ctx.stream, d + offs[0], d + offs[1], n);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess || !finish(pDst, d + offs[1], n)) { fail(UHSDR_DEVICE_ERROR, "arm_cmplx_mag_f32", e); return; }
+}
+
+void arm_lms_norm_init_f32(arm_lms_norm_instance_f32* S, uint16_t numTaps, float32_t* pCoeffs, float32_t* pState,
+                           float32_t mu, uint32_t blockSize)
+{
+    S->numTaps = numTaps;
+    S->pCoeffs = pCoeffs;
+    memset(pState, 0, (numTaps + (blockSize - 1u)) * sizeof(float32_t));
+    S->pState = pState;
+    S->mu = mu;
+    S->energy = 0.0f;
+    S->x0 = 0.0f;
+}
+
+void arm_lms_norm_f32(arm_lms_norm_instance_f32* S, float32_t* pSrc, float32_t* pRef, float32_t* pOut,
+                      float32_t* pErr, uint32_t blockSize)
+{
+    t_status = 0;
+    if (!S || !S->pState || !S->pCoeffs || !pSrc || !pRef || !pOut || !pErr || !S->numTaps || S->numTaps > MAX_LMS_TAPS)
+    { fail(UHSDR_ARGUMENT_ERROR, "arm_lms_norm_f32", hipSuccess); return; }
+    const int T = S->numTaps, B = (int)blockSize;
+    if (B <= 0) return;
+    const float ex[2] = { S->energy, S->x0 };
+    // the window [T-1 carried | block] must be contiguous: carried state and block are separate
+    // host segments, so the window is one segment built from both
+    const size_t nwin = (size_t)T - 1 + B;
+    const Seg segs[6] = { { nullptr, nwin }, { pRef, (size_t)B }, { nullptr, (size_t)B }, { nullptr, (size_t)B },
+                          { S->pCoeffs, (size_t)T }, { ex, 2 } };
+    size_t offs[6];
+    float* d = upload(segs, 6, seg_total(segs, 6), offs);
+    hipError_t e = hipSuccess;
+    if (d && T > 1) e = hipMemcpyAsync(d + offs[0], S->pState, sizeof(float) * (T - 1), hipMemcpyHostToDevice, t_ctx.stream);
+    if (d && e == hipSuccess) e = hipMemcpyAsync(d + offs[0] + T - 1, pSrc, sizeof(float) * B, hipMemcpyHostToDevice, t_ctx.stream);
+    if (!d || e != hipSuccess) { fail(UHSDR_DEVICE_ERROR, "arm_lms_norm_f32 upload", d ? e : hipGetLastError()); return; }
+    hipLaunchKernelGGL(shim_lms_norm, dim3(1), dim3(64), 0, t_ctx.stream, d + offs[0], d + offs[1], d + offs[2],
+                       d + offs[3], d + offs[4], d + offs[5], S->mu, T, B);
+    e = hipGetLastError();
+    // carried samples: the window's last T-1 (pErr may alias pSrc, so they come from the device)
+    if (e == hipSuccess && T > 1)
+        e = hipMemcpyAsync(S->pState, d + offs[0] + B, sizeof(float) * (T - 1), hipMemcpyDeviceToHost, t_ctx.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(S->pCoeffs, d + offs[4], sizeof(float) * T, hipMemcpyDeviceToHost, t_ctx.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(pOut, d + offs[2], sizeof(float) * B, hipMemcpyDeviceToHost, t_ctx.stream);
+    float exo[2];
+    if (e == hipSuccess) e = hipMemcpyAsync(exo, d + offs[5], sizeof(float) * 2, hipMemcpyDeviceToHost, t_ctx.stream);
+    if (e != hipSuccess || !finish(pErr, d + offs[3], B)) { fail(UHSDR_DEVICE_ERROR, "arm_lms_norm_f32", e); return; }
+    S->energy = exo[0];
+    S->x0 = exo[1];
 }
 
 } // extern "C"

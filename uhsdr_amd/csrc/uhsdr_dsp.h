@@ -162,6 +162,55 @@ __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&
     }
 }
 
+// RD outputs of a decimate-by-M FIR per lane (arm_fir_decimate_f32, CMSIS .../arm_fir_decimate_f32.c:
+// 141), outputs taken in pairs (r, r+1) on packed f32: acc[j] = { sum_k c[k] * win[2jM + k],
+// sum_k c[k] * win[(2j+1)M + k] } with the taps as duplicated pairs {c[k], c[k]}.  Per element this
+// is fir_block's binary32 sequence (tap order from +0.0f; F: fused); each tap's window pair comes
+// from LDS as one ds_read2_b32 (the two samples M apart), fetched a chunk of 8 taps ahead, so a pair
+// of outputs costs one packed multiply + one packed add per tap instead of two of each.
+template <int T, int RD, int M, bool F = false>
+__device__ __forceinline__ void fir_dec2(const float* win, ctaps2_t* cd, v2f (&acc)[RD / 2])
+{
+    static_assert(RD % 2 == 0, "outputs in pairs");
+    constexpr int NP = RD / 2, NCH = T / 8, TR = T % 8;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) acc[j] = v2f{ 0.0f, 0.0f };
+    v2f w[NP][8];
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) w[j][q] = v2f{ win[2 * j * M + q], win[(2 * j + 1) * M + q] };
+#pragma unroll 2
+    for (int ch = 0; ch < NCH; ++ch)
+    {
+        v2f cc[8], nw[NP][8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cc[q] = cd[8 * ch + q];
+        // the next chunk (or the tail) ahead; past the tail the loads run at most FRONT_TAIL samples
+        // beyond the data and are never used
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                nw[j][q] = v2f{ win[8 * (ch + 1) + 2 * j * M + q], win[8 * (ch + 1) + (2 * j + 1) * M + q] };
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int j = 0; j < NP; ++j) acc[j] = fir_mac<F>(acc[j], w[j][q], cc[q]);
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) w[j][q] = nw[j][q];
+    }
+#pragma unroll
+    for (int q = 0; q < TR; ++q)
+    {
+        const v2f ck = cd[8 * NCH + q];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) acc[j] = fir_mac<F>(acc[j], w[j][q], ck);
+    }
+}
+
 // samples after the end of a window that the register-window FIRs read (never use): the last
 // chunk's next-8 prefetch runs -R + 8*floor(T/8) + WA - T + 1 samples past the data, at most 8
 // for every (T, R, M) instantiated here; zeroed all the same
@@ -424,6 +473,55 @@ __device__ __forceinline__ void group_store_rows(const float* smem, int LW, floa
         h[q] = *(const vf4*)(smem + (q / hs4) * LW + nnew + 4 * (q % hs4));
 }
 
+// ---- pair history rows: a FIR pair's two T-1 sample histories stored interleaved {x0[n], x1[n]}
+//      (hist_stride(T) pairs, 2 * hist_stride(T) floats per channel), the window's own layout, so a
+//      float4 (two pairs) moves between HBM and LDS as is ----
+__host__ __device__ constexpr int hist_p4(int T) { return hist_stride(T) / 2; }       // float4s per pair row
+__host__ __device__ constexpr int hist_qp(int T) { return (hist_p4(T) + 7) / 8; }      // prefetched per lane
+
+template <int T, int HQM>
+__device__ __forceinline__ void group_load_prow(const float* row, int c0, int nlive, int lane, vf4 (&buf)[HQM])
+{
+    constexpr int hp4 = hist_p4(T), HQ = hist_qp(T);
+    const vf4* h = (const vf4*)(row + (size_t)c0 * (hp4 * 4));
+    const int qmax = nlive * hp4 - 1;                    // loads clamped to the live channels' rows
+#pragma unroll
+    for (int i = 0; i < HQ; ++i)
+    {
+        const int q = lane + FRONT_WAVE_L * i;
+        buf[i] = h[q < qmax ? q : qmax];
+    }
+}
+
+// float4 q of the group's rows is channel q / hp4, pairs 2 (q % hp4) .. + 1 of its window
+template <int T, int HQM>
+__device__ __forceinline__ void group_fill_prow(float* smem, int LW, const float* row, int c0, int cpw, int nlive,
+                                                int lane, const vf4 (&buf)[HQM])
+{
+    constexpr int hp4 = hist_p4(T), HQ = hist_qp(T);
+    const int nq = cpw * hp4;
+#pragma unroll
+    for (int i = 0; i < HQ; ++i)
+    {
+        const int q = lane + FRONT_WAVE_L * i;
+        if (q < nq) *(vf4*)(smem + (q / hp4) * LW + 4 * (q % hp4)) = buf[i];
+    }
+    const vf4* h = (const vf4*)(row + (size_t)c0 * (hp4 * 4));
+    const int qmax = nlive * hp4 - 1;
+    for (int q = lane + FRONT_WAVE_L * HQ; q < nq; q += FRONT_WAVE_L)
+        *(vf4*)(smem + (q / hp4) * LW + 4 * (q % hp4)) = h[q < qmax ? q : qmax];
+}
+
+// the next call's pair rows: window pairs nnew .. nnew + hist_stride(T) - 1 of each channel
+template <int T>
+__device__ __forceinline__ void group_store_prow(const float* smem, int LW, float* row, int c0, int nlive, int lane, int nnew)
+{
+    constexpr int hp4 = hist_p4(T);
+    vf4* h = (vf4*)(row + (size_t)c0 * (hp4 * 4));
+    for (int q = lane; q < nlive * hp4; q += FRONT_WAVE_L)
+        h[q] = *(const vf4*)(smem + (q / hp4) * LW + 2 * nnew + 4 * (q % hp4));
+}
+
 // new samples and the zero tail of one channel's window (the lane's own NV values)
 __device__ __forceinline__ void window_new2(float* W, int T, bool act, int b, int nb, const v2f* vals, int NV)
 {
@@ -579,11 +677,12 @@ static const int kB128Groups[4][16] = {
     { 32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59 },
     { 36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63 } };
 
-// extra LDS cycles of one FIR window read for lane bases g*lw + b*stride (dwords), vec 4 or 2
+// extra LDS cycles of one FIR window read for lane bases g*lw + b*stride (dwords): vec 4
+// (ds_read_b128), 2 (ds_read_b64) or 1 (ds_read_b32 / each half of ds_read2_b32: 32 banks)
 static inline int window_conflicts(int lw, int nb, int cpw, int R, int stride, int vec)
 {
     int cost = 0;
-    const int ngroups = vec == 4 ? 4 : 2, glen = vec == 4 ? 16 : 32;
+    const int ngroups = vec == 4 ? 4 : 2, glen = vec == 4 ? 16 : 32, banks = vec == 1 ? 32 : 64;
     for (int gi = 0; gi < ngroups; ++gi)
     {
         int load[64] = { 0 };
@@ -594,7 +693,7 @@ static inline int window_conflicts(int lw, int nb, int cpw, int R, int stride, i
             front_lane(l, nb, R, g, b);
             if (g >= cpw) continue;
             const int addr = g * lw + b * stride;
-            for (int d = 0; d < vec; ++d) load[(addr + d) & 63] += 1;
+            for (int d = 0; d < vec; ++d) load[(addr + d) & (banks - 1)] += 1;
         }
         int mx = 0;
         for (int k = 0; k < 64; ++k) mx = load[k] > mx ? load[k] : mx;

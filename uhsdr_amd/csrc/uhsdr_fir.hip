@@ -304,6 +304,42 @@ extern "C" uhsdr_status uhsdr_fir_reset(uhsdr_fir_handle h)
     return UHSDR_OK;
 }
 
+// waves per workgroup and the launch grid for them.  strict: the exact count or an error;
+// otherwise halved until the workgroup's LDS fits.
+static uhsdr_status fir_configure(uhsdr_fir_s* h, int waves, bool strict)
+{
+    if (waves != 1 && waves != 2 && waves != 4)
+    {
+        uhsdr_set_error("waves per workgroup %d not 1, 2 or 4", waves);
+        return UHSDR_ARGUMENT_ERROR;
+    }
+    if (!strict)
+        while (waves > 1 && fir_lds(h, waves) > 64 * 1024) waves /= 2;
+    if (fir_lds(h, waves) > 64 * 1024 || h->T - 1 + h->B > 64 * FIR_NPL)
+    {
+        uhsdr_set_error("num_taps - 1 + block_size %d too long for %d waves per workgroup", h->T - 1 + h->B, waves);
+        return UHSDR_LENGTH_ERROR;
+    }
+    // persistent grid: as many workgroups as the CUs hold at once (LDS-limited), each wave
+    // walking channel groups
+    int dev = 0, cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+        cus = prop.multiProcessorCount;
+    const size_t lds = fir_lds(h, waves);
+    int per_cu = (int)((160 * 1024) / lds);
+    const int thread_cap = 2048 / (64 * waves);
+    if (per_cu > thread_cap) per_cu = thread_cap;
+    if (per_cu < 1) per_cu = 1;
+    const int groups = (h->C + FIR_CPW - 1) / FIR_CPW;
+    const int need = (groups + waves - 1) / waves;
+    // MFMA: persistent (C5 0.69 -> 0.40 ms per call); EXACT: fir_batch_direct, one
+    // group per wave (0.99 ms; 1.20 in the persistent form)
+    h->waves = waves;
+    h->grid = (h->mode == UHSDR_FIR_MFMA && need > cus * per_cu) ? cus * per_cu : need;
+    return UHSDR_OK;
+}
+
 extern "C" uhsdr_status uhsdr_fir_create(const float* coeffs, int32_t num_taps, int32_t num_channels, int32_t block_size,
                                          int32_t mode, void* stream, uhsdr_fir_handle* out)
 {
@@ -326,45 +362,22 @@ extern "C" uhsdr_status uhsdr_fir_create(const float* coeffs, int32_t num_taps, 
     h->stream = (hipStream_t)stream;
     h->lw = (fpad(num_taps - 1 + block_size + FIR_TAIL) + 4) & ~3;
     h->cp = (h->K + 16 + 16 + 3) & ~3;
-    {
-        // waves per workgroup: EXACT 2 (one group per wave, more resident waves per CU: C5
-        // 513-tap 1.048 -> 0.927 ms per call), MFMA 4 (persistent; 0.395 ms vs 0.497 at 2);
-        // benchmarking knob UHSDR_FIR_WAVES = 1, 2 or 4
-        const char* env = getenv("UHSDR_FIR_WAVES");
-        const int wv = env ? atoi(env) : mode == UHSDR_FIR_MFMA ? 4 : 2;
-        h->waves = 4;
-        if (wv == 1 || wv == 2 || wv == 4) h->waves = wv;
-    }
-    while (h->waves > 1 && fir_lds(h, h->waves) > 64 * 1024) h->waves /= 2;
-    if (fir_lds(h, h->waves) > 64 * 1024 || num_taps - 1 + block_size > 64 * FIR_NPL)
+    // waves per workgroup: EXACT 2 (one group per wave, more resident waves per CU: C5 513-tap
+    // 1.048 -> 0.927 ms per call), MFMA 4 (persistent; 0.395 ms vs 0.497 at 2);
+    // uhsdr_fir_set_waves picks 1, 2 or 4 explicitly
+    const uhsdr_status st = fir_configure(h, mode == UHSDR_FIR_MFMA ? 4 : 2, false);
+    if (st != UHSDR_OK)
     {
         free(h);
-        uhsdr_set_error("num_taps - 1 + block_size above %d", 64 * FIR_NPL);
-        return UHSDR_LENGTH_ERROR;
+        return st;
     }
+    hipError_t e = hipMalloc((void**)&h->taps, sizeof(float) * num_taps);
+    if (e == hipSuccess)
+        e = hipMalloc((void**)&h->hist, sizeof(float) * (size_t)num_channels * (num_taps > 1 ? num_taps - 1 : 1));
+    if (e == hipSuccess) e = hipMemcpy(h->taps, coeffs, sizeof(float) * num_taps, hipMemcpyHostToDevice);
+    if (e != hipSuccess)
     {
-        // persistent grid: as many workgroups as the CUs hold at once (LDS-limited), each wave
-        // walking channel groups
-        int dev = 0, cus = 256;
-        hipDeviceProp_t prop;
-        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-            cus = prop.multiProcessorCount;
-        const size_t lds = fir_lds(h, h->waves);
-        int per_cu = (int)((160 * 1024) / lds);
-        const int thread_cap = 2048 / (64 * h->waves);
-        if (per_cu > thread_cap) per_cu = thread_cap;
-        if (per_cu < 1) per_cu = 1;
-        const int groups = (num_channels + FIR_CPW - 1) / FIR_CPW;
-        const int need = (groups + h->waves - 1) / h->waves;
-        // MFMA: persistent (C5 0.69 -> 0.40 ms per call); EXACT: fir_batch_direct, one
-        // group per wave (0.99 ms; 1.20 in the persistent form)
-        h->grid = (mode == UHSDR_FIR_MFMA && need > cus * per_cu) ? cus * per_cu : need;
-    }
-    if (hipMalloc((void**)&h->taps, sizeof(float) * num_taps) != hipSuccess ||
-        hipMalloc((void**)&h->hist, sizeof(float) * (size_t)num_channels * (num_taps > 1 ? num_taps - 1 : 1)) != hipSuccess ||
-        hipMemcpy(h->taps, coeffs, sizeof(float) * num_taps, hipMemcpyHostToDevice) != hipSuccess)
-    {
-        uhsdr_set_error("device allocation failed");
+        uhsdr_set_error("device allocation failed: %s", hipGetErrorString(e));
         uhsdr_fir_destroy(h);
         return UHSDR_DEVICE_ERROR;
     }
@@ -386,6 +399,17 @@ extern "C" uhsdr_status uhsdr_fir_process(uhsdr_fir_handle h, const float* src, 
     HIPCHK(hipGetLastError());
     return UHSDR_OK;
 }
+
+extern "C" uhsdr_status uhsdr_fir_set_waves(uhsdr_fir_handle h, int32_t waves)
+{
+    if (!h) { uhsdr_set_error("null handle"); return UHSDR_ARGUMENT_ERROR; }
+    const int old = h->waves;
+    const uhsdr_status st = fir_configure(h, waves, true);
+    if (st != UHSDR_OK) fir_configure(h, old, true);
+    return st;
+}
+
+extern "C" int32_t uhsdr_fir_get_waves(uhsdr_fir_handle h) { return h ? h->waves : 0; }
 
 extern "C" uhsdr_status uhsdr_fir_synchronize(uhsdr_fir_handle h)
 {

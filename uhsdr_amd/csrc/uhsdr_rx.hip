@@ -40,10 +40,12 @@ struct FrontArgs
 {
     const uhsdr_rx_plan* plan;
     const int2* iq;          // frame 0 of this launch; row stride ld frames (IqSample_t)
-    float* hist1_i;          // [C][HS1] stage-1 FIR history (Hilbert, or I decimator), HS = T-1 rounded to 4
-    float* hist1_q;          // [C][HS1]
-    float* hist2_i;          // [C][HS2] stage-2 history (audio decimator, or Hilbert I)
-    float* hist2_q;          // [C][HS2] (decimate-first paths: Hilbert Q)
+    float* hist1;            // [C][HS1][2] stage-1 FIR pair history {I, Q} (Hilbert, or I/Q decimators),
+                             // HS = T-1 rounded to 4
+    float* hist2;            // stage 2: [C][HS2] audio decimator history, or [C][HS2][2] pair history
+                             // (decimate-first: the Hilbert pair; stereo: the decimator pair)
+    const uint16_t* lanemap; // [64] front_lane of every lane: channel g << 8 | block b
+    int nb, cpw;             // lanes per channel, channels per wave
     float* teta;             // [3][C] auto I/Q correction low-pass state
     int* tp;                 // [5][C] twin-peaks detector: state, counter, restarts, runs, phase (f32 bits)
     unsigned* clip;          // optional [C]: ADC clip flags OR-ed in (uhsdr_rx_set_clip_output)
@@ -78,11 +80,15 @@ __device__ __forceinline__ void front_comb_block(int comb, const v2f (&h)[R], fl
 #pragma unroll
         for (int r = 0; r < R; ++r) o[r] = h[r].x;
     }
+    else if (comb == FRONT_COMB_LSB)
+    {
+#pragma unroll
+        for (int r = 0; r < R; ++r) o[r] = h[r].x - h[r].y;   // I + (-Q): the same binary32 result
+    }
     else
     {
-        const float sg = comb == FRONT_COMB_LSB ? -1.0f : 1.0f;
 #pragma unroll
-        for (int r = 0; r < R; ++r) o[r] = h[r].x + h[r].y * sg;
+        for (int r = 0; r < R; ++r) o[r] = h[r].x + h[r].y;
     }
 }
 __device__ __forceinline__ v2f front_comb2(int comb, v2f h)
@@ -200,8 +206,12 @@ __device__ __forceinline__ void convert_block(const int4 (&raw)[R / 2], const In
     }
     if (!s.iq_auto)
     {
+        // x * 1.0f == x exactly: the default gains (ts.rx_adj_gain_var 1.0) skip the multiplies
+        if (s.gi != 1.0f || s.gq != 1.0f)
+        {
 #pragma unroll
-        for (int j = 0; j < R; ++j) { xi[j] = xi[j] * s.gi; xq[j] = xq[j] * s.gq; }
+            for (int j = 0; j < R; ++j) { xi[j] = xi[j] * s.gi; xq[j] = xq[j] * s.gq; }
+        }
         if (s.ph < 0)
         {
 #pragma unroll
@@ -252,16 +262,17 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     const int N = a.N, C = a.C;
     const int lane = threadIdx.x & (FRONT_WAVE - 1);
-    const int nb = N / R;                            // lanes per channel (>= 4)
-    const int CPW = FRONT_WAVE / nb;                 // channels per wave (one channel group)
+    const int nb = a.nb;                             // lanes per channel (>= 4) = N / R
+    const int CPW = a.cpw;                           // channels per wave (one channel group)
     // (Measured and dropped: four independent waves per workgroup, 0.617 vs 0.600 ms at 1M x 64.)
-    int g, b;
-    front_lane(lane, nb, 2 * R, g, b);               // lane map for the pair window (2R floats per lane)
+    // lane map for the pair window (front_lane, 2R floats per lane), precomputed by the host
+    const unsigned lm = a.lanemap[lane];
+    const int g = (int)(lm >> 8), b = (int)(lm & 0xffu);
     const bool act = g < CPW;
     const int gs = act ? g : 0;
     const int nblk32 = N / BLK;
     constexpr int RD = R / M;                        // decimated samples per lane
-    constexpr int HQ1 = hist_q(T1), HQ2 = hist_q(T2 > 0 ? T2 : 1);
+    constexpr int HQ1 = hist_qp(T1), HQ2 = hist_q(T2 > 0 ? T2 : 1), HQP2 = hist_qp(T2 > 0 ? T2 : 1);
     const int LW = a.lw;
     float* W = smem + gs * LW;                       // this channel's window
     float* aux = smem + CPW * LW;                    // auto-IQ factors [2][CPW][nblk32], osc [2N]
@@ -286,7 +297,7 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
     // History rows move group-coalesced (group_load_rows: whole 1 KB runs per wave instruction);
     // the I/Q frames in the lane's own (channel, block) layout.
     int4 raw[R / 2];
-    vf4 hA[HQ1], hB[HQ1];
+    vf4 hA[HQ1];
     const int c = grp * CPW + g;
     const bool live = act && c < C;
     const int cl = c < C ? c : C - 1;                // loads clamped: no exec-masked load branches
@@ -296,8 +307,7 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
         const int4* src = (const int4*)(a.iq + (size_t)cl * a.ld + b * R);
 #pragma unroll
         for (int j = 0; j < R / 2; ++j) raw[j] = src[j];
-        group_load_rows<T1>(a.hist1_i, c0, nlive, lane, hA);
-        group_load_rows<T1>(a.hist1_q, c0, nlive, lane, hB);
+        group_load_prow<T1>(a.hist1, c0, nlive, lane, hA);
     }
     if (a.clip)
     {
@@ -391,11 +401,11 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
 #pragma unroll
             for (int j = 0; j < R; ++j) x2[j] = v2f{ xi[j], xq[j] };
         }
-        group_fill_rows2<T1>(smem, LW, a.hist1_i, a.hist1_q, c0, CPW, nlive, lane, hA, hB);
+        group_fill_prow<T1>(smem, LW, a.hist1, c0, CPW, nlive, lane, hA);
         wave_sync();
         window_new2(W, T1, act, b, nb, x2, R);
         wave_sync();
-        group_store_rows2<T1>(smem, LW, a.hist1_i, a.hist1_q, c0, nlive, lane, nb * R);
+        group_store_prow<T1>(smem, LW, a.hist1, c0, nlive, lane, nb * R);
 
         float o[RD];
         if constexpr (T2 == 0)
@@ -455,19 +465,18 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
         else if constexpr (!DECIM_FIRST && ST)
         {
             // stereo: {a_buffer[0], a_buffer[1]} through the decimator pair (taps2b = {dec, dec})
-            vf4 hC[HQ2], hD[HQ2];
-            group_load_rows<T2>(a.hist2_i, c0, nlive, lane, hC);
-            group_load_rows<T2>(a.hist2_q, c0, nlive, lane, hD);
+            vf4 hC[HQP2];
+            group_load_prow<T2>(a.hist2, c0, nlive, lane, hC);
             v2f h2[R], d2[RD];
             fir_block2<T1, R, 1, F>(W + 2 * b * R, tA, h2);
 #pragma unroll
             for (int r = 0; r < R; ++r) h2[r] = front_comb2(comb, h2[r]);
             wave_sync();
-            group_fill_rows2<T2>(smem, LW, a.hist2_i, a.hist2_q, c0, CPW, nlive, lane, hC, hD);
+            group_fill_prow<T2>(smem, LW, a.hist2, c0, CPW, nlive, lane, hC);
             wave_sync();
             window_new2(W, T2, act, b, nb, h2, R);
             wave_sync();
-            group_store_rows2<T2>(smem, LW, a.hist2_i, a.hist2_q, c0, nlive, lane, nb * R);
+            group_store_prow<T2>(smem, LW, a.hist2, c0, nlive, lane, nb * R);
             fir_block2<T2, RD, M, F>(W + 2 * b * R, as_taps2(a.taps2b), d2);
 #pragma unroll
             for (int r = 0; r < RD; ++r) o[r] = d2[r].x;
@@ -481,32 +490,35 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
         else if constexpr (!DECIM_FIRST)
         {
             vf4 hC[HQ2];
-            group_load_rows<T2>(a.hist2_i, c0, nlive, lane, hC);
-                v2f h2[R];
+            group_load_rows<T2>(a.hist2, c0, nlive, lane, hC);
+            v2f h2[R];
             float hs[R];
             fir_block2<T1, R, 1, F>(W + 2 * b * R, tA, h2);
             front_comb_block<R>(comb, h2, hs);
             wave_sync();
-            group_fill_rows<T2>(smem, LW, a.hist2_i, c0, CPW, nlive, lane, hC);
+            group_fill_rows<T2>(smem, LW, a.hist2, c0, CPW, nlive, lane, hC);
             wave_sync();
             window_new(W, T2, act, b, nb, hs, R);
             wave_sync();
-            group_store_rows<T2>(smem, LW, a.hist2_i, c0, nlive, lane, nb * R);
-            fir_block<T2, RD, M, 4, F>(W + b * R, as_taps(P->dec), o);
+            group_store_rows<T2>(smem, LW, a.hist2, c0, nlive, lane, nb * R);
+            // the audio decimator, its outputs in packed pairs (taps2b = {dec, dec})
+            v2f d2[RD / 2];
+            fir_dec2<T2, RD, M, F>(W + b * R, as_taps2(a.taps2b), d2);
+#pragma unroll
+            for (int j = 0; j < RD / 2; ++j) { o[2 * j] = d2[j].x; o[2 * j + 1] = d2[j].y; }
         }
         else
         {
-            vf4 hC[HQ2], hD[HQ2];
-            group_load_rows<T2>(a.hist2_i, c0, nlive, lane, hC);
-            group_load_rows<T2>(a.hist2_q, c0, nlive, lane, hD);
+            vf4 hC[HQP2];
+            group_load_prow<T2>(a.hist2, c0, nlive, lane, hC);
             v2f d2[RD], h2[RD];
             fir_block2<T1, RD, M, F>(W + 2 * b * R, tA, d2);
             wave_sync();
-            group_fill_rows2<T2>(smem, LW, a.hist2_i, a.hist2_q, c0, CPW, nlive, lane, hC, hD);
+            group_fill_prow<T2>(smem, LW, a.hist2, c0, CPW, nlive, lane, hC);
             wave_sync();
             window_new2(W, T2, act, b, nb, d2, RD);
             wave_sync();
-            group_store_rows2<T2>(smem, LW, a.hist2_i, a.hist2_q, c0, nlive, lane, nb * RD);
+            group_store_prow<T2>(smem, LW, a.hist2, c0, nlive, lane, nb * RD);
             fir_block2<T2, RD, 1, F>(W + 2 * b * RD, as_taps2(a.taps2b), h2);
             if constexpr (ST)
             {
@@ -1805,11 +1817,13 @@ __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys, in
     ou.load(a, l);
     // coefficients of the per-sample recursions into VGPRs (full-rate VOP2, no SGPR spills:
     // v_readlane refills 699 -> 104 per kernel, 0.220 -> 0.211 ms at 1M x 64)
+#ifndef UHSDR_FUSED_SGPR_COEF
     if (PRE > 0) { to_vgpr(pre.k); to_vgpr(pre.v); }
     if (AA > 0) { to_vgpr(aa.k); to_vgpr(aa.v); }
     to_vgpr(ou.b2);
     ou.lo = to_vgpr(ou.lo);
     to_vgpr(au.b1);
+#endif
     ag.agc_on = AGC_ON;
     if (DM != DM_NONE) ag.dc = true;
     else ag.dc_sel = true;
@@ -2556,7 +2570,8 @@ struct uhsdr_rx_s
     int T1, T2;
     hipStream_t stream;
     // front state
-    float *hist1_i, *hist1_q, *hist2_i, *hist2_q, *teta, *osc, *adec, *adec_q;
+    float *hist1, *hist2, *teta, *osc, *adec, *adec_q;
+    uint16_t* d_lanemap;     // [2][64] front_lane maps for R = 8 and R = 16 (g << 8 | b)
     int* tp;                 // [5][C] twin-peaks detector state
     unsigned* clip;          // user output (uhsdr_rx_set_clip_output)
     float* d_taps2;          // FIR pair tables: [2][2 * TAPS2_MAX] (pass 1, pass 2)
@@ -2671,7 +2686,10 @@ static int front_window_pitch(const uhsdr_rx_s* h)
     for (int lw = need; lw < need + 64; lw += 4)
     {
         int cost = window_conflicts(lw, nb, cpw, 2 * R, 2 * R, 4);
-        if (h->T2) cost += window_conflicts(lw, nb, cpw, 2 * R, df ? 2 * rd : pair2 ? 2 * R : R, 4);
+        // pass 2: pair windows read by ds_read_b128; the mono decimator's packed output pairs
+        // read sample pairs M apart (ds_read2_b32)
+        if (h->T2) cost += pair2 ? window_conflicts(lw, nb, cpw, 2 * R, df ? 2 * rd : 2 * R, 4)
+                                 : window_conflicts(lw, nb, cpw, 2 * R, R, 1);
         int waves = (int)(LDS_PER_CU / (sizeof(float) * ((size_t)cpw * lw + extra)));
         waves = waves > vgpr_waves ? vgpr_waves : waves;
 #ifdef UHSDR_PITCH_CONFLICTS_ONLY
@@ -2763,7 +2781,6 @@ static int resolve_schedule(const uhsdr_rx_s* h, int want)
     if (want == UHSDR_SCHEDULE_AUTO)
     {
         if (h->C < BACK_FUSED_MIN_CHANNELS) return UHSDR_SCHEDULE_SPLIT_PIPE;
-        if (chain_ok(h)) return UHSDR_SCHEDULE_CHAIN;
         return h->bv->fused ? UHSDR_SCHEDULE_SPLIT_FUSED : UHSDR_SCHEDULE_SPLIT_PIPE;
     }
     if (want == UHSDR_SCHEDULE_CHAIN) return chain_ok(h) ? want : -1;
@@ -2857,8 +2874,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     size_t fl = 0;
     auto take = [&](size_t n) { size_t o = fl; fl += (n + 63) & ~(size_t)63; return o; };
     const size_t hs1 = (h->T1 - 1 + 3) & ~3, hs2 = (h->T2 - 1 + 3) & ~3;   // padded history rows
-    const size_t o_h1i = take((size_t)C * hs1), o_h1q = take((size_t)C * hs1);
-    const size_t o_h2i = take((size_t)C * hs2), o_h2q = take((size_t)C * hs2);
+    const size_t o_h1 = take((size_t)2 * C * hs1);     // pair rows {I, Q}
+    const size_t o_h2 = take((size_t)2 * C * hs2);     // pair rows, or the scalar decimator row
     const size_t o_teta = take((size_t)3 * C), o_osc = take(4), o_tp = take((size_t)5 * C);
     const size_t o_pre = take((size_t)10 * C), o_aa = take((size_t)10 * C), o_bq1 = take((size_t)16 * C);
     const size_t o_bq2 = take((size_t)4 * C), o_ip = take((size_t)15 * C), o_ring = take(W > 0 ? (size_t)(W - 1) * C : 0);
@@ -2877,14 +2894,15 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess ||
         hipMalloc((void**)&h->adec, sizeof(float) * (size_t)C * h->Nd) != hipSuccess ||
         hipMalloc((void**)&h->d_plan, sizeof(uhsdr_rx_plan)) != hipSuccess ||
-        hipMalloc((void**)&h->d_taps2, sizeof(float) * 4 * TAPS2_MAX) != hipSuccess)
+        hipMalloc((void**)&h->d_taps2, sizeof(float) * 4 * TAPS2_MAX) != hipSuccess ||
+        hipMalloc((void**)&h->d_lanemap, sizeof(uint16_t) * 2 * 64) != hipSuccess)
     {
         uhsdr_set_error("hipMalloc failed (%zu bytes state)", h->arena_bytes);
         (void)uhsdr_rx_destroy(h);
         return UHSDR_DEVICE_ERROR;
     }
     float* A = (float*)h->arena;
-    h->hist1_i = A + o_h1i; h->hist1_q = A + o_h1q; h->hist2_i = A + o_h2i; h->hist2_q = A + o_h2q;
+    h->hist1 = A + o_h1; h->hist2 = A + o_h2;
     h->teta = A + o_teta; h->osc = A + o_osc; h->tp = (int*)(A + o_tp);
     h->bs.pre = A + o_pre; h->bs.aa = A + o_aa; h->bs.bq1 = A + o_bq1; h->bs.bq2 = A + o_bq2;
     h->bs.interp = A + o_ip; h->bs.ring = A + o_ring; h->bs.agc = A + o_agc; h->bs.agci = (int*)(A + o_agci);
@@ -2917,11 +2935,34 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         {
             pair_taps(t2, p.hilbert_i, p.hilbert_q, p.hilbert_taps);
             // stereo Hilbert-first: DECIMATE_RX_I / _Q (the same table) as a pair
-            if (h->fv->st) pair_taps(t2 + 2 * TAPS2_MAX, p.dec, p.dec, p.dec_taps);
+            // the audio decimator as duplicated pairs {dec, dec}: the stereo decimator pair
+            // (DECIMATE_RX_I / _Q, the same table) and the mono decimator's packed output pairs
+            pair_taps(t2 + 2 * TAPS2_MAX, p.dec, p.dec, p.dec_taps);
         }
         if (hipMemcpy(h->d_taps2, t2, sizeof t2, hipMemcpyHostToDevice) != hipSuccess)
         {
             uhsdr_set_error("tap upload failed");
+            (void)uhsdr_rx_destroy(h);
+            return UHSDR_DEVICE_ERROR;
+        }
+    }
+    {
+        // the front's lane -> (channel, block) maps for both block sizes (front_lane)
+        uint16_t lm[2][64] = {};
+        for (int k = 0; k < 2; ++k)
+        {
+            const int R = k ? 16 : 8, nf = front_frames(N, R), nb = nf / R;
+            if (N % R || nb < 1 || nb > 64) continue;
+            for (int l = 0; l < 64; ++l)
+            {
+                int g, b;
+                front_lane(l, nb, 2 * R, g, b);
+                lm[k][l] = (uint16_t)(g << 8 | b);
+            }
+        }
+        if (hipMemcpy(h->d_lanemap, lm, sizeof lm, hipMemcpyHostToDevice) != hipSuccess)
+        {
+            uhsdr_set_error("lane map upload failed");
             (void)uhsdr_rx_destroy(h);
             return UHSDR_DEVICE_ERROR;
         }
@@ -3023,7 +3064,10 @@ static FrontArgs front_args(const uhsdr_rx_s* h, const int32_t* iq, int f0, floa
     FrontArgs fa;
     fa.plan = h->d_plan;
     fa.iq = (const int2*)iq + f0;
-    fa.hist1_i = h->hist1_i; fa.hist1_q = h->hist1_q; fa.hist2_i = h->hist2_i; fa.hist2_q = h->hist2_q;
+    fa.hist1 = h->hist1; fa.hist2 = h->hist2;
+    fa.nb = h->Nf / h->fv->R;
+    fa.cpw = FRONT_WAVE / fa.nb;
+    fa.lanemap = h->d_lanemap + (h->fv->R == 16 ? 64 : 0);
     fa.teta = h->teta;
     fa.tp = h->tp;
     fa.clip = h->clip;
@@ -3388,6 +3432,7 @@ extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
     if (h->adec) (void)hipFree(h->adec);
     if (h->d_plan) (void)hipFree(h->d_plan);
     if (h->d_taps2) (void)hipFree(h->d_taps2);
+    if (h->d_lanemap) (void)hipFree(h->d_lanemap);
     free(h);
     return UHSDR_OK;
 }

@@ -558,16 +558,16 @@ static const uint8_t alc_params[13][2] = { { 1, 15 }, { 2, 12 }, { 4, 10 }, { 6,
 uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
 {
     if (!cfg || !p) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
-    const int fm = cfg->dmod_mode == UHSDR_DEMOD_FM;
-    if (cfg->dmod_mode != UHSDR_DEMOD_USB && cfg->dmod_mode != UHSDR_DEMOD_LSB && !fm)
+    const int fm = cfg->dmod_mode == UHSDR_DEMOD_FM, am = cfg->dmod_mode == UHSDR_DEMOD_AM;
+    if (cfg->dmod_mode != UHSDR_DEMOD_USB && cfg->dmod_mode != UHSDR_DEMOD_LSB && !fm && !am)
     {
-        uhsdr_set_error("transmit mode %d: SSB (USB/LSB) and FM voice are implemented", cfg->dmod_mode);
+        uhsdr_set_error("transmit mode %d: SSB (USB/LSB), AM and FM voice are implemented", cfg->dmod_mode);
         return UHSDR_UNSUPPORTED;
     }
-    if (fm && cfg->iq_freq_mode == UHSDR_IQ_CONV_OFF)
+    if ((fm || am) && cfg->iq_freq_mode == UHSDR_IQ_CONV_OFF)
     {
-        /* "No FM possible unless in frequency translate mode" (tx_processor.c:1009-1011) */
-        uhsdr_set_error("FM transmit needs the I/Q frequency translation");
+        /* "No AM / FM possible unless in frequency translate mode" (tx_processor.c:1000-1011) */
+        uhsdr_set_error("AM / FM transmit needs the I/Q frequency translation");
         return UHSDR_UNSUPPORTED;
     }
     if (cfg->fm_tone_burst_mode < 0 || cfg->fm_tone_burst_mode > 2)   /* FM_TONE_BURST_MAX, audio_driver.h:440 */
@@ -580,10 +580,10 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
         uhsdr_set_error("fm_subaudible_tone %d outside 0..%d", cfg->fm_subaudible_tone, uhsdr_fm_subaudible_count - 1);
         return UHSDR_ARGUMENT_ERROR;
     }
-    if (cfg->audio_source < UHSDR_TX_AUDIO_MIC || cfg->audio_source > UHSDR_TX_AUDIO_LINEIN_R)
+    if (cfg->audio_source < UHSDR_TX_AUDIO_MIC || cfg->audio_source > UHSDR_TX_AUDIO_DIGIQ)
     {
-        uhsdr_set_error("transmit audio source %d: codec sources (mic, line in) only", cfg->audio_source);
-        return UHSDR_UNSUPPORTED;
+        uhsdr_set_error("transmit audio source %d: mic, line in L / R, USB audio, USB I/Q", cfg->audio_source);
+        return UHSDR_ARGUMENT_ERROR;
     }
     memset(p, 0, sizeof *p);
     p->dmod_mode = cfg->dmod_mode;
@@ -598,9 +598,13 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
         gain_calc /= 2;                                      /* MIC_GAIN_RESCALE, audio_driver.h:399 */
         if (cfg->mic_boost > 0) gain_calc += 25.1;
     }
-    else
+    else if (cfg->audio_source == UHSDR_TX_AUDIO_LINEIN_L || cfg->audio_source == UHSDR_TX_AUDIO_LINEIN_R)
     {
         gain_calc = 20;                                      /* LINE_IN_GAIN_RESCALE, audio_driver.h:398 */
+    }
+    else
+    {
+        gain_calc = 1;                                       /* TX_AUDIO_DIG and the default (:374-381) */
     }
     gain_calc *= 0.0000152587890625;                         /* AUDIO_BIT_SCALE_DOWN, audio_driver.h:605 */
     p->in_gain = gain_calc;
@@ -608,8 +612,8 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
 
     /* TxProcessor_FilterAudio: lattice band-pass unless disabled (FM always filters,
        tx_processor.c:1012), biquads for codec sources; FM uses IIR_TX_2k7_FM (:104-107) */
-    p->run_lattice = fm || !cfg->filter_disable;
-    p->run_biquad = 1;
+    p->run_lattice = fm || !cfg->filter_disable;           /* FLAGS1_SSB / _AM_TX_FILTER_DISABLE (:991, :1003) */
+    p->run_biquad = cfg->audio_source != UHSDR_TX_AUDIO_DIG;   /* do_bass_treble (:445) */
     const int sel = fm ? 3 : cfg->tx_filter == 2 ? 1 : cfg->tx_filter == 3 ? 2 : 0;   /* TENOR, BASS, default SOPRANO */
     const uhsdr_lattice_desc* l = &uhsdr_tx_lattices[sel];
     p->lat_stages = l->stages;
@@ -630,8 +634,10 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
     else { postfilt = 4; decay_var = 10; }
     p->postfilt_gain = ((float)postfilt) / 2.0 + 0.5;
     p->alc_decay = exp10f(-((((float)decay_var) + 35.0) / 10.0));
-    p->alc_gain_scaling = fm ? 0.95 : 1.00;                  /* FM_ALC_GAIN_CORRECTION (tx_processor.c:521) /
+    p->alc_gain_scaling = fm ? 0.95 : am ? 0.23 : 1.00;      /* FM_ALC_GAIN_CORRECTION (tx_processor.c:521) /
+                                                                AM_ALC_GAIN_CORRECTION (audio_driver.h:428) /
                                                                 SSB_ALC_GAIN_CORRECTION (audio_driver.h:417) */
+    p->am = am;
 
     /* TX Hilbert pair, swapped for LSB (tx_processor.c:477-478) */
     const int T = uhsdr_tx_hilbert_taps;
@@ -660,10 +666,16 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
 
     /* TxProcessor_IqFinalProcessing (tx_processor.c:282-330) with iq_gain_comp = SSB_GAIN_COMP
        or FM_MOD_AMPLITUDE_SCALING (:500, :1014) */
-    float scaling = fm ? 0.875 : 1.133;                      /* SSB_GAIN_COMP, audio_driver.h:419 */
+    float scaling = fm ? 0.875 : 1.133;                      /* SSB_GAIN_COMP = AM_GAIN_COMP, audio_driver.h:419-421 */
     scaling *= (1 << 16);                                    /* IQ_BIT_SCALE_UP */
     p->final_i_gain = cfg->power_factor * cfg->gain_i * scaling;
     p->final_q_gain = cfg->power_factor * cfg->gain_q * scaling;
+    /* TX_AUDIO_DIGIQ (:950-961): the USB I/Q goes straight to the final stage with iq_gain_comp 1.0 */
+    p->digiq = cfg->audio_source == UHSDR_TX_AUDIO_DIGIQ;
+    float scaling1 = 1.0;
+    scaling1 *= (1 << 16);
+    p->digiq_i_gain = cfg->power_factor * cfg->gain_i * scaling1;
+    p->digiq_q_gain = cfg->power_factor * cfg->gain_q * scaling1;
     p->phase_balance = cfg->phase_balance;
 
     /* FM modulator (TxProcessor_FM, tx_processor.c:534-588) and its softdds tables */

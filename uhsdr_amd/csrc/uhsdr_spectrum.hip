@@ -28,10 +28,7 @@
 
 namespace {
 
-#ifndef UHSDR_SPEC_WAVES
-#define UHSDR_SPEC_WAVES 4
-#endif
-constexpr int SPEC_WAVES = UHSDR_SPEC_WAVES;   // waves (channels) per workgroup
+constexpr int SPEC_WAVES = 4;   // waves (channels) per workgroup
 
 struct SpecArgs
 {

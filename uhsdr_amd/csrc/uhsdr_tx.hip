@@ -318,11 +318,21 @@ __global__ void __launch_bounds__(64) tx_iq(TxIqArgs a)
     const bool up = P->shift_up;
     const float gi = P->final_i_gain, gq = P->final_q_gain, ph = P->phase_balance;
     int out[2 * R];
+    const bool am = P->am;
 #pragma unroll
     for (int r = 0; r < R; ++r)
     {
         const int n = b * R + r;
         float I = hi[r], Q = hq[r];
+        if (am)
+        {
+            // TxProcessor_AM (tx_processor.c:780-788): both sidebands and the carrier,
+            // 2 * AM_CARRIER_LEVEL (audio_driver.h:429) as the float the int constant converts to
+            const float i_am = (I - Q) + 10200.0f;
+            const float q_am = (Q - I) - 10200.0f;
+            I = i_am;
+            Q = q_am;
+        }
         if (shift)
         {
             float ib = up ? I : Q, qb = up ? Q : I;
@@ -360,6 +370,27 @@ __global__ void __launch_bounds__(64) tx_iq(TxIqArgs a)
 #pragma unroll
         for (int j = 0; j < R / 2; ++j) dst[j] = make_int4(out[4 * j], out[4 * j + 1], out[4 * j + 2], out[4 * j + 3]);
     }
+}
+
+// TX_AUDIO_DIGIQ (tx_processor.c:950-961): the USB I/Q frames, int32 -> f32, straight to
+// TxProcessor_IqFinalProcessing (:282-330) with iq_gain_comp 1.0; two frames per lane
+__global__ void __launch_bounds__(256) tx_digiq(const uhsdr_tx_plan* plan, const int4* src, int4* dst, long long pairs)
+{
+    const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (k >= pairs) return;
+    const uhsdr_tx_plan* __restrict__ P = plan;
+    const float gi = P->digiq_i_gain, gq = P->digiq_q_gain, ph = P->phase_balance;
+    const int4 v = src[k];
+    float I[2] = { (float)v.x, (float)v.z }, Q[2] = { (float)v.y, (float)v.w };
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+    {
+        I[j] = I[j] * gi;
+        Q[j] = Q[j] * gq;
+        if (ph < 0) { const float e = I[j] * ph; Q[j] = Q[j] + e; }
+        else if (ph > 0) { const float e = Q[j] * ph; I[j] = I[j] + e; }
+    }
+    dst[k] = make_int4(tx_to_int32(I[0]), tx_to_int32(Q[0]), tx_to_int32(I[1]), tx_to_int32(Q[1]));
 }
 
 // ------------------------------------------------------------------------------------
@@ -504,6 +535,15 @@ extern "C" uhsdr_status uhsdr_tx_create(const uhsdr_tx_config* cfg, int32_t C, i
 extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio, int32_t* iq, float* a0)
 {
     if (!h || !audio || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
+    if (h->plan.digiq && !h->tune)
+    {
+        // USB I/Q source: no voice chain, no modulator state advances, a0 (adb.a_buffer[0]) untouched
+        const long long pairs = (long long)h->C * h->N / 2;
+        hipLaunchKernelGGL(tx_digiq, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, h->stream, h->d_plan,
+                           (const int4*)audio, (int4*)iq, pairs);
+        HIPCHK(hipGetLastError());
+        return UHSDR_OK;
+    }
     TxVoiceArgs va;
     va.plan = h->d_plan; va.audio = (const int2*)audio; va.txa = h->txa; va.a0 = a0;
     va.lat = h->lat; va.bq = h->bq; va.alc = h->alc; va.delay = h->delay;

@@ -22,6 +22,14 @@ class FirBatch:
                    "uhsdr_fir_create")
         self.handle = h
 
+    @property
+    def waves(self) -> int:
+        """waves per workgroup of the FIR kernel (1, 2 or 4)"""
+        return int(self.lib.uhsdr_fir_get_waves(self.handle))
+
+    def set_waves(self, waves: int) -> None:
+        _abi.check(self.lib.uhsdr_fir_set_waves(self.handle, int(waves)), "uhsdr_fir_set_waves")
+
     def reset(self) -> None:
         _abi.check(self.lib.uhsdr_fir_reset(self.handle), "uhsdr_fir_reset")
 

@@ -86,3 +86,52 @@ class GatherPipeline:
         for i in range(self.issued - self.depth, self.issued):
             if i >= 0:
                 self._retire(i % self.depth)
+
+
+def timed_loop(step, sync, steps: int, warmup: int, dist=None, world: int = 1, reduce_device="cpu") -> float:
+    """The bench contract's timed region, shared by bench.py and the multi-rank tests: `warmup`
+    untimed steps, then exactly `steps` steps bracketed by a barrier + sync() on both sides; returns
+    the MAX over ranks of the elapsed seconds (all_reduce on a tensor on `reduce_device`: the GPU
+    for RCCL, the CPU for gloo).  step(s) enqueues step s; sync() waits for the device."""
+    import time
+
+    import torch
+    for s in range(warmup):
+        step(s)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        step(s)
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=reduce_device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_timed(pipe: "GatherPipeline", compute, sync, steps: int, warmup: int, dist, reduce_device="cpu") -> float:
+    """timed_loop for the gather leg: every step's output gathered to rank 0 through `pipe`
+    (overlapped with the next step), drained before each clock read; max-over-ranks seconds."""
+    import time
+
+    import torch
+    for _ in range(warmup):
+        pipe.step(compute)
+    pipe.drain()
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pipe.step(compute)
+    pipe.drain()
+    sync()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=reduce_device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -224,6 +224,10 @@ void         uhsdr_rx_config_default(uhsdr_rx_config* cfg);
 uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* plan);
 /* 1 if the device chain implements this plan, 0 otherwise */
 int          uhsdr_rx_plan_supported(const uhsdr_rx_plan* plan);
+/* 1 if uhsdr_rx_set_precision accepts UHSDR_PRECISION_FMA for this plan: the Hilbert-first
+ * families whose FMA output was measured within 1e-5 normwise of the reference
+ * (tools/fma_sweep.py, tests/test_gpu_fma.py), 0 otherwise */
+int          uhsdr_rx_plan_fma_ok(const uhsdr_rx_plan* plan);
 
 /* ---- batched device chain ---- */
 /* stream: hipStream_t to order all work of this handle on (NULL = default stream). */

@@ -116,10 +116,12 @@ def rx_bench_size(cfg, C, N, calls, gen, cw=False):
 
 @pytest.mark.parametrize("sql", [12, 0])
 def test_fm_rx_bench_size(cuda, sql):
-    """squelch 12 is the bench's setting (muted until its first decision, every 200 calls);
-    squelch 0 keeps it open, so the demodulated audio itself is compared"""
+    """squelch 12 is the bench's setting.  The receiver starts squelched and decides every 200
+    32-frame calls (audio_driver.c:475, :1600-1640), so the output is muted until then; with
+    squelch 0 the first decision opens it, and 28 launches (224 calls) compare the demodulated
+    audio itself after it."""
     cfg = U.default_config(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=sql)
-    ref = rx_bench_size(cfg, 32768, 256, 3, synth.fm_iq)
+    ref = rx_bench_size(cfg, 32768, 256, 3 if sql else 28, synth.fm_iq)
     assert sql or np.abs(ref).max() > 0
 
 

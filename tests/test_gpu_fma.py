@@ -41,13 +41,15 @@ def run(cfg, iq, N, precision):
 CASES = [
     ("p48_usb", dict(filter_path=48, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 256, 256, TOL),
     ("p48_lsb_n64", dict(filter_path=48, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 128, 64, TOL),
-    ("p60_usb_24k", dict(filter_path=60, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 96, 256, TOL),
+    ("p52_lsb", dict(filter_path=52, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 96, 256, TOL),
     ("p1_fm", dict(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=12), synth.fm_iq, 96, 256, TOL),
 ]
 
 # decimate-first families: FMA measured past 1e-5 (P35 1.7e-5, P70 AM 1.8e-5 / SAM 1.3e-5,
-# P4 CW 1.3e-5), so the library refuses it there
+# P4 CW 1.3e-5), and the 24 ksps wide paths at the bound (P55-P65: 0.76-1.22e-5), so the
+# library refuses it there
 REFUSED = [
+    ("p60_usb_24k", dict(filter_path=60, dmod_mode=U.DEMOD_USB)),
     ("p35_usb", dict(filter_path=35, dmod_mode=U.DEMOD_USB)),
     ("p70_am", dict(filter_path=70, dmod_mode=U.DEMOD_AM)),
     ("p70_sam", dict(filter_path=70, dmod_mode=U.DEMOD_SAM)),
@@ -79,9 +81,9 @@ def test_fma_within_tolerance(cuda, back, name, kw, gen, C, N, tol):
         assert not np.array_equal(got.view(np.uint32), ref.view(np.uint32)), f"{name}: FMA output is bit-exact"
 
 
-def accepted_fma_cases():
-    """Every (filter path, demodulator, stereo) the library takes FMA for: the Hilbert-first
-    families (plan.use_decimated_iq false) of every live FilterPathInfo entry."""
+def fma_candidates():
+    """Every (filter path, demodulator, stereo) with a Hilbert-first front (plan.use_decimated_iq
+    false): the family FMA can apply to, over every live FilterPathInfo entry."""
     import json
     import os
     paths = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "filter_paths.json")))
@@ -104,23 +106,20 @@ def accepted_fma_cases():
     return out
 
 
-ACCEPTED = accepted_fma_cases()
+def accepted_fma_cases(refused_too=False):
+    """The candidates the library takes FMA for (uhsdr_rx_plan_fma_ok), or all of them"""
+    return [kw for kw in fma_candidates() if refused_too or U.plan_fma_ok(U.build_plan(U.default_config(**kw)))]
 
 
-def test_fma_accepted_set():
-    """18 wide / 24 ksps paths x {USB, LSB, DIGI, SSB stereo, IQ} mono and stereo, and FM"""
-    assert len(ACCEPTED) == 129
-
-
-@pytest.mark.parametrize("kw", ACCEPTED, ids=[f"p{k['filter_path']}_m{k['dmod_mode']}_s{k['stereo_enable']}" for k in ACCEPTED])
-def test_fma_every_accepted_path(cuda, kw):
-    """Every path x demodulator that accepts FMA, both output channels in stereo, 8 calls of
-    128 frames (past the AGC ring), within 1e-5 normwise of the oracle."""
+def fma_case_error(kw):
+    """normwise error per output channel of one case: 64 channels, 128-frame launches (past the
+    AGC ring; FM: past the squelch's first decision at 200 calls, which opens it at squelch 0)"""
     import torch
     cfg = U.default_config(**kw)
     plan = U.build_plan(cfg)
-    C, N, calls = 64, 128, 8
     mode = kw["dmod_mode"]
+    C, N = 64, 128
+    calls = 56 if mode == U.DEMOD_FM else 8
     iq = synth.fm_iq(np.arange(C), 0, calls * N) if mode == U.DEMOD_FM else \
         synth.ssb_iq(np.arange(C), 0, calls * N, lsb=mode == U.DEMOD_LSB)
     chain = U.RxChain(cfg, channels=C, frames=N)
@@ -134,13 +133,48 @@ def test_fma_every_accepted_path(cuda, kw):
         g0.append(a0.cpu().numpy())
     chain.close()
     r1, r0, _ = oracle.OracleRx(plan, C).process2(iq, threads=8)
-    outs = [(np.concatenate(g1, axis=1), r1, "a_buffer[1]")]
+    outs = {"a1": (np.concatenate(g1, axis=1), r1)}
     if plan.stereo:
-        outs.append((np.concatenate(g0, axis=1), r0, "a_buffer[0]"))
-    for got, ref, what in outs:
-        assert np.isfinite(got).all()
-        err = normwise(got, ref)
-        assert err.max() <= TOL, f"{kw} {what}: normwise error {err.max():.3g} > {TOL}"
+        outs["a0"] = (np.concatenate(g0, axis=1), r0)
+    err = {}
+    for what, (got, ref) in outs.items():
+        assert np.isfinite(got).all(), f"{kw} {what}: non-finite output"
+        assert np.abs(ref).max() > 0, f"{kw} {what}: silent reference"
+        err[what] = float(normwise(got, ref).max())
+    return err
+
+
+ACCEPTED = accepted_fma_cases()
+REFUSED_SWEEP = [kw for kw in fma_candidates() if kw not in ACCEPTED]
+
+
+def test_fma_accepted_set():
+    """FM and the 12 ksps wide paths (P48-P54) accept FMA, the 24 ksps ones (P55-P65) do not"""
+    assert dict(filter_path=48, dmod_mode=U.DEMOD_USB, stereo_enable=0) in ACCEPTED
+    assert {k["filter_path"] for k in ACCEPTED} == {1, 2, 3} | set(range(48, 55))
+    assert {k["filter_path"] for k in REFUSED_SWEEP} == set(range(55, 66))
+    assert len(ACCEPTED) + len(REFUSED_SWEEP) == 129
+
+
+def _id(k):
+    return f"p{k['filter_path']}_m{k['dmod_mode']}_s{k['stereo_enable']}"
+
+
+@pytest.mark.parametrize("kw", ACCEPTED, ids=[_id(k) for k in ACCEPTED])
+def test_fma_every_accepted_path(cuda, kw):
+    """Every path x demodulator that accepts FMA, both output channels in stereo, within 1e-5
+    normwise of the oracle."""
+    err = fma_case_error(kw)
+    assert max(err.values()) <= TOL, f"{kw}: normwise error {err} > {TOL}"
+
+
+@pytest.mark.parametrize("kw", REFUSED_SWEEP, ids=[_id(k) for k in REFUSED_SWEEP])
+def test_fma_refused_paths(cuda, kw):
+    chain = U.RxChain(U.default_config(**kw), channels=64, frames=128)
+    with pytest.raises(Exception):
+        chain.set_precision(U.PRECISION_FMA)
+    assert chain.precision == U.PRECISION_EXACT
+    chain.close()
 
 
 def test_fma_toggle_back_to_exact(cuda):

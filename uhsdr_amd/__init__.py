@@ -3,7 +3,7 @@
 The product is ``uhsdr_amd/lib/libuhsdr_amd.so`` (C ABI: ``include/uhsdr.h``).  This
 package is the thin host-side mirror used by tests and the benchmark.
 """
-from ._abi import (RxConfig, RxPlan, build_plan, plan_supported, config_from_ref_args, default_config, load,  # noqa: F401
+from ._abi import (RxConfig, RxPlan, build_plan, plan_supported, plan_fma_ok, config_from_ref_args, default_config, load,  # noqa: F401
                    DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI,
                    DEMOD_SSBSTEREO, DEMOD_IQ, SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB,
                    SAM_SIDEBAND_STEREO, DSP_NOTCH_ENABLE,

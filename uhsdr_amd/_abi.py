@@ -162,6 +162,7 @@ SIGNATURES = {
     "uhsdr_rx_config_default": (None, [C.POINTER(RxConfig)]),
     "uhsdr_rx_plan_build": (C.c_int, [C.POINTER(RxConfig), C.POINTER(RxPlan)]),
     "uhsdr_rx_plan_supported": (C.c_int, [C.POINTER(RxPlan)]),
+    "uhsdr_rx_plan_fma_ok": (C.c_int, [C.POINTER(RxPlan)]),
     "uhsdr_rx_create": (C.c_int, [C.POINTER(RxConfig), C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]),
     "uhsdr_rx_reset": (C.c_int, [C.c_void_p]),
     "uhsdr_rx_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -238,6 +239,17 @@ SIGNATURES = {
 _lib = None
 
 
+def _one_hip_runtime() -> None:
+    """torch ships its own libamdhip64 (file libamdhip64.so, soname libamdhip64.so.7).  Loaded
+    after it, this library's NEEDED libamdhip64.so.7 binds to torch's copy; loaded first, it
+    maps /opt/rocm's and torch later maps a second runtime, whose device pointers this one does
+    not know ("no ROCm-capable device" on the first allocation).  So torch goes first."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load(path: str | None = None) -> C.CDLL:
     """Load libuhsdr_amd.so (built in-tree by `make`); raises if it is missing."""
     global _lib
@@ -247,8 +259,12 @@ def load(path: str | None = None) -> C.CDLL:
     p = path or os.environ.get("UHSDR_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise RuntimeError(f"{p} not built: run `make` (or __graft_entry__.build())")
+    _one_hip_runtime()
     lib = C.CDLL(p)
+    variant = p != LIB_PATH
     for name, (res, args) in SIGNATURES.items():
+        if variant and not hasattr(lib, name):
+            continue        # an A/B build of an earlier revision: entry points added since are absent
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -291,6 +307,11 @@ def build_plan(cfg: RxConfig) -> RxPlan:
 def plan_supported(plan: RxPlan) -> bool:
     """uhsdr_rx_plan_supported: the device has a kernel instantiation for this plan's family."""
     return bool(load().uhsdr_rx_plan_supported(C.byref(plan)))
+
+
+def plan_fma_ok(plan: RxPlan) -> bool:
+    """uhsdr_rx_plan_fma_ok: uhsdr_rx_set_precision takes UHSDR_PRECISION_FMA for this plan."""
+    return bool(load().uhsdr_rx_plan_fma_ok(C.byref(plan)))
 
 
 # uhsdr_ref key=value names (tests/golden) -> RxConfig fields

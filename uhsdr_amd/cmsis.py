@@ -80,6 +80,8 @@ def load(path: str | None = None) -> C.CDLL:
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise OSError(f"{p} not built: run `make` (the CMSIS shims have no CPU fallback)")
+    from ._abi import _one_hip_runtime
+    _one_hip_runtime()
     lib = C.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(lib, name)

@@ -2800,6 +2800,19 @@ extern "C" int uhsdr_rx_plan_supported(const uhsdr_rx_plan* p)
     return p && uhsdr_rx_mode_supported(p) && find_front(*p) && find_back(*p) && (!p->notch_enabled || find_notch(*p));
 }
 
+// FMA acceptance (north_star: within 1e-5 normwise), from the sweep of every Hilbert-first
+// (path, demodulator, stereo) against the oracle (tools/fma_sweep.py, profiles/r03_fma_sweep.jsonl):
+//   FM (paths 1-3)                          max 1.4e-6
+//   12 ksps wide paths (48-54, decimation 4) max 5.0e-6
+//   24 ksps wide paths (55-65, decimation 2) 7.6e-6 .. 1.22e-5: at the bound, refused
+// Decimate-first families (narrow SSB / CW, AM, SAM) exceed it (P35 1.7e-5, P70 AM 1.8e-5 /
+// SAM 1.3e-5, P4 CW 1.3e-5), refused.  Accepted cases sit at half the bound or less.
+extern "C" int uhsdr_rx_plan_fma_ok(const uhsdr_rx_plan* p)
+{
+    if (!p || p->use_decimated_iq) return 0;
+    return p->dmod_mode == UHSDR_DEMOD_FM || p->decimation_rate == 4;
+}
+
 extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
@@ -3246,12 +3259,10 @@ extern "C" uhsdr_status uhsdr_rx_set_precision(uhsdr_rx_handle h, int32_t precis
         uhsdr_set_error("unknown precision %d", (int)precision);
         return UHSDR_ARGUMENT_ERROR;
     }
-    if (precision == UHSDR_PRECISION_FMA && h->plan.use_decimated_iq)
+    if (precision == UHSDR_PRECISION_FMA && !uhsdr_rx_plan_fma_ok(&h->plan))
     {
-        // decimate-first families (narrow SSB / CW, AM, SAM): the fused FIR MACs move the output
-        // by more than north_star's 1e-5 normwise (tests/test_gpu_fma.py), so EXACT only
-        uhsdr_set_error("FMA precision exceeds 1e-5 on filter path %d (decimate-first family): EXACT only",
-                        (int)h->plan.filter_path);
+        uhsdr_set_error("FMA precision not within 1e-5 on filter path %d, demodulator %d%s: EXACT only",
+                        (int)h->plan.filter_path, (int)h->plan.dmod_mode, h->plan.stereo ? " (stereo)" : "");
         return UHSDR_UNSUPPORTED;
     }
     h->precision = precision;

@@ -67,7 +67,9 @@ __device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&
 {
     constexpr int WA = (M * (R - 1) + 8 + 7) & ~7;
     constexpr int NCH = T / 8, TR = T % 8;           // full 8-tap chunks, then TR taps
-    constexpr int ROT = WA / 8 + 1;
+    // unrolled by the window's rotation period (register renaming), or fully for short filters
+    // (the decimators: a rolled loop of few MACs per chunk waited on each chunk's LDS and tap loads)
+    constexpr int ROT = NCH <= 8 ? (NCH > 0 ? NCH : 1) : WA / 8 + 1;
     float w[WA];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.0f;
@@ -159,55 +161,6 @@ __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&
         const v2f ck = c[8 * NCH + kk];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = fir_mac<F>(acc[r], w[r * M + kk], ck);
-    }
-}
-
-// RD outputs of a decimate-by-M FIR per lane (arm_fir_decimate_f32, CMSIS .../arm_fir_decimate_f32.c:
-// 141), outputs taken in pairs (r, r+1) on packed f32: acc[j] = { sum_k c[k] * win[2jM + k],
-// sum_k c[k] * win[(2j+1)M + k] } with the taps as duplicated pairs {c[k], c[k]}.  Per element this
-// is fir_block's binary32 sequence (tap order from +0.0f; F: fused); each tap's window pair comes
-// from LDS as one ds_read2_b32 (the two samples M apart), fetched a chunk of 8 taps ahead, so a pair
-// of outputs costs one packed multiply + one packed add per tap instead of two of each.
-template <int T, int RD, int M, bool F = false>
-__device__ __forceinline__ void fir_dec2(const float* win, ctaps2_t* cd, v2f (&acc)[RD / 2])
-{
-    static_assert(RD % 2 == 0, "outputs in pairs");
-    constexpr int NP = RD / 2, NCH = T / 8, TR = T % 8;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) acc[j] = v2f{ 0.0f, 0.0f };
-    v2f w[NP][8];
-#pragma unroll
-    for (int j = 0; j < NP; ++j)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) w[j][q] = v2f{ win[2 * j * M + q], win[(2 * j + 1) * M + q] };
-#pragma unroll 2
-    for (int ch = 0; ch < NCH; ++ch)
-    {
-        v2f cc[8], nw[NP][8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) cc[q] = cd[8 * ch + q];
-        // the next chunk (or the tail) ahead; past the tail the loads run at most FRONT_TAIL samples
-        // beyond the data and are never used
-#pragma unroll
-        for (int j = 0; j < NP; ++j)
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-                nw[j][q] = v2f{ win[8 * (ch + 1) + 2 * j * M + q], win[8 * (ch + 1) + (2 * j + 1) * M + q] };
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-#pragma unroll
-            for (int j = 0; j < NP; ++j) acc[j] = fir_mac<F>(acc[j], w[j][q], cc[q]);
-#pragma unroll
-        for (int j = 0; j < NP; ++j)
-#pragma unroll
-            for (int q = 0; q < 8; ++q) w[j][q] = nw[j][q];
-    }
-#pragma unroll
-    for (int q = 0; q < TR; ++q)
-    {
-        const v2f ck = cd[8 * NCH + q];
-#pragma unroll
-        for (int j = 0; j < NP; ++j) acc[j] = fir_mac<F>(acc[j], w[j][q], ck);
     }
 }
 
@@ -522,10 +475,12 @@ __device__ __forceinline__ void group_store_prow(const float* smem, int LW, floa
         h[q] = *(const vf4*)(smem + (q / hp4) * LW + 2 * nnew + 4 * (q % hp4));
 }
 
-// new samples and the zero tail of one channel's window (the lane's own NV values)
-__device__ __forceinline__ void window_new2(float* W, int T, bool act, int b, int nb, const v2f* vals, int NV)
+// new samples of one channel's window (the lane's own NV values).  No zero tail: the windows of
+// a wave sit lw floats apart and the register-window FIRs' over-read (at most FRONT_TAIL samples
+// past the data, never used in a product) lands in the next channel's window, or, for the last
+// one, in the slack the LDS allocation adds after the windows.
+__device__ __forceinline__ void window_new2(float* W, int T, bool act, int b, const v2f* vals, int NV)
 {
-    const int nnew = nb * NV;
     if (act)
     {
         float* d = W + 2 * (T - 1 + b * NV);
@@ -534,21 +489,20 @@ __device__ __forceinline__ void window_new2(float* W, int T, bool act, int b, in
                 *(vf4*)(d + 2 * j) = vf4{ vals[j].x, vals[j].y, vals[j + 1].x, vals[j + 1].y };
         else
             for (int j = 0; j < NV; ++j) *(v2f*)(d + 2 * j) = vals[j];
-        for (int t = b; t < FRONT_TAIL; t += nb) *(v2f*)(W + 2 * (T - 1 + nnew + t)) = v2f{ 0.0f, 0.0f };
     }
 }
 
-__device__ __forceinline__ void window_new(float* W, int T, bool act, int b, int nb, const float* vals, int NV)
+__device__ __forceinline__ void window_new(float* W, int T, bool act, int b, const float* vals, int NV)
 {
-    const int nnew = nb * NV;
     if (act)
     {
         float* d = W + T - 1 + b * NV;
         if (((T - 1 + b * NV) & 3) == 0 && (NV & 3) == 0)
             for (int j = 0; j < NV; j += 4) *(vf4*)(d + j) = vf4{ vals[j], vals[j + 1], vals[j + 2], vals[j + 3] };
+        else if (((T - 1 + b * NV) & 1) == 0 && (NV & 1) == 0)
+            for (int j = 0; j < NV; j += 2) *(v2f*)(d + j) = v2f{ vals[j], vals[j + 1] };
         else
             for (int j = 0; j < NV; ++j) d[j] = vals[j];
-        for (int t = b; t < FRONT_TAIL; t += nb) W[T - 1 + nnew + t] = 0.0f;
     }
 }
 
@@ -669,37 +623,125 @@ __device__ __forceinline__ float biquad_step(float x, float& x1, float& x2, floa
     return acc;
 }
 
-// ---- host: LDS bank-conflict model of the window reads ----
-// ds_read_b128 lane groups (one LDS cycle each, MI355X_MICROARCH.md §LDS); ds_read_b64: halves
+// ---- host: LDS bank-conflict model of the front's window accesses (MI355X_MICROARCH.md §LDS) ----
+// ds_read_b128: four 16-lane groups, bank (a/4) mod 64; ds_write_b128: eight groups of 8
+// contiguous lanes, bank (a/4) mod 32; ds_write_b64: four groups of 16; ds_read/write_b32: two
+// groups of 32, bank (a/4) mod 32.  One LDS cycle per group, plus one per extra distinct dword
+// on a busy bank (identical addresses broadcast).
+enum LdsOp { LDS_R128, LDS_W128, LDS_W64, LDS_W32 };
 static const int kB128Groups[4][16] = {
     { 0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27 },
     { 4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31 },
     { 32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59 },
     { 36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63 } };
 
-// extra LDS cycles of one FIR window read for lane bases g*lw + b*stride (dwords): vec 4
-// (ds_read_b128), 2 (ds_read_b64) or 1 (ds_read_b32 / each half of ds_read2_b32: 32 banks)
-static inline int window_conflicts(int lw, int nb, int cpw, int R, int stride, int vec)
+// LDS-array cycles of one wave instruction; addr[l] < 0: lane l inactive
+static inline int lds_op_cycles(LdsOp op, const int (&addr)[64])
 {
-    int cost = 0;
-    const int ngroups = vec == 4 ? 4 : 2, glen = vec == 4 ? 16 : 32, banks = vec == 1 ? 32 : 64;
+    const int ngroups = op == LDS_R128 ? 4 : op == LDS_W128 ? 8 : op == LDS_W64 ? 4 : 2;
+    const int glen = 64 / ngroups, banks = op == LDS_R128 ? 64 : 32;
+    const int nd = op == LDS_W64 ? 2 : op == LDS_W32 ? 1 : 4;
+    int cycles = 0;
     for (int gi = 0; gi < ngroups; ++gi)
     {
-        int load[64] = { 0 };
+        int load[64] = { 0 }, seen[64], nseen = 0;
         for (int k = 0; k < glen; ++k)
         {
-            const int l = vec == 4 ? kB128Groups[gi][k] : gi * 32 + k;
-            int g, b;
-            front_lane(l, nb, R, g, b);
-            if (g >= cpw) continue;
-            const int addr = g * lw + b * stride;
-            for (int d = 0; d < vec; ++d) load[(addr + d) & (banks - 1)] += 1;
+            const int l = op == LDS_R128 ? kB128Groups[gi][k] : gi * glen + k;
+            if (addr[l] < 0) continue;
+            for (int d = 0; d < nd; ++d)
+            {
+                const int ad = addr[l] + d;
+                bool dup = false;
+                for (int i = 0; i < nseen; ++i) dup = dup || seen[i] == ad;
+                if (dup) continue;
+                if (nseen < 64) seen[nseen++] = ad;
+                load[ad & (banks - 1)] += 1;
+            }
         }
         int mx = 0;
         for (int k = 0; k < 64; ++k) mx = load[k] > mx ? load[k] : mx;
-        cost += mx - 1;
+        cycles += mx;
     }
-    return cost;
+    return cycles;
+}
+
+// lane -> (channel g, block b) maps of a front wave, packed g << 8 | b
+// (a) front_lane (below): runs of consecutive blocks per channel, laid out for the b128 read groups
+// (b) interleaved: lane l -> channel l % 4 + 4 * (l / (4 nb)), block (l % (4 nb)) / 4 -- each group
+//     of 8 contiguous lanes (a ds_write_b128 group) holds 4 channels x 2 consecutive blocks and
+//     each b128 read group 4 channels x 4 blocks of distinct b mod 4 (nb <= 16, >= 4 channels)
+__host__ __device__ inline void front_lane(int l, int nb, int S, int& g, int& b);
+static inline bool front_lane_interleaved(int l, int nb, int& g, int& b)
+{
+    if (nb > 16 || (nb & (nb - 1)) || 64 % (4 * nb)) return false;
+    g = l % 4 + 4 * (l / (4 * nb));
+    b = (l % (4 * nb)) / 4;
+    return true;
+}
+
+// modeled LDS-array cycles of one front wave's window traffic at pitch lw.  Pass 1: a FIR pair
+// over {x0, x1} (T1 taps, R outputs per lane, new pairs at 2 (T1-1)), lane map lm.
+static inline int front_lds_pass1(int lw, const uint16_t* lm, int cpw, int T1, int R)
+{
+    int addr[64], cycles = 0;
+    // new samples (R pairs per lane: ds_write_b128 two pairs at a time when aligned)
+    for (int l = 0; l < 64; ++l)
+    {
+        const int g = lm[l] >> 8, b = lm[l] & 0xff;
+        addr[l] = g < cpw ? g * lw + 2 * (T1 - 1 + b * R) : -1;
+    }
+    cycles += lds_op_cycles(((T1 - 1) & 1) ? LDS_W64 : LDS_W128, addr) * (((T1 - 1) & 1) ? R : R / 2);
+    // reads (ds_read_b128, every one at the same bank phase): the register window's first WA
+    // pairs, then 8 pairs per 8-tap chunk
+    const int WA = (R - 1 + 8 + 7) & ~7;
+    for (int l = 0; l < 64; ++l)
+    {
+        const int g = lm[l] >> 8, b = lm[l] & 0xff;
+        addr[l] = g < cpw ? g * lw + 2 * b * R : -1;
+    }
+    return cycles + lds_op_cycles(LDS_R128, addr) * (WA / 2 + (T1 / 8) * 4);
+}
+
+// Pass 2: its new samples (NV per pass-1 lane; pairs when pair2) are written by the lanes of the
+// pass-1 map lm1, its FIR (RD outputs per lane, decimation M2: a pair over a window of stride
+// 2 NV, or the mono decimator, stride NV) reads by the lanes of map lm2.
+static inline int front_lds_pass2(int lw, const uint16_t* lm1, const uint16_t* lm2, int cpw, int T2, bool pair2, int NV,
+                                  int RD, int M2)
+{
+    int addr[64], cycles = 0;
+    const int off = pair2 ? 2 * (T2 - 1) : T2 - 1, per = pair2 ? 2 * NV : NV;
+    for (int l = 0; l < 64; ++l)
+    {
+        const int g = lm1[l] >> 8, b = lm1[l] & 0xff;
+        addr[l] = g < cpw ? g * lw + off + b * per : -1;
+    }
+    LdsOp wop = LDS_W32;
+    int nw = per;
+    if ((off & 3) == 0 && (per & 3) == 0) { wop = LDS_W128; nw = per / 4; }
+    else if ((off & 1) == 0 && (per & 1) == 0) { wop = LDS_W64; nw = per / 2; }
+    cycles += lds_op_cycles(wop, addr) * nw;
+    const int WA = (M2 * (RD - 1) + 8 + 7) & ~7;
+    const int nread = pair2 ? WA / 2 + (T2 / 8) * 4 : WA / 4 + (T2 / 8) * 2;
+    for (int l = 0; l < 64; ++l)
+    {
+        const int g = lm2[l] >> 8, b = lm2[l] & 0xff;
+        addr[l] = g < cpw ? g * lw + b * per : -1;
+    }
+    return cycles + lds_op_cycles(LDS_R128, addr) * nread;
+}
+
+// extra LDS cycles of one FIR window read (ds_read_b128) for lane bases g*lw + b*stride (floats)
+// under lane map lm (TX pitch choice)
+static inline int window_conflicts(int lw, const uint16_t* lm, int cpw, int stride)
+{
+    int addr[64];
+    for (int l = 0; l < 64; ++l)
+    {
+        const int g = lm[l] >> 8, b = lm[l] & 0xff;
+        addr[l] = g < cpw ? g * lw + b * stride : -1;
+    }
+    return lds_op_cycles(LDS_R128, addr) - 4;
 }
 
 #endif /* UHSDR_DSP_H */

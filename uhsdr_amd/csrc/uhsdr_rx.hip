@@ -44,7 +44,8 @@ struct FrontArgs
                              // HS = T-1 rounded to 4
     float* hist2;            // stage 2: [C][HS2] audio decimator history, or [C][HS2][2] pair history
                              // (decimate-first: the Hilbert pair; stereo: the decimator pair)
-    const uint16_t* lanemap; // [64] front_lane of every lane: channel g << 8 | block b
+    const uint16_t* lanemap; // [64] pass-1 lane map of every lane: channel g << 8 | block b
+    const uint16_t* lanemap2; // [64] the pass-2 FIR's lane map (front_window_pitch)
     int nb, cpw;             // lanes per channel, channels per wave
     float* teta;             // [3][C] auto I/Q correction low-pass state
     int* tp;                 // [5][C] twin-peaks detector: state, counter, restarts, runs, phase (f32 bits)
@@ -403,10 +404,19 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
         }
         group_fill_prow<T1>(smem, LW, a.hist1, c0, CPW, nlive, lane, hA);
         wave_sync();
-        window_new2(W, T1, act, b, nb, x2, R);
+        window_new2(W, T1, act, b, x2, R);
         wave_sync();
         group_store_prow<T1>(smem, LW, a.hist1, c0, nlive, lane, nb * R);
 
+        // the pass-2 FIR's own lane -> (channel, block) map: its window is filled through LDS by
+        // the pass-1 lanes, so any map reads it; the host picks the one with the fewest bank
+        // conflicts for the pass-2 window stride (the sink takes this identity)
+        const unsigned lm2 = T2 ? a.lanemap2[lane] : lm;
+        const int g2 = (int)(lm2 >> 8), b2 = (int)(lm2 & 0xffu);
+        const bool act2 = g2 < CPW;
+        const int c2 = grp * CPW + g2;
+        const bool live2 = act2 && c2 < C;
+        float* const W2 = smem + (act2 ? g2 : 0) * LW;
         float o[RD];
         if constexpr (T2 == 0)
         {
@@ -474,15 +484,15 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
             wave_sync();
             group_fill_prow<T2>(smem, LW, a.hist2, c0, CPW, nlive, lane, hC);
             wave_sync();
-            window_new2(W, T2, act, b, nb, h2, R);
+            window_new2(W, T2, act, b, h2, R);
             wave_sync();
             group_store_prow<T2>(smem, LW, a.hist2, c0, nlive, lane, nb * R);
-            fir_block2<T2, RD, M, F>(W + 2 * b * R, as_taps2(a.taps2b), d2);
+            fir_block2<T2, RD, M, F>(W2 + 2 * b2 * R, as_taps2(a.taps2b), d2);
 #pragma unroll
             for (int r = 0; r < RD; ++r) o[r] = d2[r].x;
-            if (live)
+            if (live2)
             {
-                float* dst = a.adec_q + (size_t)c * a.ldd + b * RD;
+                float* dst = a.adec_q + (size_t)c2 * a.ldd + b2 * RD;
 #pragma unroll
                 for (int r = 0; r < RD; ++r) dst[r] = d2[r].y;
             }
@@ -498,14 +508,10 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
             wave_sync();
             group_fill_rows<T2>(smem, LW, a.hist2, c0, CPW, nlive, lane, hC);
             wave_sync();
-            window_new(W, T2, act, b, nb, hs, R);
+            window_new(W, T2, act, b, hs, R);
             wave_sync();
             group_store_rows<T2>(smem, LW, a.hist2, c0, nlive, lane, nb * R);
-            // the audio decimator, its outputs in packed pairs (taps2b = {dec, dec})
-            v2f d2[RD / 2];
-            fir_dec2<T2, RD, M, F>(W + b * R, as_taps2(a.taps2b), d2);
-#pragma unroll
-            for (int j = 0; j < RD / 2; ++j) { o[2 * j] = d2[j].x; o[2 * j + 1] = d2[j].y; }
+            fir_block<T2, RD, M, 4, F>(W2 + b2 * R, as_taps(P->dec), o);
         }
         else
         {
@@ -516,10 +522,10 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
             wave_sync();
             group_fill_prow<T2>(smem, LW, a.hist2, c0, CPW, nlive, lane, hC);
             wave_sync();
-            window_new2(W, T2, act, b, nb, d2, RD);
+            window_new2(W, T2, act, b, d2, RD);
             wave_sync();
             group_store_prow<T2>(smem, LW, a.hist2, c0, nlive, lane, nb * RD);
-            fir_block2<T2, RD, 1, F>(W + 2 * b * RD, as_taps2(a.taps2b), h2);
+            fir_block2<T2, RD, 1, F>(W2 + 2 * b2 * RD, as_taps2(a.taps2b), h2);
             if constexpr (ST)
             {
 #pragma unroll
@@ -529,9 +535,9 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
                     o[r] = st2.x;
                     h2[r].y = st2.y;
                 }
-                if (live)
+                if (live2)
                 {
-                    float* dst = a.adec_q + (size_t)c * a.ldd + b * RD;
+                    float* dst = a.adec_q + (size_t)c2 * a.ldd + b2 * RD;
 #pragma unroll
                     for (int r = 0; r < RD; ++r) dst[r] = h2[r].y;
                 }
@@ -541,7 +547,7 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
                 front_comb_block<RD>(comb, h2, o);
             }
         }
-        sink(live, c, g, b, o);
+        sink(live2, c2, g2, b2, o);
     }
 }
 
@@ -2571,7 +2577,8 @@ struct uhsdr_rx_s
     hipStream_t stream;
     // front state
     float *hist1, *hist2, *teta, *osc, *adec, *adec_q;
-    uint16_t* d_lanemap;     // [2][64] front_lane maps for R = 8 and R = 16 (g << 8 | b)
+    uint16_t* d_lanemap;     // [2][2][64] the front's lane maps for R = 8 / 16, pass 1 / 2 (g << 8 | b)
+    uint16_t lmap[2][2][64]; // host copies (front_window_pitch's choice)
     int* tp;                 // [5][C] twin-peaks detector state
     unsigned* clip;          // user output (uhsdr_rx_set_clip_output)
     float* d_taps2;          // FIR pair tables: [2][2 * TAPS2_MAX] (pass 1, pass 2)
@@ -2667,36 +2674,67 @@ static int kernel_waves_per_cu(const void* fn)
     const int w = 512 / alloc;
     return 4 * (w > 8 ? 8 : w);
 }
-static int front_window_pitch(const uhsdr_rx_s* h)
+// floats after the last window that the FIRs' over-read may touch (FRONT_TAIL pairs)
+constexpr int FRONT_SLACK = 2 * FRONT_TAIL;
+
+// the front's window pitch and lane maps: the most waves per CU (LDS per wave sets them: the
+// front is occupancy-sensitive), then the fewest modeled LDS-array cycles of the window traffic
+// (front_lds_pass1 / _pass2) over the pitches from the data's length up and, per pass, the lane
+// maps front_lane (runs of consecutive blocks, for the pass's window stride) and interleaved.
+// (At 1M x 64 P48 the occupancy-only choice lw = 320 = 0 mod 64 put every channel's window on
+// the same banks: 74 % of the LDS cycles were conflicts, PMC r03.)
+static int front_window_pitch(const uhsdr_rx_s* h, uint16_t (&lm1_out)[64], uint16_t (&lm2_out)[64])
 {
     const int N = h->Nf, R = h->fv->R, M = h->plan.decimation_rate;
     const bool df = h->plan.use_decimated_iq;
     const bool pair2 = df || h->fv->st;                  // pass 2 is a FIR pair over {x0, x1}
     const int nb = N / R, cpw = FRONT_WAVE / nb;
     const int n2 = df ? N / M : N;
-    int need = 2 * (h->T1 - 1 + N + FRONT_TAIL);
-    const int need2 = h->T2 ? (pair2 ? 2 : 1) * (h->T2 - 1 + n2 + FRONT_TAIL) : 0;
+    int need = 2 * (h->T1 - 1 + N);
+    const int need2 = h->T2 ? (pair2 ? 2 : 1) * (h->T2 - 1 + n2) : 0;
     need = ((need > need2 ? need : need2) + 3) & ~3;
-    const int rd = R / M;
-    // the front is occupancy-sensitive (LDS per wave sets its waves per CU): the fewest window-read
-    // conflicts among the pitches that keep the most waves per CU
-    const size_t extra = front_lds_extra(h);
+    const int RD = R / M;
+    const int NV2 = df ? RD : R, RD2 = df ? RD : RD, M2 = df ? 1 : M;   // pass 2 (front_body)
+    const int S2 = (pair2 ? 2 : 1) * NV2;                 // pass-2 window floats per lane
+    const size_t extra = front_lds_extra(h) + FRONT_SLACK;
     const int vgpr_waves = kernel_waves_per_cu((const void*)h->fv->fn);
-    int best = need, best_cost = 1 << 30, best_waves = 0;
+    // candidate maps: front_lane for the pass-1 stride, for the pass-2 stride, interleaved
+    uint16_t maps[3][64];
+    int nmaps = 0;
+    for (int m = 0; m < 3; ++m)
+    {
+        bool ok = true;
+        for (int l = 0; l < 64 && ok; ++l)
+        {
+            int g = 0, b = 0;
+            if (m == 0) front_lane(l, nb, 2 * R, g, b);
+            else if (m == 1) { ok = S2 <= 64; if (ok) front_lane(l, nb, S2, g, b); }
+            else ok = front_lane_interleaved(l, nb, g, b);
+            maps[nmaps][l] = (uint16_t)(g << 8 | b);
+        }
+        if (ok) ++nmaps;
+    }
+    int best = need, best_cost = 1 << 30, best_waves = 0, best1 = 0, best2 = 0;
     for (int lw = need; lw < need + 64; lw += 4)
     {
-        int cost = window_conflicts(lw, nb, cpw, 2 * R, 2 * R, 4);
-        // pass 2: pair windows read by ds_read_b128; the mono decimator's packed output pairs
-        // read sample pairs M apart (ds_read2_b32)
-        if (h->T2) cost += pair2 ? window_conflicts(lw, nb, cpw, 2 * R, df ? 2 * rd : 2 * R, 4)
-                                 : window_conflicts(lw, nb, cpw, 2 * R, R, 1);
         int waves = (int)(LDS_PER_CU / (sizeof(float) * ((size_t)cpw * lw + extra)));
         waves = waves > vgpr_waves ? vgpr_waves : waves;
 #ifdef UHSDR_PITCH_CONFLICTS_ONLY
         waves = 0;
 #endif
-        if (waves > best_waves || (waves == best_waves && cost < best_cost)) { best_cost = cost; best = lw; best_waves = waves; }
+        for (int m1 = 0; m1 < nmaps; ++m1)
+            for (int m2 = 0; m2 < (h->T2 ? nmaps : 1); ++m2)
+            {
+                int cost = front_lds_pass1(lw, maps[m1], cpw, h->T1, R);
+                if (h->T2) cost += front_lds_pass2(lw, maps[m1], maps[m2], cpw, h->T2, pair2, NV2, RD2, M2);
+                if (waves > best_waves || (waves == best_waves && cost < best_cost))
+                {
+                    best_cost = cost; best = lw; best_waves = waves; best1 = m1; best2 = h->T2 ? m2 : m1;
+                }
+            }
     }
+    memcpy(lm1_out, maps[best1], sizeof lm1_out);
+    memcpy(lm2_out, maps[best2], sizeof lm2_out);
     return best;
 }
 
@@ -2728,7 +2766,7 @@ static size_t front_lds(const uhsdr_rx_s* h)
 {
     const int N = h->Nf;
     const int cpw = FRONT_WAVE / (N / h->fv->R);
-    size_t f = (size_t)cpw * h->lw + front_lds_extra(h);
+    size_t f = (size_t)cpw * h->lw + front_lds_extra(h) + FRONT_SLACK;
 #ifdef UHSDR_FRONT_LDS_MIN
     // experiment builds: a floor on the front's LDS per wave (caps its waves per CU)
     if (f * sizeof(float) < (size_t)UHSDR_FRONT_LDS_MIN) return UHSDR_FRONT_LDS_MIN;
@@ -2757,11 +2795,24 @@ static uhsdr_status configure_front(uhsdr_rx_s* h, int R, bool strict)
     h->fv = fv;
     h->T1 = fv->t1; h->T2 = fv->t2;
     h->Nf = front_frames(h->N, fv->R);
-    h->lw = front_window_pitch(h);
+    uint16_t lm[2][64];
+    h->lw = front_window_pitch(h, lm[0], lm[1]);
     uhsdr_status st = UHSDR_OK;
     if (h->N % h->Nf) { uhsdr_set_error("frames_per_call %d not a multiple of %d", h->N, h->Nf); st = UHSDR_LENGTH_ERROR; }
     else if (front_lds(h) > 64 * 1024) { uhsdr_set_error("frames_per_call too long for LDS"); st = UHSDR_LENGTH_ERROR; }
     if (st != UHSDR_OK && old) { h->fv = old; h->T1 = old->t1; h->T2 = old->t2; h->Nf = oNf; h->lw = olw; }
+    if (st == UHSDR_OK)
+    {
+        // the map for this block size (a deterministic function of the handle's shape: a launch
+        // still in flight with this slot reads the same values)
+        const int k = fv->R == 16 ? 1 : 0;
+        memcpy(h->lmap[k], lm, sizeof lm);
+        if (h->d_lanemap && hipMemcpy(h->d_lanemap + 128 * k, lm, sizeof lm, hipMemcpyHostToDevice) != hipSuccess)
+        {
+            uhsdr_set_error("lane map upload failed");
+            st = UHSDR_DEVICE_ERROR;
+        }
+    }
     return st;
 }
 
@@ -2908,7 +2959,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         hipMalloc((void**)&h->adec, sizeof(float) * (size_t)C * h->Nd) != hipSuccess ||
         hipMalloc((void**)&h->d_plan, sizeof(uhsdr_rx_plan)) != hipSuccess ||
         hipMalloc((void**)&h->d_taps2, sizeof(float) * 4 * TAPS2_MAX) != hipSuccess ||
-        hipMalloc((void**)&h->d_lanemap, sizeof(uint16_t) * 2 * 64) != hipSuccess)
+        hipMalloc((void**)&h->d_lanemap, sizeof(uint16_t) * 4 * 64) != hipSuccess)
     {
         uhsdr_set_error("hipMalloc failed (%zu bytes state)", h->arena_bytes);
         (void)uhsdr_rx_destroy(h);
@@ -2960,19 +3011,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         }
     }
     {
-        // the front's lane -> (channel, block) maps for both block sizes (front_lane)
-        uint16_t lm[2][64] = {};
-        for (int k = 0; k < 2; ++k)
-        {
-            const int R = k ? 16 : 8, nf = front_frames(N, R), nb = nf / R;
-            if (N % R || nb < 1 || nb > 64) continue;
-            for (int l = 0; l < 64; ++l)
-            {
-                int g, b;
-                front_lane(l, nb, 2 * R, g, b);
-                lm[k][l] = (uint16_t)(g << 8 | b);
-            }
-        }
+        // the front's lane -> (channel, block) maps (configure_front)
+        const uint16_t (&lm)[2][2][64] = h->lmap;
         if (hipMemcpy(h->d_lanemap, lm, sizeof lm, hipMemcpyHostToDevice) != hipSuccess)
         {
             uhsdr_set_error("lane map upload failed");
@@ -3080,7 +3120,8 @@ static FrontArgs front_args(const uhsdr_rx_s* h, const int32_t* iq, int f0, floa
     fa.hist1 = h->hist1; fa.hist2 = h->hist2;
     fa.nb = h->Nf / h->fv->R;
     fa.cpw = FRONT_WAVE / fa.nb;
-    fa.lanemap = h->d_lanemap + (h->fv->R == 16 ? 64 : 0);
+    fa.lanemap = h->d_lanemap + (h->fv->R == 16 ? 128 : 0);
+    fa.lanemap2 = fa.lanemap + 64;
     fa.teta = h->teta;
     fa.tp = h->tp;
     fa.clip = h->clip;

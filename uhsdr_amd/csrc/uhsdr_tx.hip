@@ -418,10 +418,17 @@ static int tx_pitch(int Nf, int R)
 {
     const int nb = Nf / R, cpw = 64 / nb;
     const int need = (2 * (TX_T - 1 + Nf + FRONT_TAIL) + 3) & ~3;   // pair window {x, x}
+    uint16_t lm[64];
+    for (int l = 0; l < 64; ++l)
+    {
+        int g, b;
+        front_lane(l, nb, 2 * R, g, b);
+        lm[l] = (uint16_t)(g << 8 | b);
+    }
     int best = need, best_cost = 1 << 30;
     for (int lw = need; lw < need + 64; lw += 4)
     {
-        const int cost = window_conflicts(lw, nb, cpw, 2 * R, 2 * R, 4);
+        const int cost = window_conflicts(lw, lm, cpw, 2 * R);
         if (cost < best_cost) { best_cost = cost; best = lw; }
     }
     return best;

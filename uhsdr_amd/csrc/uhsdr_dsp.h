@@ -731,6 +731,26 @@ static inline int front_lds_pass2(int lw, const uint16_t* lm1, const uint16_t* l
     return cycles + lds_op_cycles(LDS_R128, addr) * nread;
 }
 
+// the history rows' LDS traffic of one pass (group_fill_prow / _rows, group_store_prow / _rows):
+// float4 q of the group's rows (hq float4s per channel) lands at (q / hq) lw + 4 (q % hq) + base
+// (the store reads the window at base = the new samples' offset); lane l moves float4s l, l + 64, ...
+static inline int front_lds_hist(int lw, int cpw, int hq, int nnew_floats)
+{
+    int addr[64], cycles = 0;
+    const int nq = cpw * hq;
+    for (int i = 0; i * 64 < nq; ++i)
+        for (int pass = 0; pass < 2; ++pass)
+        {
+            for (int l = 0; l < 64; ++l)
+            {
+                const int q = l + 64 * i;
+                addr[l] = q < nq ? (q / hq) * lw + 4 * (q % hq) + (pass ? nnew_floats : 0) : -1;
+            }
+            cycles += lds_op_cycles(pass ? LDS_R128 : LDS_W128, addr);
+        }
+    return cycles;
+}
+
 // extra LDS cycles of one FIR window read (ds_read_b128) for lane bases g*lw + b*stride (floats)
 // under lane map lm (TX pitch choice)
 static inline int window_conflicts(int lw, const uint16_t* lm, int cpw, int stride)

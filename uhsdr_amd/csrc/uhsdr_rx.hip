@@ -1796,7 +1796,7 @@ __device__ __forceinline__ void fused_store_call(const BackArgs& a, const BackLa
 // per-sample code carries no uniform branches; the AGC's DC removal is on for AM / SAM (compile-
 // time for the demodulating bodies, a select behind rx_notch)
 // LDS_IN (rx_chain): channel group grp, input from the wave's LDS hand-off adl
-template <int PRE, int AA, int L, int PH, int W, int DM, bool AGC_ON, bool CW, bool LDS_IN = false>
+template <int PRE, int AA, int L, int PH, int W, int DM, bool AGC_ON, bool CW, bool LDS_IN = false, bool DC = true>
 __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys, int grp, const float* adl = nullptr)
 {
     const BackLane l(a, grp);
@@ -1832,7 +1832,8 @@ __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys, in
 #endif
     ag.agc_on = AGC_ON;
     if (DM != DM_NONE) ag.dc = true;
-    else ag.dc_sel = true;
+    else if (DC) ag.dc_sel = true;
+    else { ag.dc = false; ag.dc_sel = false; }        // SSB / CW / DIGI: no DC removal to select
     au.cw = CW;
     for (int call = 0; call < l.calls; ++call)
     {
@@ -1872,22 +1873,25 @@ __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys, in
 }
 
 // runs the body with the launch's AGC / CW flags as template arguments
-template <int PRE, int AA, int L, int PH, int W, int DM, bool CW, bool LDS_IN = false>
+// DC: the AGC removes DC (AM / SAM; for the demodulator-free bodies only after an AM / SAM
+// demodulator that ran in rx_notch) -- a separate kernel instance for the SSB / CW / DIGI back end
+// without it (the select form cost its f64 arithmetic on every sample)
+template <int PRE, int AA, int L, int PH, int W, int DM, bool CW, bool LDS_IN = false, bool DC = true>
 __device__ __forceinline__ void back_fused_agc(const BackArgs& a, float* ys, int grp, const float* adl = nullptr)
 {
-    if (a.plan->agc.mode == 5) back_fused_body<PRE, AA, L, PH, W, DM, false, CW, LDS_IN>(a, ys, grp, adl);
-    else back_fused_body<PRE, AA, L, PH, W, DM, true, CW, LDS_IN>(a, ys, grp, adl);
+    if (a.plan->agc.mode == 5) back_fused_body<PRE, AA, L, PH, W, DM, false, CW, LDS_IN, DC>(a, ys, grp, adl);
+    else back_fused_body<PRE, AA, L, PH, W, DM, true, CW, LDS_IN, DC>(a, ys, grp, adl);
 }
 
-template <int PRE, int AA, int L, int PH, int W, int DM>
+template <int PRE, int AA, int L, int PH, int W, int DM, bool DC = true>
 __global__ void __launch_bounds__(BACK_CH) __attribute__((amdgpu_waves_per_eu(DM == DM_SAM_SB ? 1 : UHSDR_FUSED_WAVES))) rx_back_fused(BackArgs a)
 {
     __shared__ float ys[BACK_CH * FUSED_YPITCH];
     if constexpr (L == 4)
     {
-        if (a.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM, true>(a, ys, blockIdx.x); return; }
+        if (a.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM, true, false, DC>(a, ys, blockIdx.x); return; }
     }
-    back_fused_agc<PRE, AA, L, PH, W, DM, false>(a, ys, blockIdx.x);
+    back_fused_agc<PRE, AA, L, PH, W, DM, false, false, DC>(a, ys, blockIdx.x);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1923,9 +1927,9 @@ rx_chain(FrontArgs fa, BackArgs ba, int front_floats)
     }
     if constexpr (L == 4)
     {
-        if (ba.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM_NONE, true, true>(ba, smem, grp, adl); return; }
+        if (ba.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM_NONE, true, true, false>(ba, smem, grp, adl); return; }
     }
-    back_fused_agc<PRE, AA, L, PH, W, DM_NONE, false, true>(ba, smem, grp, adl);
+    back_fused_agc<PRE, AA, L, PH, W, DM_NONE, false, true, false>(ba, smem, grp, adl);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2386,7 +2390,15 @@ typedef void (*back_fn)(BackArgs);
 
 typedef void (*chain_fn)(FrontArgs, BackArgs, int);
 struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; front_fn fn_fma; int st; };
-struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; };
+// fused_nodc: rx_back_fused without the AGC's DC removal (the demodulator-free back end when the
+// AGC does not remove DC: SSB / CW / DIGI); the same kernel as `fused` for the demodulators
+struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; back_fn fused_nodc; };
+template <int PRE, int AA, int L, int PH, int W, int DM>
+constexpr back_fn fused_nodc_of()
+{
+    if constexpr (DM == DM_NONE) return rx_back_fused<PRE, AA, L, PH, W, DM, false>;
+    else return rx_back_fused<PRE, AA, L, PH, W, DM>;
+}
 // rx_chain instances: a front family (t1, t2, m, decim_first, R = 8) with a DM_NONE back end
 struct ChainVariant { int t1, t2, m, decim_first, R, pre, aa, L, ph, w; chain_fn fn, fn_fma; };
 #define CHAIN_V(t1, t2, m, df, pre, aa, ph, w) { t1, t2, m, df, 8, pre, aa, m, ph, w, \
@@ -2401,7 +2413,8 @@ struct NotchVariant { int L, dm; back_fn fn; };
 #ifdef UHSDR_ISA_P48
 // tools/isa_stats.sh: only the P48 SSB instances, so one kernel's ISA compiles in seconds
 static const FrontVariant kFront[] = { FRONT_V(89, 43, 4, false, 8) };
-#define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm> }
+#define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm>, \
+    fused_nodc_of<pre, aa, L, ph, w, dm>() }
 static const BackVariant kBack[] = { BACK_V(10, 6, 4, 1, 49, DM_NONE) };
 static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6>, nullptr };
 static const BackVariant kBackStereo[] = { { 10, 6, 4, 1, 49, DM_NONE, nullptr, nullptr } };
@@ -2426,7 +2439,8 @@ static const FrontVariant kFront[] = {
 #undef FRONT_V
 #undef FRONT_ST
 
-#define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm> }
+#define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm>, \
+    fused_nodc_of<pre, aa, L, ph, w, dm>() }
 static const BackVariant kBack[] = {
     // SSB / CW / DIGI
     BACK_V(10, 6, 4, 1, 49, DM_NONE), BACK_V(10, 0, 4, 4, 49, DM_NONE), BACK_V(0, 0, 2, 8, 97, DM_NONE),
@@ -2722,10 +2736,14 @@ static int front_window_pitch(const uhsdr_rx_s* h, uint16_t (&lm1_out)[64], uint
 #ifdef UHSDR_PITCH_CONFLICTS_ONLY
         waves = 0;
 #endif
+        // history rows: pair rows (hist_stride / 2 float4s per channel), or the mono decimator's
+        const int hist_cost = front_lds_hist(lw, cpw, hist_p4(h->T1), 2 * N) +
+                              (h->T2 ? (pair2 ? front_lds_hist(lw, cpw, hist_p4(h->T2), 2 * (df ? N / M : N))
+                                              : front_lds_hist(lw, cpw, hist_stride(h->T2) / 4, N)) : 0);
         for (int m1 = 0; m1 < nmaps; ++m1)
             for (int m2 = 0; m2 < (h->T2 ? nmaps : 1); ++m2)
             {
-                int cost = front_lds_pass1(lw, maps[m1], cpw, h->T1, R);
+                int cost = front_lds_pass1(lw, maps[m1], cpw, h->T1, R) + hist_cost;
                 if (h->T2) cost += front_lds_pass2(lw, maps[m1], maps[m2], cpw, h->T2, pair2, NV2, RD2, M2);
                 if (waves > best_waves || (waves == best_waves && cost < best_cost))
                 {
@@ -2819,7 +2837,8 @@ static uhsdr_status configure_front(uhsdr_rx_s* h, int R, bool strict)
 // can the handle run rx_chain: a chain instance, one front pass per call, LDS within a workgroup's
 static bool chain_ok(const uhsdr_rx_s* h)
 {
-    return h->cv && h->fv->R == h->cv->R && h->Nf == h->N && chain_lds(h) <= 64 * 1024;
+    // (the chain's back end has no DC removal: its paths are SSB / CW / DIGI, no notch)
+    return h->cv && h->fv->R == h->cv->R && h->Nf == h->N && chain_lds(h) <= 64 * 1024 && !h->plan.agc.remove_dc;
 }
 
 // AUTO: large batches run one kernel (rx_chain) where the path has one, else the fused back end;
@@ -3246,7 +3265,8 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             HIPCHK(hipGetLastError());
         }
         if (h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo)
-            hipLaunchKernelGGL(h->bv->fused, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
+            hipLaunchKernelGGL(h->plan.agc.remove_dc || !h->bv->fused_nodc ? h->bv->fused : h->bv->fused_nodc,
+                               dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
         else
             hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH),
                                back_lds(h), bst, ba);

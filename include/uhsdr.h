@@ -431,6 +431,14 @@ uhsdr_status uhsdr_tx_reset(uhsdr_tx_handle h);
 uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio, int32_t* iq, float* a0);
 uhsdr_status uhsdr_tx_get_plan(uhsdr_tx_handle h, uhsdr_tx_plan* plan);
 uhsdr_status uhsdr_tx_destroy(uhsdr_tx_handle h);
+/* pipelined mode (no reference counterpart; off by default): tx_iq -- the Hilbert pair, FreqShift
+ * and DAC frames -- runs on a private side stream and the compressed-audio hand-off rotates over
+ * two buffers, so tx_voice of call k+1 (one lane per channel, latency-bound) overlaps tx_iq of
+ * call k.  Outputs are bit-identical; iq of a call is complete once uhsdr_tx_join has ordered the
+ * handle's stream after the side stream (then synchronize that stream as usual). */
+uhsdr_status uhsdr_tx_set_pipelined(uhsdr_tx_handle h, int32_t enable);
+int32_t      uhsdr_tx_get_pipelined(uhsdr_tx_handle h);
+uhsdr_status uhsdr_tx_join(uhsdr_tx_handle h);
 /* TxProcessor_PrepareRun (tx_processor.c:63-66): clear the ALC look-ahead delay line only,
    the first time back to TX; all other TX state carries on */
 uhsdr_status uhsdr_tx_prepare_run(uhsdr_tx_handle h);

@@ -32,40 +32,49 @@ def tiled(fn, C, N, distinct=4096):
     return t.repeat((reps,) + (1,) * (t.dim() - 1))[:C].contiguous()
 
 
-def time_calls(fn, steps, warmup):
+def time_calls(fn, steps, warmup, join=None):
+    """ms per call on the current stream; join() (pipelined handles) orders it after the side
+    stream before the closing event"""
     import torch
     for _ in range(warmup):
         fn()
+    if join:
+        join()
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(steps):
         fn()
+    if join:
+        join()
     e1.record(s)
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / steps
 
 
-def rx_line(name, cfg, C, N, iq, steps, warmup, cw=False):
+def rx_line(name, cfg, C, N, iq, steps, warmup, cw=False, pipelined=False):
     import torch
     import bench
     import uhsdr_amd as U
     s = torch.cuda.current_stream()
     chain = U.RxChain(cfg, channels=C, frames=N, stream=s.cuda_stream)
+    if pipelined:
+        chain.set_pipelined(True)
     audio = torch.empty((C, N), dtype=torch.float32, device="cuda")
     if cw:
         sig = torch.empty((C, N // 32), dtype=torch.uint8, device="cuda")
         en = torch.empty((C, max(1, chain.cw_blocks_max)), dtype=torch.float32, device="cuda")
         chain.set_cw_outputs(sig, en)
-    ms = time_calls(lambda: chain.process(iq, audio, None), steps, warmup)
+    join = chain.join if pipelined else None
+    ms = time_calls(lambda: chain.process(iq, audio, None), steps, warmup, join)
     chain.enable_timing(True)
-    time_calls(lambda: chain.process(iq, audio, None), steps, 0)
+    time_calls(lambda: chain.process(iq, audio, None), steps, 0, join)
     kt = chain.kernel_times()
     chain.enable_timing(False)
     ab = bench.algorithmic_bytes(chain.plan, C, N, False)
     per = ab["chain"] / (C * N)
-    out = {"workload": name, "channels": C, "frames_per_call": N, "ms_per_call": round(ms, 4),
+    out = {"workload": name, "channels": C, "frames_per_call": N, "pipelined": bool(pipelined), "ms_per_call": round(ms, 4),
            "msamples_per_s": round(C * N / ms / 1e3, 1),
            "kernel_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kt.items()},
            "alg_bytes_per_frame": round(per, 2), "hbm_frac": round(C * N * per / ms / 1e6 / HBM_PEAK_GBS, 4),
@@ -80,6 +89,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--only", default="c3,c3spec,c3zoom,c4fm,c4tx,c5,c5fir")
     ap.add_argument("--fir-waves", type=int, default=0, help="c5fir: waves per workgroup (1, 2, 4; 0 = the default)")
+    ap.add_argument("--serial", action="store_true",
+                    help="C4 FM-RX / SSB-TX handles in their serial mode (default: pipelined, measured faster there; "
+                         "C3 SAM and C5 CW run serial, where the pipelined mode measured slower / the same)")
     a = ap.parse_args()
     import torch
     import uhsdr_amd as U
@@ -127,21 +139,23 @@ def main():
         C, N = 262144 // 8, 256
         cfg = U.default_config(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=12)
         lines.append(rx_line("C4 per-GPU share: FM-RX P1 (squelch 12)", cfg, C, N,
-                             tiled(synth.fm_iq, C, N), a.steps, a.warmup))
+                             tiled(synth.fm_iq, C, N), a.steps, a.warmup, pipelined=not a.serial))
     if "c4tx" in want:
         C, N = 262144 // 8, 256
         s = torch.cuda.current_stream()
         tx = U.TxChain(channels=C, frames=N, stream=s.cuda_stream)
+        if not a.serial:
+            tx.set_pipelined(True)
         audio = tiled(synth.tx_audio, C, N)
         iq = torch.empty((C, N, 2), dtype=torch.int32, device="cuda")
         a0 = torch.empty((C, N), dtype=torch.float32, device="cuda")
-        ms = time_calls(lambda: tx.process(audio, iq, a0), a.steps, a.warmup)
+        ms = time_calls(lambda: tx.process(audio, iq, a0), a.steps, a.warmup, None if a.serial else tx.join)
         # 8 B audio frame in, 8 B I/Q frame out, state (Hilbert 200, lattice 10, biquads 12, ALC,
         # 320-sample delay line) read + written once per call, the f32 hand-off between kernels
         state = 4 * (200 + 10 + 12 + 1 + 320)
         per = 16 + 2 * state / N
         lines.append({"workload": "C4 per-GPU share: SSB-TX (IIR_TX_SOPRANO + biquads + ALC + 201-tap Hilbert + Fs/4)",
-                      "channels": C, "frames_per_call": N, "ms_per_call": round(ms, 4),
+                      "channels": C, "frames_per_call": N, "pipelined": not a.serial, "ms_per_call": round(ms, 4),
                       "msamples_per_s": round(C * N / ms / 1e3, 1), "alg_bytes_per_frame": round(per, 2),
                       "hbm_frac": round(C * N * per / ms / 1e6 / HBM_PEAK_GBS, 4),
                       "finite": bool(torch.isfinite(a0).all().item()) and bool((iq != 0).any().item())})

@@ -95,7 +95,7 @@ class RxPlan(C.Structure):
 
 
 TX_HILBERT_TAPS = 201
-TX_AUDIO_MIC, TX_AUDIO_LINEIN_L, TX_AUDIO_LINEIN_R, TX_AUDIO_DIG = range(4)
+TX_AUDIO_MIC, TX_AUDIO_LINEIN_L, TX_AUDIO_LINEIN_R, TX_AUDIO_DIG, TX_AUDIO_DIGIQ = range(5)
 
 
 class TxConfig(C.Structure):
@@ -208,6 +208,9 @@ SIGNATURES = {
     "uhsdr_tx_prepare_run": (C.c_int, [C.c_void_p]),
     "uhsdr_tx_set_tune": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_tx_set_tone_burst": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_tx_set_pipelined": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_tx_get_pipelined": (C.c_int32, [C.c_void_p]),
+    "uhsdr_tx_join": (C.c_int, [C.c_void_p]),
     "uhsdr_fir_create": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                    C.POINTER(C.c_void_p)]),
     "uhsdr_fir_reset": (C.c_int, [C.c_void_p]),

@@ -70,6 +70,9 @@ __device__ __forceinline__ int tx_to_int32(float f)
 template <int S, bool FM>
 __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
 {
+    // raised issue priority: in the pipelined mode tx_iq of the previous call shares these SIMDs,
+    // and this one-lane-per-channel recursion is the call's critical path
+    __builtin_amdgcn_s_setprio(3);
     const uhsdr_tx_plan* __restrict__ P = a.plan;
     const int c = blockIdx.x * 64 + threadIdx.x;
     const bool live = c < a.C;
@@ -235,6 +238,166 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
     {
 #pragma unroll
         for (int i = 0; i < S; ++i) a.lat[i * C + c] = g[i];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) a.bq[i * C + c] = bq[i];
+        a.alc[c] = alc_val;
+    }
+}
+
+// tx_voice for SSB / AM as a two-wave pipeline over the launch's 32-frame calls (the RX back end's
+// scheme): wave 0 runs the input (codec frame / TUNE tone), the mic gain and the TX band-pass
+// lattice of call s while wave 1 runs the three biquads, the ALC with its look-ahead delay and
+// the stores of call s - 1; the call's 32 samples per channel cross in LDS (double-buffered,
+// 65-float pitch), one LDS-only barrier per call.  Per lane the same operations on the same
+// operands in the same order as tx_voice: bit-identical.  Two waves per 64 channels halve the
+// per-call critical path of this one-lane-per-channel recursion.
+constexpr int TXV_PITCH = 65;
+template <int S>
+__global__ void __launch_bounds__(128) tx_voice2(TxVoiceArgs a)
+{
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ float hand[2][BLK * TXV_PITCH];
+    const uhsdr_tx_plan* __restrict__ P = a.plan;
+    const int role = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 64 + lane;
+    const bool live = c < a.C;
+    const int cl = live ? c : a.C - 1;
+    const int C = a.C;
+    const int calls = a.N / BLK;
+    const bool tune = a.tune != 0;
+    if (role == 0)
+    {
+        float lk[S], lv[S + 1], g[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) lk[i] = P->lat_k[i];
+#pragma unroll
+        for (int i = 0; i <= S; ++i) lv[i] = P->lat_v[i];
+#pragma unroll
+        for (int i = 0; i < S; ++i) g[i] = a.lat[i * C + cl];
+        const bool right = P->audio_source == UHSDR_TX_AUDIO_LINEIN_R;
+        const bool apply_gain = P->apply_in_gain && !tune, run_lat = P->run_lattice && !tune;
+        const float in_gain = P->in_gain;
+        const int4* src = (const int4*)(a.audio + (size_t)cl * a.N);
+        int4 nxt[BLK / 2];
+#pragma unroll
+        for (int j = 0; j < BLK / 2; ++j) nxt[j] = src[j];
+        for (int k = 0; k < calls; ++k)
+        {
+            float x[BLK];
+#pragma unroll
+            for (int j = 0; j < BLK / 2; ++j)
+            {
+                const int4 v = nxt[j];
+                x[2 * j] = (float)(right ? v.y : v.x);
+                x[2 * j + 1] = (float)(right ? v.w : v.z);
+            }
+            if (k + 1 < calls)
+            {
+#pragma unroll
+                for (int j = 0; j < BLK / 2; ++j) nxt[j] = src[(k + 1) * (BLK / 2) + j];
+            }
+            if (tune)
+            {
+#pragma unroll
+                for (int m = 0; m < BLK; ++m) x[m] = tune_tone(a, P, k * BLK + m);
+            }
+            float* hb = hand[k & 1] + lane;
+#pragma unroll
+            for (int m = 0; m < BLK; ++m)
+            {
+                float v = x[m];
+                if (apply_gain) v = v * in_gain;
+                if (run_lat) v = (m & 1) ? lattice_step_pk<S, 1>(v, g, lk, lv) : lattice_step_pk<S, 0>(v, g, lk, lv);
+                hb[m * TXV_PITCH] = v;
+            }
+            lds_barrier();
+        }
+        if (live)
+        {
+#pragma unroll
+            for (int i = 0; i < S; ++i) a.lat[i * C + c] = g[i];
+        }
+        return;
+    }
+    float bc[15], bq[12];
+#pragma unroll
+    for (int i = 0; i < 15; ++i) bc[i] = P->biquad[i];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) bq[i] = a.bq[i * C + cl];
+    float alc_val = a.alc[cl];
+    const bool run_bq = P->run_biquad && !tune;
+    const bool comp = P->comp_on;
+    const float post = P->postfilt_gain, decay = P->alc_decay, gscale = P->alc_gain_scaling;
+    float dnext[BLK];
+    if (comp)
+    {
+        const float* dr = a.delay + ((size_t)((a.delay_phase + 2) % TX_DELAY_SLOTS) * BLK) * C + cl;
+#pragma unroll
+        for (int m = 0; m < BLK; ++m) dnext[m] = dr[(size_t)m * C];
+    }
+    for (int k = 0; k < calls; ++k)
+    {
+        float dly[BLK];
+#pragma unroll
+        for (int m = 0; m < BLK; ++m) dly[m] = dnext[m];
+        const int slot_in = (a.delay_phase + k + 1) % TX_DELAY_SLOTS;   // alc_delay_inbuf after += 32
+        if (comp && k + 1 < calls)
+        {
+            // the next call's delayed samples: its slot_out (k + 3) is not this call's slot_in (k + 1)
+            const float* dr = a.delay + ((size_t)((a.delay_phase + k + 3) % TX_DELAY_SLOTS) * BLK) * C + cl;
+#pragma unroll
+            for (int m = 0; m < BLK; ++m) dnext[m] = dr[(size_t)m * C];
+        }
+        lds_barrier();
+        float x[BLK];
+        const float* hb = hand[k & 1] + lane;
+#pragma unroll
+        for (int m = 0; m < BLK; ++m) x[m] = hb[m * TXV_PITCH];
+        if (run_bq)
+        {
+#pragma unroll
+            for (int m = 0; m < BLK; ++m)
+            {
+                float v = x[m];
+#pragma unroll
+                for (int st = 0; st < 3; ++st)
+                    v = biquad_step(v, bq[4 * st], bq[4 * st + 1], bq[4 * st + 2], bq[4 * st + 3], bc + 5 * st);
+                x[m] = v;
+            }
+        }
+        if (comp)
+        {
+            float* dw = a.delay + ((size_t)slot_in * BLK) * C + c;
+#pragma unroll
+            for (int m = 0; m < BLK; ++m)
+            {
+                const float v = tune ? x[m] : x[m] * post;
+                const float alc_var = (float)((double)(fabsf(v * alc_val) / 30000) - 1.0);
+                const float dec = alc_val - alc_val * decay * alc_var;
+                float att = (float)((double)alc_val - (double)alc_val * 0.1 * (double)alc_var);
+                att = ((double)att < 0.001) ? 0.001f : att;
+                alc_val = (alc_var < 0) ? dec : att;
+                if (alc_val > 1) alc_val = 1;
+                if (live) dw[(size_t)m * C] = v;
+                x[m] = dly[m] * (alc_val * gscale);
+            }
+        }
+        if (live)
+        {
+            float* d0 = a.a0 ? a.a0 + (size_t)c * a.N + k * BLK : nullptr;
+            float* dst = a.txa + (size_t)c * a.N + k * BLK;
+#pragma unroll
+            for (int m = 0; m < BLK; m += 4)
+            {
+                const float4 v = make_float4(x[m], x[m + 1], x[m + 2], x[m + 3]);
+                *(float4*)(dst + m) = v;
+                if (d0) *(float4*)(d0 + m) = v;
+            }
+        }
+    }
+    if (live)
+    {
 #pragma unroll
         for (int i = 0; i < 12; ++i) a.bq[i * C + c] = bq[i];
         a.alc[c] = alc_val;
@@ -410,6 +573,13 @@ struct uhsdr_tx_s
     long long calls_done, iq_launches;
     int tune, burst;                 // uhsdr_tx_set_tune / _set_tone_burst
     uint32_t tune_acc[2], burst_acc; // softdds accumulators (dbldds[0..1], tone_burst_dds) at the next frame
+    // pipelined mode (uhsdr_tx_set_pipelined): tx_iq on a side stream, the compressed-audio
+    // hand-off txa in two buffers, so tx_voice of call k+1 overlaps tx_iq of call k
+    int pipelined;
+    long long calls_issued;
+    hipStream_t side;
+    hipEvent_t ev_voice, ev_join, ev_iq[2];
+    float* txa2;                     // the second hand-off buffer [C][N]
 };
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { uhsdr_set_error("%s: %s", #x, hipGetErrorString(e_)); return UHSDR_DEVICE_ERROR; } } while (0)
@@ -434,9 +604,21 @@ static int tx_pitch(int Nf, int R)
     return best;
 }
 
+// the side stream's work (tx_iq of pipelined calls) ordered before the handle's stream
+static uhsdr_status tx_join(uhsdr_tx_s* h)
+{
+    if (h->pipelined)
+    {
+        HIPCHK(hipEventRecord(h->ev_join, h->side));
+        HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+    }
+    return UHSDR_OK;
+}
+
 extern "C" uhsdr_status uhsdr_tx_reset(uhsdr_tx_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
+    if (tx_join(h) != UHSDR_OK) return UHSDR_DEVICE_ERROR;
     HIPCHK(hipMemsetAsync(h->arena, 0, h->arena_bytes, h->stream));
     // ads.alc_val = 1 (TxProcessor_Init, tx_processor.c:137); oscillator {I=0, Q=1} (freq_shift.c:48-49)
     float* ones = (float*)malloc(sizeof(float) * h->C);
@@ -451,6 +633,7 @@ extern "C" uhsdr_status uhsdr_tx_reset(uhsdr_tx_handle h)
     h->tune_acc[0] = h->tune_acc[1] = 0;
     h->calls_done = 0;
     h->iq_launches = 0;
+    h->calls_issued = 0;
     return UHSDR_OK;
 }
 
@@ -544,15 +727,26 @@ extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio
     if (!h || !audio || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
     if (h->plan.digiq && !h->tune)
     {
-        // USB I/Q source: no voice chain, no modulator state advances, a0 (adb.a_buffer[0]) untouched
+        // USB I/Q source: no voice chain, no modulator state advances, a0 (adb.a_buffer[0]) untouched;
+        // pipelined: on the side stream, after the DAC frames of the calls before it
         const long long pairs = (long long)h->C * h->N / 2;
-        hipLaunchKernelGGL(tx_digiq, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, h->stream, h->d_plan,
+        const hipStream_t st = h->pipelined ? h->side : h->stream;
+        if (h->pipelined)
+        {
+            HIPCHK(hipEventRecord(h->ev_voice, h->stream));      // after this call's input is ready
+            HIPCHK(hipStreamWaitEvent(st, h->ev_voice, 0));
+        }
+        hipLaunchKernelGGL(tx_digiq, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, st, h->d_plan,
                            (const int4*)audio, (int4*)iq, pairs);
         HIPCHK(hipGetLastError());
         return UHSDR_OK;
     }
+    // pipelined: this call's hand-off buffer, free once the tx_iq that read it two calls ago is done
+    const int par = h->pipelined ? (int)(h->calls_issued & 1) : 0;
+    float* const txa = par ? h->txa2 : h->txa;
+    if (h->pipelined && !h->plan.fm) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_iq[par], 0));
     TxVoiceArgs va;
-    va.plan = h->d_plan; va.audio = (const int2*)audio; va.txa = h->txa; va.a0 = a0;
+    va.plan = h->d_plan; va.audio = (const int2*)audio; va.txa = txa; va.a0 = a0;
     va.lat = h->lat; va.bq = h->bq; va.alc = h->alc; va.delay = h->delay;
     va.fm = h->fm; va.iq = (int2*)iq;
     va.C = h->C; va.N = h->N;
@@ -576,26 +770,69 @@ extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio
         h->calls_done += h->N / BLK;
         return UHSDR_OK;
     }
-    hipLaunchKernelGGL((tx_voice<10, false>), dim3((h->C + 63) / 64), dim3(64), 0, h->stream, va);
+    hipLaunchKernelGGL(tx_voice2<10>, dim3((h->C + 63) / 64), dim3(128), 0, h->stream, va);
     HIPCHK(hipGetLastError());
+    const hipStream_t ist = h->pipelined ? h->side : h->stream;
+    if (h->pipelined)
+    {
+        HIPCHK(hipEventRecord(h->ev_voice, h->stream));
+        HIPCHK(hipStreamWaitEvent(ist, h->ev_voice, 0));
+    }
     const int cpw = 64 / (h->Nf / h->R);
     const size_t lds = sizeof(float) * ((size_t)cpw * h->lw + (h->plan.shift_kind == 2 ? 2 * h->Nf : 0));
     for (int f0 = 0; f0 < h->N; f0 += h->Nf)
     {
         TxIqArgs ia;
-        ia.plan = h->d_plan; ia.txa = h->txa + f0; ia.hist = h->hist;
+        ia.plan = h->d_plan; ia.txa = txa + f0; ia.hist = h->hist;
         ia.osc_in = h->osc + 2 * (h->iq_launches & 1);
         ia.osc_out = h->osc + 2 * ((h->iq_launches + 1) & 1);
         ia.iq = (int2*)iq + f0;
         ia.C = h->C; ia.N = h->Nf; ia.ld = h->N; ia.lw = h->lw;
         ia.taps2 = h->d_taps2;
-        hipLaunchKernelGGL(tx_iq<8>, dim3((h->C + cpw - 1) / cpw), dim3(64), lds, h->stream, ia);
+        hipLaunchKernelGGL(tx_iq<8>, dim3((h->C + cpw - 1) / cpw), dim3(64), lds, ist, ia);
         HIPCHK(hipGetLastError());
         h->iq_launches += 1;
     }
+    if (h->pipelined) HIPCHK(hipEventRecord(h->ev_iq[par], ist));
+    h->calls_issued += 1;
     h->calls_done += h->N / BLK;
     return UHSDR_OK;
 }
+
+extern "C" uhsdr_status uhsdr_tx_join(uhsdr_tx_handle h)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    return tx_join(h);
+}
+
+extern "C" uhsdr_status uhsdr_tx_set_pipelined(uhsdr_tx_handle h, int32_t enable)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    if (enable && !h->side)
+    {
+        HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_voice, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i) HIPCHK(hipEventCreateWithFlags(&h->ev_iq[i], hipEventDisableTiming));
+        // no call has run on the side stream yet: the events start complete
+        for (int i = 0; i < 2; ++i) HIPCHK(hipEventRecord(h->ev_iq[i], h->side));
+    }
+    if (enable && !h->txa2 && !h->plan.fm)
+        HIPCHK(hipMalloc((void**)&h->txa2, sizeof(float) * (size_t)h->C * h->N));
+    if (!enable && h->pipelined && tx_join(h) != UHSDR_OK) return UHSDR_DEVICE_ERROR;
+    if (enable && !h->pipelined)
+    {
+        // the side stream starts after everything the handle's stream has queued (state it reads)
+        HIPCHK(hipEventRecord(h->ev_voice, h->stream));
+        HIPCHK(hipStreamWaitEvent(h->side, h->ev_voice, 0));
+        for (int i = 0; i < 2; ++i) HIPCHK(hipEventRecord(h->ev_iq[i], h->side));
+        h->calls_issued = 0;
+    }
+    h->pipelined = enable != 0;
+    return UHSDR_OK;
+}
+
+extern "C" int32_t uhsdr_tx_get_pipelined(uhsdr_tx_handle h) { return h ? h->pipelined : 0; }
 
 extern "C" uhsdr_status uhsdr_tx_get_plan(uhsdr_tx_handle h, uhsdr_tx_plan* plan)
 {
@@ -608,6 +845,15 @@ extern "C" uhsdr_status uhsdr_tx_destroy(uhsdr_tx_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
     (void)hipStreamSynchronize(h->stream);
+    if (h->side)
+    {
+        (void)hipStreamSynchronize(h->side);
+        (void)hipStreamDestroy(h->side);
+        (void)hipEventDestroy(h->ev_voice);
+        (void)hipEventDestroy(h->ev_join);
+        for (int i = 0; i < 2; ++i) (void)hipEventDestroy(h->ev_iq[i]);
+    }
+    if (h->txa2) (void)hipFree(h->txa2);
     (void)hipFree(h->arena);
     (void)hipFree(h->d_plan);
     (void)hipFree(h->d_taps2);

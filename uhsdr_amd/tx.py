@@ -39,6 +39,19 @@ class TxChain:
         _abi.check(self.lib.uhsdr_tx_process(self.handle, C.c_void_p(audio.data_ptr()), C.c_void_p(iq.data_ptr()),
                                              C.c_void_p(a0.data_ptr() if a0 is not None else 0)), "uhsdr_tx_process")
 
+    def set_pipelined(self, enable: bool) -> None:
+        """tx_iq on a side stream, overlapping the next call's tx_voice (uhsdr_tx_set_pipelined);
+        call join() before reading iq."""
+        _abi.check(self.lib.uhsdr_tx_set_pipelined(self.handle, int(bool(enable))), "uhsdr_tx_set_pipelined")
+
+    @property
+    def pipelined(self) -> bool:
+        return bool(self.lib.uhsdr_tx_get_pipelined(self.handle))
+
+    def join(self) -> None:
+        """order the handle's stream after the pipelined mode's side stream (uhsdr_tx_join)"""
+        _abi.check(self.lib.uhsdr_tx_join(self.handle), "uhsdr_tx_join")
+
     def set_tune(self, tune: int) -> None:
         """TUNE for the following calls: TUNE_OFF, TUNE_SINGLE (750 Hz) or TUNE_TWO (750 + 1950 Hz)."""
         _abi.check(self.lib.uhsdr_tx_set_tune(self.handle, int(tune)), "uhsdr_tx_set_tune")

@@ -112,7 +112,7 @@ def main():
         ms = time_calls(lambda: spec.process(iq, None, avg), a.steps, a.warmup)
         byts = C * N * (8 + 4) + C * L * 8
         lines.append({"workload": "C3 spectrum 1024-point (Hann, CFFT, magnitude, IIR average)", "channels": C,
-                      "frames_per_call": N, "waves_per_workgroup": waves, "ms_per_call": round(ms, 4), "msamples_per_s": round(C * N / ms / 1e3, 1),
+                      "frames_per_call": N, "ms_per_call": round(ms, 4), "msamples_per_s": round(C * N / ms / 1e3, 1),
                       "alg_bytes_per_frame": round(byts / (C * N), 2),
                       "hbm_frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4),
                       "finite": bool(torch.isfinite(avg).all().item())})

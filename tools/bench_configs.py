@@ -53,12 +53,17 @@ def time_calls(fn, steps, warmup, join=None):
     return e0.elapsed_time(e1) / steps
 
 
+FRONT_BLOCK = 0     # --front-block: the RX lines' front outputs per lane (0 = the library's choice)
+
+
 def rx_line(name, cfg, C, N, iq, steps, warmup, cw=False, pipelined=False):
     import torch
     import bench
     import uhsdr_amd as U
     s = torch.cuda.current_stream()
     chain = U.RxChain(cfg, channels=C, frames=N, stream=s.cuda_stream)
+    if FRONT_BLOCK:
+        chain.set_front_block(FRONT_BLOCK)
     if pipelined:
         chain.set_pipelined(True)
     audio = torch.empty((C, N), dtype=torch.float32, device="cuda")
@@ -92,7 +97,10 @@ def main():
     ap.add_argument("--serial", action="store_true",
                     help="C4 FM-RX / SSB-TX handles in their serial mode (default: pipelined, measured faster there; "
                          "C3 SAM and C5 CW run serial, where the pipelined mode measured slower / the same)")
+    ap.add_argument("--front-block", type=int, default=0, choices=[0, 8, 16], help="RX lines: front outputs per lane")
     a = ap.parse_args()
+    global FRONT_BLOCK
+    FRONT_BLOCK = a.front_block
     import torch
     import uhsdr_amd as U
     from uhsdr_amd import synth

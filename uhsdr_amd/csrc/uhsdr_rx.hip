@@ -2934,7 +2934,13 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     uhsdr_status bst = uhsdr_rx_plan_build(cfg, &h->plan);
     if (bst != UHSDR_OK) { free(h); return bst; }
     const uhsdr_rx_plan& p = h->plan;
-    h->fv = find_front(p, N);
+    // 8 FIR outputs per lane, or 16 for the narrow (decimate-first SSB / CW / DIGI) family on large
+    // batches, whose 199-tap Hilbert pair at the decimated rate then gets 4 outputs per register
+    // window instead of 2 (C5, 131072 x 256: 0.394 -> 0.359 ms per call; the wide, AM / SAM and
+    // FM families measured slower at 16: 1M x 64 P48 0.695 vs 0.573 ms front, C3 SAM 0.129 vs
+    // 0.115, C4 FM 0.108 vs 0.094; uhsdr_rx_set_front_block overrides)
+    const bool narrow = p.use_decimated_iq && p.hilbert_taps > 0;     // the front's pass 2 is the Hilbert pair
+    h->fv = find_front(p, N, narrow && C >= 65536 ? 16 : 8);
     h->bv = find_back(p);
     h->nv = find_notch(p);
     h->cv = find_chain(p, h->bv);

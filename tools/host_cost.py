@@ -1,10 +1,14 @@
 """Host-side submission cost of one RxChain.process call (C2 shape), serial and pipelined:
 30 calls timed without synchronising (the GPU queue does not fill), then the GPU time of the
 same 30 calls after a sync."""
+import os
+import sys
 import time
-import torch
-import uhsdr_amd as U
-from uhsdr_amd import synth
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import uhsdr_amd as U  # noqa: E402
+from uhsdr_amd import synth  # noqa: E402
 
 C, N = 4096, 256
 dev = torch.device("cuda:0")

@@ -28,6 +28,7 @@
 // (tests/test_gpu_parity.py).
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
@@ -2573,9 +2574,16 @@ static const BackVariant* find_back(const uhsdr_rx_plan& p)
 constexpr int TAPS2_MAX = (UHSDR_MAX_FIR_TAPS + 7) & ~7;   // taps per pair table
 constexpr int BACK_FUSED_MIN_CHANNELS = 131072;   // measured crossover (64-frame calls)
 
-// pipelined mode: hand-off buffers in rotation, so rx_front can run up to two calls ahead of
-// rx_back and the side stream's wait on it is already satisfied when rx_back gets there
-constexpr int PIPE_BUFS = 3;
+// pipelined mode: hand-off buffers in rotation, so rx_front runs ahead of rx_back and the side
+// stream's wait on it is already satisfied when rx_back gets there.  The buffers' reuse is
+// ordered per group of PIPE_GROUP calls, not per call: rx_back records a completion event at
+// the end of each group, and the first rx_front of a group waits for the group two before it
+// (PIPE_BUFS = 2 PIPE_GROUP buffers).  With the front's and back's events folded into their
+// launches (hipExtLaunchKernelGGL) a call costs the host 2 launches + 1 stream wait (+1 per
+// group) instead of 2 launches + 2 records + 2 waits: C2's host submission, 22-25 us per call,
+// was as long as the GPU's, and the GPU idled between calls (rocprofv3 kernel trace, r03).
+constexpr int PIPE_GROUP = 4;
+constexpr int PIPE_BUFS = 2 * PIPE_GROUP;
 
 struct uhsdr_rx_s
 {
@@ -2615,10 +2623,11 @@ struct uhsdr_rx_s
     // rotated over PIPE_BUFS buffers so the next calls' rx_front overlaps this call's rx_back
     int pipelined;
     hipStream_t side;
-    hipEvent_t ev_front, ev_join, ev_back[PIPE_BUFS];
+    hipEvent_t ev_front, ev_join, ev_back[2];  // ev_back[g % 2]: end of group g's rx_back
     hipEvent_t ev_switch;    // uhsdr_rx_set_stream: new stream after the old one's work
     float *adecp[PIPE_BUFS - 1], *adec_qp[PIPE_BUFS - 1];  // the pipelined mode's other hand-off buffers
-    long long calls_issued;  // process() calls (hand-off buffer index)
+    long long calls_issued;  // process() calls
+    long long pipe_calls;    // calls since the pipelined mode was entered (buffer index, group)
     // per-kernel timing (uhsdr_rx_enable_timing)
     int timing;               // 0 off, else every timing-th call is bracketed
     int tsample;              // the call being enqueued is a timed one
@@ -3240,20 +3249,29 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
     }
     else
     {
-        // hand-off buffers of this call; pipelined: rotate, and wait until the rx_back that read
-        // this buffer PIPE_BUFS calls ago has finished
-        const int par = h->pipelined ? (int)(h->calls_issued % PIPE_BUFS) : 0;
+        // hand-off buffers of this call; pipelined: rotate, and at the start of a group wait
+        // until the rx_back of the group two before it (the last readers of its buffers) is done
+        const long long pk = h->pipe_calls;
+        const int par = h->pipelined ? (int)(pk % PIPE_BUFS) : 0;
+        const int grp = (int)((pk / PIPE_GROUP) & 1);
+        const bool group_end = h->pipelined && pk % PIPE_GROUP == PIPE_GROUP - 1;
         float* adec = par ? h->adecp[par - 1] : h->adec;
         float* adec_q = par ? h->adec_qp[par - 1] : h->adec_q;
-        if (side_mode(h)) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[par], 0));
+        if (side_mode(h) && pk % PIPE_GROUP == 0) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[grp], 0));
         time_mark(h, K_FRONT, 0);
         const int cpw = FRONT_WAVE / (h->Nf / h->fv->R);
         const size_t lds = front_lds(h);
+        const bool side = side_mode(h);
         for (int f0 = 0; f0 < h->N; f0 += h->Nf)
         {
             const FrontArgs fa = front_args(h, iq, f0, adec, adec_q);
-            hipLaunchKernelGGL(fma ? h->fv->fn_fma : h->fv->fn, dim3((h->C + cpw - 1) / cpw), dim3(FRONT_WAVE), lds,
-                               h->stream, fa);
+            const auto fn = fma ? h->fv->fn_fma : h->fv->fn;
+            const dim3 grid((h->C + cpw - 1) / cpw), block(FRONT_WAVE);
+            // pipelined: the call's last front launch records ev_front as it completes
+            if (side && f0 + h->Nf >= h->N)
+                hipExtLaunchKernelGGL(fn, grid, block, lds, h->stream, nullptr, h->ev_front, 0, fa);
+            else
+                hipLaunchKernelGGL(fn, grid, block, lds, h->stream, fa);
             HIPCHK(hipGetLastError());
             h->front_launches += 1;
         }
@@ -3261,26 +3279,26 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
 
         const BackArgs ba = back_args(h, adec, adec_q, audio, audio0, dst);
         const hipStream_t bst = back_stream(h);
-        if (side_mode(h))
-        {
-            HIPCHK(hipEventRecord(h->ev_front, h->stream));
-            HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
-        }
+        if (side) HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
         time_mark(h, K_BACK, 0);
         if (h->nv)
         {
             hipLaunchKernelGGL(h->nv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
             HIPCHK(hipGetLastError());
         }
-        if (h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo)
-            hipLaunchKernelGGL(h->plan.agc.remove_dc || !h->bv->fused_nodc ? h->bv->fused : h->bv->fused_nodc,
-                               dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
+        const bool fused = h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo;
+        const back_fn bfn = fused ? (h->plan.agc.remove_dc || !h->bv->fused_nodc ? h->bv->fused : h->bv->fused_nodc)
+                                  : h->bv->fn;
+        const dim3 bgrid((h->C + BACK_CH - 1) / BACK_CH), bblock(fused ? BACK_CH : back_roles(h->bv->dm) * BACK_CH);
+        const size_t blds = fused ? 0 : back_lds(h);
+        // pipelined: the group's last rx_back records ev_back[grp] as it completes
+        if (side && group_end)
+            hipExtLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, nullptr, h->ev_back[grp], 0, ba);
         else
-            hipLaunchKernelGGL(h->bv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(back_roles(h->bv->dm) * BACK_CH),
-                               back_lds(h), bst, ba);
+            hipLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, ba);
         HIPCHK(hipGetLastError());
         time_mark(h, K_BACK, 1);
-        if (side_mode(h)) HIPCHK(hipEventRecord(h->ev_back[par], bst));
+        if (h->pipelined) h->pipe_calls += 1;
     }
     h->calls_issued += 1;
     if (h->tsample) h->nev++;
@@ -3395,13 +3413,10 @@ extern "C" uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable
     {
         const size_t nd = (size_t)h->C * h->Nd;
         HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&h->ev_front, hipEventDisableTiming));
+        // ev_front / ev_back are recorded by hipExtLaunchKernel as their kernels complete
+        HIPCHK(hipEventCreate(&h->ev_front));
         HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
-        for (int i = 0; i < PIPE_BUFS; ++i)
-        {
-            HIPCHK(hipEventCreateWithFlags(&h->ev_back[i], hipEventDisableTiming));
-            HIPCHK(hipEventRecord(h->ev_back[i], h->side));
-        }
+        for (int i = 0; i < 2; ++i) HIPCHK(hipEventCreate(&h->ev_back[i]));
         for (int i = 0; i < PIPE_BUFS - 1; ++i)
         {
             HIPCHK(hipMalloc((void**)&h->adecp[i], sizeof(float) * nd));
@@ -3414,6 +3429,15 @@ extern "C" uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable
     {
         const uhsdr_status st = uhsdr_rx_join(h);
         if (st != UHSDR_OK) return st;
+    }
+    if (enable && !h->pipelined)
+    {
+        // entering it: the side stream starts after the handle stream's work (the state the first
+        // rx_back reads), and both group events start out complete
+        HIPCHK(hipEventRecord(h->ev_join, h->stream));
+        HIPCHK(hipStreamWaitEvent(h->side, h->ev_join, 0));
+        for (int i = 0; i < 2; ++i) HIPCHK(hipEventRecord(h->ev_back[i], h->side));
+        h->pipe_calls = 0;
     }
     h->pipelined = enable != 0;
     return UHSDR_OK;
@@ -3493,7 +3517,7 @@ extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
     {
         (void)hipEventDestroy(h->ev_front);
         (void)hipEventDestroy(h->ev_join);
-        for (int i = 0; i < PIPE_BUFS; ++i) (void)hipEventDestroy(h->ev_back[i]);
+        for (int i = 0; i < 2; ++i) (void)hipEventDestroy(h->ev_back[i]);
         (void)hipStreamDestroy(h->side);
         for (int i = 0; i < PIPE_BUFS - 1; ++i)
         {

@@ -19,8 +19,13 @@ def main():
     from uhsdr_amd import synth
     Cn = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-    chain = U.RxChain(U.default_config(), channels=Cn, frames=N, schedule=U.SCHEDULE_SPLIT_PIPE)
-    x = synth.ssb_iq_torch(0, Cn, 0, N, "cuda")
+    sam = len(sys.argv) > 3 and sys.argv[3] == "sam"          # C3's SAM P70 chain (demod role first)
+    cfg = U.default_config(filter_path=70, dmod_mode=U.DEMOD_SAM) if sam else U.default_config()
+    chain = U.RxChain(cfg, channels=Cn, frames=N, schedule=U.SCHEDULE_SPLIT_PIPE)
+    if sam:
+        x = torch.from_numpy(synth.am_iq(np.arange(Cn), 0, N)).cuda()
+    else:
+        x = synth.ssb_iq_torch(0, Cn, 0, N, "cuda")
     audio = torch.empty((Cn, N), dtype=torch.float32, device="cuda")
     for _ in range(5):
         chain.process(x, audio)
@@ -30,13 +35,13 @@ def main():
     lib.uhsdr_trace_read.argtypes = [C.c_void_p]
     assert lib.uhsdr_trace_read(buf.ctypes.data_as(C.c_void_p)) == 0
     calls = N // 32
-    roles = 5
+    roles = 6 if sam else 5
     its = calls + roles - 1
     t = buf[:, :roles, :its, :].astype(np.int64)
     t0 = t[:, :, 0, 0].min(axis=1)[:, None, None]
     work = (t[:, :, :, 1] - t[:, :, :, 0])
     wait = (t[:, :, :, 2] - t[:, :, :, 1])
-    names = ["pre", "agc", "audio", "aa", "output"]
+    names = (["demod"] if sam else []) + ["pre", "agc", "audio", "aa", "output"]
     print(f"C={Cn} N={N}: per-step cycles (median over workgroups), work / barrier wait")
     for it in range(its):
         row = " ".join(f"{names[r]:>6} {int(np.median(work[:, r, it])):6d}/{int(np.median(wait[:, r, it])):6d}" for r in range(roles))

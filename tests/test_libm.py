@@ -28,6 +28,14 @@ def test_atan2f_matches_glibc(tmp_path):
     assert " 0 of " in r.stdout
 
 
+def test_atan2f_x_one_matches_glibc(tmp_path):
+    """atan2f(y, 1) -- fdlibm's atanf(y) case, which the branch-free ul_atan2f folds into its main
+    path: every 4099th binary32 y here, every y in the exhaustive run (libm_pin.txt)."""
+    r = subprocess.run([_build(tmp_path), "atan2x1", "4099"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout
+    assert " 0 of " in r.stdout
+
+
 def test_asinf_matches_glibc(tmp_path):
     """The twin-peaks detector's asinf (audio_driver.c:2211); exhaustive run in libm_pin.txt."""
     r = subprocess.run([_build(tmp_path), "asin", "127"], capture_output=True, text=True, timeout=120)

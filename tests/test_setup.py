@@ -63,7 +63,10 @@ def test_plan_rejects_bad_config():
     lib = U.load()
     plan = U.RxPlan()
     for over in [dict(filter_path=0), dict(filter_path=87), dict(dmod_mode=9),
-                 dict(filter_path=1)]:   # FM-only path for USB
+                 dict(filter_path=1),    # FM-only path for USB
+                 # SAM PLL menu ranges (ui_configuration.c:214-216)
+                 dict(sam_pll_fmax=49), dict(sam_pll_fmax=8001), dict(sam_zeta=0), dict(sam_zeta=101),
+                 dict(sam_omega_n=14), dict(sam_omega_n=1001)]:
         cfg = U.default_config(**over)
         assert lib.uhsdr_rx_plan_build(C.byref(cfg), C.byref(plan)) == -1, over
 

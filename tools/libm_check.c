@@ -2,6 +2,7 @@
  *   libm_check sincos <stride>   every stride-th float in [0, 2*pi] and (-2*pi, 0)
  *   libm_check atan2 <count>     random + structured operand pairs
  *   libm_check asin <stride>     every stride-th float in [-1, 1] (and NaN operands past it)
+ *   libm_check atan2x1 <stride>  every stride-th binary32 y (all signs) against atan2f(y, 1.0f)
  * Prints mismatches (first 10) and a summary line; exit status 1 on any mismatch. */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -52,6 +53,21 @@ int main(int argc, char** argv)
                 }
             }
         printf("asinf: %ld of %ld arguments differ\n", bad, n);
+    }
+    else if (!strcmp(argv[1], "atan2x1"))
+    {
+        const long stride = atol(argv[2]);
+        for (uint64_t u = 0; u <= 0xffffffffull; u += stride)
+        {
+            const float y = ul_asfloat((uint32_t)u);
+            const float r0 = atan2f(y, 1.0f), r1 = ul_atan2f(y, 1.0f);
+            ++n;
+            if (ul_asuint(r0) != ul_asuint(r1) && !(isnan(r0) && isnan(r1)))
+            {
+                if (bad++ < 10) printf("atan2f(%a, 1): glibc %a, ours %a\n", y, r0, r1);
+            }
+        }
+        printf("atan2f(y, 1): %ld of %ld arguments differ\n", bad, n);
     }
     else
     {

@@ -159,49 +159,31 @@ UHSDR_LIBM_FN float ul_atan2f(float y, float x)
     const int32_t hx = (int32_t)ul_asuint(x), hy = (int32_t)ul_asuint(y);
     const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
     const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);      /* 2*sign(x) + sign(y) */
-    /* rare operands (NaN, x = 1, zeros, infinities): wave-uniformly skipped when no lane has one */
-    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;   /* NaN */
-    if (hx == 0x3f800000) return ul_atanf(y);               /* x = 1.0 */
-    if (iy == 0)
-    {
-        switch (m)
-        {
-        case 0:
-        case 1: return y;                                   /* atan(+-0, +anything) = +-0 */
-        case 2: return pi + tiny;                           /* atan(+0, -anything) = pi */
-        default: return -pi - tiny;                         /* atan(-0, -anything) = -pi */
-        }
-    }
-    if (ix == 0) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
-    if (ix == 0x7f800000)
-    {
-        if (iy == 0x7f800000)
-        {
-            switch (m)
-            {
-            case 0: return pi_o_4 + tiny;
-            case 1: return -pi_o_4 - tiny;
-            case 2: return 3.0f * pi_o_4 + tiny;
-            default: return -3.0f * pi_o_4 - tiny;
-            }
-        }
-        switch (m)
-        {
-        case 0: return 0.0f;
-        case 1: return -0.0f;
-        case 2: return pi + tiny;
-        default: return -pi - tiny;
-        }
-    }
-    if (iy == 0x7f800000) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    /* Branch-free: fdlibm's main path (e_atan2f.c, the k / atanf / quadrant tail) runs for
+     * every operand pair and the rare operands (NaN, zeros, infinities) select their results
+     * after it, lowest precedence first, so the SAM PLL's per-sample chain stays one basic
+     * block and consecutive samples' chains can interleave.  x = 1.0 (fdlibm: atanf(y)) needs
+     * no case of its own: y / 1 = y, atanf is odd and the |y/x| > 2^26 override is skipped for
+     * it -- pinned for every binary32 y by tools/libm_check.c "atan2x1". */
     const int32_t k = (iy - ix) >> 23;
     float z = ul_atanf(fabsf(y / x));
     z = (hx < 0 && k < -26) ? 0.0f : z;                     /* |y|/x < -2^26 */
-    z = (k > 26) ? pi_o_2 + 0.5f * pi_lo : z;               /* |y/x| > 2^26 */
+    z = (k > 26 && hx != 0x3f800000) ? pi_o_2 + 0.5f * pi_lo : z;   /* |y/x| > 2^26 */
     const float zm = z - pi_lo;
     const float r2 = pi - zm, r3 = zm - pi;
     const float r1 = ul_asfloat(ul_asuint(z) ^ 0x80000000u);
-    return (m & 2) ? ((m & 1) ? r3 : r2) : ((m & 1) ? r1 : z);
+    float r = (m & 2) ? ((m & 1) ? r3 : r2) : ((m & 1) ? r1 : z);
+    const float pm_pi = (m & 1) ? -pi - tiny : pi + tiny;   /* +-pi by sign(y) */
+    const float pm_pi_o_2 = (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    r = (iy == 0x7f800000) ? pm_pi_o_2 : r;                 /* y = +-inf, x finite */
+    const float inf_inf = (m & 2) ? ((m & 1) ? -3.0f * pi_o_4 - tiny : 3.0f * pi_o_4 + tiny)
+                                  : ((m & 1) ? -pi_o_4 - tiny : pi_o_4 + tiny);
+    const float inf_fin = (m & 2) ? pm_pi : ((m & 1) ? -0.0f : 0.0f);
+    r = (ix == 0x7f800000) ? ((iy == 0x7f800000) ? inf_inf : inf_fin) : r;   /* x = +-inf */
+    r = (ix == 0) ? pm_pi_o_2 : r;                          /* x = +-0 */
+    r = (iy == 0) ? ((m & 2) ? pm_pi : y) : r;              /* y = +-0 */
+    r = (ix > 0x7f800000 || iy > 0x7f800000) ? x + y : r;   /* NaN */
+    return r;
 }
 
 /* ---- asinf (glibc sysdeps/ieee754/flt-32/e_asinf.c: fdlibm binary32 with a degree-4 minimax

@@ -426,6 +426,17 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
         p->stereo = (two && cfg->stereo_enable) ? (mode == UHSDR_DEMOD_SSBSTEREO ? 1 : mode == UHSDR_DEMOD_IQ ? 2 : 3) : 0;
     }
     p->fade_leveler = cfg->fade_leveler != 0;
+    /* the menu's ranges (ui_configuration.c:214-216); within them the PLL's per-sample phase
+       step |g1 * phzerror + omega2| <= g1 * pi + 2 pi fmax / 12000 < 4.7 stays below 2 pi, so the
+       phase wrap (audio_driver.c:2143-2146) takes at most one iteration each way and the device
+       demodulator (DemodStage::step) evaluates it as two selects */
+    if (cfg->sam_pll_fmax < 50 || cfg->sam_pll_fmax > 8000 || cfg->sam_zeta < 1 || cfg->sam_zeta > 100 ||
+        cfg->sam_omega_n < 15 || cfg->sam_omega_n > 1000)
+    {
+        uhsdr_set_error("SAM PLL parameters (fmax %d, zeta %d, omegaN %d) outside 50..8000, 1..100, 15..1000",
+                        cfg->sam_pll_fmax, cfg->sam_zeta, cfg->sam_omega_n);
+        return UHSDR_ARGUMENT_ERROR;
+    }
     {
         const float decimSampleRate = p->decimated_freq;
         const float pll_fmax = cfg->sam_pll_fmax;

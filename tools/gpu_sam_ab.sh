@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 V=uhsdr_amd/lib/variants
-for t in trace traceold; do
+for t in trace; do
   [ -f $V/libuhsdr_amd_$t.so ] || continue
   UHSDR_LIB=$V/libuhsdr_amd_$t.so timeout -k 10 180 python tools/trace_back.py 32768 1024 sam \
       > gpurun_out/sam_$t.txt 2>&1 || { tail -20 gpurun_out/sam_$t.txt; exit 1; }

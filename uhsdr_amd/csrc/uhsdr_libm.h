@@ -37,6 +37,22 @@ UHSDR_LIBM_FN uint32_t ul_asuint(float f) { uint32_t u; memcpy(&u, &f, 4); retur
 UHSDR_LIBM_FN float ul_asfloat(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 /* top 12 bits of |x|: exponent and 3 mantissa bits (s_sincosf.c abstop12) */
 UHSDR_LIBM_FN uint32_t ul_abstop12(float x) { return (ul_asuint(x) >> 20) & 0x7ff; }
+UHSDR_LIBM_FN uint64_t ul_asuint64(double f) { uint64_t u; memcpy(&u, &f, 8); return u; }
+UHSDR_LIBM_FN double ul_asdouble(uint64_t u) { double f; memcpy(&f, &u, 8); return f; }
+/* c ? a : b as a bit-mask blend.  clang emits a conditional operator with non-constant arms as
+   a branch diamond, and the ones the optimizer does not fold back become exec-masked regions
+   (separate basic blocks) on the GPU -- which keeps the scheduler from overlapping two PLL
+   samples -- or, for a chain over an index, a table load.  The blend is one v_cndmask. */
+UHSDR_LIBM_FN float ul_sel(int c, float a, float b)
+{
+    const uint32_t m = 0u - (uint32_t)(c != 0);
+    return ul_asfloat((ul_asuint(a) & m) | (ul_asuint(b) & ~m));
+}
+UHSDR_LIBM_FN double ul_seld(int c, double a, double b)
+{
+    const uint64_t m = 0ull - (uint64_t)(c != 0);
+    return ul_asdouble((ul_asuint64(a) & m) | (ul_asuint64(b) & ~m));
+}
 
 /* ---- sincosf, |y| < 120 (the PLL phase is in [0, 2*pi)) ---- */
 typedef struct
@@ -81,8 +97,8 @@ UHSDR_LIBM_FN void ul_sincosf_poly(double x, double x2, const ul_sincos_t* p, in
     const double c = fma(x4, p->c2, c1);
     const float rs = (float)fma(x5, s1, s);
     const float rc = (float)fma(x6, c2, c);
-    *sinp = (n & 1) ? rc : rs;                       /* quadrant swap */
-    *cosp = (n & 1) ? rs : rc;
+    *sinp = ul_sel(n & 1, rc, rs);                   /* quadrant swap */
+    *cosp = ul_sel(n & 1, rs, rc);
 }
 
 /* s_sincosf.c for |y| < 120 (callers guarantee the range; the Payne-Hanek branch for huge
@@ -99,17 +115,18 @@ UHSDR_LIBM_FN void ul_sincosf(float y, float* sinp, float* cosp)
     const double r = x * p0->hpi_inv;
     const int n = ((int32_t)r + 0x800000) >> 24;
     x = fma(-(double)n, p0->hpi, x);
-    const double s = (n & 1) ? ((n & 2) ? p0->sign[3] : p0->sign[1]) : ((n & 2) ? p0->sign[2] : p0->sign[0]);
+    /* sign[n & 3] = +1, -1, -1, +1: negative when bit 1 of n + 1 is set */
+    const double s = ul_asdouble(0x3ff0000000000000ull | ((uint64_t)((n + 1) & 2) << 62));
     ul_sincos_t q;
     const int h = (n & 2) != 0;
-    q.c0 = h ? p1->c0 : p0->c0; q.c1 = h ? p1->c1 : p0->c1; q.s1 = h ? p1->s1 : p0->s1;
-    q.c2 = h ? p1->c2 : p0->c2; q.s2 = h ? p1->s2 : p0->s2; q.c3 = h ? p1->c3 : p0->c3;
-    q.s3 = h ? p1->s3 : p0->s3; q.c4 = h ? p1->c4 : p0->c4;
+    q.c0 = ul_seld(h, p1->c0, p0->c0); q.c1 = ul_seld(h, p1->c1, p0->c1); q.s1 = ul_seld(h, p1->s1, p0->s1);
+    q.c2 = ul_seld(h, p1->c2, p0->c2); q.s2 = ul_seld(h, p1->s2, p0->s2); q.c3 = ul_seld(h, p1->c3, p0->c3);
+    q.s3 = ul_seld(h, p1->s3, p0->s3); q.c4 = ul_seld(h, p1->c4, p0->c4);
     float sv, cv;
     ul_sincosf_poly(x * s, x * x, &q, n, &sv, &cv);
     const int tiny = ul_abstop12(y) < ul_abstop12(0x1p-12f);
-    *sinp = tiny ? y : sv;
-    *cosp = tiny ? 1.0f : cv;
+    *sinp = ul_sel(tiny, y, sv);
+    *cosp = ul_sel(tiny, 1.0f, cv);
 }
 
 /* ---- atanf / atan2f (fdlibm binary32) ---- */
@@ -135,20 +152,20 @@ UHSDR_LIBM_FN float ul_atanf(float x)
     const float n0 = 2.0f * ax - 1.0f, d0 = 2.0f + ax;
     const float n1 = ax - 1.0f, d1 = ax + 1.0f;
     const float n2 = ax - 1.5f, d2 = 1.0f + 1.5f * ax;
-    const float num = lo2 ? (i0 ? n0 : n1) : (i2 ? n2 : -1.0f);
-    const float den = lo2 ? (i0 ? d0 : d1) : (i2 ? d2 : ax);
-    const float hi = lo2 ? (i0 ? atanhi[0] : atanhi[1]) : (i2 ? atanhi[2] : atanhi[3]);
-    const float lo = lo2 ? (i0 ? atanlo[0] : atanlo[1]) : (i2 ? atanlo[2] : atanlo[3]);
-    const float xr = small ? x : num / den;
+    const float num = ul_sel(lo2, ul_sel(i0, n0, n1), ul_sel(i2, n2, -1.0f));
+    const float den = ul_sel(lo2, ul_sel(i0, d0, d1), ul_sel(i2, d2, ax));
+    const float hi = ul_sel(lo2, ul_sel(i0, atanhi[0], atanhi[1]), ul_sel(i2, atanhi[2], atanhi[3]));
+    const float lo = ul_sel(lo2, ul_sel(i0, atanlo[0], atanlo[1]), ul_sel(i2, atanlo[2], atanlo[3]));
+    const float xr = ul_sel(small, x, num / den);
     const float z = xr * xr;
     const float w = z * z;
     const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
     const float s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
     const float zz = hi - ((xr * (s1 + s2) - lo) - xr);
-    float r = small ? xr - xr * (s1 + s2) : ((hx >> 31) ? -zz : zz);
-    r = (ix < 0x31000000) ? x : r;                                      /* |x| < 2^-29 */
-    const float huge = (hx >> 31) ? -atanhi[3] - atanlo[3] : atanhi[3] + atanlo[3];
-    r = (ix >= 0x4c000000) ? ((ix > 0x7f800000) ? x + x : huge) : r;   /* |x| >= 2^25, NaN */
+    float r = ul_sel(small, xr - xr * (s1 + s2), ul_sel(hx >> 31, -zz, zz));
+    r = ul_sel(ix < 0x31000000, x, r);                                  /* |x| < 2^-29 */
+    const float huge = ul_sel(hx >> 31, -atanhi[3] - atanlo[3], atanhi[3] + atanlo[3]);
+    r = ul_sel(ix >= 0x4c000000, ul_sel(ix > 0x7f800000, x + x, huge), r);   /* |x| >= 2^25, NaN */
     return r;
 }
 
@@ -167,22 +184,22 @@ UHSDR_LIBM_FN float ul_atan2f(float y, float x)
      * it -- pinned for every binary32 y by tools/libm_check.c "atan2x1". */
     const int32_t k = (iy - ix) >> 23;
     float z = ul_atanf(fabsf(y / x));
-    z = (hx < 0 && k < -26) ? 0.0f : z;                     /* |y|/x < -2^26 */
-    z = (k > 26 && hx != 0x3f800000) ? pi_o_2 + 0.5f * pi_lo : z;   /* |y/x| > 2^26 */
+    z = ul_sel(hx < 0 && k < -26, 0.0f, z);                 /* |y|/x < -2^26 */
+    z = ul_sel(k > 26 && hx != 0x3f800000, pi_o_2 + 0.5f * pi_lo, z);   /* |y/x| > 2^26 */
     const float zm = z - pi_lo;
     const float r2 = pi - zm, r3 = zm - pi;
     const float r1 = ul_asfloat(ul_asuint(z) ^ 0x80000000u);
-    float r = (m & 2) ? ((m & 1) ? r3 : r2) : ((m & 1) ? r1 : z);
-    const float pm_pi = (m & 1) ? -pi - tiny : pi + tiny;   /* +-pi by sign(y) */
-    const float pm_pi_o_2 = (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
-    r = (iy == 0x7f800000) ? pm_pi_o_2 : r;                 /* y = +-inf, x finite */
-    const float inf_inf = (m & 2) ? ((m & 1) ? -3.0f * pi_o_4 - tiny : 3.0f * pi_o_4 + tiny)
-                                  : ((m & 1) ? -pi_o_4 - tiny : pi_o_4 + tiny);
-    const float inf_fin = (m & 2) ? pm_pi : ((m & 1) ? -0.0f : 0.0f);
-    r = (ix == 0x7f800000) ? ((iy == 0x7f800000) ? inf_inf : inf_fin) : r;   /* x = +-inf */
-    r = (ix == 0) ? pm_pi_o_2 : r;                          /* x = +-0 */
-    r = (iy == 0) ? ((m & 2) ? pm_pi : y) : r;              /* y = +-0 */
-    r = (ix > 0x7f800000 || iy > 0x7f800000) ? x + y : r;   /* NaN */
+    float r = ul_sel(m & 2, ul_sel(m & 1, r3, r2), ul_sel(m & 1, r1, z));
+    const float pm_pi = ul_sel(m & 1, -pi - tiny, pi + tiny);   /* +-pi by sign(y) */
+    const float pm_pi_o_2 = ul_sel(hy < 0, -pi_o_2 - tiny, pi_o_2 + tiny);
+    r = ul_sel(iy == 0x7f800000, pm_pi_o_2, r);             /* y = +-inf, x finite */
+    const float inf_inf = ul_sel(m & 2, ul_sel(m & 1, -3.0f * pi_o_4 - tiny, 3.0f * pi_o_4 + tiny),
+                                 ul_sel(m & 1, -pi_o_4 - tiny, pi_o_4 + tiny));
+    const float inf_fin = ul_sel(m & 2, pm_pi, ul_sel(m & 1, -0.0f, 0.0f));
+    r = ul_sel(ix == 0x7f800000, ul_sel(iy == 0x7f800000, inf_inf, inf_fin), r);   /* x = +-inf */
+    r = ul_sel(ix == 0, pm_pi_o_2, r);                      /* x = +-0 */
+    r = ul_sel(iy == 0, ul_sel(m & 2, pm_pi, y), r);        /* y = +-0 */
+    r = ul_sel(ix > 0x7f800000 || iy > 0x7f800000, x + y, r);   /* NaN */
     return r;
 }
 

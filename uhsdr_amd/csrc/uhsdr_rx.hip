@@ -1405,38 +1405,38 @@ struct DemodStage
             {
                 audio = corr0;
             }
-            // The whole SAM step is one basic block (fade leveler and phase wrap as selects,
-            // ul_atan2f branch-free): sample n + 1's phase needs only fil_out(n - 1), so the
+            // The whole SAM step is one basic block (fade leveler and phase wrap as bit-mask
+            // selects, ul_sel; ul_sincosf / ul_atan2f branch-free): sample n + 1's phase needs only fil_out(n - 1), so the
             // scheduler overlaps two samples' sincosf -> atan2f chains.
             {
                 // AudioDriver_FadeLeveler(0, ...), audio_driver.c:1911-1923
                 const float d27 = mtauR * dc27 + onem_mtauR * audio;
                 const float dci = mtauI * dc_insert + onem_mtauI * corr0;
                 const float lev = audio + dci - d27;
-                dc27 = fade ? d27 : dc27; dc_insert = fade ? dci : dc_insert;
-                audio = fade ? lev : audio;
+                dc27 = ul_sel(fade, d27, dc27); dc_insert = ul_sel(fade, dci, dc_insert);
+                audio = ul_sel(fade, lev, audio);
                 if (DM == DM_SAM_ST)
                 {
                     // AudioDriver_FadeLeveler(1, ...)
                     const float d27_1 = mtauR * dc27_1 + onem_mtauR * y1;
                     const float dci_1 = mtauI * dc_insert_1 + onem_mtauI * corr0;
                     const float lev1 = y1 + dci_1 - d27_1;
-                    dc27_1 = fade ? d27_1 : dc27_1; dc_insert_1 = fade ? dci_1 : dc_insert_1;
-                    y1 = fade ? lev1 : y1;
+                    dc27_1 = ul_sel(fade, d27_1, dc27_1); dc_insert_1 = ul_sel(fade, dci_1, dc_insert_1);
+                    y1 = ul_sel(fade, lev1, y1);
                 }
             }
             // PLL (audio_driver.c:2128-2147)
             const float phzerror = ul_atan2f(corr1, corr0);
             const float del_out = fil_out;
             omega2 = omega2 + g2 * phzerror;
-            omega2 = (omega2 < omega_min) ? omega_min : ((omega2 > omega_max) ? omega_max : omega2);
+            omega2 = ul_sel(omega2 < omega_min, omega_min, ul_sel(omega2 > omega_max, omega_max, omega2));
             fil_out = g1 * phzerror + omega2;
             phs = phs + del_out;
             // the reference's while loops (in double: 2.0 * PI is a double) run at most once each:
             // |del_out| <= g1 * pi + omega_max < 2 pi for the plan's parameter ranges
             // (uhsdr_setup.c), so phs + del_out stays inside (-2 pi, 4 pi)
-            phs = ((double)phs >= two_pi) ? (float)((double)phs - two_pi) : phs;
-            phs = ((double)phs < 0.0) ? (float)((double)phs + two_pi) : phs;
+            phs = ul_sel((double)phs >= two_pi, (float)((double)phs - two_pi), phs);
+            phs = ul_sel((double)phs < 0.0, (float)((double)phs + two_pi), phs);
         }
         return audio;
     }

@@ -36,6 +36,14 @@ def test_atan2f_x_one_matches_glibc(tmp_path):
     assert " 0 of " in r.stdout
 
 
+def test_atanf_nonnegative_matches_glibc(tmp_path):
+    """ul_atanf_pos, atan2f's reduction of |y / x|: every 1021st float of [0, inf] here, every one in
+    the exhaustive run (libm_pin.txt)."""
+    r = subprocess.run([_build(tmp_path), "atanpos", "1021"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout
+    assert " 0 of " in r.stdout
+
+
 def test_asinf_matches_glibc(tmp_path):
     """The twin-peaks detector's asinf (audio_driver.c:2211); exhaustive run in libm_pin.txt."""
     r = subprocess.run([_build(tmp_path), "asin", "127"], capture_output=True, text=True, timeout=120)

@@ -111,6 +111,11 @@ def main():
         cfg = U.default_config(filter_path=70, dmod_mode=U.DEMOD_SAM)
         lines.append(rx_line("C3 SAM P70 RX (PLL 2500/0.65/250, fade on)", cfg, C, N,
                              tiled(synth.am_iq, C, N), a.steps, a.warmup))
+    if "c3pipe" in want:                                 # C3 in the pipelined mode (A/B; not a default line)
+        C, N = 32768, 1024
+        cfg = U.default_config(filter_path=70, dmod_mode=U.DEMOD_SAM)
+        lines.append(rx_line("C3 SAM P70 RX (PLL 2500/0.65/250, fade on)", cfg, C, N,
+                             tiled(synth.am_iq, C, N), a.steps, a.warmup, pipelined=True))
     if "c3spec" in want:
         C, N, L = 32768, 1024, 1024
         s = torch.cuda.current_stream()

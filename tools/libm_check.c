@@ -3,6 +3,7 @@
  *   libm_check atan2 <count>     random + structured operand pairs
  *   libm_check asin <stride>     every stride-th float in [-1, 1] (and NaN operands past it)
  *   libm_check atan2x1 <stride>  every stride-th binary32 y (all signs) against atan2f(y, 1.0f)
+ *   libm_check atanpos <stride>  ul_atanf_pos (atan2f's reduction) on every stride-th float in [0, inf]
  * Prints mismatches (first 10) and a summary line; exit status 1 on any mismatch. */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -53,6 +54,21 @@ int main(int argc, char** argv)
                 }
             }
         printf("asinf: %ld of %ld arguments differ\n", bad, n);
+    }
+    else if (!strcmp(argv[1], "atanpos"))
+    {
+        const long stride = atol(argv[2]);
+        for (uint64_t u = 0; u <= 0x7f800000u; u += stride)
+        {
+            const float a = ul_asfloat((uint32_t)u);
+            const float r0 = atanf(a), r1 = ul_atanf_pos(a);
+            ++n;
+            if (ul_asuint(r0) != ul_asuint(r1))
+            {
+                if (bad++ < 10) printf("atanf(%a): glibc %a, ours %a\n", a, r0, r1);
+            }
+        }
+        printf("atanf(a >= 0): %ld of %ld arguments differ\n", bad, n);
     }
     else if (!strcmp(argv[1], "atan2x1"))
     {

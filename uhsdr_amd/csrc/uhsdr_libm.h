@@ -39,52 +39,42 @@ UHSDR_LIBM_FN float ul_asfloat(uint32_t u) { float f; memcpy(&f, &u, 4); return 
 UHSDR_LIBM_FN uint32_t ul_abstop12(float x) { return (ul_asuint(x) >> 20) & 0x7ff; }
 UHSDR_LIBM_FN uint64_t ul_asuint64(double f) { uint64_t u; memcpy(&u, &f, 8); return u; }
 UHSDR_LIBM_FN double ul_asdouble(uint64_t u) { double f; memcpy(&f, &u, 8); return f; }
-/* c ? a : b as a bit-mask blend.  clang emits a conditional operator with non-constant arms as
-   a branch diamond, and the ones the optimizer does not fold back become exec-masked regions
-   (separate basic blocks) on the GPU -- which keeps the scheduler from overlapping two PLL
-   samples -- or, for a chain over an index, a table load.  The blend is one v_cndmask. */
-UHSDR_LIBM_FN float ul_sel(int c, float a, float b)
-{
-    const uint32_t m = 0u - (uint32_t)(c != 0);
-    return ul_asfloat((ul_asuint(a) & m) | (ul_asuint(b) & ~m));
-}
-UHSDR_LIBM_FN double ul_seld(int c, double a, double b)
-{
-    const uint64_t m = 0ull - (uint64_t)(c != 0);
-    return ul_asdouble((ul_asuint64(a) & m) | (ul_asuint64(b) & ~m));
-}
+/* c ? a : b on operands already evaluated.  clang emits a conditional operator whose arms
+   compute something as a branch diamond, and the ones the optimizer does not fold back become
+   exec-masked regions (separate basic blocks) on the GPU -- which keeps the scheduler from
+   overlapping two PLL samples -- or, for a chain over an index, a table load.  As a function of
+   its evaluated parameters the diamond is empty and folds into one v_cndmask. */
+UHSDR_LIBM_FN float ul_sel(int c, float a, float b) { return c ? a : b; }
 
 /* ---- sincosf, |y| < 120 (the PLL phase is in [0, 2*pi)) ---- */
 typedef struct
 {
-    double sign[4];          /* sign of sine in quadrants 0..3 */
     double hpi_inv;          /* 2/pi * 2^24 (no round-to-int intrinsics on x86-64) */
     double hpi;              /* pi/2 */
     double c0, c1, s1, c2, s2, c3, s3, c4;
 } ul_sincos_t;
 
+/* __sincosf_table[0]; table[1] (quadrants 2 and 3) holds the same sine coefficients and the
+   cosine ones negated -- see ul_sincosf */
 #ifdef __HIPCC__
 __host__ __device__
 #endif
-static inline const ul_sincos_t* ul_sincosf_table(int k)
+static inline const ul_sincos_t* ul_sincosf_table(void)
 {
 #ifdef __HIPCC__
-    static __constant__ const ul_sincos_t t[2] = {
+    static __constant__ const ul_sincos_t t = {
 #else
-    static const ul_sincos_t t[2] = {
+    static const ul_sincos_t t = {
 #endif
-        { { 1.0, -1.0, -1.0, 1.0 }, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
-          0x1p+0, -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
-          0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16 },
-        { { 1.0, -1.0, -1.0, 1.0 }, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
-          -0x1p+0, 0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5,
-          0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16 },
+        0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+        0x1p+0, -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
+        0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16,
     };
-    return &t[k];
+    return &t;
 }
 
-/* sincosf.h sincosf_poly (FMA build); the quadrant swap as selects */
-UHSDR_LIBM_FN void ul_sincosf_poly(double x, double x2, const ul_sincos_t* p, int n, float* sinp, float* cosp)
+/* sincosf.h sincosf_poly (FMA build) before its quadrant swap */
+UHSDR_LIBM_FN void ul_sincosf_poly(double x, double x2, const ul_sincos_t* p, float* rsp, float* rcp)
 {
     const double x4 = x2 * x2;
     const double x3 = x2 * x;
@@ -95,35 +85,31 @@ UHSDR_LIBM_FN void ul_sincosf_poly(double x, double x2, const ul_sincos_t* p, in
     const double x6 = x4 * x2;
     const double s = fma(x3, p->s1, x);
     const double c = fma(x4, p->c2, c1);
-    const float rs = (float)fma(x5, s1, s);
-    const float rc = (float)fma(x6, c2, c);
-    *sinp = ul_sel(n & 1, rc, rs);                   /* quadrant swap */
-    *cosp = ul_sel(n & 1, rs, rc);
+    *rsp = (float)fma(x5, s1, s);
+    *rcp = (float)fma(x6, c2, c);
 }
 
 /* s_sincosf.c for |y| < 120 (callers guarantee the range; the Payne-Hanek branch for huge
    arguments is not needed by the PLL).  Branch-free: for |y| < pi/4 the reduction yields
    n = 0, x - 0*pi/2 = x (exact) and sign +1, i.e. exactly the small branch's polynomial call,
    so one path serves both and a wave's lanes never split between them; |y| < 2^-12 selects
-   (y, 1) at the end.  The quadrant's table is chosen by selects on its coefficients. */
+   (y, 1) at the end.  Quadrants 2 and 3 evaluate the cosine polynomial with every coefficient
+   negated (table[1]): round-to-nearest is symmetric and none of its partial sums is zero for
+   |x| <= pi/4, so that is exactly table 0's result with the sign flipped. */
 UHSDR_LIBM_FN void ul_sincosf(float y, float* sinp, float* cosp)
 {
     double x = y;
-    const ul_sincos_t* p0 = ul_sincosf_table(0);
-    const ul_sincos_t* p1 = ul_sincosf_table(1);
+    const ul_sincos_t* p = ul_sincosf_table();
     /* reduce_fast, !TOINT_INTRINSICS */
-    const double r = x * p0->hpi_inv;
+    const double r = x * p->hpi_inv;
     const int n = ((int32_t)r + 0x800000) >> 24;
-    x = fma(-(double)n, p0->hpi, x);
-    /* sign[n & 3] = +1, -1, -1, +1: negative when bit 1 of n + 1 is set */
-    const double s = ul_asdouble(0x3ff0000000000000ull | ((uint64_t)((n + 1) & 2) << 62));
-    ul_sincos_t q;
-    const int h = (n & 2) != 0;
-    q.c0 = ul_seld(h, p1->c0, p0->c0); q.c1 = ul_seld(h, p1->c1, p0->c1); q.s1 = ul_seld(h, p1->s1, p0->s1);
-    q.c2 = ul_seld(h, p1->c2, p0->c2); q.s2 = ul_seld(h, p1->s2, p0->s2); q.c3 = ul_seld(h, p1->c3, p0->c3);
-    q.s3 = ul_seld(h, p1->s3, p0->s3); q.c4 = ul_seld(h, p1->c4, p0->c4);
-    float sv, cv;
-    ul_sincosf_poly(x * s, x * x, &q, n, &sv, &cv);
+    x = fma(-(double)n, p->hpi, x);
+    /* x * sign[n & 3], sign = +1, -1, -1, +1: negative when bit 1 of n + 1 is set */
+    const double xs = ul_asdouble(ul_asuint64(x) ^ ((uint64_t)((n + 1) & 2) << 62));
+    float rs, rc;
+    ul_sincosf_poly(xs, x * x, p, &rs, &rc);
+    rc = ul_asfloat(ul_asuint(rc) ^ ((uint32_t)(n & 2) << 30));     /* table[1] */
+    const float sv = ul_sel(n & 1, rc, rs), cv = ul_sel(n & 1, rs, rc);   /* quadrant swap */
     const int tiny = ul_abstop12(y) < ul_abstop12(0x1p-12f);
     *sinp = ul_sel(tiny, y, sv);
     *cosp = ul_sel(tiny, 1.0f, cv);
@@ -169,36 +155,61 @@ UHSDR_LIBM_FN float ul_atanf(float x)
     return r;
 }
 
+/* ul_atanf for a >= +0 (atan2f's |y / x|), NaN operands left to the caller.  fdlibm's four
+ * reductions are (ka a - kb) / (ka + kb a) with ka = 2, 1, 1, 0 and kb = 1, 1, 1.5, 1: ka a is
+ * exact, so the numerator is one fused operation with fdlibm's rounding, and kb a + ka rounds
+ * like fdlibm's denominators (1.5f * a, then the sum; the other products are exact). */
+UHSDR_LIBM_FN float ul_atanf_pos(float a)
+{
+    const float atanhi[4] = { 4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f };
+    const float atanlo[4] = { 5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f };
+    const float aT[11] = { 3.3333334327e-01f, -2.0000000298e-01f, 1.4285714924e-01f, -1.1111110449e-01f,
+                           9.0908870101e-02f, -7.6918758452e-02f, 6.6610731184e-02f, -5.8335702866e-02f,
+                           4.9768779427e-02f, -3.6531571299e-02f, 1.6285819933e-02f };
+    const uint32_t ia = ul_asuint(a);
+    const int small = ia < 0x3ee00000, lo2 = ia < 0x3f980000, i0 = ia < 0x3f300000, i2 = ia < 0x401c0000;
+    const float ka = ul_sel(i0, 2.0f, ul_sel(i2, 1.0f, 0.0f));
+    const float kb = ul_sel(!lo2 && i2, 1.5f, 1.0f);
+    const float num = fmaf(ka, a, -kb);
+    const float den = kb * a + ka;
+    const float hi = ul_sel(lo2, ul_sel(i0, atanhi[0], atanhi[1]), ul_sel(i2, atanhi[2], atanhi[3]));
+    const float lo = ul_sel(lo2, ul_sel(i0, atanlo[0], atanlo[1]), ul_sel(i2, atanlo[2], atanlo[3]));
+    const float xr = ul_sel(small, a, num / den);
+    const float z = xr * xr;
+    const float w = z * z;
+    const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const float s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    const float t = xr * (s1 + s2);
+    float r = ul_sel(small, xr - t, hi - ((t - lo) - xr));
+    r = ul_sel(ia < 0x31000000, a, r);                                  /* a < 2^-29 */
+    return ul_sel(ia >= 0x4c000000, atanhi[3] + atanlo[3], r);         /* a >= 2^25 */
+}
+
 UHSDR_LIBM_FN float ul_atan2f(float y, float x)
 {
     const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f,
                 pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
     const int32_t hx = (int32_t)ul_asuint(x), hy = (int32_t)ul_asuint(y);
     const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
-    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);      /* 2*sign(x) + sign(y) */
     /* Branch-free: fdlibm's main path (e_atan2f.c, the k / atanf / quadrant tail) runs for
-     * every operand pair and the rare operands (NaN, zeros, infinities) select their results
-     * after it, lowest precedence first, so the SAM PLL's per-sample chain stays one basic
-     * block and consecutive samples' chains can interleave.  x = 1.0 (fdlibm: atanf(y)) needs
-     * no case of its own: y / 1 = y, atanf is odd and the |y/x| > 2^26 override is skipped for
-     * it -- pinned for every binary32 y by tools/libm_check.c "atan2x1". */
+     * every operand pair and the operands it does not cover select their results after it,
+     * lowest precedence first, so the SAM PLL's per-sample chain stays one basic block.
+     * The main path already gives fdlibm's special results for y = +-0 with x != 0 (z = 0) and
+     * for x = +-inf with y finite (y / x = +-0); x = 1.0 (fdlibm: atanf(y)) needs no case either:
+     * y / 1 = y, atanf is odd and the |y/x| > 2^26 override is skipped for it.  Pinned for
+     * every binary32 y at x = 1 (tools/libm_check.c "atan2x1") and on random and special pairs. */
     const int32_t k = (iy - ix) >> 23;
-    float z = ul_atanf(fabsf(y / x));
+    float z = ul_atanf_pos(fabsf(y / x));
     z = ul_sel(hx < 0 && k < -26, 0.0f, z);                 /* |y|/x < -2^26 */
     z = ul_sel(k > 26 && hx != 0x3f800000, pi_o_2 + 0.5f * pi_lo, z);   /* |y/x| > 2^26 */
-    const float zm = z - pi_lo;
-    const float r2 = pi - zm, r3 = zm - pi;
-    const float r1 = ul_asfloat(ul_asuint(z) ^ 0x80000000u);
-    float r = ul_sel(m & 2, ul_sel(m & 1, r3, r2), ul_sel(m & 1, r1, z));
-    const float pm_pi = ul_sel(m & 1, -pi - tiny, pi + tiny);   /* +-pi by sign(y) */
-    const float pm_pi_o_2 = ul_sel(hy < 0, -pi_o_2 - tiny, pi_o_2 + tiny);
-    r = ul_sel(iy == 0x7f800000, pm_pi_o_2, r);             /* y = +-inf, x finite */
-    const float inf_inf = ul_sel(m & 2, ul_sel(m & 1, -3.0f * pi_o_4 - tiny, 3.0f * pi_o_4 + tiny),
-                                 ul_sel(m & 1, -pi_o_4 - tiny, pi_o_4 + tiny));
-    const float inf_fin = ul_sel(m & 2, pm_pi, ul_sel(m & 1, -0.0f, 0.0f));
-    r = ul_sel(ix == 0x7f800000, ul_sel(iy == 0x7f800000, inf_inf, inf_fin), r);   /* x = +-inf */
-    r = ul_sel(ix == 0, pm_pi_o_2, r);                      /* x = +-0 */
-    r = ul_sel(iy == 0, ul_sel(m & 2, pm_pi, y), r);        /* y = +-0 */
+    /* fdlibm's quadrants: z, -z, pi - (z - pi_lo), (z - pi_lo) - pi; z and pi - (z - pi_lo) are
+       positive and round-to-nearest is symmetric, so the sign of y goes on last */
+    float r = copysignf(ul_sel(hx < 0, pi - (z - pi_lo), z), y);
+    r = ul_sel(iy == 0x7f800000,                           /* y = +-inf */
+               copysignf(ul_sel(ix == 0x7f800000, ul_sel(hx < 0, 3.0f * pi_o_4 + tiny, pi_o_4 + tiny),
+                                pi_o_2 + tiny), y), r);
+    r = ul_sel(ix == 0,                                     /* x = +-0 */
+               ul_sel(iy == 0, ul_sel(hx < 0, copysignf(pi + tiny, y), y), copysignf(pi_o_2 + tiny, y)), r);
     r = ul_sel(ix > 0x7f800000 || iy > 0x7f800000, x + y, r);   /* NaN */
     return r;
 }

@@ -1070,8 +1070,10 @@ struct AgcStage
         cmax[AGC_Q - 2] = pmax;
     }
 
-    // which[0]: the prep() side (ring, averages, DC state), which[1]: the recur() side
-    __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l, const bool (&which)[2] = { true, true })
+    // which[0]: the prep() side (ring, averages, DC state), which[1]: the recur() side;
+    // wold_out false: the DC state belongs to another role (rx_back's audio role with DM)
+    __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l, const bool (&which)[2] = { true, true },
+                                          bool wold_out = true)
     {
         if (!l.live) return;
         const int C = l.C, c = l.c;
@@ -1086,7 +1088,7 @@ struct AgcStage
         if (!which[0]) return;
         a.s.agc[3 * C + c] = fast_bavg;
         a.s.agc[4 * C + c] = hang_bavg;
-        a.s.agc[5 * C + c] = wold[0];
+        if (wold_out) a.s.agc[5 * C + c] = wold[0];
 #pragma unroll
         for (int i = 0; i < AGC_Q - 1; ++i) a.s.agc[(6 + i) * C + c] = cmax[i];
         a.s.agc[(5 + AGC_Q) * C + c] = leave_last[0];
@@ -1285,9 +1287,13 @@ __device__ __forceinline__ void back_store4(const BackArgs& a, const BackLane& l
 
 // ---- demod stage: AudioDriver_DemodSAM (audio_driver.c:1990-2166): AM envelope
 //      (:2008-2020) or the SAM PLL (:2021-2147), fade leveler (:1911-1923) ----
-template <int L, int DM>
+// LEV false (rx_back, DM_SAM): the fade leveler runs in the pre role (FadeStage) on the
+// demodulated audio and corr0 (step's `corr`), which owns its state; the PLL role is the wave
+// pipeline's longest, and the leveler is not part of its recursion
+template <int L, int DM, bool LEV = true>
 struct DemodStage
 {
+    static_assert(LEV || DM == DM_SAM, "the leveler leaves the demod role only for DM_SAM");
     static constexpr int NDC = BLK / L;
     static constexpr bool SB = DM == DM_SAM_SB || DM == DM_SAM_ST;   // allpass sideband selector
     static constexpr int NA = SB ? 24 : 1;                // allpass delay lines (sam_data.a..d)
@@ -1296,6 +1302,7 @@ struct DemodStage
     float mtauR, onem_mtauR, mtauI, onem_mtauI;
     float g1, g2, omega_min, omega_max;
     float phs, omega2, fil_out, dsI, dsQ, dc27, dc_insert;
+    float corr;                                           // !LEV: the last step's corr0
     float ap[4][NA];
     float inext[NDC], qnext[NDC];
     float xi[NDC], xq[NDC];
@@ -1405,9 +1412,11 @@ struct DemodStage
             {
                 audio = corr0;
             }
+            corr = corr0;
             // The whole SAM step is one basic block (fade leveler and phase wrap as bit-mask
             // selects, ul_sel; ul_sincosf / ul_atan2f branch-free): sample n + 1's phase needs only fil_out(n - 1), so the
             // scheduler overlaps two samples' sincosf -> atan2f chains.
+            if (LEV)
             {
                 // AudioDriver_FadeLeveler(0, ...), audio_driver.c:1911-1923
                 const float d27 = mtauR * dc27 + onem_mtauR * audio;
@@ -1432,11 +1441,15 @@ struct DemodStage
             omega2 = ul_sel(omega2 < omega_min, omega_min, ul_sel(omega2 > omega_max, omega_max, omega2));
             fil_out = g1 * phzerror + omega2;
             phs = phs + del_out;
-            // the reference's while loops (in double: 2.0 * PI is a double) run at most once each:
+            // The reference's while loops (in double: 2.0 * PI is a double) run at most once each:
             // |del_out| <= g1 * pi + omega_max < 2 pi for the plan's parameter ranges
-            // (uhsdr_setup.c), so phs + del_out stays inside (-2 pi, 4 pi)
-            phs = ul_sel((double)phs >= two_pi, (float)((double)phs - two_pi), phs);
-            phs = ul_sel((double)phs < 0.0, (float)((double)phs + two_pi), phs);
+            // (uhsdr_setup.c), so phs + del_out stays inside (-2 pi, 4 pi).  2 pi is a binary32
+            // value T, so the comparisons are exact in binary32; phs - T is exact (Sterbenz, phs in
+            // [T, 2T)); phs + T for phs in (-T, 0) is exact in double unless |phs| < 2^-27, where
+            // both roundings give T -- so binary32 arithmetic returns the reference's value.
+            const float two_pi_f = (float)two_pi;
+            phs = ul_sel(phs >= two_pi_f, phs - two_pi_f, phs);
+            phs = ul_sel(phs < 0.0f, phs + two_pi_f, phs);
         }
         return audio;
     }
@@ -1447,7 +1460,7 @@ struct DemodStage
         const int C = l.C, c = l.c;
         a.s.sam[0 * C + c] = phs; a.s.sam[1 * C + c] = omega2; a.s.sam[2 * C + c] = fil_out;
         a.s.sam[3 * C + c] = dsI; a.s.sam[4 * C + c] = dsQ;
-        a.s.sam[5 * C + c] = dc27; a.s.sam[6 * C + c] = dc_insert;
+        if (LEV) { a.s.sam[5 * C + c] = dc27; a.s.sam[6 * C + c] = dc_insert; }
         if (DM == DM_SAM_ST) { a.s.sam[103 * C + c] = dc27_1; a.s.sam[104 * C + c] = dc_insert_1; }
         if (SB)
         {
@@ -1456,6 +1469,39 @@ struct DemodStage
 #pragma unroll
                 for (int j = 0; j < NA; ++j) a.s.sam[(7 + f * 24 + j) * C + c] = ap[f][j];
         }
+    }
+};
+
+// ---- fade leveler of the SAM demodulator (AudioDriver_FadeLeveler(0, ...), audio_driver.c:
+//      1911-1923) as its own stage: rx_back's pre role runs it for DM_SAM (DemodStage LEV false),
+//      with the state DemodStage keeps otherwise (BackState.sam rows 5, 6) ----
+struct FadeStage
+{
+    bool fade;
+    float mtauR, onem_mtauR, mtauI, onem_mtauI, dc27, dc_insert;
+
+    __device__ __forceinline__ void load(const BackArgs& a, const BackLane& l)
+    {
+        const uhsdr_rx_plan* __restrict__ P = a.plan;
+        fade = P->fade_leveler;
+        mtauR = P->fade_mtauR; onem_mtauR = P->fade_onem_mtauR;
+        mtauI = P->fade_mtauI; onem_mtauI = P->fade_onem_mtauI;
+        dc27 = a.s.sam[5 * l.C + l.cl]; dc_insert = a.s.sam[6 * l.C + l.cl];
+    }
+
+    __device__ __forceinline__ float step(float audio, float corr)
+    {
+        const float d27 = mtauR * dc27 + onem_mtauR * audio;
+        const float dci = mtauI * dc_insert + onem_mtauI * corr;
+        const float lev = audio + dci - d27;
+        dc27 = ul_sel(fade, d27, dc27); dc_insert = ul_sel(fade, dci, dc_insert);
+        return ul_sel(fade, lev, audio);
+    }
+
+    __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l)
+    {
+        if (!l.live) return;
+        a.s.sam[5 * l.C + l.c] = dc27; a.s.sam[6 * l.C + l.c] = dc_insert;
     }
 };
 
@@ -1493,14 +1539,20 @@ __device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
     constexpr int NDC = BLK / L;
-    DemodStage<L, DM> s;
+    constexpr bool LEV = DM != DM_SAM;                   // DM_SAM: the leveler runs in the pre role
+    DemodStage<L, DM, LEV> s;
     s.load(a, l);
     s.fetch(a, l, 0);
     BACK_ROLE_LOOP(0)
         s.begin(a, l, call);
         float* dout = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
+        float* cout = lds.prep + (call & 1) * NDC * BACK_CH + l.lane;   // corr0 (prep is free with DM)
 #pragma unroll
-        for (int m = 0; m < NDC; ++m) dout[m * BACK_CH] = s.step(m);
+        for (int m = 0; m < NDC; ++m)
+        {
+            dout[m * BACK_CH] = s.step(m);
+            if (!LEV) cout[m * BACK_CH] = s.corr;
+        }
     BACK_ROLE_END
     s.store(a, l);
 }
@@ -1531,6 +1583,8 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
         ag.load(a, l, A);
         ag.fetch(a, l, 0);
     }
+    FadeStage fl;
+    if (DM == DM_SAM) fl.load(a, l);
     BACK_ROLE_LOOP(DM ? 1 : 0)
         float xin[NDC];
         if (DM)
@@ -1538,6 +1592,15 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
             const float* di = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
 #pragma unroll
             for (int m = 0; m < NDC; ++m) xin[m] = di[m * BACK_CH];
+            if (DM == DM_SAM)
+            {
+                const float* ci = lds.prep + (call & 1) * NDC * BACK_CH + l.lane;
+                float cr[NDC];
+#pragma unroll
+                for (int m = 0; m < NDC; ++m) cr[m] = ci[m * BACK_CH];
+#pragma unroll
+                for (int m = 0; m < NDC; ++m) xin[m] = fl.step(xin[m], cr[m]);
+            }
         }
         else
             in.begin(a, l, call, xin);
@@ -1570,6 +1633,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
         }
     BACK_ROLE_END
     s.store(l, a.s.pre);
+    if (DM == DM_SAM) fl.store(a, l);
     if (prep) ag.store(a, l, { true, false });
 }
 
@@ -1611,10 +1675,12 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
         else
         {
         s.begin(a, l, call);
-        if (back_agc_split(DM) && !A.remove_dc)
+        if ((back_agc_split(DM) && !A.remove_dc) || DM)
         {
-            // volts to the audio role through the demod role's (unused) hand-off buffer
-            float* vo = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
+            // volts to the audio role, which applies the gain (and with DM the DC removal after
+            // it): through the demod role's hand-off buffer (unused without DM), or with DM the
+            // second slab of `prep` (the first carries the demod role's corr0)
+            float* vo = (DM ? lds.prep + 2 * NDC * BACK_CH : lds.dem) + (call & 1) * NDC * BACK_CH + l.lane;
 #pragma unroll
             for (int m = 0; m < NDC; ++m)
             {
@@ -1632,7 +1698,7 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
         s.end(l);
         }
     BACK_ROLE_END
-    s.store(a, l, { !prep, true });
+    s.store(a, l, { !prep, true }, !DM);
 }
 
 template <int L, int PH, int W, int DM>
@@ -1644,21 +1710,34 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
     s.load(a, l);
     const uhsdr_agc_plan A = a.plan->agc;
     const bool agc_on = A.mode != 5;
+    // DM: the AGC's DC removal (audio_agc.c:575-593) runs here after the gain, with its state
+    float wold = DM ? a.s.agc[5 * l.C + l.cl] : 0.0f;
+    const bool dc = DM && agc_on && A.remove_dc;
     BACK_ROLE_LOOP(DM ? 3 : 2)
         const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
         float* mo = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
         float x[NDC];
 #pragma unroll
         for (int m = 0; m < NDC; ++m) x[m] = ai[m * BACK_CH];
-        if (back_agc_split(DM) && agc_on && !A.remove_dc)
+        if (agc_on && (DM || (back_agc_split(DM) && !A.remove_dc)))
         {
             // the AGC role's gain step (AgcStage::gain) on its delayed samples
-            const float* vi = lds.dem + (call & 1) * NDC * BACK_CH + l.lane;
+            const float* vi = (DM ? lds.prep + 2 * NDC * BACK_CH : lds.dem) + (call & 1) * NDC * BACK_CH + l.lane;
             float v[NDC];
 #pragma unroll
             for (int m = 0; m < NDC; ++m) v[m] = vi[m * BACK_CH];
 #pragma unroll
             for (int m = 0; m < NDC; ++m) x[m] = x[m] * AgcStage<L, W, 1>::gain(v[m], A);
+            if (dc)
+            {
+#pragma unroll
+                for (int m = 0; m < NDC; ++m)
+                {
+                    const float w = (float)((double)x[m] + (double)wold * 0.9999);
+                    x[m] = w - wold;
+                    wold = w;
+                }
+            }
         }
 #pragma unroll
         for (int m = 0; m < NDC; ++m)
@@ -1671,6 +1750,7 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
         s.end(a, l, call);
     BACK_ROLE_END
     s.store(a, l);
+    if (DM && l.live) a.s.agc[5 * l.C + l.c] = wold;
 }
 
 // anti-alias lattice at 48 ksps
@@ -1745,6 +1825,12 @@ __global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
     __builtin_amdgcn_s_setprio(3);
     // readfirstlane makes the role provably wave-uniform (scalar branches)
     const int role = __builtin_amdgcn_readfirstlane(threadIdx.x / BACK_CH) - (DM ? 1 : 0);
+#ifndef UHSDR_ROLE_PRIO
+#define UHSDR_ROLE_PRIO 1
+#endif
+    // AM / SAM: the demod role (the per-sample PLL recursion) is the pipeline's longest; the other
+    // roles, sharing its SIMD, issue after it (still above a concurrent rx_front)
+    if (UHSDR_ROLE_PRIO && DM && role >= 0) __builtin_amdgcn_s_setprio(2);
     if (role < 0)
         rx_back_demod<L, DM>(a, lds);
     else if (role == 0)

@@ -1896,7 +1896,9 @@ __device__ __forceinline__ void fused_store_call(const BackArgs& a, const BackLa
 // per-sample code carries no uniform branches; the AGC's DC removal is on for AM / SAM (compile-
 // time for the demodulating bodies, a select behind rx_notch)
 // LDS_IN (rx_chain): channel group grp, input from the wave's LDS hand-off adl
-template <int PRE, int AA, int L, int PH, int W, int DM, bool AGC_ON, bool CW, bool LDS_IN = false, bool DC = true>
+// B1S: biquad_1's taps stay in SGPRs (it runs once per decimated sample; 20 VGPRs freed)
+template <int PRE, int AA, int L, int PH, int W, int DM, bool AGC_ON, bool CW, bool LDS_IN = false, bool DC = true,
+          bool B1S = false>
 __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys, int grp, const float* adl = nullptr)
 {
     const BackLane l(a, grp);
@@ -1928,7 +1930,7 @@ __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys, in
     if (AA > 0) { to_vgpr(aa.k); to_vgpr(aa.v); }
     to_vgpr(ou.b2);
     ou.lo = to_vgpr(ou.lo);
-    to_vgpr(au.b1);
+    if (!B1S) to_vgpr(au.b1);
 #endif
     ag.agc_on = AGC_ON;
     if (DM != DM_NONE) ag.dc = true;
@@ -1983,10 +1985,23 @@ __device__ __forceinline__ void back_fused_agc(const BackArgs& a, float* ys, int
     else back_fused_body<PRE, AA, L, PH, W, DM, true, CW, LDS_IN, DC>(a, ys, grp, adl);
 }
 
-template <int PRE, int AA, int L, int PH, int W, int DM, bool DC = true>
-__global__ void __launch_bounds__(BACK_CH) __attribute__((amdgpu_waves_per_eu(DM == DM_SAM_SB ? 1 : UHSDR_FUSED_WAVES))) rx_back_fused(BackArgs a)
+// FORM 0: the launch's AGC / CW flags dispatched inside the kernel (its registers are the
+// largest body's: 199 VGPRs at P48, 2 waves per SIMD).  FORM 1: AGC on, CW off only (the SSB /
+// DIGI default, the north-star chain), one body with biquad_1's taps in SGPRs: 160 VGPRs at P48,
+// no scratch, 3 waves per SIMD.
+// (the compiler's resource report: the 24 ksps bodies with a pre-filter lattice need 207-220
+// VGPRs at FORM 0 and spill to scratch at 3 waves, so they keep 2)
+__host__ __device__ constexpr int fused1_waves(int pre, int L) { return (L == 2 && pre > 0) ? 2 : 3; }
+template <int PRE, int AA, int L, int PH, int W, int DM, bool DC = true, int FORM = 0>
+__global__ void __launch_bounds__(BACK_CH)
+__attribute__((amdgpu_waves_per_eu(FORM == 1 ? fused1_waves(PRE, L) : DM == DM_SAM_SB ? 1 : UHSDR_FUSED_WAVES))) rx_back_fused(BackArgs a)
 {
     __shared__ float ys[BACK_CH * FUSED_YPITCH];
+    if constexpr (FORM == 1)
+    {
+        back_fused_body<PRE, AA, L, PH, W, DM, true, false, false, DC, true>(a, ys, blockIdx.x);
+        return;
+    }
     if constexpr (L == 4)
     {
         if (a.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM, true, false, DC>(a, ys, blockIdx.x); return; }
@@ -2492,12 +2507,19 @@ typedef void (*chain_fn)(FrontArgs, BackArgs, int);
 struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; front_fn fn_fma; int st; };
 // fused_nodc: rx_back_fused without the AGC's DC removal (the demodulator-free back end when the
 // AGC does not remove DC: SSB / CW / DIGI); the same kernel as `fused` for the demodulators
-struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; back_fn fused_nodc; };
+// fused_ssb: fused_nodc for a launch with the AGC on and the CW decoder off (FORM 1), or null
+struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; back_fn fused_nodc; back_fn fused_ssb; };
 template <int PRE, int AA, int L, int PH, int W, int DM>
 constexpr back_fn fused_nodc_of()
 {
     if constexpr (DM == DM_NONE) return rx_back_fused<PRE, AA, L, PH, W, DM, false>;
     else return rx_back_fused<PRE, AA, L, PH, W, DM>;
+}
+template <int PRE, int AA, int L, int PH, int W, int DM>
+constexpr back_fn fused_ssb_of()
+{
+    if constexpr (DM == DM_NONE) return rx_back_fused<PRE, AA, L, PH, W, DM, false, 1>;
+    else return nullptr;
 }
 // rx_chain instances: a front family (t1, t2, m, decim_first, R = 8) with a DM_NONE back end
 struct ChainVariant { int t1, t2, m, decim_first, R, pre, aa, L, ph, w; chain_fn fn, fn_fma; };
@@ -2514,7 +2536,7 @@ struct NotchVariant { int L, dm; back_fn fn; };
 // tools/isa_stats.sh: only the P48 SSB instances, so one kernel's ISA compiles in seconds
 static const FrontVariant kFront[] = { FRONT_V(89, 43, 4, false, 8) };
 #define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm>, \
-    fused_nodc_of<pre, aa, L, ph, w, dm>() }
+    fused_nodc_of<pre, aa, L, ph, w, dm>(), fused_ssb_of<pre, aa, L, ph, w, dm>() }
 static const BackVariant kBack[] = { BACK_V(10, 6, 4, 1, 49, DM_NONE) };
 static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6>, nullptr };
 static const BackVariant kBackStereo[] = { { 10, 6, 4, 1, 49, DM_NONE, nullptr, nullptr } };
@@ -2540,7 +2562,7 @@ static const FrontVariant kFront[] = {
 #undef FRONT_ST
 
 #define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm>, \
-    fused_nodc_of<pre, aa, L, ph, w, dm>() }
+    fused_nodc_of<pre, aa, L, ph, w, dm>(), fused_ssb_of<pre, aa, L, ph, w, dm>() }
 static const BackVariant kBack[] = {
     // SSB / CW / DIGI
     BACK_V(10, 6, 4, 1, 49, DM_NONE), BACK_V(10, 0, 4, 4, 49, DM_NONE), BACK_V(0, 0, 2, 8, 97, DM_NONE),
@@ -2967,6 +2989,17 @@ static int resolve_schedule(const uhsdr_rx_s* h, int want)
     return -1;
 }
 
+// the fused back-end kernel of a launch: FORM 1 (one body, 3 waves per SIMD) when the AGC is on,
+// no DC removal and no CW decoder front end (only the L == 4 bodies carry one); else the kernel
+// that dispatches the AGC / CW flags itself
+static back_fn fused_back_fn(const uhsdr_rx_s* h)
+{
+    const BackVariant* bv = h->bv;
+    if (h->plan.agc.remove_dc || !bv->fused_nodc) return bv->fused;
+    if (bv->fused_ssb && h->plan.agc.mode != 5 && (!h->plan.cw_enabled || bv->L != 4)) return bv->fused_ssb;
+    return bv->fused_nodc;
+}
+
 static size_t back_lds(const uhsdr_rx_s* h)
 {
     if (h->bv->dm == DM_FM) return sizeof(float) * (size_t)BACK_CH * 2 * (BLK + 1);
@@ -3384,8 +3417,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             HIPCHK(hipGetLastError());
         }
         const bool fused = h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo;
-        const back_fn bfn = fused ? (h->plan.agc.remove_dc || !h->bv->fused_nodc ? h->bv->fused : h->bv->fused_nodc)
-                                  : h->bv->fn;
+        const back_fn bfn = fused ? fused_back_fn(h) : h->bv->fn;
         const dim3 bgrid((h->C + BACK_CH - 1) / BACK_CH), bblock(fused ? BACK_CH : back_roles(h->bv->dm) * BACK_CH);
         const size_t blds = fused ? 0 : back_lds(h);
         // pipelined: the group's last rx_back records ev_back[grp] as it completes

@@ -115,7 +115,21 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(4))) v2f ctaps2_t;
 __device__ __forceinline__ ctaps2_t* as_taps2(const float* p) { return (ctaps2_t*)p; }
 
-template <int T, int R, int M, bool F = false>
+// Padded pair window (pass 1 of the one- and two-channel-per-wave front shapes, R = 8 outputs per
+// lane): PB floats after every 8 pairs.  Lane bases then lie 16 + PB floats apart, so the 16 lanes
+// of a ds_read_b128 group hit 16 distinct bank quads at PB = 4 (20-float stride) instead of 4 of
+// them at 16 floats (one channel: 74 % of the front's LDS cycles were conflicts, PMC r03).  A
+// register-window read (2 pairs, even pair index) never straddles a pad, so its offset is the lane
+// base plus a compile-time constant.
+template <int PB>
+__host__ __device__ constexpr int pwin_off(int i) { return 2 * i + PB * (i >> 3); }
+// the front's pass-1 padding (floats per 8 pairs) for a family: R outputs per lane, decimate-first,
+// decimation M (1: FM)
+__host__ __device__ constexpr int front_pad1(int R, bool decim_first, int M) { return R == 8 && (decim_first || M == 1) ? 4 : 0; }
+
+// PB: the window's pad floats per 8 pairs (pwin_off); win is the lane's first window pair, which
+// starts an 8-pair block when PB > 0
+template <int T, int R, int M, bool F = false, int PB = 0>
 __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&acc)[R])
 {
     constexpr int WA = (M * (R - 1) + 8 + 7) & ~7;   // window pairs in registers
@@ -127,7 +141,7 @@ __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&
 #pragma unroll
     for (int j = 0; j < WA; j += 2)
     {
-        const vf4 v = *(const vf4*)(win + 2 * j);
+        const vf4 v = *(const vf4*)(win + pwin_off<PB>(j));
         w[j] = v.xy; w[j + 1] = v.zw;
     }
     // unrolled by the rotation period, the window slide is pure register renaming
@@ -141,7 +155,8 @@ __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&
 #pragma unroll
         for (int q = 0; q < 8; q += 2)
         {
-            const vf4 v = *(const vf4*)(win + 2 * (8 * ch + WA + q));
+            // pair 8 ch + WA + q: block ch + (WA + q) / 8 (WA is a multiple of 8, q < 8)
+            const vf4 v = *(const vf4*)(win + (16 + PB) * ch + pwin_off<PB>(WA + q));
             nw[q] = v.xy; nw[q + 1] = v.zw;
         }
 #pragma unroll
@@ -447,7 +462,8 @@ __device__ __forceinline__ void group_load_prow(const float* row, int c0, int nl
 }
 
 // float4 q of the group's rows is channel q / hp4, pairs 2 (q % hp4) .. + 1 of its window
-template <int T, int HQM>
+// PB: padded window (pwin_off)
+template <int T, int PB = 0, int HQM>
 __device__ __forceinline__ void group_fill_prow(float* smem, int LW, const float* row, int c0, int cpw, int nlive,
                                                 int lane, const vf4 (&buf)[HQM])
 {
@@ -457,38 +473,40 @@ __device__ __forceinline__ void group_fill_prow(float* smem, int LW, const float
     for (int i = 0; i < HQ; ++i)
     {
         const int q = lane + FRONT_WAVE_L * i;
-        if (q < nq) *(vf4*)(smem + (q / hp4) * LW + 4 * (q % hp4)) = buf[i];
+        if (q < nq) *(vf4*)(smem + (q / hp4) * LW + pwin_off<PB>(2 * (q % hp4))) = buf[i];
     }
     const vf4* h = (const vf4*)(row + (size_t)c0 * (hp4 * 4));
     const int qmax = nlive * hp4 - 1;
     for (int q = lane + FRONT_WAVE_L * HQ; q < nq; q += FRONT_WAVE_L)
-        *(vf4*)(smem + (q / hp4) * LW + 4 * (q % hp4)) = h[q < qmax ? q : qmax];
+        *(vf4*)(smem + (q / hp4) * LW + pwin_off<PB>(2 * (q % hp4))) = h[q < qmax ? q : qmax];
 }
 
 // the next call's pair rows: window pairs nnew .. nnew + hist_stride(T) - 1 of each channel
-template <int T>
+template <int T, int PB = 0>
 __device__ __forceinline__ void group_store_prow(const float* smem, int LW, float* row, int c0, int nlive, int lane, int nnew)
 {
     constexpr int hp4 = hist_p4(T);
     vf4* h = (vf4*)(row + (size_t)c0 * (hp4 * 4));
     for (int q = lane; q < nlive * hp4; q += FRONT_WAVE_L)
-        h[q] = *(const vf4*)(smem + (q / hp4) * LW + 2 * nnew + 4 * (q % hp4));
+        h[q] = *(const vf4*)(smem + (q / hp4) * LW + pwin_off<PB>(nnew + 2 * (q % hp4)));
 }
 
 // new samples of one channel's window (the lane's own NV values).  No zero tail: the windows of
 // a wave sit lw floats apart and the register-window FIRs' over-read (at most FRONT_TAIL samples
 // past the data, never used in a product) lands in the next channel's window, or, for the last
 // one, in the slack the LDS allocation adds after the windows.
+// PB: padded window (pwin_off); two pairs at an even index never straddle a pad
+template <int PB = 0>
 __device__ __forceinline__ void window_new2(float* W, int T, bool act, int b, const v2f* vals, int NV)
 {
     if (act)
     {
-        float* d = W + 2 * (T - 1 + b * NV);
+        const int i0 = T - 1 + b * NV;
         if (((T - 1) & 1) == 0)                           // 16-byte aligned: two pairs per store
             for (int j = 0; j < NV; j += 2)
-                *(vf4*)(d + 2 * j) = vf4{ vals[j].x, vals[j].y, vals[j + 1].x, vals[j + 1].y };
+                *(vf4*)(W + pwin_off<PB>(i0 + j)) = vf4{ vals[j].x, vals[j].y, vals[j + 1].x, vals[j + 1].y };
         else
-            for (int j = 0; j < NV; ++j) *(v2f*)(d + 2 * j) = vals[j];
+            for (int j = 0; j < NV; ++j) *(v2f*)(W + pwin_off<PB>(i0 + j)) = vals[j];
     }
 }
 
@@ -682,14 +700,15 @@ static inline bool front_lane_interleaved(int l, int nb, int& g, int& b)
 
 // modeled LDS-array cycles of one front wave's window traffic at pitch lw.  Pass 1: a FIR pair
 // over {x0, x1} (T1 taps, R outputs per lane, new pairs at 2 (T1-1)), lane map lm.
-static inline int front_lds_pass1(int lw, const uint16_t* lm, int cpw, int T1, int R)
+static inline int front_lds_pass1(int lw, const uint16_t* lm, int cpw, int T1, int R, int pb = 0)
 {
+    auto off = [&](int i) { return 2 * i + pb * (i >> 3); };     // pwin_off
     int addr[64], cycles = 0;
     // new samples (R pairs per lane: ds_write_b128 two pairs at a time when aligned)
     for (int l = 0; l < 64; ++l)
     {
         const int g = lm[l] >> 8, b = lm[l] & 0xff;
-        addr[l] = g < cpw ? g * lw + 2 * (T1 - 1 + b * R) : -1;
+        addr[l] = g < cpw ? g * lw + off(T1 - 1 + b * R) : -1;
     }
     cycles += lds_op_cycles(((T1 - 1) & 1) ? LDS_W64 : LDS_W128, addr) * (((T1 - 1) & 1) ? R : R / 2);
     // reads (ds_read_b128, every one at the same bank phase): the register window's first WA
@@ -698,7 +717,7 @@ static inline int front_lds_pass1(int lw, const uint16_t* lm, int cpw, int T1, i
     for (int l = 0; l < 64; ++l)
     {
         const int g = lm[l] >> 8, b = lm[l] & 0xff;
-        addr[l] = g < cpw ? g * lw + 2 * b * R : -1;
+        addr[l] = g < cpw ? g * lw + off(b * R) : -1;
     }
     return cycles + lds_op_cycles(LDS_R128, addr) * (WA / 2 + (T1 / 8) * 4);
 }

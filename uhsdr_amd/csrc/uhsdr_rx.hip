@@ -276,6 +276,9 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
     constexpr int RD = R / M;                        // decimated samples per lane
     constexpr int HQ1 = hist_qp(T1), HQ2 = hist_q(T2 > 0 ? T2 : 1), HQP2 = hist_qp(T2 > 0 ? T2 : 1);
     const int LW = a.lw;
+    // pass 1's pair window padded (pwin_off) where a wave holds few channels: the decimate-first
+    // families (AM / SAM, narrow SSB / CW) and FM, at 8 outputs per lane (host: front_pad1)
+    constexpr int PB1 = front_pad1(R, DECIM_FIRST, M);
     float* W = smem + gs * LW;                       // this channel's window
     float* aux = smem + CPW * LW;                    // auto-IQ factors [2][CPW][nblk32], osc [2N]
     float* m1 = aux;
@@ -403,11 +406,11 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
 #pragma unroll
             for (int j = 0; j < R; ++j) x2[j] = v2f{ xi[j], xq[j] };
         }
-        group_fill_prow<T1>(smem, LW, a.hist1, c0, CPW, nlive, lane, hA);
+        group_fill_prow<T1, PB1>(smem, LW, a.hist1, c0, CPW, nlive, lane, hA);
         wave_sync();
-        window_new2(W, T1, act, b, x2, R);
+        window_new2<PB1>(W, T1, act, b, x2, R);
         wave_sync();
-        group_store_prow<T1>(smem, LW, a.hist1, c0, nlive, lane, nb * R);
+        group_store_prow<T1, PB1>(smem, LW, a.hist1, c0, nlive, lane, nb * R);
 
         // the pass-2 FIR's own lane -> (channel, block) map: its window is filled through LDS by
         // the pass-1 lanes, so any map reads it; the host picks the one with the fewest bank
@@ -426,7 +429,7 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
             // FM: the Hilbert / low-pass pair at 48 ksps (:2748-2753), no decimation.
             // The demodulator in rx_back / rx_fm takes both I and Q.
                 v2f d2[RD];
-            fir_block2<T1, RD, M, F>(W + 2 * b * R, tA, d2);
+            fir_block2<T1, RD, M, F, PB1>(W + pwin_off<PB1>(b * R), tA, d2);
             if constexpr (M == 1)
             {
                 // FM (the only undecimated pair): the discriminator's angle per sample
@@ -479,7 +482,7 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
             vf4 hC[HQP2];
             group_load_prow<T2>(a.hist2, c0, nlive, lane, hC);
             v2f h2[R], d2[RD];
-            fir_block2<T1, R, 1, F>(W + 2 * b * R, tA, h2);
+            fir_block2<T1, R, 1, F, PB1>(W + pwin_off<PB1>(b * R), tA, h2);
 #pragma unroll
             for (int r = 0; r < R; ++r) h2[r] = front_comb2(comb, h2[r]);
             wave_sync();
@@ -504,7 +507,7 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
             group_load_rows<T2>(a.hist2, c0, nlive, lane, hC);
             v2f h2[R];
             float hs[R];
-            fir_block2<T1, R, 1, F>(W + 2 * b * R, tA, h2);
+            fir_block2<T1, R, 1, F, PB1>(W + pwin_off<PB1>(b * R), tA, h2);
             front_comb_block<R>(comb, h2, hs);
             wave_sync();
             group_fill_rows<T2>(smem, LW, a.hist2, c0, CPW, nlive, lane, hC);
@@ -519,7 +522,7 @@ __device__ __forceinline__ void front_body(const FrontArgs& a, const int grp, fl
             vf4 hC[HQP2];
             group_load_prow<T2>(a.hist2, c0, nlive, lane, hC);
             v2f d2[RD], h2[RD];
-            fir_block2<T1, RD, M, F>(W + 2 * b * R, tA, d2);
+            fir_block2<T1, RD, M, F, PB1>(W + pwin_off<PB1>(b * R), tA, d2);
             wave_sync();
             group_fill_prow<T2>(smem, LW, a.hist2, c0, CPW, nlive, lane, hC);
             wave_sync();
@@ -2834,7 +2837,9 @@ static int front_window_pitch(const uhsdr_rx_s* h, uint16_t (&lm1_out)[64], uint
     const bool pair2 = df || h->fv->st;                  // pass 2 is a FIR pair over {x0, x1}
     const int nb = N / R, cpw = FRONT_WAVE / nb;
     const int n2 = df ? N / M : N;
-    int need = 2 * (h->T1 - 1 + N);
+    const int pb1 = front_pad1(R, h->fv->decim_first != 0, h->fv->m);
+    // a padded pass-1 window holds its FIRs' over-read (FRONT_TAIL pairs) inside the pitch
+    int need = pb1 ? pwin_off<4>(h->T1 - 1 + N + FRONT_TAIL) : 2 * (h->T1 - 1 + N);   // pb1: 0 or 4
     const int need2 = h->T2 ? (pair2 ? 2 : 1) * (h->T2 - 1 + n2) : 0;
     need = ((need > need2 ? need : need2) + 3) & ~3;
     const int RD = R / M;
@@ -2873,7 +2878,7 @@ static int front_window_pitch(const uhsdr_rx_s* h, uint16_t (&lm1_out)[64], uint
         for (int m1 = 0; m1 < nmaps; ++m1)
             for (int m2 = 0; m2 < (h->T2 ? nmaps : 1); ++m2)
             {
-                int cost = front_lds_pass1(lw, maps[m1], cpw, h->T1, R) + hist_cost;
+                int cost = front_lds_pass1(lw, maps[m1], cpw, h->T1, R, pb1) + hist_cost;
                 if (h->T2) cost += front_lds_pass2(lw, maps[m1], maps[m2], cpw, h->T2, pair2, NV2, RD2, M2);
                 if (waves > best_waves || (waves == best_waves && cost < best_cost))
                 {

@@ -12,8 +12,8 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD S
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  echo "=== pass $i: $grp"
+  echo "=== pass $i: $grp" >&2
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_$tag/p$i -o pmc -- python "$@" > gpurun_out/pmc_$tag/p$i.log 2>&1 || { echo "pass $i failed"; tail -20 gpurun_out/pmc_$tag/p$i.log; exit 1; }
 done
 python tools/pmc_summary.py $tag
-echo PMC_DONE
+echo PMC_DONE >&2

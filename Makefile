@@ -11,7 +11,7 @@ HIPCC   ?= /opt/rocm/bin/hipcc
 CC      ?= gcc
 ARCH    ?= gfx950
 HOSTCFLAGS := -O2 -fPIC -ffp-contract=off -std=gnu11 -Wall -Wno-unused-function
-HIPFLAGS   := --offload-arch=$(ARCH) -O3 -fPIC -ffp-contract=off -fno-slp-vectorize -std=c++17 -Wno-unused-result
+HIPFLAGS   := --offload-arch=$(ARCH) -Iuhsdr_amd/csrc -O3 -fPIC -ffp-contract=off -fno-slp-vectorize -std=c++17 -Wno-unused-result
 
 LIB     := uhsdr_amd/lib/libuhsdr_amd.so
 CMSISLIB := uhsdr_amd/lib/libuhsdr_cmsis.so
@@ -22,7 +22,7 @@ HOST_SRCS := uhsdr_amd/csrc/uhsdr_setup.c uhsdr_amd/csrc/uhsdr_filter_tables.c
 HIP_SRCS  := uhsdr_amd/csrc/uhsdr_rx.hip uhsdr_amd/csrc/uhsdr_tx.hip uhsdr_amd/csrc/uhsdr_spectrum.hip uhsdr_amd/csrc/uhsdr_i2s.hip uhsdr_amd/csrc/uhsdr_fir.hip
 HOST_OBJS := $(patsubst uhsdr_amd/csrc/%.c,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS  := $(patsubst uhsdr_amd/csrc/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
-HDRS := include/uhsdr.h uhsdr_amd/csrc/uhsdr_internal.h uhsdr_amd/csrc/uhsdr_dsp.h uhsdr_amd/csrc/uhsdr_libm.h uhsdr_amd/csrc/uhsdr_cfft.h
+HDRS := uhsdr_amd/csrc/uhsdr_rx_variants.inc include/uhsdr.h uhsdr_amd/csrc/uhsdr_internal.h uhsdr_amd/csrc/uhsdr_dsp.h uhsdr_amd/csrc/uhsdr_libm.h uhsdr_amd/csrc/uhsdr_cfft.h
 
 EXAMPLE := examples/build/rx_batch
 
@@ -69,7 +69,7 @@ clean:
 # compile-time variants of libuhsdr_amd.so for A/B measurement (bench.py with UHSDR_LIB=<path>):
 #   make variant VTAG=w3 VFLAGS=-DUHSDR_FUSED_WAVES=3
 # every HIP source is rebuilt with VFLAGS into its own object directory, so a flag read by any
-# source takes effect (-DUHSDR_ISA_P48 builds only the P48 receive kernels: quick A/B builds)
+# source takes effect (VFLAGS=-Itools/isa builds only the P48 receive kernels: quick A/B builds)
 VARIANT_DIR := uhsdr_amd/lib/variants
 VOBJDIR = $(OBJDIR)/v_$(VTAG)
 VHIP_OBJS = $(patsubst uhsdr_amd/csrc/%.hip,$(VOBJDIR)/%.o,$(HIP_SRCS))

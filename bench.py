@@ -135,7 +135,7 @@ SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain"}
 
 
 def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, pool, want_dst, pipelined=False,
-              precision=0, schedule=None, front_block=0):
+              precision=0, schedule=None, front_block=0, reduce_dev=None):
     """W untimed + K timed steps of one RxChain on this rank; returns (max-rank seconds,
     per-kernel (total ms, launches) from HIP events on the library's stream, plan, finite)."""
     cfg = U.default_config()
@@ -157,11 +157,16 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     # throughput: K calls with nothing but the calls themselves inside the timed region
     # (shard.timed_loop: warm-up, barrier + sync brackets, max over ranks)
     elapsed = shard.timed_loop(lambda s: chain.process(inputs[s % pool], audio, dst),
-                               lambda: torch.cuda.synchronize(dev), steps, warmup, dist, world, dev)
+                               lambda: torch.cuda.synchronize(dev), steps, warmup, dist, world,
+                               dev if reduce_dev is None else reduce_dev)
     # per-kernel breakdown in a separate pass: HIP events on the library's own stream bracket
     # every kernel of every call (the records cost host time, so they never share a clock with
     # the throughput loop above)
     tsteps = max(10, min(steps, 200))
+    if pipelined:
+        # serial for the event pass: with call k+1's rx_front overlapping call k's rx_back the
+        # events of each kernel would include the other's time
+        chain.set_pipelined(False)
     chain.enable_timing(True, every=1)
     for s in range(tsteps):
         chain.process(inputs[s % pool], audio, dst)
@@ -174,21 +179,36 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     return elapsed, ktimes, plan, ok, sched
 
 
-def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup):
+def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, backend="nccl", pool=4, sink=None):
     """The same chain with every launch's f32 audio gathered to rank 0
     through shard.GatherPipeline: double-buffered outputs, the gather of launch k (RCCL
     grouped send/recv over xGMI, rank 0 receiving from every peer on its own link) in flight
-    while launch k+1 computes.  Returns max-rank seconds for `steps` steps."""
+    while launch k+1 computes.  Step s processes the rank's block s % pool of consecutive
+    48 kHz blocks.  With the gloo test hook the device audio is copied to host buffers and
+    those are gathered.  `sink(step, parts)` (rank 0) sees every step's per-rank blocks in
+    step order.  Returns max-rank seconds for `steps` steps."""
     cfg = U.default_config()
     comp = torch.cuda.current_stream(dev)
     chain = U.RxChain(cfg, channels=C, frames=N, stream=comp.cuda_stream)
-    x = synth.ssb_iq_torch(shard.channel_range(C, rank)[0], C, 0, N, dev)
+    c0 = shard.channel_range(C, rank)[0]
+    xs = [synth.ssb_iq_torch(c0, C, k * N, N, dev) for k in range(pool)]
+    host = backend != "nccl"
+    dev_out = torch.empty((C, N), dtype=torch.float32, device=dev) if host else None
     pipe = shard.GatherPipeline(dist, world, rank,
-                                lambda: torch.empty((C, N), dtype=torch.float32, device=dev))
+                                lambda: torch.empty((C, N), dtype=torch.float32, device="cpu" if host else dev),
+                                sink=sink)
+    st = {"s": 0}
 
     def compute(out):
-        chain.process(x, out, None)
-    t = shard.gather_timed(pipe, compute, lambda: torch.cuda.synchronize(dev), steps, warmup, dist, dev)
+        x = xs[st["s"] % pool]
+        st["s"] += 1
+        if host:
+            chain.process(x, dev_out, None)
+            out.copy_(dev_out.cpu())
+        else:
+            chain.process(x, out, None)
+    t = shard.gather_timed(pipe, compute, lambda: torch.cuda.synchronize(dev), steps, warmup, dist,
+                           "cpu" if host else dev)
     chain.close()
     return t
 
@@ -203,6 +223,25 @@ def roofline_of(ab, ktimes, traffic):
             "kernel": dominant, "alg_bytes_per_launch": ab[dominant],
             "mean_launch_ms": round(kms[dominant], 5)}
     return roof, kms
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` with no WORLD_SIZE in the environment: run N ranks of this same
+    command line as children of torch.distributed.run (one process per GPU, RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment) and return its exit code.  Called before
+    anything in this process imports torch.cuda state or touches HIP, and the children are
+    started as child processes (never an exec of this one)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -230,10 +269,17 @@ def main():
     ap.add_argument("--pool", type=int, default=8, help="distinct input blocks cycled through")
     ap.add_argument("--schedule", default="auto", choices=sorted(SCHEDULES),
                     help="kernel schedule of a call (uhsdr_rx_set_schedule); auto: the library's choice "
-                         "(rx_chain from 131072 channels on, else rx_front + the back-end wave pipeline)")
+                         "(rx_front + rx_back_fused from 131072 channels on, else rx_front + the back-end wave "
+                         "pipeline; rx_chain only when asked for)")
     ap.add_argument("--front-block", type=int, default=0, choices=[0, 8, 16],
                     help="FIR outputs per lane of rx_front (uhsdr_rx_set_front_block; 0: the library default)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group of an N > 1 run: nccl (= RCCL over xGMI, one GPU per rank) or gloo "
+                         "(test hook: ranks may share one GPU, the gather leg moves host copies)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -243,11 +289,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE is {world}", file=sys.stderr)
+        sys.exit(2)
+    if args.dist_backend == "nccl":
+        dev = torch.device("cuda", local)
+    else:
+        # gloo test hook: ranks may outnumber the GPUs of the box and share them
+        dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    reduce_dev = dev if args.dist_backend == "nccl" else "cpu"
 
     prec = U.PRECISION_FMA if args.precision == "fma" else U.PRECISION_EXACT
     wl = WORKLOADS[args.workload]
@@ -256,16 +312,19 @@ def main():
     pipelined = args.pipelined or (not args.serial and args.workload != "northstar")
     elapsed, ktimes, plan, ok, sched = timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, args.steps,
                                                  args.warmup, max(1, args.pool), args.dst, pipelined, prec,
-                                                 SCHEDULES[args.schedule], args.front_block)
+                                                 SCHEDULES[args.schedule], args.front_block, reduce_dev)
 
     gather = None
     if world > 1 and not args.no_gather:
         gs = max(10, args.steps // 4)
-        gt = gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, gs, 5)
+        gt = gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, gs, 5, args.dist_backend)
         gather = {"value": round(world * C * N * gs / gt / 1e6, 2), "unit": "Msamples/s", "steps": gs,
                   "ms_per_step": round(gt / gs * 1e3, 5),
-                  "how": "every launch's f32 audio gathered to rank 0 (torch.distributed.gather = grouped RCCL "
-                         "send/recv over xGMI) on a comm stream, overlapped with the next launch (double-buffered)"}
+                  "backend": args.dist_backend,
+                  "how": ("every launch's f32 audio gathered to rank 0 (torch.distributed.gather = grouped RCCL "
+                          "send/recv over xGMI) on a comm stream, overlapped with the next launch (double-buffered)"
+                          if args.dist_backend == "nccl" else
+                          "gloo test hook: every launch's audio copied to host and gathered to rank 0 over gloo")}
 
     def north_star_leg(precision):
         nw = WORKLOADS["northstar"]
@@ -278,7 +337,10 @@ def main():
         return {"workload": nw["desc"], "value": round(nw["channels"] * nw["frames"] * NS_STEPS / n_el / 1e6, 2),
                 "unit": "Msamples/s", "steps": NS_STEPS, "ms_per_step": round(n_el / NS_STEPS * 1e3, 5), "roofline": n_roof,
                 "kernel_ms": {k: round(v, 5) for k, v in n_kms.items()},
-                "chain_hbm_frac": round(n_ab["chain"] / (n_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                # the chain's algorithmic bytes over the wall clock of a step (everything between
+                # the kernels included), and over the sum of the kernels' own event times
+                "chain_hbm_frac": round(n_ab["chain"] / n_el * NS_STEPS / 1e9 / HBM_PEAK_GBS, 4),
+                "chain_hbm_frac_kernel_events": round(n_ab["chain"] / (n_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "alg_bytes_per_sample": round(n_ab["chain"] / (nw["channels"] * nw["frames"]), 2),
                 "schedule": n_sched, "outputs_finite": n_ok}
 
@@ -321,12 +383,12 @@ def main():
                   "kernel_ms": {k: round(v, 5) for k, v in kms.items()},
                   "alg_bytes_per_sample": round(ab["chain"] / (C * N), 2),
                   "s_live_bytes_per_channel": ab["s_live_bytes"],
-                  "hbm_frac": round(chain_gbs / HBM_PEAK_GBS, 4),
+                  "hbm_frac": round(ab["chain"] / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                  "hbm_frac_kernel_events": round(chain_gbs / HBM_PEAK_GBS, 4),
                   "note": "C2 (4096 channels) is latency-bound: one lane per channel for the recursive "
                           "stages leaves most of the 256 CUs idle; see DESIGN.md and north_star"
-                          + ("; pipelined: rx_front of the next call overlaps rx_back, so the kernels' "
-                             "event times (and device_ms_per_step, their sum) exceed ms_per_step"
-                             if pipelined else "")},
+                          + ("; pipelined: rx_front of the next call overlaps rx_back in the timed loop; the "
+                             "kernel event times come from a separate serial pass" if pipelined else "")},
         "outputs_finite": ok,
     }
     if ns:

@@ -279,8 +279,8 @@ int32_t      uhsdr_rx_get_precision(uhsdr_rx_handle h);   /* -1 for a null handl
 uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h);
 
 /* Kernel schedule of a call (a launch-shape choice: outputs are bit-identical under every one).
- *   AUTO        (default) CHAIN where supported from 131072 channels on, else SPLIT_FUSED from
- *               131072 channels on, else SPLIT_PIPE
+ *   AUTO        (default) SPLIT_FUSED from 131072 channels on, else SPLIT_PIPE; CHAIN only
+ *               when requested
  *   SPLIT_PIPE  rx_front, then rx_back: one wave per back-end stage, a pipeline over 32-frame
  *               calls (short per-call critical path: small batches)
  *   SPLIT_FUSED rx_front, then rx_back_fused: every back-end stage in one wave per 64 channels

@@ -1126,6 +1126,16 @@ static void tx_call(const uhsdr_tx_plan* p, uo_tx_state* s, const int32_t* audio
         if (a0) memcpy(a0, s->a0, sizeof(float) * n);
         return;
     }
+    if ((p->am || p->fm) && p->freq_shift_hz == 0)
+    {
+        /* USB I/Q source under TUNE in AM / FM without frequency translation (the plan admits it
+           only with DIGIQ): the AM / FM branch is skipped (tx_processor.c:996-1016), signal_active
+           stays false and zeroed I/Q goes through the final stage: zero DAC frames */
+        for (int i = 0; i < n; i++) { ib[i] = 0.0f; qb[i] = 0.0f; }
+        tx_final(p, p->final_i_gain, p->final_q_gain, ib, qb, iq, n);
+        if (a0) memcpy(a0, s->a0, sizeof(float) * n);
+        return;
+    }
     /* TxProcessor_AudioBufferFill (tx_processor.c:339-405) */
     if (s->tune)
     {

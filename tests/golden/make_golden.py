@@ -158,10 +158,14 @@ TX_CONFIGS = {
     # USB I/Q source (TX_AUDIO_DIGIQ, :950-961): the frames are the I/Q; TUNE runs the voice path
     "usb_digiq": {"mode": 0, "path": 48, "txsrc": 4, "txgi": 0.98, "txphase": -0.01},
     "am_digiq_m6k": {"mode": 3, "path": 70, "txsrc": 4, "iqmode": 2, "txpwr": 0.9},
+    # USB I/Q source in AM / FM with the frequency translation OFF: the passthrough branch comes
+    # first (:950), so the I/Q is transmitted; under TUNE the AM / FM branch does nothing (:996-1016)
+    "am_digiq_off_tune": {"mode": 3, "path": 70, "txsrc": 4, "iqmode": 0, "tune": "8:24:1"},
+    "fm_digiq_off_tune": {"mode": 5, "path": 1, "txsrc": 4, "iqmode": 0, "tune": "16:32:2"},
 }
 # TX_AUDIO_DIGIQ fixtures take 16-bit I/Q (the USB audio class delivers int16 samples; the final
 # stage scales by 2^16 with no headroom for the codec's left-aligned frames)
-TX_DIGIQ_INPUT = ("usb_digiq", "am_digiq_m6k")
+TX_DIGIQ_INPUT = ("usb_digiq", "am_digiq_m6k", "am_digiq_off_tune", "fm_digiq_off_tune")
 
 
 def make_tx(name: str):

@@ -15,7 +15,7 @@ from uhsdr_amd import synth
 pytestmark = pytest.mark.gpu
 
 
-def run_pipelined(cfg, iq, N, toggle_at=None, join_each=False):
+def run_pipelined(cfg, iq, N, toggle_at=None, join_each=False, switch=None):
     import torch
     C, n, _ = iq.shape
     calls = n // N
@@ -30,6 +30,8 @@ def run_pipelined(cfg, iq, N, toggle_at=None, join_each=False):
             chain.set_pipelined(False)
         if toggle_at is not None and k == toggle_at + 1:
             chain.set_pipelined(True)
+        if switch is not None and k in switch:
+            chain.set_schedule(switch[k])     # change kernel schedule between calls, still pipelined
         chain.process(xs[k], audio[k], dst[k])
         if join_each:
             chain.join()
@@ -50,10 +52,16 @@ CASES = [
 ]
 
 
+# The hand-off buffers are reused per group of PIPE_GROUP = 4 calls (PIPE_BUFS = 8): group g waits
+# for the last rx_back of group g-2.  15 calls = groups 0..3, the last one partial, so every buffer
+# is reused and the cross-group wait runs.
+CALLS = 15
+
+
 @pytest.mark.parametrize("name,kw,gen,C,N", CASES, ids=[c[0] for c in CASES])
 def test_pipelined_matches_oracle(cuda, back, name, kw, gen, C, N):
     cfg = U.default_config(**kw)
-    iq = gen(np.arange(C), 0, 8 * N)
+    iq = gen(np.arange(C), 0, CALLS * N)
     a1, dst = run_pipelined(cfg, iq, N)
     ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
     assert_bitexact(a1, ref_a1, f"pipelined {name}")
@@ -63,12 +71,27 @@ def test_pipelined_matches_oracle(cuda, back, name, kw, gen, C, N):
 def test_pipelined_toggle_and_join(cuda):
     cfg = U.default_config()
     C, N = 96, 128
-    iq = synth.ssb_iq(np.arange(C), 0, 8 * N)
+    iq = synth.ssb_iq(np.arange(C), 0, 17 * N)
     ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
     a1, dst = run_pipelined(cfg, iq, N, toggle_at=3)
     assert_bitexact(a1, ref_a1, "pipelined, off for call 3")
+    a1, dst = run_pipelined(cfg, iq, N, toggle_at=10)
+    assert_bitexact(a1, ref_a1, "pipelined, off for call 10 (inside group 2)")
     a1, dst = run_pipelined(cfg, iq, N, join_each=True)
     assert_bitexact(a1, ref_a1, "pipelined, join after every call")
+    np.testing.assert_array_equal(dst, ref_dst)
+
+
+@pytest.mark.parametrize("first,second", [(1, 2), (2, 1)], ids=["pipe_then_fused", "fused_then_pipe"])
+def test_pipelined_schedule_switch_mid_group(cuda, first, second):
+    """Pipelined across 17 calls while the schedule switches to CHAIN inside group 1 and back
+    inside group 2: the hand-off buffers and their events must stay ordered."""
+    cfg = U.default_config()
+    C, N = 96, 128
+    iq = synth.ssb_iq(np.arange(C), 0, 17 * N)
+    ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    a1, dst = run_pipelined(cfg, iq, N, switch={0: first, 5: 3, 9: second, 14: first})
+    assert_bitexact(a1, ref_a1, f"pipelined, schedule {first} -> chain -> {second} -> {first}")
     np.testing.assert_array_equal(dst, ref_dst)
 
 

@@ -64,11 +64,26 @@ def test_plan_rejects_bad_config():
     plan = U.RxPlan()
     for over in [dict(filter_path=0), dict(filter_path=87), dict(dmod_mode=9),
                  dict(filter_path=1),    # FM-only path for USB
-                 # SAM PLL menu ranges (ui_configuration.c:214-216)
-                 dict(sam_pll_fmax=49), dict(sam_pll_fmax=8001), dict(sam_zeta=0), dict(sam_zeta=101),
-                 dict(sam_omega_n=14), dict(sam_omega_n=1001)]:
+                 # SAM PLL menu ranges (ui_configuration.c:214-216), checked in SAM only
+                 dict(sam_pll_fmax=49, dmod_mode=U.DEMOD_SAM, filter_path=70),
+                 dict(sam_pll_fmax=8001, dmod_mode=U.DEMOD_SAM, filter_path=70),
+                 dict(sam_zeta=0, dmod_mode=U.DEMOD_SAM, filter_path=70),
+                 dict(sam_zeta=101, dmod_mode=U.DEMOD_SAM, filter_path=70),
+                 dict(sam_omega_n=14, dmod_mode=U.DEMOD_SAM, filter_path=70),
+                 dict(sam_omega_n=1001, dmod_mode=U.DEMOD_SAM, filter_path=70)]:
         cfg = U.default_config(**over)
         assert lib.uhsdr_rx_plan_build(C.byref(cfg), C.byref(plan)) == -1, over
+
+
+def test_sam_pll_fields_ignored_outside_sam():
+    """A USB / CW / FM / AM config whose unused SAM PLL fields are zero (not built by
+    config_default) still builds: the menu ranges apply in SAM only."""
+    lib = U.load()
+    plan = U.RxPlan()
+    for kw in [dict(), dict(dmod_mode=U.DEMOD_CW, filter_path=4), dict(dmod_mode=U.DEMOD_FM, filter_path=1),
+               dict(dmod_mode=U.DEMOD_AM, filter_path=70)]:
+        cfg = U.default_config(sam_pll_fmax=0, sam_zeta=0, sam_omega_n=0, **kw)
+        assert lib.uhsdr_rx_plan_build(C.byref(cfg), C.byref(plan)) == 0, kw
 
 
 @pytest.mark.parametrize("path", [p for p in golden_files() if "notch_mu" in load(p)["setup"]],

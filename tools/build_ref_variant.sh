@@ -10,7 +10,7 @@ mkdir -p uhsdr_amd/lib/variants "$tmp/obj"
 for f in "$tmp"/uhsdr_amd/csrc/*.hip; do
   [ "$(basename $f)" = uhsdr_cmsis.hip ] && continue
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -ffp-contract=off -fno-slp-vectorize -std=c++17 -Wno-unused-result \
-      -DUHSDR_ISA_P48 "$@" -I"$tmp/include" -I"$tmp/uhsdr_amd/csrc" -c "$f" -o "$tmp/obj/$(basename $f .hip).o" &
+      -I"$(pwd)/tools/isa" "$@" -I"$tmp/include" -I"$tmp/uhsdr_amd/csrc" -c "$f" -o "$tmp/obj/$(basename $f .hip).o" &
 done
 for f in "$tmp"/uhsdr_amd/csrc/*.c; do
   gcc -O2 -fPIC -ffp-contract=off -std=gnu11 -I"$tmp/include" -I"$tmp/uhsdr_amd/csrc" -c "$f" -o "$tmp/obj/$(basename $f .c).o" &

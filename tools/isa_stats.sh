@@ -5,7 +5,7 @@ set -e
 src=$1; pat=$2
 out=/tmp/isa_$(basename $src .hip)
 mkdir -p $out
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -DUHSDR_ISA_P48 $ISAFLAGS -O3 -ffp-contract=off -fno-slp-vectorize -std=c++17 -Wno-unused-result \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -Itools/isa $ISAFLAGS -O3 -ffp-contract=off -fno-slp-vectorize -std=c++17 -Wno-unused-result \
   -Iinclude -Iuhsdr_amd/csrc --offload-device-only -S -o $out/k.s $src -Rpass-analysis=kernel-resource-usage 2> $out/res.txt
 name=$(grep -o "^${pat}[^:]*:" $out/k.s | head -1 | tr -d :)
 echo "kernel: $name"

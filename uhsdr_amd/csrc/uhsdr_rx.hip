@@ -2535,88 +2535,7 @@ struct ChainVariant { int t1, t2, m, decim_first, R, pre, aa, L, ph, w; chain_fn
 #define FRONT_V(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false>, R, rx_front<t1, t2, m, df, R, true>, 0 }
 #define FRONT_ST(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false, true>, R, rx_front<t1, t2, m, df, R, true, true>, 1 }
 struct NotchVariant { int L, dm; back_fn fn; };
-#ifdef UHSDR_ISA_P48
-// tools/isa_stats.sh: only the P48 SSB instances, so one kernel's ISA compiles in seconds
-static const FrontVariant kFront[] = { FRONT_V(89, 43, 4, false, 8) };
-#define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm>, \
-    fused_nodc_of<pre, aa, L, ph, w, dm>(), fused_ssb_of<pre, aa, L, ph, w, dm>() }
-static const BackVariant kBack[] = { BACK_V(10, 6, 4, 1, 49, DM_NONE) };
-static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6>, nullptr };
-static const BackVariant kBackStereo[] = { { 10, 6, 4, 1, 49, DM_NONE, nullptr, nullptr } };
-static const NotchVariant kNotch[] = { { 4, DM_NONE, nullptr } };
-static const ChainVariant kChain[] = { CHAIN_V(89, 43, 4, false, 10, 6, 1, 49) };
-#undef BACK_V
-#undef FRONT_V
-#undef FRONT_ST
-#else
-static const FrontVariant kFront[] = {
-    FRONT_V(89, 43, 4, false, 16), FRONT_V(89, 43, 4, false, 8),     // wide SSB/CW  (P48-54)
-    FRONT_V(89, 4, 2, false, 16), FRONT_V(89, 4, 2, false, 8),       // 24 ksps SSB   (P55-65)
-    FRONT_V(83, 199, 4, true, 16), FRONT_V(83, 199, 4, true, 8),     // narrow SSB/CW (P4-47)
-    FRONT_V(89, 0, 4, true, 16), FRONT_V(89, 0, 4, true, 8),         // AM / SAM, 12 ksps (P66-82)
-    FRONT_V(89, 0, 2, true, 16), FRONT_V(89, 0, 2, true, 8),         // AM / SAM, 24 ksps (P83-86)
-    FRONT_V(89, 0, 1, false, 16), FRONT_V(89, 0, 1, false, 8),       // FM, 48 ksps Hilbert pair (P1-3)
-    // OVI40 stereo (DEMOD_SSBSTEREO / DEMOD_IQ with use_stereo): two channels out
-    FRONT_ST(89, 43, 4, false, 16), FRONT_ST(89, 43, 4, false, 8),
-    FRONT_ST(89, 4, 2, false, 16), FRONT_ST(89, 4, 2, false, 8),
-    FRONT_ST(83, 199, 4, true, 16), FRONT_ST(83, 199, 4, true, 8),
-};
-#undef FRONT_V
-#undef FRONT_ST
-
-#define BACK_V(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back<pre, aa, L, ph, w, dm>, rx_back_fused<pre, aa, L, ph, w, dm>, \
-    fused_nodc_of<pre, aa, L, ph, w, dm>(), fused_ssb_of<pre, aa, L, ph, w, dm>() }
-static const BackVariant kBack[] = {
-    // SSB / CW / DIGI
-    BACK_V(10, 6, 4, 1, 49, DM_NONE), BACK_V(10, 0, 4, 4, 49, DM_NONE), BACK_V(0, 0, 2, 8, 97, DM_NONE),
-    BACK_V(0, 6, 2, 2, 97, DM_NONE), BACK_V(10, 0, 2, 8, 97, DM_NONE), BACK_V(8, 0, 2, 8, 97, DM_NONE),
-    BACK_V(8, 6, 2, 2, 97, DM_NONE),
-    // AM / SAM paths P66-86
-    BACK_V(10, 0, 4, 4, 49, DM_AM), BACK_V(10, 6, 4, 1, 49, DM_AM), BACK_V(10, 0, 2, 8, 97, DM_AM),
-    BACK_V(8, 0, 2, 8, 97, DM_AM), BACK_V(8, 6, 2, 2, 97, DM_AM),
-    BACK_V(10, 0, 4, 4, 49, DM_SAM), BACK_V(10, 6, 4, 1, 49, DM_SAM), BACK_V(10, 0, 2, 8, 97, DM_SAM),
-    BACK_V(8, 0, 2, 8, 97, DM_SAM), BACK_V(8, 6, 2, 2, 97, DM_SAM),
-    BACK_V(10, 0, 4, 4, 49, DM_SAM_SB), BACK_V(10, 6, 4, 1, 49, DM_SAM_SB), BACK_V(10, 0, 2, 8, 97, DM_SAM_SB),
-    BACK_V(8, 0, 2, 8, 97, DM_SAM_SB), BACK_V(8, 6, 2, 2, 97, DM_SAM_SB),
-};
-// FM: its own kernel (squelch lattice stages)
-static const BackVariant kBackFm = { 0, 0, 1, 1, 0, DM_FM, rx_fm<6>, nullptr };
-#undef BACK_V
-
-// OVI40 stereo back ends (rx_back_stereo): SSB stereo / IQ families, and SAM stereo
-#define BACK_ST(pre, aa, L, ph, w, dm) { pre, aa, L, ph, w, dm, rx_back_stereo<pre, aa, L, ph, w, dm>, rx_back_stereo<pre, aa, L, ph, w, dm> }
-static const BackVariant kBackStereo[] = {
-    BACK_ST(10, 6, 4, 1, 49, DM_NONE), BACK_ST(10, 0, 4, 4, 49, DM_NONE), BACK_ST(0, 0, 2, 8, 97, DM_NONE),
-    BACK_ST(0, 6, 2, 2, 97, DM_NONE), BACK_ST(10, 0, 2, 8, 97, DM_NONE), BACK_ST(8, 0, 2, 8, 97, DM_NONE),
-    BACK_ST(8, 6, 2, 2, 97, DM_NONE),
-    BACK_ST(10, 0, 4, 4, 49, DM_SAM_ST), BACK_ST(10, 6, 4, 1, 49, DM_SAM_ST), BACK_ST(10, 0, 2, 8, 97, DM_SAM_ST),
-    BACK_ST(8, 0, 2, 8, 97, DM_SAM_ST), BACK_ST(8, 6, 2, 2, 97, DM_SAM_ST),
-};
-#undef BACK_ST
-
-// LMS auto notch (+ the AM / SAM demodulator ahead of it): decimation L, demodulator DM
-static const NotchVariant kNotch[] = {
-    { 4, DM_NONE, rx_notch<4, DM_NONE> }, { 2, DM_NONE, rx_notch<2, DM_NONE> },
-    { 4, DM_AM, rx_notch<4, DM_AM> }, { 2, DM_AM, rx_notch<2, DM_AM> },
-    { 4, DM_SAM, rx_notch<4, DM_SAM> }, { 2, DM_SAM, rx_notch<2, DM_SAM> },
-    { 4, DM_SAM_SB, rx_notch<4, DM_SAM_SB> }, { 2, DM_SAM_SB, rx_notch<2, DM_SAM_SB> },
-    { 4, DM_SAM_ST, rx_notch<4, DM_SAM_ST> }, { 2, DM_SAM_ST, rx_notch<2, DM_SAM_ST> },
-};
-
-// one front pass + back end per wave: the SSB / CW / DIGI families of kFront x kBack (DM_NONE)
-static const ChainVariant kChain[] = {
-    CHAIN_V(89, 43, 4, false, 10, 6, 1, 49),             // wide SSB, 12 ksps (P48 ...)
-    CHAIN_V(89, 43, 4, false, 10, 0, 4, 49),
-    CHAIN_V(83, 199, 4, true, 10, 6, 1, 49),             // narrow SSB / CW, 12 ksps
-    CHAIN_V(83, 199, 4, true, 10, 0, 4, 49),
-    CHAIN_V(89, 4, 2, false, 0, 0, 8, 97),               // 24 ksps SSB
-    CHAIN_V(89, 4, 2, false, 0, 6, 2, 97),
-    CHAIN_V(89, 4, 2, false, 10, 0, 8, 97),
-    CHAIN_V(89, 4, 2, false, 8, 0, 8, 97),
-    CHAIN_V(89, 4, 2, false, 8, 6, 2, 97),
-};
-
-#endif
+#include <uhsdr_rx_variants.inc>
 #undef CHAIN_V
 
 static int plan_dm(const uhsdr_rx_plan& p)
@@ -2868,9 +2787,6 @@ static int front_window_pitch(const uhsdr_rx_s* h, uint16_t (&lm1_out)[64], uint
     {
         int waves = (int)(LDS_PER_CU / (sizeof(float) * ((size_t)cpw * lw + extra)));
         waves = waves > vgpr_waves ? vgpr_waves : waves;
-#ifdef UHSDR_PITCH_CONFLICTS_ONLY
-        waves = 0;
-#endif
         // history rows: pair rows (hist_stride / 2 float4s per channel), or the mono decimator's
         const int hist_cost = front_lds_hist(lw, cpw, hist_p4(h->T1), 2 * N) +
                               (h->T2 ? (pair2 ? front_lds_hist(lw, cpw, hist_p4(h->T2), 2 * (df ? N / M : N))
@@ -2920,10 +2836,6 @@ static size_t front_lds(const uhsdr_rx_s* h)
     const int N = h->Nf;
     const int cpw = FRONT_WAVE / (N / h->fv->R);
     size_t f = (size_t)cpw * h->lw + front_lds_extra(h) + FRONT_SLACK;
-#ifdef UHSDR_FRONT_LDS_MIN
-    // experiment builds: a floor on the front's LDS per wave (caps its waves per CU)
-    if (f * sizeof(float) < (size_t)UHSDR_FRONT_LDS_MIN) return UHSDR_FRONT_LDS_MIN;
-#endif
     return f * sizeof(float);
 }
 

@@ -430,8 +430,8 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
        step |g1 * phzerror + omega2| <= g1 * pi + 2 pi fmax / 12000 < 4.7 stays below 2 pi, so the
        phase wrap (audio_driver.c:2143-2146) takes at most one iteration each way and the device
        demodulator (DemodStage::step) evaluates it as two selects */
-    if (cfg->sam_pll_fmax < 50 || cfg->sam_pll_fmax > 8000 || cfg->sam_zeta < 1 || cfg->sam_zeta > 100 ||
-        cfg->sam_omega_n < 15 || cfg->sam_omega_n > 1000)
+    if (mode == UHSDR_DEMOD_SAM && (cfg->sam_pll_fmax < 50 || cfg->sam_pll_fmax > 8000 || cfg->sam_zeta < 1 || cfg->sam_zeta > 100 ||
+        cfg->sam_omega_n < 15 || cfg->sam_omega_n > 1000))
     {
         uhsdr_set_error("SAM PLL parameters (fmax %d, zeta %d, omegaN %d) outside 50..8000, 1..100, 15..1000",
                         cfg->sam_pll_fmax, cfg->sam_zeta, cfg->sam_omega_n);
@@ -575,9 +575,12 @@ uhsdr_status uhsdr_tx_plan_build(const uhsdr_tx_config* cfg, uhsdr_tx_plan* p)
         uhsdr_set_error("transmit mode %d: SSB (USB/LSB), AM and FM voice are implemented", cfg->dmod_mode);
         return UHSDR_UNSUPPORTED;
     }
-    if ((fm || am) && cfg->iq_freq_mode == UHSDR_IQ_CONV_OFF)
+    if ((fm || am) && cfg->iq_freq_mode == UHSDR_IQ_CONV_OFF && cfg->audio_source != UHSDR_TX_AUDIO_DIGIQ)
     {
-        /* "No AM / FM possible unless in frequency translate mode" (tx_processor.c:1000-1011) */
+        /* "No AM / FM possible unless in frequency translate mode" (tx_processor.c:1000-1011).
+           With the USB I/Q source the passthrough branch (:950-961) comes first and transmits
+           the I/Q as is; only TUNE then reaches the AM / FM branch, which produces no signal
+           (uhsdr_tx_process writes zero I/Q, the reference's signal_active == false) */
         uhsdr_set_error("AM / FM transmit needs the I/Q frequency translation");
         return UHSDR_UNSUPPORTED;
     }

@@ -727,18 +727,26 @@ extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio
     if (!h || !audio || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
     if (h->plan.digiq && !h->tune)
     {
-        // USB I/Q source: no voice chain, no modulator state advances, a0 (adb.a_buffer[0]) untouched;
-        // pipelined: on the side stream, after the DAC frames of the calls before it
+        // USB I/Q source: no voice chain, no modulator state advances, a0 (adb.a_buffer[0]) untouched.
+        // Pipelined: the handle's stream first waits for the side stream (the DAC frames of the
+        // voice calls before it), then tx_digiq runs on the handle's stream itself, so the input
+        // buffer is read in stream order exactly as in serial mode
         const long long pairs = (long long)h->C * h->N / 2;
-        const hipStream_t st = h->pipelined ? h->side : h->stream;
-        if (h->pipelined)
-        {
-            HIPCHK(hipEventRecord(h->ev_voice, h->stream));      // after this call's input is ready
-            HIPCHK(hipStreamWaitEvent(st, h->ev_voice, 0));
-        }
+        const hipStream_t st = h->stream;
+        if (tx_join(h) != UHSDR_OK) return UHSDR_DEVICE_ERROR;
         hipLaunchKernelGGL(tx_digiq, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, st, h->d_plan,
                            (const int4*)audio, (int4*)iq, pairs);
         HIPCHK(hipGetLastError());
+        return UHSDR_OK;
+    }
+    if ((h->plan.am || h->plan.fm) && h->plan.freq_shift_hz == 0)
+    {
+        // DIGIQ source with TUNE in AM / FM without frequency translation: the reference's AM / FM
+        // branch does nothing (tx_processor.c:996-1016), signal_active stays false and the zeroed
+        // I/Q goes through the final stage (:1021-1025, :282-330): all-zero DAC frames, no state
+        // advances, a0 untouched
+        if (tx_join(h) != UHSDR_OK) return UHSDR_DEVICE_ERROR;
+        HIPCHK(hipMemsetAsync(iq, 0, sizeof(int32_t) * 2 * (size_t)h->C * h->N, h->stream));
         return UHSDR_OK;
     }
     // pipelined: this call's hand-off buffer, free once the tx_iq that read it two calls ago is done

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define UHSDR_ABI_VERSION 2
+#define UHSDR_ABI_VERSION 3
 
 typedef enum
 {
@@ -124,8 +124,21 @@ typedef struct uhsdr_rx_config
     int32_t beep_loudness;        /* ts.beep_loudness (DEFAULT_BEEP_LOUDNESS 10) */
     int32_t stereo_enable;        /* ts.stereo_enable: two-channel audio in DEMOD_SSBSTEREO, DEMOD_IQ and
                                      SAM with UHSDR_SAM_SIDEBAND_STEREO (audio_driver.c:2618) */
-    int32_t reserved[11];
+    /* ABI 3 */
+    int32_t board;                /* UHSDR_BOARD_OVI40 (default: USE_TWO_CHANNEL_AUDIO, the oracle's build)
+                                     or UHSDR_BOARD_MCHF (single-channel audio, UI_BRD_MCHF) */
+    int32_t spkr_gain;            /* ts.rx_gain[RX_AUDIO_SPKR].value (mcHF: a software gain above
+                                     CODEC_SPEAKER_MAX_VOLUME 16, audio_driver.c:2880-2885) */
+    int32_t reserved[9];
 } uhsdr_rx_config;
+
+/* the UI board the firmware is built for (hardware/uhsdr_board_config.h:16-24): its output stage
+   (audio_driver.c:2856-2897).  OVI40 (USE_TWO_CHANNEL_AUDIO): a_buffer[1] x10 in place, a_buffer[0]
+   its copy (or the second channel), key beep on both.  mcHF (no USE_TWO_CHANNEL_AUDIO): a_buffer[0]
+   = 10 x a_buffer[1] (line out), a_buffer[1] the speaker channel with the software gain
+   (spkr_gain / 2.5 - 5.35, ui_driver.c:3083-3092) above volume 16, key beep on a_buffer[1] only; no
+   two-channel modes (DEMOD_SSBSTEREO / DEMOD_IQ unsupported, no SAM_SIDEBAND_STEREO). */
+enum { UHSDR_BOARD_OVI40 = 0, UHSDR_BOARD_MCHF = 1 };
 
 /* AudioAgc_SetupAgcWdsp() results (audio_agc.c:126-339) */
 typedef struct uhsdr_agc_plan
@@ -214,7 +227,13 @@ typedef struct uhsdr_rx_plan
        (a_buffer[0] = I + Q, [1] = I - Q), 2 IQ (a_buffer[0] = I, [1] = Q), 3 SAM stereo */
     int32_t stereo;
     int16_t dds_table[1024];      /* softdds DDS_TABLE (softdds/dds_table.c) */
-    int32_t reserved[32];
+    /* ABI 3: output stage of the board (uhsdr_rx_config.board).  line_out_scale above scales
+       a_buffer[1] (OVI40: LINE_OUT_SCALING_FACTOR; mcHF: the speaker software gain, 1 at volume
+       <= 16); line_out0_scale makes a_buffer[0] from the same biquad_2 output (mcHF only:
+       LINE_OUT_SCALING_FACTOR; OVI40's a_buffer[0] is a_buffer[1]'s copy) */
+    int32_t single_channel;       /* 1: mcHF output stage */
+    float   line_out0_scale;
+    int32_t reserved[30];
 } uhsdr_rx_plan;
 
 typedef struct uhsdr_rx_s* uhsdr_rx_handle;
@@ -239,7 +258,8 @@ uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h);
 uhsdr_status uhsdr_rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, int32_t* dst);
 /* OVI40 two-channel modes (plan.stereo != 0): audio = adb.a_buffer[1] (channel 0, codec left),
    audio0 = adb.a_buffer[0] (channel 1, codec right), dst = both channels {l, r}; either may be
-   NULL.  Without stereo, audio0 is not written (a_buffer[0] is a copy of a_buffer[1]). */
+   NULL.  Without stereo on OVI40, audio0 is not written (a_buffer[0] is a copy of a_buffer[1]);
+   on mcHF (uhsdr_rx_config.board) audio0 gets a_buffer[0], the line-out channel. */
 uhsdr_status uhsdr_rx_process_stereo(uhsdr_rx_handle h, const int32_t* iq, float* audio, float* audio0, int32_t* dst);
 /* Same with host buffers: copies in, processes, copies out, synchronises. */
 uhsdr_status uhsdr_rx_process_host(uhsdr_rx_handle h, const int32_t* iq, float* audio, int32_t* dst);

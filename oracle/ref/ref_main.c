@@ -23,6 +23,10 @@
  *   beepfreq= beeploud=   ts.beep_frequency / ts.beep_loudness
  *   stereo=1       ts.stereo_enable (two-channel modes: mode=7 SSB stereo, mode=8 IQ, SAM sam_sb=3)
  *   out_a0=<file>  f32 adb.a_buffer[0] after each call (the second channel in stereo)
+ *   board=         0 OVI40 (this build's default), 1 mcHF: must match the build (the mcHF variant,
+ *                  make mchf, compiles the sources without USE_TWO_CHANNEL_AUDIO)
+ *   spkr=          ts.rx_gain[RX_AUDIO_SPKR].value (AUDIO_GAIN_DEFAULT 16); its active_value as the
+ *                  UI's volume update sets it (ui_driver.c:3083-3092)
  *   out_clip=<file> uint8 per call: ads.adc_clip | adc_half_clip << 1 | adc_quarter_clip << 2,
  *                  read and cleared after every call (the UI's role)
  *   out_tp=<file>  uint8 per call: ts.twinpeaks_tested after the call (AudioDriver_RxHandleTwinpeaks)
@@ -51,6 +55,7 @@
 #include "cw_decoder.h"
 #include "dds_table.h"
 #include "audio_management.h"
+#include "codec.h"
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -252,7 +257,17 @@ int main(int argc, char** argv)
     ts.dsp.peak_frequency = iarg(argc, argv, "peak", 750);
     ts.dsp.bass_gain = iarg(argc, argv, "bass", 2);
     ts.dsp.treble_gain = iarg(argc, argv, "treble", 0);
+#ifdef USE_TWO_CHANNEL_AUDIO
     ts.stereo_enable = iarg(argc, argv, "stereo", 0);
+    if (iarg(argc, argv, "board", 0) != 0) { fprintf(stderr, "board=1 needs the mcHF build (make mchf)\n"); return 2; }
+#else
+    if (iarg(argc, argv, "board", 1) != 1) { fprintf(stderr, "this is the mcHF build: board=1\n"); return 2; }
+#endif
+    /* speaker volume and its software gain (UiDriver_TaskHandler_HighPrioTasks, ui_driver.c:3083-3092) */
+    ts.rx_gain[RX_AUDIO_SPKR].value = iarg(argc, argv, "spkr", AUDIO_GAIN_DEFAULT);
+    ts.rx_gain[RX_AUDIO_SPKR].active_value = 1;
+    if (ts.rx_gain[RX_AUDIO_SPKR].value > CODEC_SPEAKER_MAX_VOLUME)
+        ts.rx_gain[RX_AUDIO_SPKR].active_value = (((float32_t)ts.rx_gain[RX_AUDIO_SPKR].value) / 2.5) - 5.35;
     /* LMS auto notch (audio_driver.c:1166-1186; defaults audio_driver.h:486-495) */
     ts.dsp.notch_numtaps = DSP_NOTCH_NUMTAPS_DEFAULT;
     ts.dsp.notch_delaybuf_len = DSP_NOTCH_DELAYBUF_DEFAULT;

@@ -763,12 +763,19 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
         const int beep = beep_on(p, s);
         for (int i = 0; i < n; i++)
         {
-            float v = active ? a1[i] * p->line_out_scale : 0.0f;    /* mute when squelched, :2843-2850 */
-            if (beep) v += beep_next(p, s);
-            out_a1[i] = v;
-            if (out_a0) out_a0[i] = v;
-            const int32_t d = active ? to_dma(v) : 0;
-            if (dst) { dst[2 * i] = d; dst[2 * i + 1] = d; }
+            /* mute when squelched (:2843-2850), else the board's line-out stage (:2856-2885) */
+            float v1 = 0.0f, v0 = 0.0f;
+            if (active && p->single_channel) { v0 = a1[i] * p->line_out0_scale; v1 = a1[i] * p->line_out_scale; }
+            else if (active) v0 = v1 = a1[i] * p->line_out_scale;
+            if (beep)
+            {
+                const float t = beep_next(p, s);
+                v1 += t;
+                if (!p->single_channel) v0 += t;             /* mcHF: the speaker channel only, :2896 */
+            }
+            out_a1[i] = v1;
+            if (out_a0) out_a0[i] = v0;
+            if (dst) { dst[2 * i] = active ? to_dma(v1) : 0; dst[2 * i + 1] = active ? to_dma(v0) : 0; }
         }
         return;
     }
@@ -829,14 +836,24 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
 
     biquad_df1(p->biquad2, 1, s->bq2, a1, n);          /* audio_driver.c:2832 */
     if (st) biquad_df1(p->biquad2, 1, s->bq2_1, a0o, n);
-    for (int i = 0; i < n; i++) a1[i] = a1[i] * p->line_out_scale;   /* :2860 (OVI40) */
-    if (st) for (int i = 0; i < n; i++) a0o[i] = a0o[i] * p->line_out_scale;
-    else for (int i = 0; i < n; i++) a0o[i] = a1[i];                  /* :2868 copy */
+    if (p->single_channel)
+    {
+        /* mcHF (no USE_TWO_CHANNEL_AUDIO, :2870-2885): line out into a_buffer[0], then the
+           speaker's software gain on a_buffer[1] (1 at volume <= 16: exact) */
+        for (int i = 0; i < n; i++) a0o[i] = a1[i] * p->line_out0_scale;
+        for (int i = 0; i < n; i++) a1[i] = a1[i] * p->line_out_scale;
+    }
+    else
+    {
+        for (int i = 0; i < n; i++) a1[i] = a1[i] * p->line_out_scale;   /* :2860 (OVI40) */
+        if (st) for (int i = 0; i < n; i++) a0o[i] = a0o[i] * p->line_out_scale;
+        else for (int i = 0; i < n; i++) a0o[i] = a1[i];                  /* :2868 copy */
+    }
     if (beep_on(p, s))
         for (int i = 0; i < n; i++)
         {
             const float t = beep_next(p, s);
-            a0o[i] += t;
+            if (!p->single_channel) a0o[i] += t;     /* mcHF: softdds_addSingleTone on a_buffer[1], :2896 */
             a1[i] += t;
         }
     for (int i = 0; i < n; i++)

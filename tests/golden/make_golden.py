@@ -39,6 +39,12 @@ sys.path.insert(0, ROOT)
 from uhsdr_amd import synth  # noqa: E402
 
 REF = os.path.join(ROOT, "oracle", "_ref", "uhsdr_ref")
+# the mcHF output-stage variant (single-channel audio; make -C oracle/ref mchf), for board=1
+REF_MCHF = os.path.join(ROOT, "oracle", "_ref", "mchf", "uhsdr_ref")
+
+
+def ref_bin(args: dict) -> str:
+    return REF_MCHF if int(args.get("board", 0)) == 1 else REF
 NCH = 4
 NFRAMES = 2048
 
@@ -113,6 +119,16 @@ CONFIGS = {
     "p48_ssbstereo_mono": ({"mode": 7, "path": 48}, {}),
     "p70_sam_stereo": ({"mode": 4, "path": 70, "sam_sb": 3, "stereo": 1}, {"am": True}),
     "p83_sam_stereo": ({"mode": 4, "path": 83, "sam_sb": 3, "stereo": 1, "fade": 0}, {"am": True}),
+    # mcHF (board=1: the reference built without USE_TWO_CHANNEL_AUDIO, with UI_BRD_MCHF): a_buffer[0]
+    # = 10 x a_buffer[1] (line out), the speaker's software gain above volume 16, the key beep on
+    # a_buffer[1] only (audio_driver.c:2870-2897); a0 stored too
+    "p48_usb_mchf": ({"mode": 0, "path": 48, "board": 1}, {}),
+    "p48_beep_mchf_spkr24": ({"mode": 0, "path": 48, "board": 1, "spkr": 24, "beep": "8:20"}, {}),
+    "p35_lsb_mchf_spkr30": ({"mode": 1, "path": 35, "board": 1, "spkr": 30}, {"lsb": True}),
+    "p70_sam_mchf_beep": ({"mode": 4, "path": 70, "board": 1, "spkr": 17, "beep": "16:33"}, {"am": True}),
+    "p1_fm_mchf_beep": ({"mode": 5, "path": 1, "board": 1, "sql": 0, "spkr": 20, "beep": "40:100"},
+                        {"fm": True, "frames": 8192}),
+    "p1_fm_mchf_squelched": ({"mode": 5, "path": 1, "board": 1, "spkr": 28, "beep": "8:20"}, {"fm": True, "frames": 4096}),
     "p70_sam_stereo_mono": ({"mode": 4, "path": 70, "sam_sb": 3}, {"am": True}),
     "p48_ssbstereo_notch_beep": ({"mode": 7, "path": 48, "stereo": 1, "dsp": 4, "beep": "16:20"}, {}),
     "p70_sam_stereo_notch": ({"mode": 4, "path": 70, "sam_sb": 3, "stereo": 1, "dsp": 4}, {"am": True}),
@@ -337,7 +353,7 @@ def run_ref(args: dict, iq: np.ndarray, want_a0: bool = False):
     with tempfile.TemporaryDirectory() as td:
         fin, fa, fd, fa0 = (os.path.join(td, x) for x in ("in.bin", "a.bin", "d.bin", "a0.bin"))
         iq.astype(np.int32).tofile(fin)
-        cmd = [REF, f"in={fin}", f"n={n}", f"out_a={fa}", f"out_dst={fd}"]
+        cmd = [ref_bin(args), f"in={fin}", f"n={n}", f"out_a={fa}", f"out_dst={fd}"]
         if want_a0:
             cmd.append(f"out_a0={fa0}")
         cmd += [f"{k}={v}" for k, v in args.items()]
@@ -350,7 +366,7 @@ def run_ref(args: dict, iq: np.ndarray, want_a0: bool = False):
 
 
 def ref_json(args: dict, what: str):
-    cmd = [REF, f"dump={what}"] + [f"{k}={v}" for k, v in args.items()]
+    cmd = [ref_bin(args), f"dump={what}"] + [f"{k}={v}" for k, v in args.items()]
     return json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True).stdout)
 
 
@@ -365,7 +381,8 @@ def make(name: str):
     elif sig.pop("am", False):
         iq = synth.am_iq(np.arange(NCH), 0, NFRAMES)
     else:
-        iq = synth.ssb_iq(np.arange(NCH), 0, NFRAMES, carrier=center if center is not None else 12000.0, **sig)
+        carrier = sig.pop("carrier", 12000.0)
+        iq = synth.ssb_iq(np.arange(NCH), 0, NFRAMES, carrier=center if center is not None else carrier, **sig)
     C = iq.shape[0]
     a1 = np.empty((C, iq.shape[1]), np.float32)
     dst = np.empty((C, iq.shape[1], 2), np.int32)
@@ -408,6 +425,8 @@ def main():
     a = ap.parse_args()
     if not os.path.exists(REF):
         sys.exit(f"{REF} missing: run `make -C oracle/ref` (needs /root/reference)")
+    if not os.path.exists(REF_MCHF):
+        sys.exit(f"{REF_MCHF} missing: run `make -C oracle/ref mchf`")
     if a.only == "cmsis":
         make_cmsis()
         return

@@ -76,30 +76,51 @@ def test_fir_bench_size(cuda, mode, C):
         assert normwise(got, ref) < 1e-5
 
 
-def rx_bench_size(cfg, C, N, calls, gen, cw=False):
+def rx_bench_size(cfg, C, N, calls, gen, cw=False, pipelined=False):
+    """`calls` launches over C channels.  Serial: one call at a time, outputs copied back after
+    each.  Pipelined (how tools/bench_configs.py / bench.py time it): every call enqueued back to
+    back with no host sync or join in between -- rx_front of call k+1 overlapping rx_back of call
+    k, the hand-off buffers rotating -- into per-call outputs, one join at the end."""
     import torch
     pk = picks(C)
     tp = torch.from_numpy(pk).cuda()
     chain = U.RxChain(cfg, channels=C, frames=N)
-    audio = torch.empty((C, N), dtype=torch.float32, device="cuda")
-    dst = torch.empty((C, N, 2), dtype=torch.int32, device="cuda")
+    if pipelined:
+        chain.set_pipelined(True)
+    nbuf = calls if pipelined else 1
+    audio = [torch.empty((C, N), dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+    dst = [torch.empty((C, N, 2), dtype=torch.int32, device="cuda") for _ in range(nbuf)]
     if cw:
         sig = torch.zeros((C, N // 32), dtype=torch.uint8, device="cuda")
         en = torch.zeros((C, max(1, chain.cw_blocks_max)), dtype=torch.float32, device="cuda")
         chain.set_cw_outputs(sig, en)
     ins, outs, douts, sigs, ens = [], [], [], [], []
+    xs = [gen_rows(gen, C, k * N, N) for k in range(calls)] if pipelined else None
     for k in range(calls):
-        x = gen_rows(gen, C, k * N, N)
-        chain.process(x, audio, dst)
+        x = xs[k] if pipelined else gen_rows(gen, C, k * N, N)
+        b = k % nbuf
+        chain.process(x, audio[b], dst[b])
+        if pipelined:
+            continue
         torch.cuda.synchronize()
-        assert bool(torch.isfinite(audio).all().item())
+        assert bool(torch.isfinite(audio[0]).all().item())
         ins.append(x[tp].cpu().numpy())
-        outs.append(audio[tp].cpu().numpy())
-        douts.append(dst[tp].cpu().numpy())
+        outs.append(audio[0][tp].cpu().numpy())
+        douts.append(dst[0][tp].cpu().numpy())
         if cw:
             sigs.append(sig[tp].cpu().numpy())
             ens.append(en[tp, :chain.cw_blocks_last].cpu().numpy())
         del x
+    if pipelined:
+        assert not cw
+        chain.join()
+        torch.cuda.synchronize()
+        for k in range(calls):
+            assert bool(torch.isfinite(audio[k]).all().item())
+            ins.append(xs[k][tp].cpu().numpy())
+            outs.append(audio[k][tp].cpu().numpy())
+            douts.append(dst[k][tp].cpu().numpy())
+        del xs
     chain.close()
     iq = np.concatenate(ins, axis=1)
     o = oracle.OracleRx(U.build_plan(cfg), len(pk))
@@ -109,20 +130,31 @@ def rx_bench_size(cfg, C, N, calls, gen, cw=False):
         assert_bitexact(np.concatenate(ens, 1), ref_en, "CW energy")
     else:
         ref_a, ref_d = o.process(iq, threads=8)
-    assert_bitexact(np.concatenate(outs, 1), ref_a, f"{C} x {N}")
+    assert_bitexact(np.concatenate(outs, 1), ref_a, f"{C} x {N}{' pipelined' if pipelined else ''}")
     np.testing.assert_array_equal(np.concatenate(douts, 1), ref_d)
     return ref_a
 
 
+@pytest.mark.parametrize("pipelined", [False, True], ids=["serial", "pipelined"])
 @pytest.mark.parametrize("sql", [12, 0])
-def test_fm_rx_bench_size(cuda, sql):
+def test_fm_rx_bench_size(cuda, sql, pipelined):
     """squelch 12 is the bench's setting.  The receiver starts squelched and decides every 200
     32-frame calls (audio_driver.c:475, :1600-1640), so the output is muted until then; with
     squelch 0 the first decision opens it, and 28 launches (224 calls) compare the demodulated
     audio itself after it."""
     cfg = U.default_config(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=sql)
-    ref = rx_bench_size(cfg, 32768, 256, 3 if sql else 28, synth.fm_iq)
+    ref = rx_bench_size(cfg, 32768, 256, 3 if sql else 28, synth.fm_iq, pipelined=pipelined)
     assert sql or np.abs(ref).max() > 0
+
+
+@pytest.mark.parametrize("name,kw", [("sam_p70", dict(dmod_mode=U.DEMOD_SAM)), ("am_p70", dict(dmod_mode=U.DEMOD_AM))])
+def test_c3_bench_size(cuda, name, kw):
+    """C3 as tools/bench_configs.py times it: 32768 channels x 1024-frame calls (two 512-frame
+    front launches per call, one channel per wave, padded pair window; the SAM PLL,
+    audio_driver.c:1990-2166), 3 calls."""
+    cfg = U.default_config(filter_path=70, **kw)
+    ref = rx_bench_size(cfg, 32768, 1024, 3, synth.am_iq)
+    assert np.abs(ref).max() > 0
 
 
 def test_cw_bench_size(cuda):
@@ -131,24 +163,38 @@ def test_cw_bench_size(cuda):
     assert np.abs(ref).max() > 0
 
 
-def test_ssb_tx_bench_size(cuda):
+@pytest.mark.parametrize("pipelined", [False, True], ids=["serial", "pipelined"])
+def test_ssb_tx_bench_size(cuda, pipelined):
+    """SSB-TX at the C4 per-GPU share; pipelined is how tools/bench_configs.py times it (tx_voice2
+    of call k+1 beside tx_iq of call k)."""
     import torch
-    C, N, calls = 32768, 256, 3
+    C, N, calls = 32768, 256, 5
     cfg = U.default_tx_config()
     pk = picks(C)
     tp = torch.from_numpy(pk).cuda()
     tx = U.TxChain(cfg, channels=C, frames=N)
-    iq = torch.empty((C, N, 2), dtype=torch.int32, device="cuda")
-    a0 = torch.empty((C, N), dtype=torch.float32, device="cuda")
+    if pipelined:
+        tx.set_pipelined(True)
+    nbuf = calls if pipelined else 1
+    iq = [torch.empty((C, N, 2), dtype=torch.int32, device="cuda") for _ in range(nbuf)]
+    a0 = [torch.empty((C, N), dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+    xs = [gen_rows(synth.tx_audio, C, k * N, N) for k in range(calls)]
     ins, outs, aouts = [], [], []
     for k in range(calls):
-        x = gen_rows(synth.tx_audio, C, k * N, N)
-        tx.process(x, iq, a0)
+        b = k % nbuf
+        tx.process(xs[k], iq[b], a0[b])      # pipelined: no sync or join between calls
+        if pipelined:
+            continue
         torch.cuda.synchronize()
-        ins.append(x[tp].cpu().numpy())
-        outs.append(iq[tp].cpu().numpy())
-        aouts.append(a0[tp].cpu().numpy())
-        del x
+        outs.append(iq[0][tp].cpu().numpy())
+        aouts.append(a0[0][tp].cpu().numpy())
+    if pipelined:
+        tx.join()
+        torch.cuda.synchronize()
+        outs = [iq[k][tp].cpu().numpy() for k in range(calls)]
+        aouts = [a0[k][tp].cpu().numpy() for k in range(calls)]
+    ins = [x[tp].cpu().numpy() for x in xs]
+    del xs
     tx.close()
     ref_iq, ref_a0 = oracle.OracleTx(U.build_tx_plan(cfg), len(pk)).process(np.concatenate(ins, 1), threads=8)
     np.testing.assert_array_equal(np.concatenate(aouts, 1).view(np.uint32), ref_a0.view(np.uint32))

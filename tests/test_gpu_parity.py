@@ -45,13 +45,14 @@ class DeviceStream:
         import torch
         self.torch = torch
         self.chain = U.RxChain(cfg, channels=channels, frames=frames)
-        self.stereo = bool(self.chain.plan.stereo)
+        # a_buffer[0] is an output of its own in stereo and on mcHF (the line-out channel)
+        self.stereo = bool(self.chain.plan.stereo) or bool(self.chain.plan.single_channel)
         self.audio = torch.empty((channels, frames), dtype=torch.float32, device="cuda")
         self.audio0 = torch.empty((channels, frames), dtype=torch.float32, device="cuda")
         self.dst = torch.empty((channels, frames, 2), dtype=torch.int32, device="cuda")
 
     def __call__(self, iq_block):
-        """(a_buffer[1], a_buffer[0], dst); a_buffer[0] is a copy of [1] without stereo"""
+        """(a_buffer[1], a_buffer[0], dst); a_buffer[0] is a copy of [1] in OVI40 mono"""
         self.chain.process_stereo(self.torch.from_numpy(iq_block).cuda(), self.audio, self.audio0, self.dst)
         self.torch.cuda.synchronize()
         a1 = self.audio.cpu().numpy()
@@ -77,6 +78,20 @@ def test_device_call_granularity(cuda, back, frames):
     cfg = U.config_from_ref_args(g["args"])
     a1, _ = run_device(cfg, g["iq"], frames, want_dst=False)
     assert_bitexact(a1, g["a1"], f"frames={frames}")
+
+
+@pytest.mark.parametrize("frames", [512, 1024, 2048])
+@pytest.mark.parametrize("name", ["p70_sam", "p70_am", "p35_usb", "p4_cw", "p86_sam"])
+def test_device_call_granularity_decimate_first(cuda, back, name, frames):
+    """The decimate-first fronts (AM / SAM, narrow SSB / CW) at the call sizes C3 is timed at
+    (1024 frames: two 512-frame front launches per call, one channel per wave, through the padded
+    pair window) against the reference firmware's own outputs (audio_driver.c:1990-2166,
+    :2718-2746)."""
+    g = load(golden_file(name))
+    cfg = U.config_from_ref_args(g["args"])
+    a1, dst = run_device(cfg, g["iq"], frames)
+    assert_bitexact(a1, g["a1"], f"{name} frames={frames}")
+    np.testing.assert_array_equal(dst, g["dst"])
 
 
 @pytest.mark.parametrize("path,channels", [(48, 1000), (35, 333), (55, 130), (4, 65)])
@@ -295,3 +310,46 @@ def test_device_fm_matches_oracle(cuda, path, sql, channels):
     ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), channels).process(iq, threads=8)
     assert_bitexact(a1, ref_a1, f"FM P{path} sql={sql} C={channels}")
     np.testing.assert_array_equal(dst, ref_dst)
+
+
+MCHF_CASES = [
+    ("p48_usb_spkr24", dict(filter_path=48, spkr_gain=24), synth.ssb_iq, 1000, 256),
+    ("p35_lsb", dict(filter_path=35, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 333, 512),
+    ("p70_sam_spkr30", dict(filter_path=70, dmod_mode=U.DEMOD_SAM, spkr_gain=30), synth.am_iq, 130, 1024),
+    ("p1_fm_sql0_spkr20", dict(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=0, spkr_gain=20), synth.fm_iq, 129, 256),
+]
+
+
+@pytest.mark.parametrize("name,kw,gen,C,N", MCHF_CASES, ids=[c[0] for c in MCHF_CASES])
+def test_device_mchf_matches_oracle(cuda, back, name, kw, gen, C, N):
+    """mcHF output stage (single-channel audio, audio_driver.c:2870-2897) on ragged batches with a
+    key beep across calls: a_buffer[1] (speaker, software gain), a_buffer[0] (line out) and the
+    codec frames {a1, a0}, every schedule, against the oracle."""
+    import torch
+    cfg = U.default_config(board=U.BOARD_MCHF, **kw)
+    n = 8 * N
+    iq = gen(np.arange(C), 0, n)
+    o = oracle.OracleRx(U.build_plan(cfg), C)
+    chain = U.RxChain(cfg, channels=C, frames=N)
+    audio = torch.empty((C, N), dtype=torch.float32, device="cuda")
+    audio0 = torch.empty((C, N), dtype=torch.float32, device="cuda")
+    dst = torch.empty((C, N, 2), dtype=torch.int32, device="cuda")
+    got, ref = [[], [], []], [[], [], []]
+    for k in range(n // N):
+        if k == 2:
+            chain.key_beep(N // 32 + 3)
+            o.key_beep(N // 32 + 3)
+        blk = np.ascontiguousarray(iq[:, k * N:(k + 1) * N])
+        chain.process_stereo(torch.from_numpy(blk).cuda(), audio, audio0, dst)
+        torch.cuda.synchronize()
+        for lst, t in zip(got, (audio, audio0, dst)):
+            lst.append(t.cpu().numpy())
+        for lst, r in zip(ref, o.process2(blk)):
+            lst.append(r)
+    chain.close()
+    got = [np.concatenate(x, axis=1) for x in got]
+    ref = [np.concatenate(x, axis=1) for x in ref]
+    assert_bitexact(got[0], ref[0], f"mcHF {name} a_buffer[1]")
+    assert_bitexact(got[1], ref[1], f"mcHF {name} a_buffer[0]")
+    np.testing.assert_array_equal(got[2], ref[2])
+    assert np.abs(ref[1]).max() > 0

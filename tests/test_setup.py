@@ -108,3 +108,23 @@ def test_notch_beep_tone_setup_matches_reference(path):
     expect_notch = bool(dsp & 4) and mode not in (U.DEMOD_CW, U.DEMOD_FM) and not (mode == U.DEMOD_SAM and
                                                                                   p.decimated_freq == 24000)
     assert bool(p.notch_enabled) == expect_notch
+
+
+def test_mchf_board_output_stage_setup():
+    """mcHF (no USE_TWO_CHANNEL_AUDIO, UI_BRD_MCHF): a_buffer[1]'s factor is the speaker's software
+    gain (ui_driver.c:3083-3092: value / 2.5 - 5.35 in double, stored as float) above
+    CODEC_SPEAKER_MAX_VOLUME 16 (codec.h:26-27), else 1; a_buffer[0] = 10 x (audio_driver.c:2873).
+    The two-channel demodulators and the SAM stereo sideband do not exist there."""
+    for v in (0, 5, 16, 17, 20, 24, 30):
+        p = U.build_plan(U.default_config(board=U.BOARD_MCHF, spkr_gain=v))
+        want = np.float32(np.float64(np.float32(v)) / 2.5 - 5.35) if v > 16 else np.float32(1.0)
+        assert np.float32(p.line_out_scale).view(np.uint32) == want.view(np.uint32), v
+        assert p.single_channel == 1 and p.line_out0_scale == 10.0
+    p = U.build_plan(U.default_config(spkr_gain=30))            # OVI40: the speaker gain is the codec's
+    assert p.single_channel == 0 and p.line_out_scale == 10.0 and p.line_out0_scale == 10.0
+    for kw, code in [(dict(dmod_mode=U.DEMOD_SSBSTEREO), U.UHSDR_UNSUPPORTED), (dict(dmod_mode=U.DEMOD_IQ), U.UHSDR_UNSUPPORTED),
+                     (dict(filter_path=70, dmod_mode=U.DEMOD_SAM, sam_sideband=U.SAM_SIDEBAND_STEREO), U.UHSDR_ARGUMENT_ERROR),
+                     (dict(board=2), U.UHSDR_ARGUMENT_ERROR)]:
+        cfg = U.default_config(**{"board": U.BOARD_MCHF, **kw})
+        plan = U.RxPlan()
+        assert U.load().uhsdr_rx_plan_build(C.byref(cfg), C.byref(plan)) == code, kw

@@ -6,7 +6,8 @@ package is the thin host-side mirror used by tests and the benchmark.
 from ._abi import (RxConfig, RxPlan, build_plan, plan_supported, plan_fma_ok, config_from_ref_args, default_config, load,  # noqa: F401
                    DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI,
                    DEMOD_SSBSTEREO, DEMOD_IQ, SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB,
-                   SAM_SIDEBAND_STEREO, DSP_NOTCH_ENABLE,
+                   SAM_SIDEBAND_STEREO, DSP_NOTCH_ENABLE, BOARD_OVI40, BOARD_MCHF,
+                   UHSDR_OK, UHSDR_ARGUMENT_ERROR, UHSDR_UNSUPPORTED,
                    PRECISION_EXACT, PRECISION_FMA,
                    SCHEDULE_AUTO, SCHEDULE_SPLIT_PIPE, SCHEDULE_SPLIT_FUSED, SCHEDULE_CHAIN, ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP,
                    TWINPEAKS_SAMPLING, TWINPEAKS_DONE, TWINPEAKS_WAIT, TWINPEAKS_UNCORRECTABLE,

@@ -26,6 +26,7 @@ UHSDR_DEVICE_ERROR = -11
 
 DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI, DEMOD_SSBSTEREO, DEMOD_IQ = range(9)
 SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB, SAM_SIDEBAND_STEREO = range(4)
+BOARD_OVI40, BOARD_MCHF = 0, 1                 # uhsdr_rx_config.board: the UI board's output stage
 DSP_NOTCH_ENABLE, DSP_MNOTCH_ENABLE, DSP_MPEAK_ENABLE = 0x04, 0x10, 0x20
 PRECISION_EXACT, PRECISION_FMA = 0, 1          # uhsdr_rx_set_precision
 SCHEDULE_AUTO, SCHEDULE_SPLIT_PIPE, SCHEDULE_SPLIT_FUSED, SCHEDULE_CHAIN = range(4)   # uhsdr_rx_set_schedule
@@ -47,7 +48,8 @@ class RxConfig(C.Structure):
         ("cw_sidetone_freq", C.c_int32), ("cw_decoder_blocksize", C.c_int32), ("cw_decoder_thresh", C.c_int32),
         ("cw_decoder_noisecancel", C.c_int32),
         ("notch_mu", C.c_int32), ("fm_tone_det", C.c_int32), ("beep_frequency", C.c_int32),
-        ("beep_loudness", C.c_int32), ("stereo_enable", C.c_int32), ("reserved", C.c_int32 * 11),
+        ("beep_loudness", C.c_int32), ("stereo_enable", C.c_int32),
+        ("board", C.c_int32), ("spkr_gain", C.c_int32), ("reserved", C.c_int32 * 9),
     ]
 
 
@@ -90,7 +92,7 @@ class RxPlan(C.Structure):
         ("notch_mu", C.c_float), ("tone_det_enabled", C.c_int32), ("tone_r", C.c_float * 3),
         ("tone_cos", C.c_float * 3), ("tone_sin", C.c_float * 3), ("beep_step", C.c_uint32),
         ("beep_scale", C.c_float), ("stereo", C.c_int32), ("dds_table", C.c_int16 * 1024),
-        ("reserved", C.c_int32 * 32),
+        ("single_channel", C.c_int32), ("line_out0_scale", C.c_float), ("reserved", C.c_int32 * 30),
     ]
 
 
@@ -328,6 +330,7 @@ REF_ARG_MAP = {
     "sidetone": "cw_sidetone_freq", "cwblock": "cw_decoder_blocksize", "cwthresh": "cw_decoder_thresh",
     "cwnc": "cw_decoder_noisecancel", "notch_mu": "notch_mu", "tonedet": "fm_tone_det",
     "beepfreq": "beep_frequency", "beeploud": "beep_loudness", "stereo": "stereo_enable",
+    "board": "board", "spkr": "spkr_gain",
 }
 # uhsdr_ref run-time controls that are calls, not configuration (tests drive them through the ABI)
 REF_RUNTIME_ARGS = {"beep", "uiperiod"}

@@ -617,7 +617,7 @@ struct BackArgs
     const float* adec;   // [C][Nd]  (AM / SAM: decimated I)
     const float* adec_q; // [C][Nd]  AM / SAM: decimated Q
     float* audio;        // [C][N]  or null: adb.a_buffer[1]
-    float* audio0;       // [C][N]  or null: adb.a_buffer[0], stereo only (the second channel)
+    float* audio0;       // [C][N]  or null: adb.a_buffer[0], stereo (the second channel) or mcHF (line out)
     int2* dst;           // [C][N]  or null
     BackState s;
     int C, N, Nd;
@@ -1244,8 +1244,8 @@ struct AudioStage
     }
 };
 
-// ---- output stage: biquad_2 (audio_driver.c:2832), line-out scale (:2860); f32 audio and
-//      int32 codec frames (:2911-2923) by the caller ----
+// ---- output stage: biquad_2 (audio_driver.c:2832); the board's line-out stage (:2845-2897) and
+//      the f32 audio and int32 codec frames (:2911-2923) by the caller (line_out4) ----
 struct OutputStage
 {
     float bq2[4], b2[5], lo;
@@ -1262,8 +1262,7 @@ struct OutputStage
 
     __device__ __forceinline__ float step(float v)
     {
-        v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
-        return v * lo;
+        return biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
     }
 
     __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l)
@@ -1274,18 +1273,62 @@ struct OutputStage
     }
 };
 
-// four consecutive output frames n0..n0+3 of a call: f32 audio and int32 codec frames
-__device__ __forceinline__ void back_store4(const BackArgs& a, const BackLane& l, int call, int n0, const float (&y)[4])
+// The mono output stage of the board on four consecutive frames fr0..fr0+3 of a channel, from
+// biquad_2's outputs v (audio_driver.c:2845-2923); row = the offset of frame fr0 in the [C][N]
+// outputs (f32 audio, int32 codec frames, and on mcHF the line-out channel a_buffer[0] when
+// audio0 is given).  on == false: do_mute_output (FM squelch) zeroes both buffers and the codec
+// frames, the key beep is still added to the audio.
+//  * OVI40 (USE_TWO_CHANNEL_AUDIO, :2856-2869): a_buffer[1] = v x LINE_OUT_SCALING_FACTOR, a_buffer[0]
+//    its copy; the beep on both (softdds_addSingleToneToTwobuffers, :2893-2894); dst {a1, a1}.
+//  * mcHF (single channel, :2870-2885): a_buffer[0] = v x 10 (line out), a_buffer[1] = v x the
+//    speaker's software gain (the multiply by 1 is exact at volume <= 16); the beep on a_buffer[1]
+//    only (softdds_addSingleTone, :2896); dst {a1, a0}.
+__device__ __forceinline__ void line_out4(const BackArgs& a, size_t row, int fr0, const float (&v)[4], bool on = true)
+{
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    const float lo = P->line_out_scale;
+    float y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = on ? v[j] * lo : 0.0f;
+    if (a.beep_n1 > fr0 && a.beep_n0 < fr0 + 4)
+    {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (fr0 + j >= a.beep_n0 && fr0 + j < a.beep_n1) y[j] += beep_tone(a, fr0 + j);
+    }
+    if (a.audio) *(float4*)(a.audio + row) = make_float4(y[0], y[1], y[2], y[3]);
+    float y0[4];
+    if (P->single_channel)
+    {
+        const float lo0 = P->line_out0_scale;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y0[j] = on ? v[j] * lo0 : 0.0f;
+        if (a.audio0) *(float4*)(a.audio0 + row) = make_float4(y0[0], y0[1], y0[2], y0[3]);
+    }
+    if (!a.dst) return;
+    int2* dd = a.dst + row;
+    int d1[4], d0[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d1[j] = on ? to_dma(y[j]) : 0;
+    if (P->single_channel)
+    {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d0[j] = on ? to_dma(y0[j]) : 0;
+    }
+    else
+    {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d0[j] = d1[j];
+    }
+    *(int4*)(dd) = make_int4(d1[0], d0[0], d1[1], d0[1]);
+    *(int4*)(dd + 2) = make_int4(d1[2], d0[2], d1[3], d0[3]);
+}
+
+// four consecutive output frames n0..n0+3 of a call from biquad_2's outputs: f32 audio and int32 codec frames
+__device__ __forceinline__ void back_store4(const BackArgs& a, const BackLane& l, int call, int n0, const float (&v)[4])
 {
     if (!l.live) return;
-    if (a.audio) *(float4*)(a.audio + (size_t)l.c * a.N + call * BLK + n0) = make_float4(y[0], y[1], y[2], y[3]);
-    if (a.dst)
-    {
-        int2* dd = a.dst + (size_t)l.c * a.N + call * BLK;
-        const int d0 = to_dma(y[0]), d1 = to_dma(y[1]), d2 = to_dma(y[2]), d3 = to_dma(y[3]);
-        *(int4*)(dd + n0) = make_int4(d0, d0, d1, d1);
-        *(int4*)(dd + n0 + 2) = make_int4(d2, d2, d3, d3);
-    }
+    line_out4(a, (size_t)l.c * a.N + call * BLK + n0, call * BLK + n0, v);
 }
 
 // ---- demod stage: AudioDriver_DemodSAM (audio_driver.c:1990-2166): AM envelope
@@ -1794,15 +1837,6 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
         for (int n = 0; n < BLK; ++n) y[n] = mi[n * BACK_CH];      // one batch of LDS reads
 #pragma unroll
         for (int n = 0; n < BLK; ++n) y[n] = s.step(y[n]);
-        if (a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK)   // key beep in this call
-        {
-#pragma unroll
-            for (int n = 0; n < BLK; ++n)
-            {
-                const int fr = call * BLK + n;
-                if (fr >= a.beep_n0 && fr < a.beep_n1) y[n] += beep_tone(a, fr);
-            }
-        }
 #pragma unroll
         for (int n0 = 0; n0 < BLK; n0 += 4)
         {
@@ -1861,36 +1895,19 @@ __device__ __forceinline__ void fused_store_call(const BackArgs& a, const BackLa
 {
     wave_sync();                                         // the wave's rows are complete
     const int g = l.lane >> 3, j = l.lane & 7;
-    const bool beep = a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK;
     const int c0 = l.c - l.lane;
 #pragma unroll
     for (int k = 0; k < 8; ++k)
     {
         const int cc = 8 * k + g;
         const float* r = ys + cc * FUSED_YPITCH + 4 * j;
-        float y[4] = { r[0], r[1], r[2], r[3] };
-        if (beep)
-        {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-            {
-                const int fr = call * BLK + 4 * j + i;
-                if (fr >= a.beep_n0 && fr < a.beep_n1) y[i] += beep_tone(a, fr);
-            }
-        }
+        const float v[4] = { r[0], r[1], r[2], r[3] };
         const int c = c0 + cc;
         if (c >= a.C) continue;
         // uniform base of rows c0 + 8k.. (SGPRs) + the lane's 32-bit offset
         const size_t rb = (size_t)(c0 + 8 * k) * a.N + call * BLK;
         const unsigned off = (unsigned)g * (unsigned)a.N + 4 * j;
-        if (a.audio) *(float4*)(a.audio + rb + off) = make_float4(y[0], y[1], y[2], y[3]);
-        if (a.dst)
-        {
-            int2* dd = a.dst + rb + off;
-            const int d0 = to_dma(y[0]), d1 = to_dma(y[1]), d2 = to_dma(y[2]), d3 = to_dma(y[3]);
-            *(int4*)(dd) = make_int4(d0, d0, d1, d1);
-            *(int4*)(dd + 2) = make_int4(d2, d2, d3, d3);
-        }
+        line_out4(a, rb + off, call * BLK + 4 * j, v);
     }
     wave_sync();                                         // rows read before the next call writes
 }
@@ -1932,7 +1949,6 @@ __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys, in
     if (PRE > 0) { to_vgpr(pre.k); to_vgpr(pre.v); }
     if (AA > 0) { to_vgpr(aa.k); to_vgpr(aa.v); }
     to_vgpr(ou.b2);
-    ou.lo = to_vgpr(ou.lo);
     if (!B1S) to_vgpr(au.b1);
 #endif
     ag.agc_on = AGC_ON;
@@ -2119,8 +2135,8 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_stereo(BackArgs a)
 #pragma unroll
             for (int j = 0; j < L; ++j)
             {
-                y0[m * L + j] = ou0.step(aa0.step(u0[j]));
-                y1[m * L + j] = ou1.step(aa1.step(u1[j]));
+                y0[m * L + j] = ou0.step(aa0.step(u0[j])) * ou0.lo;
+                y1[m * L + j] = ou1.step(aa1.step(u1[j])) * ou1.lo;
             }
         }
         if (a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK)
@@ -2453,7 +2469,7 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
         for (int i = 0; i < 5; ++i) b2[i] = P->biquad2[i];
 #pragma unroll
         for (int i = 0; i < 4; ++i) bq2[i] = a.s.bq2[i * C + cl];
-        const float lo = P->line_out_scale, fs = P->fm_scale;
+        const float fs = P->fm_scale;
         for (int it = 0; it <= calls; ++it)
         {
             if (it > 0)
@@ -2461,33 +2477,15 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                 const int call = it - 1;
                 const float* mi = dem + (call & 1) * BLK * BACK_CH + lane;
                 const bool on = act[(call & 1) * BACK_CH + lane] != 0.0f;
-                float* ao = a.audio ? a.audio + (size_t)c * a.N + call * BLK : nullptr;
-                int2* dd = a.dst ? a.dst + (size_t)c * a.N + call * BLK : nullptr;
 #pragma unroll 2
                 for (int n0 = 0; n0 < BLK; n0 += 4)
                 {
-                    float y[4];
+                    float v[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                    {
-                        float v = mi[(n0 + j) * BACK_CH] * fs;
-                        v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
-                        y[j] = on ? v * lo : 0.0f;
-                        // the beep is added after muting (audio_driver.c:2891-2898); dst stays 0 when muted
-                        const int fr = call * BLK + n0 + j;
-                        if (fr >= a.beep_n0 && fr < a.beep_n1) y[j] += beep_tone(a, fr);
-                    }
-                    if (live)
-                    {
-                        if (ao) *(float4*)(ao + n0) = make_float4(y[0], y[1], y[2], y[3]);
-                        if (dd)
-                        {
-                            const int d0 = on ? to_dma(y[0]) : 0, d1 = on ? to_dma(y[1]) : 0;
-                            const int d2 = on ? to_dma(y[2]) : 0, d3 = on ? to_dma(y[3]) : 0;
-                            *(int4*)(dd + n0) = make_int4(d0, d0, d1, d1);
-                            *(int4*)(dd + n0 + 2) = make_int4(d2, d2, d3, d3);
-                        }
-                    }
+                        v[j] = biquad_step(mi[(n0 + j) * BACK_CH] * fs, bq2[0], bq2[1], bq2[2], bq2[3], b2);
+                    // muted: both buffers zero, the beep still added (audio_driver.c:2845-2898)
+                    if (live) line_out4(a, (size_t)c * a.N + call * BLK + n0, call * BLK + n0, v, on);
                 }
             }
             lds_barrier();
@@ -3230,7 +3228,7 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     ba.adec = adec;
     ba.adec_q = adec_q;
     ba.audio = audio;
-    ba.audio0 = h->plan.stereo ? audio0 : nullptr;
+    ba.audio0 = (h->plan.stereo || h->plan.single_channel) ? audio0 : nullptr;   // mcHF: the line-out channel
     ba.dst = (int2*)dst;
     ba.s = h->bs;
     ba.C = h->C; ba.N = h->N; ba.Nd = h->Nd;

@@ -28,6 +28,7 @@
 #define POST_AGC_GAIN_SCALING_DECIMATE_4 3.46                               /* audio_driver.h:362 */
 #define POST_AGC_GAIN_SCALING_DECIMATE_2 (POST_AGC_GAIN_SCALING_DECIMATE_4 * 0.6) /* :364 */
 #define LINE_OUT_SCALING_FACTOR 10          /* audio_driver.h:396 */
+#define MCHF_SPEAKER_MAX_VOLUME 16          /* CODEC_SPEAKER_MAX_VOLUME with UI_BRD_MCHF, codec.h:26-27 */
 #define FILTER_MODE_CW 0
 #define FILTER_MODE_SSB 1
 #define FILTER_MODE_AM 2
@@ -92,6 +93,8 @@ void uhsdr_rx_config_default(uhsdr_rx_config* c)
     c->beep_frequency = 1000;                    /* DEFAULT_BEEP_FREQUENCY, audio_driver.h:455 */
     c->beep_loudness = 10;                       /* DEFAULT_BEEP_LOUDNESS, audio_driver.h:460 */
     c->stereo_enable = 0;
+    c->board = UHSDR_BOARD_OVI40;
+    c->spkr_gain = 16;                           /* AUDIO_GAIN_DEFAULT, ui_configuration.h:74; ui_configuration.c:71 */
 }
 
 /* AudioFilter_CalcGoertzel, audio_filter.c:1281-1288 (Goertzel.a is an int) */
@@ -411,7 +414,31 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
     const float post_agc_gain_scaling = (f->sample_rate_dec == 4) ? POST_AGC_GAIN_SCALING_DECIMATE_4
                                                                   : POST_AGC_GAIN_SCALING_DECIMATE_2;
     p->post_agc_scale = post_agc_gain_scaling * (is_am ? 0.5 : 0.333);
-    p->line_out_scale = LINE_OUT_SCALING_FACTOR;
+    /* output stage of the board, audio_driver.c:2856-2885 */
+    if (cfg->board != UHSDR_BOARD_OVI40 && cfg->board != UHSDR_BOARD_MCHF)
+    { uhsdr_set_error("board %d: UHSDR_BOARD_OVI40 or UHSDR_BOARD_MCHF", cfg->board); return UHSDR_ARGUMENT_ERROR; }
+    p->single_channel = cfg->board == UHSDR_BOARD_MCHF;
+    if (p->single_channel)
+    {
+        /* no USE_TWO_CHANNEL_AUDIO: use_stereo is false (:2620), the two-channel demodulators are
+           not compiled (:2769-2778) and SAM_SIDEBAND_STEREO does not exist (audio_driver.h:186-188) */
+        if (mode == UHSDR_DEMOD_SSBSTEREO || mode == UHSDR_DEMOD_IQ)
+        { uhsdr_set_error("dmod_mode %d needs two-channel audio (OVI40)", mode); return UHSDR_UNSUPPORTED; }
+        if (mode == UHSDR_DEMOD_SAM && cfg->sam_sideband == UHSDR_SAM_SIDEBAND_STEREO)
+        { uhsdr_set_error("SAM stereo sideband needs two-channel audio (OVI40)"); return UHSDR_ARGUMENT_ERROR; }
+        /* UiDriver's volume update (ui_driver.c:3083-3092) feeds the software gain the driver
+           applies above the codec's range (audio_driver.c:2880-2885, CODEC_SPEAKER_MAX_VOLUME 16
+           for UI_BRD_MCHF, codec.h:26-27) */
+        float active_value = 1;
+        if (cfg->spkr_gain > MCHF_SPEAKER_MAX_VOLUME) active_value = (((float)cfg->spkr_gain) / 2.5) - 5.35;
+        p->line_out_scale = active_value;
+        p->line_out0_scale = LINE_OUT_SCALING_FACTOR;
+    }
+    else
+    {
+        p->line_out_scale = LINE_OUT_SCALING_FACTOR;
+        p->line_out0_scale = LINE_OUT_SCALING_FACTOR;
+    }
 
     setup_agc(&p->agc, cfg, (float)p->decimated_freq, is_am);
 

@@ -190,7 +190,7 @@ typedef struct uhsdr_rx_plan
     float   biquad1[20];          /* IIR_biquad_1: 4 stages {b0,b1,b2,a1,a2} */
     float   biquad2[5];           /* IIR_biquad_2: 1 stage */
     float   post_agc_scale;       /* audio_driver.c:2513-2524 */
-    float   line_out_scale;       /* LINE_OUT_SCALING_FACTOR, audio_driver.h:396 */
+    float   line_out_scale;       /* LINE_OUT_SCALING_FACTOR, audio_driver.h:396 (mcHF: 1, see below) */
     uhsdr_agc_plan agc;
     /* AM / SAM (AudioDriver_DemodSAM, audio_driver.c:1990-2166) */
     float   dec_q[UHSDR_MAX_DEC_TAPS];  /* DECIMATE_RX_Q taps: the path's Q table for AM/SAM (audio_filter.c:1167-1176) */
@@ -227,13 +227,14 @@ typedef struct uhsdr_rx_plan
        (a_buffer[0] = I + Q, [1] = I - Q), 2 IQ (a_buffer[0] = I, [1] = Q), 3 SAM stereo */
     int32_t stereo;
     int16_t dds_table[1024];      /* softdds DDS_TABLE (softdds/dds_table.c) */
-    /* ABI 3: output stage of the board (uhsdr_rx_config.board).  line_out_scale above scales
-       a_buffer[1] (OVI40: LINE_OUT_SCALING_FACTOR; mcHF: the speaker software gain, 1 at volume
-       <= 16); line_out0_scale makes a_buffer[0] from the same biquad_2 output (mcHF only:
-       LINE_OUT_SCALING_FACTOR; OVI40's a_buffer[0] is a_buffer[1]'s copy) */
+    /* ABI 3: output stage of the board (uhsdr_rx_config.board).  line_out_scale above is
+       LINE_OUT_SCALING_FACTOR on OVI40 (a_buffer[1] x10 in place) and 1 on mcHF, where a_buffer[0]
+       = line_out0_scale (LINE_OUT_SCALING_FACTOR) x biquad_2's output and a_buffer[1] = spkr_scale
+       (the speaker's software gain, 1 at volume <= 16) x the same */
     int32_t single_channel;       /* 1: mcHF output stage */
     float   line_out0_scale;
-    int32_t reserved[30];
+    float   spkr_scale;
+    int32_t reserved[29];
 } uhsdr_rx_plan;
 
 typedef struct uhsdr_rx_s* uhsdr_rx_handle;

@@ -765,7 +765,7 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
         {
             /* mute when squelched (:2843-2850), else the board's line-out stage (:2856-2885) */
             float v1 = 0.0f, v0 = 0.0f;
-            if (active && p->single_channel) { v0 = a1[i] * p->line_out0_scale; v1 = a1[i] * p->line_out_scale; }
+            if (active && p->single_channel) { v0 = a1[i] * p->line_out0_scale; v1 = a1[i] * p->spkr_scale; }
             else if (active) v0 = v1 = a1[i] * p->line_out_scale;
             if (beep)
             {
@@ -841,7 +841,7 @@ static void rx_call(const uhsdr_rx_plan* p, uo_rx_state* s, const int32_t* iq, f
         /* mcHF (no USE_TWO_CHANNEL_AUDIO, :2870-2885): line out into a_buffer[0], then the
            speaker's software gain on a_buffer[1] (1 at volume <= 16: exact) */
         for (int i = 0; i < n; i++) a0o[i] = a1[i] * p->line_out0_scale;
-        for (int i = 0; i < n; i++) a1[i] = a1[i] * p->line_out_scale;
+        for (int i = 0; i < n; i++) a1[i] = a1[i] * p->spkr_scale;
     }
     else
     {

@@ -118,8 +118,8 @@ def test_mchf_board_output_stage_setup():
     for v in (0, 5, 16, 17, 20, 24, 30):
         p = U.build_plan(U.default_config(board=U.BOARD_MCHF, spkr_gain=v))
         want = np.float32(np.float64(np.float32(v)) / 2.5 - 5.35) if v > 16 else np.float32(1.0)
-        assert np.float32(p.line_out_scale).view(np.uint32) == want.view(np.uint32), v
-        assert p.single_channel == 1 and p.line_out0_scale == 10.0
+        assert np.float32(p.spkr_scale).view(np.uint32) == want.view(np.uint32), v
+        assert p.single_channel == 1 and p.line_out0_scale == 10.0 and p.line_out_scale == 1.0
     p = U.build_plan(U.default_config(spkr_gain=30))            # OVI40: the speaker gain is the codec's
     assert p.single_channel == 0 and p.line_out_scale == 10.0 and p.line_out0_scale == 10.0
     for kw, code in [(dict(dmod_mode=U.DEMOD_SSBSTEREO), U.UHSDR_UNSUPPORTED), (dict(dmod_mode=U.DEMOD_IQ), U.UHSDR_UNSUPPORTED),

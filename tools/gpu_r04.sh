@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 tag=${1:-a}
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu_$tag.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu_$tag.log 2>&1; rc=$?
 tail -5 gpurun_out/pytest_gpu_$tag.log
 [ $rc -eq 0 ] || { tail -80 gpurun_out/pytest_gpu_$tag.log; exit $rc; }
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench20_$tag.json 2> gpurun_out/bench20_$tag.err || { tail -30 gpurun_out/bench20_$tag.err; exit 1; }

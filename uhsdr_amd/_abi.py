@@ -92,7 +92,8 @@ class RxPlan(C.Structure):
         ("notch_mu", C.c_float), ("tone_det_enabled", C.c_int32), ("tone_r", C.c_float * 3),
         ("tone_cos", C.c_float * 3), ("tone_sin", C.c_float * 3), ("beep_step", C.c_uint32),
         ("beep_scale", C.c_float), ("stereo", C.c_int32), ("dds_table", C.c_int16 * 1024),
-        ("single_channel", C.c_int32), ("line_out0_scale", C.c_float), ("reserved", C.c_int32 * 30),
+        ("single_channel", C.c_int32), ("line_out0_scale", C.c_float), ("spkr_scale", C.c_float),
+        ("reserved", C.c_int32 * 29),
     ]
 
 

@@ -617,7 +617,8 @@ struct BackArgs
     const float* adec;   // [C][Nd]  (AM / SAM: decimated I)
     const float* adec_q; // [C][Nd]  AM / SAM: decimated Q
     float* audio;        // [C][N]  or null: adb.a_buffer[1]
-    float* audio0;       // [C][N]  or null: adb.a_buffer[0], stereo (the second channel) or mcHF (line out)
+    float* audio0;       // [C][N]  or null: adb.a_buffer[0], stereo only (the second channel)
+    uint8_t* mute;       // [C][N/32] or null: mcHF FM, the squelch's on / off per 32-frame call
     int2* dst;           // [C][N]  or null
     BackState s;
     int C, N, Nd;
@@ -1244,8 +1245,9 @@ struct AudioStage
     }
 };
 
-// ---- output stage: biquad_2 (audio_driver.c:2832); the board's line-out stage (:2845-2897) and
-//      the f32 audio and int32 codec frames (:2911-2923) by the caller (line_out4) ----
+// ---- output stage: biquad_2 (audio_driver.c:2832), line-out scale (:2860; 1 on mcHF); the rest
+//      of the board's output stage and the f32 audio / int32 codec frames (:2845-2923) by the
+//      caller (line_out4) ----
 struct OutputStage
 {
     float bq2[4], b2[5], lo;
@@ -1262,7 +1264,8 @@ struct OutputStage
 
     __device__ __forceinline__ float step(float v)
     {
-        return biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
+        v = biquad_step(v, bq2[0], bq2[1], bq2[2], bq2[3], b2);
+        return v * lo;
     }
 
     __device__ __forceinline__ void store(const BackArgs& a, const BackLane& l)
@@ -1273,62 +1276,80 @@ struct OutputStage
     }
 };
 
-// The mono output stage of the board on four consecutive frames fr0..fr0+3 of a channel, from
-// biquad_2's outputs v (audio_driver.c:2845-2923); row = the offset of frame fr0 in the [C][N]
-// outputs (f32 audio, int32 codec frames, and on mcHF the line-out channel a_buffer[0] when
-// audio0 is given).  on == false: do_mute_output (FM squelch) zeroes both buffers and the codec
-// frames, the key beep is still added to the audio.
-//  * OVI40 (USE_TWO_CHANNEL_AUDIO, :2856-2869): a_buffer[1] = v x LINE_OUT_SCALING_FACTOR, a_buffer[0]
-//    its copy; the beep on both (softdds_addSingleToneToTwobuffers, :2893-2894); dst {a1, a1}.
-//  * mcHF (single channel, :2870-2885): a_buffer[0] = v x 10 (line out), a_buffer[1] = v x the
-//    speaker's software gain (the multiply by 1 is exact at volume <= 16); the beep on a_buffer[1]
-//    only (softdds_addSingleTone, :2896); dst {a1, a0}.
-__device__ __forceinline__ void line_out4(const BackArgs& a, size_t row, int fr0, const float (&v)[4], bool on = true)
+// The OVI40 output stage on four consecutive frames fr0..fr0+3 of a channel (audio_driver.c:
+// 2845-2923; USE_TWO_CHANNEL_AUDIO: a_buffer[1] x LINE_OUT_SCALING_FACTOR in place, a_buffer[0] its
+// copy, the key beep on both, dst {a1, a1}) from u = biquad_2's output x plan.line_out_scale
+// (OutputStage::step); rb + off = the offset of frame fr0 in the [C][N] outputs (the fused back
+// end passes a wave-uniform rb, so its addresses are an SGPR base plus a 32-bit lane offset); call = its 32-frame call (the key
+// beep's test per call is wave-uniform).  on == false:
+// do_mute_output (FM squelch) zeroes both buffers and the codec frames; the key beep is still
+// added to the audio.  mcHF plans run these kernels with line_out_scale 1, no beep and no codec
+// frames into a scratch row, and rx_line_out_mchf finishes their output stage.
+__device__ __forceinline__ void line_out4(const BackArgs& a, size_t rb, unsigned off, int call, int fr0,
+                                          const float (&u)[4], bool on = true)
 {
-    const uhsdr_rx_plan* __restrict__ P = a.plan;
-    const float lo = P->line_out_scale;
     float y[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) y[j] = on ? v[j] * lo : 0.0f;
-    if (a.beep_n1 > fr0 && a.beep_n0 < fr0 + 4)
+    for (int j = 0; j < 4; ++j) y[j] = on ? u[j] : 0.0f;
+    if (a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK)      // key beep in this call
     {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             if (fr0 + j >= a.beep_n0 && fr0 + j < a.beep_n1) y[j] += beep_tone(a, fr0 + j);
     }
-    if (a.audio) *(float4*)(a.audio + row) = make_float4(y[0], y[1], y[2], y[3]);
-    float y0[4];
-    if (P->single_channel)
+    if (a.audio) *(float4*)((a.audio + rb) + off) = make_float4(y[0], y[1], y[2], y[3]);
+    if (a.dst)
     {
-        const float lo0 = P->line_out0_scale;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) y0[j] = on ? v[j] * lo0 : 0.0f;
-        if (a.audio0) *(float4*)(a.audio0 + row) = make_float4(y0[0], y0[1], y0[2], y0[3]);
+        int2* dd = (a.dst + rb) + off;
+        const int d0 = on ? to_dma(y[0]) : 0, d1 = on ? to_dma(y[1]) : 0;
+        const int d2 = on ? to_dma(y[2]) : 0, d3 = on ? to_dma(y[3]) : 0;
+        *(int4*)(dd) = make_int4(d0, d0, d1, d1);
+        *(int4*)(dd + 2) = make_int4(d2, d2, d3, d3);
     }
-    if (!a.dst) return;
-    int2* dd = a.dst + row;
-    int d1[4], d0[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) d1[j] = on ? to_dma(y[j]) : 0;
-    if (P->single_channel)
-    {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d0[j] = on ? to_dma(y0[j]) : 0;
-    }
-    else
-    {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d0[j] = d1[j];
-    }
-    *(int4*)(dd) = make_int4(d1[0], d0[0], d1[1], d0[1]);
-    *(int4*)(dd + 2) = make_int4(d1[2], d0[2], d1[3], d0[3]);
 }
 
-// four consecutive output frames n0..n0+3 of a call from biquad_2's outputs: f32 audio and int32 codec frames
-__device__ __forceinline__ void back_store4(const BackArgs& a, const BackLane& l, int call, int n0, const float (&v)[4])
+// mcHF output stage (no USE_TWO_CHANNEL_AUDIO, audio_driver.c:2870-2897, 2911-2923) after any back
+// end: u = biquad_2's output (the back end ran with line_out_scale 1, no beep, no codec frames);
+// a_buffer[0] = u x LINE_OUT_SCALING_FACTOR (line out), a_buffer[1] = u x the speaker's software
+// gain (spkr_scale), the key beep on a_buffer[1] only (softdds_addSingleTone, :2896), dst {a1, a0};
+// FM: a squelched call (mute) gives a1 = the beep alone, a0 = 0, dst 0.  Four frames per lane.
+__global__ void __launch_bounds__(256) rx_line_out_mchf(BackArgs a, const float* __restrict__ u, const uint8_t* __restrict__ mute)
+{
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;       // quad of frames
+    const int qpc = a.N / 4;
+    if (q >= (size_t)a.C * qpc) return;
+    const int fr0 = (int)(q % qpc) * 4;
+    const size_t row = q * 4;
+    const float4 x = *(const float4*)(u + row);
+    const bool on = !mute || mute[row / BLK] != 0;
+    const float sp = P->spkr_scale, lo0 = P->line_out0_scale;
+    const float v[4] = { x.x, x.y, x.z, x.w };
+    float y1[4], y0[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+    {
+        y1[j] = v[j] * sp;                   // v == +0 when squelched: the product is +0 as the fill's
+        y0[j] = v[j] * lo0;
+        if (fr0 + j >= a.beep_n0 && fr0 + j < a.beep_n1) y1[j] += beep_tone(a, fr0 + j);
+    }
+    if (a.audio) *(float4*)(a.audio + row) = make_float4(y1[0], y1[1], y1[2], y1[3]);
+    if (a.audio0) *(float4*)(a.audio0 + row) = make_float4(y0[0], y0[1], y0[2], y0[3]);
+    if (a.dst)
+    {
+        int d1[4], d0[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { d1[j] = on ? to_dma(y1[j]) : 0; d0[j] = on ? to_dma(y0[j]) : 0; }
+        *(int4*)(a.dst + row) = make_int4(d1[0], d0[0], d1[1], d0[1]);
+        *(int4*)(a.dst + row + 2) = make_int4(d1[2], d0[2], d1[3], d0[3]);
+    }
+}
+
+// four consecutive output frames n0..n0+3 of a call (OutputStage::step's): f32 audio and int32 codec frames
+__device__ __forceinline__ void back_store4(const BackArgs& a, const BackLane& l, int call, int n0, const float (&u)[4])
 {
     if (!l.live) return;
-    line_out4(a, (size_t)l.c * a.N + call * BLK + n0, call * BLK + n0, v);
+    line_out4(a, (size_t)l.c * a.N + call * BLK + n0, 0u, call, call * BLK + n0, u);
 }
 
 // ---- demod stage: AudioDriver_DemodSAM (audio_driver.c:1990-2166): AM envelope
@@ -1907,7 +1928,7 @@ __device__ __forceinline__ void fused_store_call(const BackArgs& a, const BackLa
         // uniform base of rows c0 + 8k.. (SGPRs) + the lane's 32-bit offset
         const size_t rb = (size_t)(c0 + 8 * k) * a.N + call * BLK;
         const unsigned off = (unsigned)g * (unsigned)a.N + 4 * j;
-        line_out4(a, rb + off, call * BLK + 4 * j, v);
+        line_out4(a, rb, off, call, call * BLK + 4 * j, v);
     }
     wave_sync();                                         // rows read before the next call writes
 }
@@ -1949,6 +1970,7 @@ __device__ __forceinline__ void back_fused_body(const BackArgs& a, float* ys, in
     if (PRE > 0) { to_vgpr(pre.k); to_vgpr(pre.v); }
     if (AA > 0) { to_vgpr(aa.k); to_vgpr(aa.v); }
     to_vgpr(ou.b2);
+    ou.lo = to_vgpr(ou.lo);
     if (!B1S) to_vgpr(au.b1);
 #endif
     ag.agc_on = AGC_ON;
@@ -2135,8 +2157,8 @@ __global__ void __launch_bounds__(BACK_CH) rx_back_stereo(BackArgs a)
 #pragma unroll
             for (int j = 0; j < L; ++j)
             {
-                y0[m * L + j] = ou0.step(aa0.step(u0[j])) * ou0.lo;
-                y1[m * L + j] = ou1.step(aa1.step(u1[j])) * ou1.lo;
+                y0[m * L + j] = ou0.step(aa0.step(u0[j]));
+                y1[m * L + j] = ou1.step(aa1.step(u1[j]));
             }
         }
         if (a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK)
@@ -2469,7 +2491,7 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
         for (int i = 0; i < 5; ++i) b2[i] = P->biquad2[i];
 #pragma unroll
         for (int i = 0; i < 4; ++i) bq2[i] = a.s.bq2[i * C + cl];
-        const float fs = P->fm_scale;
+        const float lo = P->line_out_scale, fs = P->fm_scale;
         for (int it = 0; it <= calls; ++it)
         {
             if (it > 0)
@@ -2483,10 +2505,12 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                     float v[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        v[j] = biquad_step(mi[(n0 + j) * BACK_CH] * fs, bq2[0], bq2[1], bq2[2], bq2[3], b2);
+                        v[j] = biquad_step(mi[(n0 + j) * BACK_CH] * fs, bq2[0], bq2[1], bq2[2], bq2[3], b2) * lo;
                     // muted: both buffers zero, the beep still added (audio_driver.c:2845-2898)
-                    if (live) line_out4(a, (size_t)c * a.N + call * BLK + n0, call * BLK + n0, v, on);
+                    if (live) line_out4(a, (size_t)c * a.N + call * BLK + n0, 0u, call, call * BLK + n0, v, on);
                 }
+                // mcHF: the call's do_mute_output for rx_line_out_mchf
+                if (a.mute && live) a.mute[(size_t)c * (a.N / BLK) + call] = on ? 1 : 0;
             }
             lds_barrier();
         }
@@ -2665,6 +2689,8 @@ struct uhsdr_rx_s
     hipEvent_t ev_front, ev_join, ev_back[2];  // ev_back[g % 2]: end of group g's rx_back
     hipEvent_t ev_switch;    // uhsdr_rx_set_stream: new stream after the old one's work
     float *adecp[PIPE_BUFS - 1], *adec_qp[PIPE_BUFS - 1];  // the pipelined mode's other hand-off buffers
+    float* mchf_u;           // mcHF: [C][N] biquad_2 output of the call (rx_line_out_mchf's input)
+    uint8_t* mchf_mute;      // mcHF FM: [C][N/32] squelch on / off per 32-frame call
     long long calls_issued;  // process() calls
     long long pipe_calls;    // calls since the pipelined mode was entered (buffer index, group)
     // per-kernel timing (uhsdr_rx_enable_timing)
@@ -3035,6 +3061,9 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const size_t o_notch = take(h->nv ? (size_t)(2 * NOTCH_TAPS + 2 + NOTCH_DELAY) * C : 0);
     const bool cw = p.cw_enabled && p.decimation_rate == 4;
     const size_t o_cw = take(cw ? (size_t)5 * C : 0);
+    const bool mc = p.single_channel != 0;
+    const size_t o_mu = take(mc ? (size_t)C * N : 0);
+    const size_t o_mute = take(mc && h->bv->dm == DM_FM ? ((size_t)C * (N / BLK) + 3) / 4 : 0);
     h->arena_bytes = fl * sizeof(float);
     if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess ||
         hipMalloc((void**)&h->adec, sizeof(float) * (size_t)C * h->Nd) != hipSuccess ||
@@ -3058,6 +3087,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->bs.pre1 = st ? A + o_pre1 : nullptr; h->bs.aa1 = st ? A + o_aa1 : nullptr;
     h->bs.bq1_1 = st ? A + o_bq1_1 : nullptr; h->bs.bq2_1 = st ? A + o_bq2_1 : nullptr;
     h->bs.interp1 = st ? A + o_ip1 : nullptr;
+    h->mchf_u = mc ? A + o_mu : nullptr;
+    h->mchf_mute = mc && h->bv->dm == DM_FM ? (uint8_t*)(A + o_mute) : nullptr;
     {
         // blocks per call: one completes at the end of every ceil(blocksize / NDC)-th call
         const int ndc = BLK / p.decimation_rate, cpb = (p.cw_blocksize + ndc - 1) / ndc;
@@ -3228,7 +3259,8 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     ba.adec = adec;
     ba.adec_q = adec_q;
     ba.audio = audio;
-    ba.audio0 = (h->plan.stereo || h->plan.single_channel) ? audio0 : nullptr;   // mcHF: the line-out channel
+    ba.audio0 = h->plan.stereo ? audio0 : nullptr;
+    ba.mute = nullptr;
     ba.dst = (int2*)dst;
     ba.s = h->bs;
     ba.C = h->C; ba.N = h->N; ba.Nd = h->Nd;
@@ -3267,6 +3299,28 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     return ba;
 }
 
+// mcHF: the back kernels' arguments (their OVI40 output stage reduced to biquad_2's output into
+// the scratch row) and the finishing pass over it, ordered after them on their stream
+static BackArgs back_kernel_args(const uhsdr_rx_s* h, const BackArgs& ba)
+{
+    if (!h->plan.single_channel) return ba;
+    BackArgs bk = ba;
+    bk.audio = h->mchf_u;
+    bk.audio0 = nullptr;
+    bk.dst = nullptr;
+    bk.beep_n0 = bk.beep_n1 = 0;
+    bk.mute = h->mchf_mute;
+    return bk;
+}
+static void line_out_mchf(const uhsdr_rx_s* h, BackArgs ba, float* audio0, hipStream_t s)
+{
+    if (!h->plan.single_channel) return;
+    ba.audio0 = audio0;
+    const size_t quads = (size_t)h->C * h->N / 4;
+    hipLaunchKernelGGL(rx_line_out_mchf, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, ba,
+                       (const float*)h->mchf_u, (const uint8_t*)h->mchf_mute);
+}
+
 static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, float* audio0, int32_t* dst)
 {
     if (!h || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
@@ -3287,7 +3341,8 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         const BackArgs ba = back_args(h, nullptr, nullptr, audio, audio0, dst);
         time_mark(h, K_CHAIN, 0);
         hipLaunchKernelGGL(fma ? h->cv->fn_fma : h->cv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(FRONT_WAVE),
-                           chain_lds(h), h->stream, fa, ba, (int)chain_front_floats(h));
+                           chain_lds(h), h->stream, fa, back_kernel_args(h, ba), (int)chain_front_floats(h));
+        line_out_mchf(h, ba, audio0, h->stream);
         HIPCHK(hipGetLastError());
         time_mark(h, K_CHAIN, 1);
         h->front_launches += 1;
@@ -3323,23 +3378,35 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         time_mark(h, K_FRONT, 1);
 
         const BackArgs ba = back_args(h, adec, adec_q, audio, audio0, dst);
+        const BackArgs bk = back_kernel_args(h, ba);
         const hipStream_t bst = back_stream(h);
         if (side) HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
         time_mark(h, K_BACK, 0);
         if (h->nv)
         {
-            hipLaunchKernelGGL(h->nv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, ba);
+            hipLaunchKernelGGL(h->nv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, bk);
             HIPCHK(hipGetLastError());
         }
         const bool fused = h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo;
         const back_fn bfn = fused ? fused_back_fn(h) : h->bv->fn;
         const dim3 bgrid((h->C + BACK_CH - 1) / BACK_CH), bblock(fused ? BACK_CH : back_roles(h->bv->dm) * BACK_CH);
         const size_t blds = fused ? 0 : back_lds(h);
-        // pipelined: the group's last rx_back records ev_back[grp] as it completes
-        if (side && group_end)
-            hipExtLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, nullptr, h->ev_back[grp], 0, ba);
+        // pipelined: the group's last rx_back (mcHF: its finishing pass) records ev_back[grp] as it completes
+        const bool mc = h->plan.single_channel != 0;
+        if (side && group_end && !mc)
+            hipExtLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, nullptr, h->ev_back[grp], 0, bk);
         else
-            hipLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, ba);
+            hipLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, bk);
+        if (mc && side && group_end)
+        {
+            BackArgs bo = ba;
+            bo.audio0 = audio0;
+            const size_t quads = (size_t)h->C * h->N / 4;
+            hipExtLaunchKernelGGL(rx_line_out_mchf, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, bst, nullptr,
+                                  h->ev_back[grp], 0, bo, (const float*)h->mchf_u, (const uint8_t*)h->mchf_mute);
+        }
+        else
+            line_out_mchf(h, ba, audio0, bst);
         HIPCHK(hipGetLastError());
         time_mark(h, K_BACK, 1);
         if (h->pipelined) h->pipe_calls += 1;

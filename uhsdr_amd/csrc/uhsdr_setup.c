@@ -431,13 +431,15 @@ uhsdr_status uhsdr_rx_plan_build(const uhsdr_rx_config* cfg, uhsdr_rx_plan* p)
            for UI_BRD_MCHF, codec.h:26-27) */
         float active_value = 1;
         if (cfg->spkr_gain > MCHF_SPEAKER_MAX_VOLUME) active_value = (((float)cfg->spkr_gain) / 2.5) - 5.35;
-        p->line_out_scale = active_value;
+        p->line_out_scale = 1;
         p->line_out0_scale = LINE_OUT_SCALING_FACTOR;
+        p->spkr_scale = active_value;
     }
     else
     {
         p->line_out_scale = LINE_OUT_SCALING_FACTOR;
         p->line_out0_scale = LINE_OUT_SCALING_FACTOR;
+        p->spkr_scale = 1;
     }
 
     setup_agc(&p->agc, cfg, (float)p->decimated_freq, is_am);

@@ -460,6 +460,16 @@ uhsdr_status uhsdr_tx_destroy(uhsdr_tx_handle h);
 uhsdr_status uhsdr_tx_set_pipelined(uhsdr_tx_handle h, int32_t enable);
 int32_t      uhsdr_tx_get_pipelined(uhsdr_tx_handle h);
 uhsdr_status uhsdr_tx_join(uhsdr_tx_handle h);
+/* Arithmetic of the 201-tap Hilbert pair in tx_iq (no reference counterpart; EXACT by default).
+   EXACT: a rounded multiply then a rounded add per tap, in tap order -- arm_fir_f32's binary32
+   sequence, bit-identical DAC frames.  FMA: one fused multiply-add per tap (v_pk_fma_f32), half
+   the pair's VALU issue; the DAC frames stay within north_star's 1e-5 normwise relative tolerance
+   (max|diff| / max|ref| per channel) of the reference.  The voice chain (lattice, biquads, ALC)
+   and FM always run the reference sequence: the pair's output feeds no recursion, so its rounding
+   difference is not amplified (every SSB / AM mode and frequency translation measured, tests/
+   test_gpu_tx_precision.py).  Takes effect from the next uhsdr_tx_process. */
+uhsdr_status uhsdr_tx_set_precision(uhsdr_tx_handle h, int32_t precision);
+int32_t      uhsdr_tx_get_precision(uhsdr_tx_handle h);   /* -1 for a null handle */
 /* TxProcessor_PrepareRun (tx_processor.c:63-66): clear the ALC look-ahead delay line only,
    the first time back to TX; all other TX state carries on */
 uhsdr_status uhsdr_tx_prepare_run(uhsdr_tx_handle h);

@@ -92,7 +92,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--only", default="c3,c3spec,c3zoom,c4fm,c4tx,c5,c5fir")
+    ap.add_argument("--only", default="c3,c3spec,c3zoom,c4fm,c4tx,c4txfma,c5,c5fir")
     ap.add_argument("--fir-waves", type=int, default=0, help="c5fir: waves per workgroup (1, 2, 4; 0 = the default)")
     ap.add_argument("--serial", action="store_true",
                     help="C4 FM-RX / SSB-TX handles in their serial mode (default: pipelined, measured faster there; "
@@ -153,12 +153,17 @@ def main():
         cfg = U.default_config(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=12)
         lines.append(rx_line("C4 per-GPU share: FM-RX P1 (squelch 12)", cfg, C, N,
                              tiled(synth.fm_iq, C, N), a.steps, a.warmup, pipelined=not a.serial))
-    if "c4tx" in want:
+    for key in ("c4tx", "c4txfma"):
+        if key not in want:
+            continue
+        fma = key == "c4txfma"
         C, N = 262144 // 8, 256
         s = torch.cuda.current_stream()
         tx = U.TxChain(channels=C, frames=N, stream=s.cuda_stream)
         if not a.serial:
             tx.set_pipelined(True)
+        if fma:
+            tx.set_precision(U.PRECISION_FMA)
         audio = tiled(synth.tx_audio, C, N)
         iq = torch.empty((C, N, 2), dtype=torch.int32, device="cuda")
         a0 = torch.empty((C, N), dtype=torch.float32, device="cuda")
@@ -168,7 +173,7 @@ def main():
         state = 4 * (200 + 10 + 12 + 1 + 320)
         per = 16 + 2 * state / N
         lines.append({"workload": "C4 per-GPU share: SSB-TX (IIR_TX_SOPRANO + biquads + ALC + 201-tap Hilbert + Fs/4)",
-                      "channels": C, "frames_per_call": N, "pipelined": not a.serial, "ms_per_call": round(ms, 4),
+                      "precision": "fma (Hilbert pair, 1e-5 normwise)" if fma else "exact", "channels": C, "frames_per_call": N, "pipelined": not a.serial, "ms_per_call": round(ms, 4),
                       "msamples_per_s": round(C * N / ms / 1e3, 1), "alg_bytes_per_frame": round(per, 2),
                       "hbm_frac": round(C * N * per / ms / 1e6 / HBM_PEAK_GBS, 4),
                       "finite": bool(torch.isfinite(a0).all().item()) and bool((iq != 0).any().item())})

@@ -214,6 +214,8 @@ SIGNATURES = {
     "uhsdr_tx_set_pipelined": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_tx_get_pipelined": (C.c_int32, [C.c_void_p]),
     "uhsdr_tx_join": (C.c_int, [C.c_void_p]),
+    "uhsdr_tx_set_precision": (C.c_int, [C.c_void_p, C.c_int32]),
+    "uhsdr_tx_get_precision": (C.c_int32, [C.c_void_p]),
     "uhsdr_fir_create": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                    C.POINTER(C.c_void_p)]),
     "uhsdr_fir_reset": (C.c_int, [C.c_void_p]),

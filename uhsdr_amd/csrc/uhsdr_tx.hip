@@ -65,6 +65,19 @@ __device__ __forceinline__ int tx_to_int32(float f)
     return (f > -2147483904.0f && f < 2147483648.0f) ? (int)f : INT32_MIN;
 }
 
+// x / 30000 in binary32 (ALC_KNEE, tx_processor.c:202) without the IEEE division sequence:
+// q0 = x * (1/30000) and one FMA residual correction give the correctly rounded quotient for
+// every normal quotient (exhaustive over all binary32 x: tools/div_check.c); tiny, huge, inf and
+// NaN inputs take the division itself
+__device__ __forceinline__ float alc_knee_div(float x)
+{
+    constexpr float y = 30000.0f, z = 1.0f / 30000.0f;
+    const float q0 = x * z;
+    float q = __builtin_fmaf(__builtin_fmaf(-q0, y, x), z, q0);
+    if (!(x >= 0x1.0p-100f && x <= 0x1.0p+127f)) q = x / y;
+    return q;
+}
+
 // TxProcessor_AudioBufferFill + _FilterAudio + _VoiceCompressor, one lane per channel; with FM
 // also TxProcessor_FM (tx_processor.c:534-588) and TxProcessor_IqFinalProcessing (:282-330)
 template <int S, bool FM>
@@ -152,7 +165,7 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
             {
                 const float v = tune ? x[m] : x[m] * post;
                 // ALC (tx_processor.c:197-221)
-                const float alc_var = (float)((double)(fabsf(v * alc_val) / 30000) - 1.0);
+                const float alc_var = (float)((double)alc_knee_div(fabsf(v * alc_val)) - 1.0);
                 // both branches evaluated and selected: lanes of a wave no longer split
                 const float dec = alc_val - alc_val * decay * alc_var;
                 float att = (float)((double)alc_val - (double)alc_val * 0.1 * (double)alc_var);
@@ -373,7 +386,7 @@ __global__ void __launch_bounds__(128) tx_voice2(TxVoiceArgs a)
             for (int m = 0; m < BLK; ++m)
             {
                 const float v = tune ? x[m] : x[m] * post;
-                const float alc_var = (float)((double)(fabsf(v * alc_val) / 30000) - 1.0);
+                const float alc_var = (float)((double)alc_knee_div(fabsf(v * alc_val)) - 1.0);
                 const float dec = alc_val - alc_val * decay * alc_var;
                 float att = (float)((double)alc_val - (double)alc_val * 0.1 * (double)alc_var);
                 att = ((double)att < 0.001) ? 0.001f : att;
@@ -416,7 +429,8 @@ struct TxIqArgs
     int C, N, ld, lw;
 };
 
-template <int R>
+// F: UHSDR_PRECISION_FMA (uhsdr_tx_set_precision): the Hilbert pair's MACs fused (v_pk_fma_f32)
+template <int R, bool F>
 __global__ void __launch_bounds__(64) tx_iq(TxIqArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -474,7 +488,7 @@ __global__ void __launch_bounds__(64) tx_iq(TxIqArgs a)
     for (int j = 0; j < R; ++j) x2[j] = v2f{ xv[j], xv[j] };
     front_fill2<TX_T, HQ, true>(W, a.hist, a.hist, c, act, live, b, nb, hA, hA, x2, R);
     v2f h2[R];
-    fir_block2<TX_T, R, 1>(W + 2 * b * R, as_taps2(a.taps2), h2);
+    fir_block2<TX_T, R, 1, F>(W + 2 * b * R, as_taps2(a.taps2), h2);
     float hi[R], hq[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) { hi[r] = h2[r].x; hq[r] = h2[r].y; }
@@ -580,6 +594,7 @@ struct uhsdr_tx_s
     hipStream_t side;
     hipEvent_t ev_voice, ev_join, ev_iq[2];
     float* txa2;                     // the second hand-off buffer [C][N]
+    int precision;                   // uhsdr_tx_set_precision
 };
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { uhsdr_set_error("%s: %s", #x, hipGetErrorString(e_)); return UHSDR_DEVICE_ERROR; } } while (0)
@@ -788,6 +803,7 @@ extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio
     }
     const int cpw = 64 / (h->Nf / h->R);
     const size_t lds = sizeof(float) * ((size_t)cpw * h->lw + (h->plan.shift_kind == 2 ? 2 * h->Nf : 0));
+    void (*const iq_fn)(TxIqArgs) = h->precision == UHSDR_PRECISION_FMA ? tx_iq<8, true> : tx_iq<8, false>;
     for (int f0 = 0; f0 < h->N; f0 += h->Nf)
     {
         TxIqArgs ia;
@@ -797,7 +813,7 @@ extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio
         ia.iq = (int2*)iq + f0;
         ia.C = h->C; ia.N = h->Nf; ia.ld = h->N; ia.lw = h->lw;
         ia.taps2 = h->d_taps2;
-        hipLaunchKernelGGL(tx_iq<8>, dim3((h->C + cpw - 1) / cpw), dim3(64), lds, ist, ia);
+        hipLaunchKernelGGL(iq_fn, dim3((h->C + cpw - 1) / cpw), dim3(64), lds, ist, ia);
         HIPCHK(hipGetLastError());
         h->iq_launches += 1;
     }
@@ -806,6 +822,20 @@ extern "C" uhsdr_status uhsdr_tx_process(uhsdr_tx_handle h, const int32_t* audio
     h->calls_done += h->N / BLK;
     return UHSDR_OK;
 }
+
+extern "C" uhsdr_status uhsdr_tx_set_precision(uhsdr_tx_handle h, int32_t precision)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    if (precision != UHSDR_PRECISION_EXACT && precision != UHSDR_PRECISION_FMA)
+    {
+        uhsdr_set_error("unknown precision %d", (int)precision);
+        return UHSDR_ARGUMENT_ERROR;
+    }
+    h->precision = precision;
+    return UHSDR_OK;
+}
+
+extern "C" int32_t uhsdr_tx_get_precision(uhsdr_tx_handle h) { return h ? h->precision : -1; }
 
 extern "C" uhsdr_status uhsdr_tx_join(uhsdr_tx_handle h)
 {

@@ -48,6 +48,15 @@ class TxChain:
     def pipelined(self) -> bool:
         return bool(self.lib.uhsdr_tx_get_pipelined(self.handle))
 
+    def set_precision(self, precision: int) -> None:
+        """PRECISION_EXACT (bit-identical, default) or PRECISION_FMA (fused MACs in the Hilbert pair,
+        1e-5 normwise on the DAC frames; uhsdr_tx_set_precision)."""
+        _abi.check(self.lib.uhsdr_tx_set_precision(self.handle, int(precision)), "uhsdr_tx_set_precision")
+
+    @property
+    def precision(self) -> int:
+        return self.lib.uhsdr_tx_get_precision(self.handle)
+
     def join(self) -> None:
         """order the handle's stream after the pipelined mode's side stream (uhsdr_tx_join)"""
         _abi.check(self.lib.uhsdr_tx_join(self.handle), "uhsdr_tx_join")

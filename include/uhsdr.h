@@ -519,9 +519,10 @@ uhsdr_status uhsdr_fir_reset(uhsdr_fir_handle h);
 uhsdr_status uhsdr_fir_process(uhsdr_fir_handle h, const float* src, float* dst);
 uhsdr_status uhsdr_fir_synchronize(uhsdr_fir_handle h);
 uhsdr_status uhsdr_fir_destroy(uhsdr_fir_handle h);
-/* waves per workgroup of the FIR kernel: 1, 2 or 4 (default EXACT 2, MFMA 4; results do not
- * depend on it).  UHSDR_ARGUMENT_ERROR for another value, UHSDR_LENGTH_ERROR when that
- * many windows do not fit one workgroup's LDS (the setting is then unchanged). */
+/* waves per workgroup of the FIR kernel (results do not depend on it): EXACT 1, 2 or 4 (default
+ * 2); MFMA 1 .. 16 (default: as many as one workgroup's LDS holds, up to 16).
+ * UHSDR_ARGUMENT_ERROR for another value, UHSDR_LENGTH_ERROR when that many windows do not fit
+ * one workgroup's LDS (the setting is then unchanged). */
 uhsdr_status uhsdr_fir_set_waves(uhsdr_fir_handle h, int32_t waves);
 int32_t uhsdr_fir_get_waves(uhsdr_fir_handle h);
 

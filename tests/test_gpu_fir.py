@@ -75,8 +75,10 @@ def test_fir_matches_oracle_distinct_channels(cuda, mode, T, B):
         assert normwise(got, ref) < TOL
 
 
-@pytest.mark.parametrize("mode", [U.fir.EXACT, U.fir.MFMA], ids=["exact", "mfma"])
-@pytest.mark.parametrize("waves", [1, 2, 4])
+WAVE_CASES = [(m, w) for m in (U.fir.EXACT, U.fir.MFMA) for w in (1, 2, 4)] + [(U.fir.MFMA, w) for w in (7, 16)]
+
+
+@pytest.mark.parametrize("mode,waves", WAVE_CASES, ids=[f"{'mfma' if m else 'exact'}-{w}" for m, w in WAVE_CASES])
 @pytest.mark.parametrize("T,B", [(513, 256), (89, 512)])
 def test_fir_waves_per_workgroup(cuda, mode, waves, T, B):
     """uhsdr_fir_set_waves changes the launch shape only: every count gives the oracle's output
@@ -87,7 +89,7 @@ def test_fir_waves_per_workgroup(cuda, mode, waves, T, B):
     taps = np.load(os.path.join(GOLD, "fir513_kaiser.npy")) if T == 513 else rng.uniform(-0.3, 0.3, T).astype(np.float32)
     x = rng.normal(0, 1000, (C, 2 * B)).astype(np.float32)
     fir = U.FirBatch(taps, C, B, mode)
-    assert fir.waves == (4 if mode == U.fir.MFMA else 2)
+    assert fir.waves == (16 if mode == U.fir.MFMA else 2)       # MFMA: 16 windows fit these shapes
     fir.set_waves(waves)
     assert fir.waves == waves
     got = run(fir, x, B)
@@ -106,6 +108,12 @@ def test_fir_set_waves_rejects(cuda):
         with pytest.raises(RuntimeError):
             fir.set_waves(bad)
         assert fir.waves == 2
+    fir.close()
+    fir = U.FirBatch(np.ones(9, np.float32), 4, 256, U.fir.MFMA)
+    for bad in (0, 17, -1):
+        with pytest.raises(RuntimeError):
+            fir.set_waves(bad)
+        assert fir.waves == 16
     fir.close()
 
 

@@ -93,7 +93,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--only", default="c3,c3spec,c3zoom,c4fm,c4tx,c4txfma,c5,c5fir")
-    ap.add_argument("--fir-waves", type=int, default=0, help="c5fir: waves per workgroup (1, 2, 4; 0 = the default)")
+    ap.add_argument("--fir-waves", type=int, default=0, help="c5fir: waves per workgroup (EXACT 1, 2, 4; MFMA 1 .. 16; 0 = the default)")
     ap.add_argument("--serial", action="store_true",
                     help="C4 FM-RX / SSB-TX handles in their serial mode (default: pipelined, measured faster there; "
                          "C3 SAM and C5 CW run serial, where the pipelined mode measured slower / the same)")

@@ -18,7 +18,7 @@ for f in sorted(glob.glob(os.path.join(base, "p*", "pmc_counter_collection.csv")
     for row in csv.DictReader(open(f)):
         name = row["Kernel_Name"]
         for k in ("rx_front", "rx_back_dec", "rx_back_out", "rx_back", "rx_fm", "rx_notch", "tx_voice", "tx_iq", "spectrum_frames",
-                  "spectrum_accumulate", "spectrum_zoom", "fir_batch_direct", "fir_batch"):
+                  "spectrum_accumulate", "spectrum_zoom", "fir_batch_direct", "fir_batch", "fir_mfma"):
             if k in name:
                 break
         else:
@@ -45,7 +45,7 @@ for k, cs in vals.items():
     if "SQ_BUSY_CYCLES" in m and "GRBM_GUI_ACTIVE" in m:
         d["busy_frac"] = round(m["SQ_BUSY_CYCLES"] / max(m["GRBM_GUI_ACTIVE"], 1), 3)
     if "SQ_VALU_MFMA_BUSY_CYCLES" in m and "GRBM_GUI_ACTIVE" in m:
-        # summed over the chip's 1024 SIMDs (256 CUs x 4)
-        d["mfma_busy_frac"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / max(m["GRBM_GUI_ACTIVE"] * 1024, 1), 3)
+        # MFMA busy cycles summed over the chip's 1024 SIMDs; GRBM_GUI_ACTIVE summed over its 8 XCDs
+        d["mfma_busy_frac"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / max(m["GRBM_GUI_ACTIVE"] / 8 * 1024, 1), 3)
     out[k] = d
 print(json.dumps(out, indent=1))

@@ -10,17 +10,18 @@
 //                    16 x 16 tile Y[m][i] = y[16m + i] = sum_j X[m][j] Cm[j][i] with
 //                    X[m][j] = w[16m + j] (overlapping rows of the channel's window) and the
 //                    Toeplitz tap matrix Cm[j][i] = c[j - i] (zero outside 0..T-1), depth
-//                    K = T + 15 rounded up to 4 (+3 % MACs at 513 taps), on
-//                    v_mfma_f32_16x16x4_f32.  That instruction is an fmaf chain in k order
-//                    (cdna_hip_programming.md §3), so every output is the reference's tap-ordered
-//                    sum with each multiply-add fused: within ~1e-7 * sum|c x| of it, not
-//                    bit-identical (tests/test_gpu_fir.py: 1e-5 relative, north_star's bar).
+//                    K = T + 15 rounded up to 16 (+3 % MACs at 513 taps), on
+//                    v_mfma_f32_16x16x4_f32: each output the tap sum with every multiply-add
+//                    fused, summed in a permuted tap order (fir_group), within ~1e-7 * sum|c x|
+//                    of the reference's, not bit-identical (tests/test_gpu_fir.py: 1e-5
+//                    relative, north_star's bar).
 //
 // Layout: one wave owns FIR_CPW = 4 channels (4 independent MFMA accumulators hide the
 // 40-cycle dependent latency); each channel's window [T-1 carried | B new | 32 zero] sits in
-// LDS with one pad word per 16 (fpad), so the 16 rows of an A fragment (stride 16 samples)
-// land in distinct banks; the taps sit once per workgroup in LDS with 16 zeros on each side,
-// so the B fragment c[k - i] is one LDS read per lane.  B % 256 == 0; a channel's block is
+// LDS (EXACT: one pad word per 16, fpad, so its lanes 16 samples apart hit distinct banks;
+// MFMA: plain, for 16-byte aligned ds_read_b128 operand loads); the taps sit in LDS once per
+// workgroup with 16 zeros on each side (MFMA: four copies, copy p shifted by p, so every lane's
+// four consecutive B values start 16-byte aligned).  B % 256 == 0; a channel's block is
 // B / 256 tiles.  HBM per channel and call: 4 B in + 4 B out per sample, the carried samples
 // read and written once.
 
@@ -34,8 +35,20 @@
 namespace {
 
 constexpr int FIR_TILE = 256;   // outputs of one 16 x 16 MFMA tile
-constexpr int FIR_CPW = 4;      // channels per wave
+constexpr int FIR_CPW = 4;      // EXACT: channels per wave
+// MFMA: channels per wave and group.  One (one accumulator chain per wave, 16 waves per CU
+// cover its 40-cycle dependent latency); two measured the same (0.355 vs 0.353 ms at C5, 12
+// waves per CU, the B reads shared)
+constexpr int FIR_MCPW = 1;
+
+// MFMA window layout: float4 chunk u of a window sits at chunk u ^ 2 in odd 64-float rows
+// (bit 4 of u set).  A lane's A fragment reads chunk 4(r + q) + kq; unswizzled, the 16 lanes of a
+// ds_read_b128 group hit 8 bank quads twice (39 % of the LDS cycles were conflicts, PMC r04); with
+// the swizzle they hit 16 distinct ones for every chunk q.  An involution within 16-float
+// blocks: the glds fill writes physical chunk P from logical chunk swz(P).
+__host__ __device__ constexpr int fir_swz(int i) { return i ^ ((i >> 3) & 8); }   // float index
 constexpr int FIR_TAIL = 32;    // zero samples after a window (K round-up, EXACT chunk over-read)
+constexpr int FIR_MTAIL = 64;   // MFMA: K round-up plus the operand prefetch two chunks past the last
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -47,62 +60,20 @@ struct FirArgs
     float* hist;         // [C][T-1] carried samples (oldest first)
     const float* src;    // [C][B]
     float* dst;          // [C][B]
-    int C, B, T, K;      // K: MFMA depth, T + 15 rounded up to 4
+    int C, B, T, K;      // K: MFMA depth, T + 15 rounded up to 16
     int lw;              // LDS floats per channel window
-    int cp;              // LDS floats of the padded tap copy
+    int cp;              // LDS floats of the tap copies (MFMA 4, EXACT 1)
+    int cpl;             // floats per tap copy: copy p holds cp0[y - p], cp0[16 + k] = c[k], zeros around
+    int v4;              // MFMA: 16-byte window fills (carried length % 4 == 0, block 16-byte aligned)
 };
 
-// the tiles of one channel group from its LDS windows Wb (4 channels from c0)
-template <bool MFMA>
+// EXACT: the tiles of one channel group from its LDS windows Wb (4 channels from c0)
 __device__ __forceinline__ void fir_group(const FirArgs& a, const float* Wb, const float* cp, int c0, int lane)
 {
     const int r = lane & 15, kq = lane >> 4;
     for (int t = 0; t < a.B / FIR_TILE; ++t)
     {
         const int base = FIR_TILE * t;
-        if constexpr (MFMA)
-        {
-            // A[m = r][k] = w[base + 16r + k0 + kq]; B[k][i = r] = c[k0 + kq - r]
-            f32x4 acc[FIR_CPW];
-#pragma unroll
-            for (int j = 0; j < FIR_CPW; ++j) acc[j] = f32x4{ 0.0f, 0.0f, 0.0f, 0.0f };
-            const float* bp = cp + 16 + kq - r;
-            const int ab = base + 16 * r + kq;
-            // fpad(ab + k0) for k0 = 16q + s, s in {0, 4, 8, 12}: kq + s < 16, so the padded
-            // address is a0 + 17q + s -- per 16-deep chunk one pointer step, the four k-steps
-            // and the four channels as immediate LDS offsets
-            const float* ap = Wb + fpad(ab);
-            const int nq = a.K / 16;
-            for (int q = 0; q < nq; ++q, ap += 17, bp += 16)
-            {
-#pragma unroll
-                for (int s = 0; s < 16; s += 4)
-                {
-                    const float bv = bp[s];
-#pragma unroll
-                    for (int j = 0; j < FIR_CPW; ++j)
-                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[j * a.lw + s], bv, acc[j], 0, 0, 0);
-                }
-            }
-            for (int k0 = 16 * nq; k0 < a.K; k0 += 4)      // K % 16 tail
-            {
-                const float bv = cp[16 + kq - r + k0];
-#pragma unroll
-                for (int j = 0; j < FIR_CPW; ++j)
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(Wb[j * a.lw + fpad(ab + k0)], bv, acc[j], 0, 0, 0);
-            }
-            // D[row = 4 kq + i][col = r] is output 16 row + col of the tile
-#pragma unroll
-            for (int j = 0; j < FIR_CPW; ++j)
-            {
-                const int c = c0 + j;
-                if (c >= a.C) continue;
-                float* d = a.dst + (size_t)c * a.B + base + 64 * kq + r;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) d[16 * i] = acc[j][i];
-            }
-        }
-        else
         {
             // lane (channel j = kq, block r): 16 consecutive outputs, a 32-sample register
             // window sliding 16 samples per 16-tap chunk, taps from LDS (VGPR operands)
@@ -159,15 +130,14 @@ __device__ __forceinline__ void fir_group(const FirArgs& a, const float* Wb, con
     }
 }
 
-// One group per wave, windows filled straight from HBM (EXACT: VALU-bound, the fill hides behind
-// the other waves; the persistent form's prefetch registers cost it 20 %)
-template <bool MFMA>
+// EXACT: one group per wave, windows filled straight from HBM (VALU-bound: the fill hides behind
+// the other waves; a persistent form's prefetch registers cost it 20 %)
 __global__ void __launch_bounds__(256) fir_batch_direct(FirArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int H = a.T - 1, n = H + a.B;
-    float* cp = sm;
+    float* cp = sm;                                   // cp[16 + k] = c[k], zeros around
     for (int i = threadIdx.x; i < a.cp; i += blockDim.x)
         cp[i] = (i >= 16 && i < 16 + a.T) ? a.taps[i - 16] : 0.0f;
     float* Wb = sm + a.cp + (size_t)w * FIR_CPW * a.lw;
@@ -194,87 +164,194 @@ __global__ void __launch_bounds__(256) fir_batch_direct(FirArgs a)
             for (int i = lane; i < H; i += 64) a.hist[(size_t)c * H + i] = W[fpad(i + a.B)];
         }
     }
-    fir_group<MFMA>(a, Wb, cp, c0, lane);
+    fir_group(a, Wb, cp, c0, lane);
 }
 
-// floats of a channel's window each lane carries in registers between groups (n <= 64 * FIR_NPL)
-constexpr int FIR_NPL = 16;
+// ---- MFMA ----
+// One wave owns FIR_MCPW channels per group, persistent over groups; up to 16 waves per
+// workgroup, one workgroup per CU (the waves' windows fill its LDS).  Windows [carried | block |
+// zeros] (fir_swz layout) are double-buffered in LDS: the next group's windows stream in by
+// global_load_lds (no VGPRs, no VALU) while this group's MFMAs run, and the only waits on HBM
+// are for loads issued a whole group earlier.
 
-// Persistent: each wave walks channel groups g = wave, wave + waves in grid, ...  The next
-// group's window (carried samples + block) is loaded into registers while the current group's
-// tiles run from LDS, then written into the wave's LDS windows -- the HBM latency of the fill
-// hides behind the MFMA (or VALU) chain instead of stalling the wave between groups.
-template <bool MFMA>
-__global__ void __launch_bounds__(256) fir_batch(FirArgs a)
+// the glds fill of one window: SZ bytes per lane (16 when the carried length keeps float4s
+// aligned, else 4); lanes past the data are masked off, so the slots after it keep their zeros
+template <int SZ>
+__device__ __forceinline__ void fir_fill_glds(float* W, const float* hrow, const float* srow, int H, int n, int lane)
+{
+    constexpr int F = SZ / 4, STEP = 64 * F;
+    for (int k0 = 0; k0 < n; k0 += STEP)
+    {
+        const int e = fir_swz(k0 + lane * F);        // the logical sample this lane's slot holds
+        const float* g = e < H ? hrow + e : srow + (e - H);
+        const __attribute__((address_space(1))) void* gs = (const __attribute__((address_space(1))) void*)g;
+        __attribute__((address_space(3))) void* ls = (__attribute__((address_space(3))) void*)(W + k0);
+        if (e < n)
+        {
+            if constexpr (SZ == 16) __builtin_amdgcn_global_load_lds(gs, ls, 16, 0, 0);
+            else __builtin_amdgcn_global_load_lds(gs, ls, 4, 0, 0);
+        }
+    }
+}
+
+// the MFMAs of one 16-deep chunk: lane (r, kq) holds window samples 16q + 4kq + s (s = 0..3) of
+// its row and taps c[16q + 4kq - r + s]
+__device__ __forceinline__ void fir_chunk(f32x4 (&acc)[FIR_MCPW], const f32x4 (&av)[FIR_MCPW], const f32x4& bv)
+{
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < FIR_MCPW; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][s], bv[s], acc[j], 0, 0, 0);
+}
+
+// One 256-output tile per channel of the group.  A[m = r][k] = w[base + 16r + k], B[k][i = r] =
+// c[k - i].  The MFMA's k-sum is a permutation away from any other, so in 16-deep chunk q lane
+// (r, kq) takes k = 16q + 4kq + s in k-step s: its four A values are four consecutive window
+// samples (one ds_read_b128 per channel for four k-steps) and its four B values four consecutive
+// taps, read from tap copy p = r & 3 (shifted by p) where they start 16-byte aligned.  The
+// operands of chunk q + 1 load into the other register set while chunk q's MFMAs run.
+__device__ __forceinline__ void fir_tile(const FirArgs& a, const float* Wg, const float* cp, int base, int lane,
+                                         f32x4 (&acc)[FIR_MCPW])
+{
+    const int r = lane & 15, kq = lane >> 4;
+    const int ai = base + 16 * r + 4 * kq;           // logical window index of chunk 0's A values
+    auto aptr = [&](int q, int j) { return (const f32x4*)(Wg + j * a.lw + fir_swz(ai + 16 * q)); };
+    const float* bp = cp + (r & 3) * a.cpl + 16 + 4 * kq - 4 * (r >> 2);
+    const int nq = a.K / 16;
+#pragma unroll
+    for (int j = 0; j < FIR_MCPW; ++j) acc[j] = f32x4{ 0.0f, 0.0f, 0.0f, 0.0f };
+    // Three operand sets in rotation: chunk q + 2's loads are issued as chunk q's MFMAs start,
+    // two chunks before their use, so the wait before a chunk leaves the next set in flight
+    // (explicit waits, which the compiler's waitcnt pass counts, and scheduling barriers keep it
+    // from waiting on loads it has just issued).  Reads past the last chunk land in the window's
+    // zero tail and the tap copy's slack, unused.
+    constexpr int NL = FIR_MCPW + 1;                 // LDS reads per set
+    // s_waitcnt lgkmcnt(NL): all but the last set issued have landed (vmcnt, expcnt: no wait)
+    constexpr unsigned LGKM_NL = 0xC07F | (NL << 8);
+    f32x4 av[3][FIR_MCPW], bv[3];
+    auto load = [&](int set, int qq) {
+#pragma unroll
+        for (int j = 0; j < FIR_MCPW; ++j) av[set][j] = *aptr(qq, j);
+        bv[set] = *(const f32x4*)(bp + 16 * qq);
+    };
+    load(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    load(1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    int q = 0;
+#define FIR_STEP(S, QQ)                                                                         \
+    __builtin_amdgcn_s_waitcnt(LGKM_NL);                                                        \
+    load(((S) + 2) % 3, (QQ) + 2);                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                                          \
+    fir_chunk(acc, av[S], bv[S]);                                                               \
+    __builtin_amdgcn_sched_barrier(0);
+    for (; q + 3 <= nq; q += 3)
+    {
+        FIR_STEP(0, q)
+        FIR_STEP(1, q + 1)
+        FIR_STEP(2, q + 2)
+    }
+    if (q < nq) { FIR_STEP(0, q) }
+    if (q + 1 < nq) { FIR_STEP(1, q + 1) }
+#undef FIR_STEP
+}
+
+// D[row = 4 kq + i][col = r] of channel c0 + j's tile at `base` is output base + 16 row + col
+__device__ __forceinline__ void fir_store_tile(const FirArgs& a, int c0, int base, int lane, const f32x4 (&acc)[FIR_MCPW])
+{
+    const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < FIR_MCPW; ++j)
+    {
+        const int c = c0 + j;
+        if (c >= a.C) continue;
+        float* d = a.dst + (size_t)c * a.B + base + 64 * kq + r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d[16 * i] = acc[j][i];
+    }
+}
+
+__global__ void __launch_bounds__(1024) fir_mfma(FirArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int H = a.T - 1, n = H + a.B;
-    float* cp = sm;                                   // cp[16 + k] = c[k], zeros around
+    float* cp = sm;
     for (int i = threadIdx.x; i < a.cp; i += blockDim.x)
-        cp[i] = (i >= 16 && i < 16 + a.T) ? a.taps[i - 16] : 0.0f;
-    float* Wb = sm + a.cp + (size_t)w * FIR_CPW * a.lw;
-    // windows: [carried samples | block | zero tail]; the tail is written once
-#pragma unroll
-    for (int j = 0; j < FIR_CPW; ++j)
-        for (int i = n + lane; i < n + FIR_TAIL; i += 64) Wb[j * a.lw + fpad(i)] = 0.0f;
-    __syncthreads();                                  // taps (whole workgroup) ready
-    const int ng = (a.C + FIR_CPW - 1) / FIR_CPW;
+    {
+        const int x = i % a.cpl - i / a.cpl - 16;    // copy i / cpl, shifted by its index
+        cp[i] = (x >= 0 && x < a.T) ? a.taps[x] : 0.0f;
+    }
+    float* const Wb = sm + a.cp + (size_t)w * 2 * FIR_MCPW * a.lw;   // [buffer][channel][lw]
+    for (int i = lane; i < 2 * FIR_MCPW * a.lw; i += 64) Wb[i] = 0.0f;
+    __syncthreads();                                  // taps ready, windows zeroed
+    const bool v4 = a.v4 != 0;
+    const int ng = (a.C + FIR_MCPW - 1) / FIR_MCPW;
     const int nwt = gridDim.x * nw;
-    float pf[FIR_CPW][FIR_NPL];
-    auto fetch = [&](int g) {
+    auto fill = [&](int g, int buf) {
 #pragma unroll
-        for (int j = 0; j < FIR_CPW; ++j)
+        for (int j = 0; j < FIR_MCPW; ++j)
         {
-            const int c = g * FIR_CPW + j;
-            const int cl = c < a.C ? c : a.C - 1;     // loads clamped: no exec-masked load branches
-            const float* h = a.hist + (size_t)cl * H;
-            const float* s = a.src + (size_t)cl * a.B;
-#pragma unroll
-            for (int k = 0; k < FIR_NPL; ++k)
-            {
-                const int i = lane + 64 * k;
-                const int is = i - H < a.B ? i - H : a.B - 1;
-                pf[j][k] = *(i < H ? h + i : s + is);
-            }
+            const int c = g * FIR_MCPW + j;
+            const int cl = c < a.C ? c : a.C - 1;
+            float* W = Wb + (buf * FIR_MCPW + j) * a.lw;
+            if (v4) fir_fill_glds<16>(W, a.hist + (size_t)cl * H, a.src + (size_t)cl * a.B, H, n, lane);
+            else fir_fill_glds<4>(W, a.hist + (size_t)cl * H, a.src + (size_t)cl * a.B, H, n, lane);
         }
     };
-    int g = blockIdx.x * nw + w;
-    if (g < ng) fetch(g);
-    for (; g < ng; g += nwt)
+    int g = blockIdx.x * nw + w, buf = 0;
+    if (g < ng) fill(g, 0);
+    // the last tile's outputs are stored one group later, after that group's wait: the wait then
+    // never covers stores issued just before it
+    f32x4 last[FIR_MCPW];
+    int last_c0 = -1;
+    for (; g < ng; g += nwt, buf ^= 1)
     {
-        wave_sync();                                  // every lane is done with the last group's windows
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this group's windows have landed
+        if (g + nwt < ng) fill(g + nwt, buf ^ 1);
+        if (last_c0 >= 0) fir_store_tile(a, last_c0, a.B - FIR_TILE, lane, last);
+        const float* Wg = Wb + buf * FIR_MCPW * a.lw;
+        const int c0 = g * FIR_MCPW;
+        // the next call's carried samples: window [B, B + H)
 #pragma unroll
-        for (int j = 0; j < FIR_CPW; ++j)
-#pragma unroll
-            for (int k = 0; k < FIR_NPL; ++k)
-            {
-                const int i = lane + 64 * k;
-                if (i < n) Wb[j * a.lw + fpad(i)] = pf[j][k];
-            }
-        wave_sync();
-        if (g + nwt < ng) fetch(g + nwt);             // in flight while this group computes
-        const int c0 = g * FIR_CPW;
-        // the next call's carried samples: the window's last T-1
-#pragma unroll
-        for (int j = 0; j < FIR_CPW; ++j)
+        for (int j = 0; j < FIR_MCPW; ++j)
         {
             const int c = c0 + j;
-            if (c < a.C)
+            if (c >= a.C) continue;
+            const float* W = Wg + j * a.lw + a.B;
+            float* hr = a.hist + (size_t)c * H;
+            if (v4)   // B % 256 == 0: window chunks of the carried samples stay whole
+                for (int i = 4 * lane; i < H; i += 256) *(f32x4*)(hr + i) = *(const f32x4*)(W + fir_swz(a.B + i) - a.B);
+            else
+                for (int i = lane; i < H; i += 64) hr[i] = W[fir_swz(a.B + i) - a.B];
+        }
+        for (int t = 0; t < a.B / FIR_TILE; ++t)
+        {
+            f32x4 acc[FIR_MCPW];
+            fir_tile(a, Wg, cp, FIR_TILE * t, lane, acc);
+            if (t + 1 < a.B / FIR_TILE) fir_store_tile(a, c0, FIR_TILE * t, lane, acc);
+            else
             {
-                const float* W = Wb + j * a.lw;
-                for (int i = lane; i < H; i += 64) a.hist[(size_t)c * H + i] = W[fpad(i + a.B)];
+#pragma unroll
+                for (int j = 0; j < FIR_MCPW; ++j) last[j] = acc[j];
             }
         }
-        fir_group<MFMA>(a, Wb, cp, c0, lane);
+        last_c0 = c0;
+        // every lane's LDS reads of this buffer are done before the fill two groups on reuses it
+        wave_sync();
     }
+    if (last_c0 >= 0) fir_store_tile(a, last_c0, a.B - FIR_TILE, lane, last);
 }
 
 } // namespace
 
+constexpr size_t LDS_PER_CU = 160 * 1024;        // MI355X_MICROARCH.md §LDS
+
 struct uhsdr_fir_s
 {
-    int C, B, T, K, mode, lw, cp, waves, grid;
+    int C, B, T, K, mode, lw, cp, cpl, waves, grid;
     hipStream_t stream;
     float* taps;
     float* hist;
@@ -282,9 +359,11 @@ struct uhsdr_fir_s
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { uhsdr_set_error("%s: %s", #x, hipGetErrorString(e_)); return UHSDR_DEVICE_ERROR; } } while (0)
 
+// the workgroup's LDS: tap copies + per wave its windows (MFMA: two buffers of FIR_MCPW)
 static size_t fir_lds(const uhsdr_fir_s* h, int waves)
 {
-    return sizeof(float) * ((size_t)h->cp + (size_t)waves * FIR_CPW * h->lw);
+    const size_t per_wave = h->mode == UHSDR_FIR_MFMA ? 2 * FIR_MCPW : FIR_CPW;
+    return sizeof(float) * ((size_t)h->cp + (size_t)waves * per_wave * h->lw);
 }
 
 extern "C" uhsdr_status uhsdr_fir_destroy(uhsdr_fir_handle h)
@@ -308,17 +387,26 @@ extern "C" uhsdr_status uhsdr_fir_reset(uhsdr_fir_handle h)
 // otherwise halved until the workgroup's LDS fits.
 static uhsdr_status fir_configure(uhsdr_fir_s* h, int waves, bool strict)
 {
-    if (waves != 1 && waves != 2 && waves != 4)
+    const bool mf = h->mode == UHSDR_FIR_MFMA;
+    if (mf ? (waves < 1 || waves > 16) : (waves != 1 && waves != 2 && waves != 4))
     {
-        uhsdr_set_error("waves per workgroup %d not 1, 2 or 4", waves);
+        uhsdr_set_error("waves per workgroup %d not %s", waves, mf ? "1 .. 16" : "1, 2 or 4");
         return UHSDR_ARGUMENT_ERROR;
     }
+    // MFMA: one workgroup may hold the whole CU's LDS (MI355X_MICROARCH.md §LDS)
+    const size_t cap = mf ? LDS_PER_CU : 64 * 1024;
     if (!strict)
-        while (waves > 1 && fir_lds(h, waves) > 64 * 1024) waves /= 2;
-    if (fir_lds(h, waves) > 64 * 1024 || h->T - 1 + h->B > 64 * FIR_NPL)
+        while (waves > 1 && fir_lds(h, waves) > cap) waves = mf ? waves - 1 : waves / 2;
+    if (fir_lds(h, waves) > cap)
     {
         uhsdr_set_error("num_taps - 1 + block_size %d too long for %d waves per workgroup", h->T - 1 + h->B, waves);
         return UHSDR_LENGTH_ERROR;
+    }
+    if (mf && fir_lds(h, waves) > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)fir_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fir_lds(h, waves)) != hipSuccess)
+    {
+        uhsdr_set_error("cannot raise the MFMA FIR kernel's LDS to %zu bytes", fir_lds(h, waves));
+        return UHSDR_DEVICE_ERROR;
     }
     // persistent grid: as many workgroups as the CUs hold at once (LDS-limited), each wave
     // walking channel groups
@@ -327,14 +415,15 @@ static uhsdr_status fir_configure(uhsdr_fir_s* h, int waves, bool strict)
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
         cus = prop.multiProcessorCount;
     const size_t lds = fir_lds(h, waves);
-    int per_cu = (int)((160 * 1024) / lds);
+    int per_cu = (int)(LDS_PER_CU / lds);
     const int thread_cap = 2048 / (64 * waves);
     if (per_cu > thread_cap) per_cu = thread_cap;
     if (per_cu < 1) per_cu = 1;
-    const int groups = (h->C + FIR_CPW - 1) / FIR_CPW;
+    const int cpg = h->mode == UHSDR_FIR_MFMA ? FIR_MCPW : FIR_CPW;
+    const int groups = (h->C + cpg - 1) / cpg;
     const int need = (groups + waves - 1) / waves;
-    // MFMA: persistent (C5 0.69 -> 0.40 ms per call); EXACT: fir_batch_direct, one
-    // group per wave (0.99 ms; 1.20 in the persistent form)
+    // MFMA: persistent (fir_mfma); EXACT: fir_batch_direct, one group per wave (0.99 ms; 1.20 in
+    // a persistent form)
     h->waves = waves;
     h->grid = (h->mode == UHSDR_FIR_MFMA && need > cus * per_cu) ? cus * per_cu : need;
     return UHSDR_OK;
@@ -358,14 +447,17 @@ extern "C" uhsdr_status uhsdr_fir_create(const float* coeffs, int32_t num_taps, 
     uhsdr_fir_s* h = (uhsdr_fir_s*)calloc(1, sizeof(uhsdr_fir_s));
     if (!h) return UHSDR_DEVICE_ERROR;
     h->C = num_channels; h->B = block_size; h->T = num_taps; h->mode = mode;
-    h->K = (num_taps + 15 + 3) & ~3;
+    h->K = (num_taps + 15 + 15) & ~15;                 // MFMA depth: 16-deep chunks
     h->stream = (hipStream_t)stream;
-    h->lw = (fpad(num_taps - 1 + block_size + FIR_TAIL) + 4) & ~3;
-    h->cp = (h->K + 16 + 16 + 3) & ~3;
+    const bool mf = mode == UHSDR_FIR_MFMA;
+    // MFMA: a multiple of 16 floats (fir_swz permutes within 16-float blocks)
+    h->lw = mf ? (num_taps - 1 + block_size + FIR_MTAIL + 15) & ~15 : (fpad(num_taps - 1 + block_size + FIR_TAIL) + 4) & ~3;
+    h->cpl = h->K + FIR_MTAIL;
+    h->cp = (mf ? 4 : 1) * h->cpl;
     // waves per workgroup: EXACT 2 (one group per wave, more resident waves per CU: C5 513-tap
-    // 1.048 -> 0.927 ms per call), MFMA 4 (persistent; 0.395 ms vs 0.497 at 2);
-    // uhsdr_fir_set_waves picks 1, 2 or 4 explicitly
-    const uhsdr_status st = fir_configure(h, mode == UHSDR_FIR_MFMA ? 4 : 2, false);
+    // 1.048 -> 0.927 ms per call); MFMA as many as one workgroup's LDS holds, up to 16 (one
+    // persistent workgroup per CU); uhsdr_fir_set_waves picks the count explicitly
+    const uhsdr_status st = fir_configure(h, mode == UHSDR_FIR_MFMA ? 16 : 2, false);
     if (st != UHSDR_OK)
     {
         free(h);
@@ -390,12 +482,14 @@ extern "C" uhsdr_status uhsdr_fir_process(uhsdr_fir_handle h, const float* src, 
     if (!h || !src || !dst) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
     FirArgs a;
     a.taps = h->taps; a.hist = h->hist; a.src = src; a.dst = dst;
-    a.C = h->C; a.B = h->B; a.T = h->T; a.K = h->K; a.lw = h->lw; a.cp = h->cp;
+    a.C = h->C; a.B = h->B; a.T = h->T; a.K = h->K; a.lw = h->lw; a.cp = h->cp; a.cpl = h->cpl;
+    // 16-byte window fills: carried rows and the caller's block 16-byte aligned
+    a.v4 = (h->T - 1) % 4 == 0 && ((uintptr_t)src & 15) == 0;
     const dim3 grid(h->grid), block(64 * h->waves);
     if (h->mode == UHSDR_FIR_MFMA)
-        hipLaunchKernelGGL(fir_batch<true>, grid, block, fir_lds(h, h->waves), h->stream, a);
+        hipLaunchKernelGGL(fir_mfma, grid, block, fir_lds(h, h->waves), h->stream, a);
     else
-        hipLaunchKernelGGL(fir_batch_direct<false>, grid, block, fir_lds(h, h->waves), h->stream, a);
+        hipLaunchKernelGGL(fir_batch_direct, grid, block, fir_lds(h, h->waves), h->stream, a);
     HIPCHK(hipGetLastError());
     return UHSDR_OK;
 }

@@ -194,17 +194,6 @@ __device__ __forceinline__ void fir_fill_glds(float* W, const float* hrow, const
     }
 }
 
-// the MFMAs of one 16-deep chunk: lane (r, kq) holds window samples 16q + 4kq + s (s = 0..3) of
-// its row and taps c[16q + 4kq - r + s]
-__device__ __forceinline__ void fir_chunk(f32x4 (&acc)[FIR_MCPW], const f32x4 (&av)[FIR_MCPW], const f32x4& bv)
-{
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int j = 0; j < FIR_MCPW; ++j)
-            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][s], bv[s], acc[j], 0, 0, 0);
-}
-
 // One 256-output tile per channel of the group.  A[m = r][k] = w[base + 16r + k], B[k][i = r] =
 // c[k - i].  The MFMA's k-sum is a permutation away from any other, so in 16-deep chunk q lane
 // (r, kq) takes k = 16q + 4kq + s in k-step s: its four A values are four consecutive window
@@ -214,47 +203,63 @@ __device__ __forceinline__ void fir_chunk(f32x4 (&acc)[FIR_MCPW], const f32x4 (&
 __device__ __forceinline__ void fir_tile(const FirArgs& a, const float* Wg, const float* cp, int base, int lane,
                                          f32x4 (&acc)[FIR_MCPW])
 {
+    static_assert(FIR_MCPW == 1, "one window per wave");
     const int r = lane & 15, kq = lane >> 4;
     const int ai = base + 16 * r + 4 * kq;           // logical window index of chunk 0's A values
-    auto aptr = [&](int q, int j) { return (const f32x4*)(Wg + j * a.lw + fir_swz(ai + 16 * q)); };
+    // fir_swz flips bit 3 of a window index by its bit 6, so the layout repeats every 128 floats:
+    // chunk 8t + k of this lane sits at aoff[k] + 128 t from pa
+    const float* pa = Wg + ai;
+    int aoff[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) aoff[k] = fir_swz(ai + 16 * k) - ai;
     const float* bp = cp + (r & 3) * a.cpl + 16 + 4 * kq - 4 * (r >> 2);
     const int nq = a.K / 16;
-#pragma unroll
-    for (int j = 0; j < FIR_MCPW; ++j) acc[j] = f32x4{ 0.0f, 0.0f, 0.0f, 0.0f };
-    // Three operand sets in rotation: chunk q + 2's loads are issued as chunk q's MFMAs start,
-    // two chunks before their use, so the wait before a chunk leaves the next set in flight
-    // (explicit waits, which the compiler's waitcnt pass counts, and scheduling barriers keep it
-    // from waiting on loads it has just issued).  Reads past the last chunk land in the window's
-    // zero tail and the tap copy's slack, unused.
-    constexpr int NL = FIR_MCPW + 1;                 // LDS reads per set
-    // s_waitcnt lgkmcnt(NL): all but the last set issued have landed (vmcnt, expcnt: no wait)
-    constexpr unsigned LGKM_NL = 0xC07F | (NL << 8);
-    f32x4 av[3][FIR_MCPW], bv[3];
-    auto load = [&](int set, int qq) {
-#pragma unroll
-        for (int j = 0; j < FIR_MCPW; ++j) av[set][j] = *aptr(qq, j);
-        bv[set] = *(const f32x4*)(bp + 16 * qq);
-    };
-    load(0, 0);
+    // one accumulator chain per wave: 16 waves per CU cover its 40-cycle dependent latency (two
+    // alternating accumulators measured the same, 0.351 vs 0.345 ms)
+    acc[0] = f32x4{ 0.0f, 0.0f, 0.0f, 0.0f };
+    // Four operand sets in rotation: chunk q + 2's loads are issued as chunk q's MFMAs start, two
+    // chunks before their use, so the wait before a chunk leaves the next set in flight (explicit
+    // waits, which the compiler's waitcnt pass counts, and scheduling barriers keep it from
+    // waiting on loads it has just issued).  Unrolled by the layout's 8-chunk period, every
+    // address is a per-lane offset plus an immediate: one VALU add per chunk.  Reads past the
+    // last chunk land in the window's zero tail and the tap copy's slack, unused.
+    constexpr unsigned LGKM2 = 0xC07F | (2 << 8);    // s_waitcnt lgkmcnt(2) (vmcnt, expcnt: no wait)
+    f32x4 av[4], bv[4];
+    // chunk 8t + k (k may pass 7: the next period) from the period's pointers pt = pa + 128 t, bt
+#define FIR_LOAD(SET, K, PT, BT)                                                                \
+    av[SET] = *(const f32x4*)((PT) + aoff[(K) & 7] + 128 * ((K) >> 3));                         \
+    bv[SET] = *(const f32x4*)((BT) + 16 * (K));
+#define FIR_STEP(K, PT, BT)                                                                     \
+    __builtin_amdgcn_s_waitcnt(LGKM2);                                                          \
+    FIR_LOAD(((K) + 2) & 3, (K) + 2, PT, BT)                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                          \
+    acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[(K) & 3][0], bv[(K) & 3][0], acc[0], 0, 0, 0); \
+    acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[(K) & 3][1], bv[(K) & 3][1], acc[0], 0, 0, 0); \
+    acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[(K) & 3][2], bv[(K) & 3][2], acc[0], 0, 0, 0); \
+    acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[(K) & 3][3], bv[(K) & 3][3], acc[0], 0, 0, 0); \
     __builtin_amdgcn_sched_barrier(0);
-    load(1, 1);
+    const float* pt = pa;
+    const float* bt = bp;
+    FIR_LOAD(0, 0, pt, bt)
+    __builtin_amdgcn_sched_barrier(0);
+    FIR_LOAD(1, 1, pt, bt)
     __builtin_amdgcn_sched_barrier(0);
     int q = 0;
-#define FIR_STEP(S, QQ)                                                                         \
-    __builtin_amdgcn_s_waitcnt(LGKM_NL);                                                        \
-    load(((S) + 2) % 3, (QQ) + 2);                                                              \
-    __builtin_amdgcn_sched_barrier(0);                                                          \
-    fir_chunk(acc, av[S], bv[S]);                                                               \
-    __builtin_amdgcn_sched_barrier(0);
-    for (; q + 3 <= nq; q += 3)
+    for (; q + 8 <= nq; q += 8, pt += 128, bt += 128)
     {
-        FIR_STEP(0, q)
-        FIR_STEP(1, q + 1)
-        FIR_STEP(2, q + 2)
+        FIR_STEP(0, pt, bt) FIR_STEP(1, pt, bt) FIR_STEP(2, pt, bt) FIR_STEP(3, pt, bt)
+        FIR_STEP(4, pt, bt) FIR_STEP(5, pt, bt) FIR_STEP(6, pt, bt) FIR_STEP(7, pt, bt)
     }
-    if (q < nq) { FIR_STEP(0, q) }
-    if (q + 1 < nq) { FIR_STEP(1, q + 1) }
+    const int rem = nq - q;                          // 0 .. 7 chunks left, the pipeline continues
+    if (rem > 0) { FIR_STEP(0, pt, bt) }
+    if (rem > 1) { FIR_STEP(1, pt, bt) }
+    if (rem > 2) { FIR_STEP(2, pt, bt) }
+    if (rem > 3) { FIR_STEP(3, pt, bt) }
+    if (rem > 4) { FIR_STEP(4, pt, bt) }
+    if (rem > 5) { FIR_STEP(5, pt, bt) }
+    if (rem > 6) { FIR_STEP(6, pt, bt) }
 #undef FIR_STEP
+#undef FIR_LOAD
 }
 
 // D[row = 4 kq + i][col = r] of channel c0 + j's tile at `base` is output base + 16 row + col

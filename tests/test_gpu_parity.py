@@ -94,6 +94,29 @@ def test_device_call_granularity_decimate_first(cuda, back, name, frames):
     np.testing.assert_array_equal(dst, g["dst"])
 
 
+SEG_CASES = [(mode, iqmode, kw) for mode in (U.DEMOD_AM, U.DEMOD_SAM) for iqmode in (0, 1, 3)
+             for kw in ({}, dict(iq_gain_i=1.02, iq_gain_q=0.97, iq_phase_balance=-0.01))]
+SEG_CASES += [(U.DEMOD_SAM, 2, {}), (U.DEMOD_AM, 0, dict(iq_auto_correction=1))]
+
+
+@pytest.mark.parametrize("mode,iqmode,kw", SEG_CASES,
+                         ids=[f"{'am' if m == U.DEMOD_AM else 'sam'}-iq{q}-{'imb' if 'iq_gain_i' in k else 'auto' if k else 'plain'}"
+                              for m, q, k in SEG_CASES])
+@pytest.mark.parametrize("frames", [1024, 2048])
+def test_device_long_calls_decimate_first(cuda, mode, iqmode, kw, frames):
+    """AM / SAM calls longer than one front wave's 512 frames (two or four front launches per
+    call, each carrying the pass-1 history to the next) with the manual I/Q gain / phase
+    correction, the Fs/4 exchanges (iq modes 1, 3), the +6 kHz oscillator (iq mode 2) and auto
+    I/Q correction: bit-exact to the oracle on a ragged batch."""
+    C = 67
+    cfg = U.default_config(filter_path=70, dmod_mode=mode, iq_freq_mode=iqmode, **kw)
+    iq = synth.am_iq(np.arange(C), 0, 2 * frames)
+    a1, dst = run_device(cfg, iq, frames)
+    ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    assert_bitexact(a1, ref_a1, f"mode {mode} iq {iqmode} {kw} frames={frames}")
+    np.testing.assert_array_equal(dst, ref_dst)
+
+
 @pytest.mark.parametrize("path,channels", [(48, 1000), (35, 333), (55, 130), (4, 65)])
 def test_device_matches_oracle_ragged_batches(cuda, back, path, channels):
     mode = U.DEMOD_CW if path == 4 else U.DEMOD_USB

@@ -65,6 +65,9 @@ __device__ __forceinline__ int tx_to_int32(float f)
     return (f > -2147483904.0f && f < 2147483648.0f) ? (int)f : INT32_MIN;
 }
 
+// The ALC's double-precision steps that binary32 reproduces exactly (exhaustive over all binary32
+// inputs, tools/alc_check.c): (float)((double)q - 1.0) is q - 1.0f, and (double)a < 0.001 is
+// a < 0.001f; the 0.1 attack step stays in double.
 // x / 30000 in binary32 (ALC_KNEE, tx_processor.c:202) without the IEEE division sequence:
 // q0 = x * (1/30000) and one FMA residual correction give the correctly rounded quotient for
 // every normal quotient (exhaustive over all binary32 x: tools/div_check.c); tiny, huge, inf and
@@ -165,11 +168,11 @@ __global__ void __launch_bounds__(64) tx_voice(TxVoiceArgs a)
             {
                 const float v = tune ? x[m] : x[m] * post;
                 // ALC (tx_processor.c:197-221)
-                const float alc_var = (float)((double)alc_knee_div(fabsf(v * alc_val)) - 1.0);
+                const float alc_var = alc_knee_div(fabsf(v * alc_val)) - 1.0f;   // == (float)((double)q - 1.0)
                 // both branches evaluated and selected: lanes of a wave no longer split
                 const float dec = alc_val - alc_val * decay * alc_var;
                 float att = (float)((double)alc_val - (double)alc_val * 0.1 * (double)alc_var);
-                att = ((double)att < 0.001) ? 0.001f : att;
+                att = (att < 0.001f) ? 0.001f : att;                 // == (double)att < 0.001
                 alc_val = (alc_var < 0) ? dec : att;
                 if (alc_val > 1) alc_val = 1;
                 if (live) dw[(size_t)m * C] = v;                        // into the delay buffer
@@ -386,10 +389,10 @@ __global__ void __launch_bounds__(128) tx_voice2(TxVoiceArgs a)
             for (int m = 0; m < BLK; ++m)
             {
                 const float v = tune ? x[m] : x[m] * post;
-                const float alc_var = (float)((double)alc_knee_div(fabsf(v * alc_val)) - 1.0);
+                const float alc_var = alc_knee_div(fabsf(v * alc_val)) - 1.0f;   // == (float)((double)q - 1.0)
                 const float dec = alc_val - alc_val * decay * alc_var;
                 float att = (float)((double)alc_val - (double)alc_val * 0.1 * (double)alc_var);
-                att = ((double)att < 0.001) ? 0.001f : att;
+                att = (att < 0.001f) ? 0.001f : att;                 // == (double)att < 0.001
                 alc_val = (alc_var < 0) ? dec : att;
                 if (alc_val > 1) alc_val = 1;
                 if (live) dw[(size_t)m * C] = v;

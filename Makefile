@@ -69,7 +69,8 @@ clean:
 # compile-time variants of libuhsdr_amd.so for A/B measurement (bench.py with UHSDR_LIB=<path>):
 #   make variant VTAG=w3 VFLAGS=-DUHSDR_FUSED_WAVES=3
 # every HIP source is rebuilt with VFLAGS into its own object directory, so a flag read by any
-# source takes effect (VFLAGS=-Itools/isa builds only the P48 receive kernels: quick A/B builds)
+# source takes effect (VFLAGS=-Itools/isa builds only the P48 receive kernels: quick A/B builds;
+# VFLAGS comes first on the line, so its -I wins over csrc for uhsdr_rx_variants.inc)
 VARIANT_DIR := uhsdr_amd/lib/variants
 VOBJDIR = $(OBJDIR)/v_$(VTAG)
 VHIP_OBJS = $(patsubst uhsdr_amd/csrc/%.hip,$(VOBJDIR)/%.o,$(HIP_SRCS))
@@ -77,7 +78,7 @@ $(OBJDIR)/v_%/.dir:
 	mkdir -p $(dir $@) && touch $@
 .PRECIOUS: $(OBJDIR)/v_%/.dir
 $(VOBJDIR)/%.o: uhsdr_amd/csrc/%.hip $(HDRS) | $(VOBJDIR)/.dir
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $< -o $@
+	$(HIPCC) $(VFLAGS) $(HIPFLAGS) -c $< -o $@
 variant: $(HOST_OBJS) $(VHIP_OBJS)
 	mkdir -p $(VARIANT_DIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(VARIANT_DIR)/libuhsdr_amd_$(VTAG).so $(HOST_OBJS) $(VHIP_OBJS) -lm

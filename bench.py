@@ -68,7 +68,9 @@ def algorithmic_bytes(plan, C: int, N: int, write_dst: bool):
     chain = C * ((8 + out_b) * N + 2 * 4 * (fir_hist + back_state) + ring)
     s_live = 4 * (fir_hist + back_state + (AGC_Q * (BLK // M) if plan.agc.mode != 5 else 0))
     # rx_chain (one kernel per call, the hand-off in LDS) moves exactly the chain's bytes
-    return {"rx_front": front, "rx_back": back, "rx_chain": chain, "chain": chain, "s_live_bytes": s_live}
+    # rx_stream (one launch: the hand-off crosses L2 between its front and back-end workgroups)
+    return {"rx_front": front, "rx_back": back, "rx_chain": chain, "rx_stream": chain, "chain": chain,
+            "s_live_bytes": s_live}
 
 
 BLK = 32
@@ -130,8 +132,8 @@ def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
                       f"(affinity mask has {cpus} CPUs), channels split evenly; host CPU: {model}"}
 
 
-SCHEDULES = {"auto": None, "pipe": 1, "fused": 2, "chain": 3}   # uhsdr_rx_set_schedule
-SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain"}
+SCHEDULES = {"auto": None, "pipe": 1, "fused": 2, "chain": 3, "stream": 4}   # uhsdr_rx_set_schedule
+SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain", 4: "stream"}
 
 
 def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, pool, want_dst, pipelined=False,
@@ -179,14 +181,16 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     return elapsed, ktimes, plan, ok, sched
 
 
-def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, backend="nccl", pool=4, sink=None):
+def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, backend="nccl", pool=4, sink=None,
+               always_collective=False):
     """The same chain with every launch's f32 audio gathered to rank 0
     through shard.GatherPipeline: double-buffered outputs, the gather of launch k (RCCL
     grouped send/recv over xGMI, rank 0 receiving from every peer on its own link) in flight
     while launch k+1 computes.  Step s processes the rank's block s % pool of consecutive
     48 kHz blocks.  With the gloo test hook the device audio is copied to host buffers and
     those are gathered.  `sink(step, parts)` (rank 0) sees every step's per-rank blocks in
-    step order.  Returns max-rank seconds for `steps` steps."""
+    step order.  `always_collective`: issue the gather even on a one-rank group (the RCCL leg's
+    readiness test on a one-GPU box).  Returns max-rank seconds for `steps` steps."""
     cfg = U.default_config()
     comp = torch.cuda.current_stream(dev)
     chain = U.RxChain(cfg, channels=C, frames=N, stream=comp.cuda_stream)
@@ -196,7 +200,7 @@ def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warm
     dev_out = torch.empty((C, N), dtype=torch.float32, device=dev) if host else None
     pipe = shard.GatherPipeline(dist, world, rank,
                                 lambda: torch.empty((C, N), dtype=torch.float32, device="cpu" if host else dev),
-                                sink=sink)
+                                sink=sink, always=always_collective)
     st = {"s": 0}
 
     def compute(out):

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define UHSDR_ABI_VERSION 3
+#define UHSDR_ABI_VERSION 4
 
 typedef enum
 {
@@ -309,13 +309,24 @@ uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h);
  *               their back end, the decimated hand-off kept in LDS (large batches).  SSB / CW /
  *               DIGI mono paths (no notch, no stereo, not AM / SAM / FM) with one front pass per
  *               call; elsewhere UHSDR_UNSUPPORTED.
+ *   STREAM      rx_stream: one kernel per call for small batches.  Front and back end run side
+ *               by side on disjoint CUs (one workgroup per CU): front waves filter the call's
+ *               32-frame blocks in time order and publish each block's decimated output, and the
+ *               rx_back wave pipeline of each 64-channel group starts on block 0 while the front
+ *               still filters the rest.  No side stream, no event: outputs are complete in the
+ *               handle's stream order, whatever uhsdr_rx_set_pipelined says.  Wide SSB / CW / DIGI
+ *               mono paths (Hilbert-first, no notch), without the oscillator shift or automatic
+ *               I/Q correction, with at most (CUs / 3) * 64 channels; elsewhere UHSDR_UNSUPPORTED.
  * Stereo, AM / SAM / FM and the LMS notch have their own back-end kernels and ignore SPLIT_*.
  * Returns UHSDR_UNSUPPORTED (handle unchanged) for a schedule the handle's path cannot run.
  * Takes effect from the next uhsdr_rx_process; get returns the resolved schedule. */
 enum { UHSDR_SCHEDULE_AUTO = 0, UHSDR_SCHEDULE_SPLIT_PIPE = 1, UHSDR_SCHEDULE_SPLIT_FUSED = 2,
-       UHSDR_SCHEDULE_CHAIN = 3 };
+       UHSDR_SCHEDULE_CHAIN = 3, UHSDR_SCHEDULE_STREAM = 4 };
 uhsdr_status uhsdr_rx_set_schedule(uhsdr_rx_handle h, int32_t schedule);
 int32_t      uhsdr_rx_get_schedule(uhsdr_rx_handle h);    /* -1 for a null handle */
+/* STREAM's bounded polls: 1 if one gave up (its launch then completed on whatever the hand-off
+   buffer held), 0 if none did since the last uhsdr_rx_reset, -1 on error.  Synchronises. */
+int32_t      uhsdr_rx_stream_timeouts(uhsdr_rx_handle h);
 /* FIR outputs per lane of the front passes: 8 (default: more waves per batch) or 16 (fewer LDS
    window reads per MAC); UHSDR_UNSUPPORTED when the call size does not admit it.  Bit-identical. */
 uhsdr_status uhsdr_rx_set_front_block(uhsdr_rx_handle h, int32_t outputs_per_lane);
@@ -631,6 +642,9 @@ uhsdr_status uhsdr_rx_key_beep(uhsdr_rx_handle h, int32_t calls);
 
 /* ---- diagnostics ---- */
 const char*  uhsdr_version(void);
+/* UHSDR_ABI_VERSION the library was built with: a binding compares it with the header it mirrors
+   (a stale library would otherwise ignore config words it does not know) */
+int32_t      uhsdr_abi_version(void);
 /* sizeof(uhsdr_rx_config), sizeof(uhsdr_rx_plan): lets FFI bindings check their layouts */
 int32_t      uhsdr_sizeof_config(void);
 int32_t      uhsdr_sizeof_plan(void);

@@ -112,3 +112,44 @@ def test_bench_gather_run_bit_exact(cuda, tmp_path):
     ref, _ = oracle.OracleRx(U.build_plan(U.default_config()), C).process(iq, threads=8)
     assert got.shape == ref.shape
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def _nccl_world1_main(rank, world, port, out_path):
+    """bench.gather_run over a one-rank RCCL group with the collective forced on: device output
+    buffers, dist.gather(async_op=True) on the process group's stream, Work.wait() ordering the
+    compute stream -- the path the driver's N > 1 bench takes, on the one GPU of the box."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    got = {}
+
+    def sink(step, parts):
+        assert len(parts) == 1 and parts[0].is_cuda
+        got[step] = parts[0].clone().cpu().numpy()
+
+    el = bench.gather_run(U, synth, shard, torch, dist, dev, world, rank, PER_RANK, FRAMES, STEPS, 0,
+                          backend="nccl", pool=STEPS, sink=sink, always_collective=True)
+    assert el > 0
+    assert sorted(got) == list(range(STEPS)), sorted(got)
+    np.save(out_path, np.concatenate([got[s] for s in range(STEPS)], axis=1))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_gather_run_nccl_world1_bit_exact(cuda, tmp_path):
+    """VERDICT r04 next #7: the RCCL gather leg executed on hardware (one rank, collective forced)."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "gathered_nccl.npy")
+    mp.start_processes(_nccl_world1_main, args=(1, _free_port(), out), nprocs=1, start_method="spawn")
+    got = np.load(out)
+    iq = np.concatenate([synth.ssb_iq_torch(0, PER_RANK, k * FRAMES, FRAMES, cuda).cpu().numpy()
+                         for k in range(STEPS)], axis=1)
+    ref, _ = oracle.OracleRx(U.build_plan(U.default_config()), PER_RANK).process(iq, threads=8)
+    assert got.shape == ref.shape
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))

@@ -127,3 +127,49 @@ def test_pipelined_host_entry(cuda):
     chain.close()
     ref_a1, _ = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
     assert_bitexact(np.concatenate([o[0] for o in outs], axis=1), ref_a1, "pipelined host entry")
+
+
+# mcHF in the pipelined mode: the group's last finishing pass
+# (rx_line_out_mchf) records the group event instead of the back end, and every call's back end
+# writes the single [C][N] scratch row and FM mute array that the finishing pass reads on the
+# side stream.  No synchronisation between calls; a key beep starts in the last call of group 0
+# and runs into group 1.
+MCHF_PIPE_CASES = [
+    ("p48_usb", dict(filter_path=48, spkr_gain=24), synth.ssb_iq, 130, 256, 15),
+    ("p70_sam", dict(filter_path=70, dmod_mode=U.DEMOD_SAM, spkr_gain=30), synth.am_iq, 97, 256, 17),
+    # 16 x 32-frame calls per launch: the squelch's first decision (every 200 calls) falls in call 12
+    ("p1_fm_sql0", dict(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=0, spkr_gain=20), synth.fm_iq, 65, 512, 16),
+]
+
+
+@pytest.mark.parametrize("name,kw,gen,C,N,calls", MCHF_PIPE_CASES, ids=[c[0] for c in MCHF_PIPE_CASES])
+def test_pipelined_mchf_matches_oracle(cuda, name, kw, gen, C, N, calls):
+    import torch
+    cfg = U.default_config(board=U.BOARD_MCHF, **kw)
+    iq = gen(np.arange(C), 0, calls * N)
+    o = oracle.OracleRx(U.build_plan(cfg), C)
+    chain = U.RxChain(cfg, channels=C, frames=N)
+    chain.set_pipelined(True)
+    xs = [torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda() for k in range(calls)]
+    a1 = torch.empty((calls, C, N), dtype=torch.float32, device="cuda")
+    a0 = torch.empty((calls, C, N), dtype=torch.float32, device="cuda")
+    dst = torch.empty((calls, C, N, 2), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    beep_at, beep_calls = 3, N // 32 + 5
+    ref = [[], [], []]
+    for k in range(calls):
+        if k == beep_at:
+            chain.key_beep(beep_calls)
+            o.key_beep(beep_calls)
+        chain.process_stereo(xs[k], a1[k], a0[k], dst[k])
+        for lst, r in zip(ref, o.process2(np.ascontiguousarray(iq[:, k * N:(k + 1) * N]))):
+            lst.append(r)
+    chain.synchronize()
+    got = [t.permute(1, 0, *range(2, t.dim())).reshape((C, calls * N) + tuple(t.shape[3:])).cpu().numpy()
+           for t in (a1, a0, dst)]
+    chain.close()
+    ref = [np.concatenate(x, axis=1) for x in ref]
+    assert_bitexact(got[0], ref[0], f"pipelined mcHF {name} a_buffer[1]")
+    assert_bitexact(got[1], ref[1], f"pipelined mcHF {name} a_buffer[0]")
+    np.testing.assert_array_equal(got[2], ref[2])
+    assert np.abs(ref[0]).max() > 0

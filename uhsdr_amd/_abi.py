@@ -18,6 +18,7 @@ MAX_INTERP = 16
 IQ_BLOCK_SIZE = 32
 FILTER_PATH_NUM = 87
 
+ABI_VERSION = 4   # include/uhsdr.h UHSDR_ABI_VERSION: checked against the library at load()
 UHSDR_OK = 0
 UHSDR_ARGUMENT_ERROR = -1
 UHSDR_LENGTH_ERROR = -2
@@ -29,7 +30,7 @@ SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB, SAM_SIDEBAND_STEREO = ran
 BOARD_OVI40, BOARD_MCHF = 0, 1                 # uhsdr_rx_config.board: the UI board's output stage
 DSP_NOTCH_ENABLE, DSP_MNOTCH_ENABLE, DSP_MPEAK_ENABLE = 0x04, 0x10, 0x20
 PRECISION_EXACT, PRECISION_FMA = 0, 1          # uhsdr_rx_set_precision
-SCHEDULE_AUTO, SCHEDULE_SPLIT_PIPE, SCHEDULE_SPLIT_FUSED, SCHEDULE_CHAIN = range(4)   # uhsdr_rx_set_schedule
+SCHEDULE_AUTO, SCHEDULE_SPLIT_PIPE, SCHEDULE_SPLIT_FUSED, SCHEDULE_CHAIN, SCHEDULE_STREAM = range(5)   # uhsdr_rx_set_schedule
 ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP = 1, 2, 4   # uhsdr_rx_set_clip_output bits
 TWINPEAKS_SAMPLING, TWINPEAKS_DONE, TWINPEAKS_WAIT, TWINPEAKS_UNCORRECTABLE, TWINPEAKS_CODEC_RESTART = range(5)
 
@@ -177,6 +178,7 @@ SIGNATURES = {
     "uhsdr_version": (C.c_char_p, []),
     "uhsdr_last_error": (C.c_char_p, []),
     "uhsdr_sizeof_config": (C.c_int32, []),
+    "uhsdr_abi_version": (C.c_int32, []),
     "uhsdr_sizeof_plan": (C.c_int32, []),
     "uhsdr_rx_kernel_count": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
@@ -189,6 +191,7 @@ SIGNATURES = {
     "uhsdr_rx_get_precision": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_set_schedule": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_rx_get_schedule": (C.c_int32, [C.c_void_p]),
+    "uhsdr_rx_stream_timeouts": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_set_front_block": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_rx_set_cw_outputs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "uhsdr_rx_cw_blocks_max": (C.c_int32, [C.c_void_p]),
@@ -276,6 +279,9 @@ def load(path: str | None = None) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if not variant and lib.uhsdr_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{p} was built for ABI {lib.uhsdr_abi_version()}, this binding mirrors include/uhsdr.h "
+                           f"ABI {ABI_VERSION}: rebuild with `make`")
     if lib.uhsdr_sizeof_config() != C.sizeof(RxConfig) or lib.uhsdr_sizeof_plan() != C.sizeof(RxPlan):
         raise RuntimeError("ctypes layout of uhsdr_rx_config / uhsdr_rx_plan does not match include/uhsdr.h")
     if lib.uhsdr_sizeof_tx_config() != C.sizeof(TxConfig) or lib.uhsdr_sizeof_tx_plan() != C.sizeof(TxPlan):

@@ -407,10 +407,12 @@ static uhsdr_status fir_configure(uhsdr_fir_s* h, int waves, bool strict)
         uhsdr_set_error("num_taps - 1 + block_size %d too long for %d waves per workgroup", h->T - 1 + h->B, waves);
         return UHSDR_LENGTH_ERROR;
     }
+    // the attribute belongs to the kernel, not to this handle: raise it once to the whole CU's LDS,
+    // so a later handle of another shape never lowers the cap an earlier handle launches with
     if (mf && fir_lds(h, waves) > 64 * 1024 &&
-        hipFuncSetAttribute((const void*)fir_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fir_lds(h, waves)) != hipSuccess)
+        hipFuncSetAttribute((const void*)fir_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_PER_CU) != hipSuccess)
     {
-        uhsdr_set_error("cannot raise the MFMA FIR kernel's LDS to %zu bytes", fir_lds(h, waves));
+        uhsdr_set_error("cannot raise the MFMA FIR kernel's LDS to %zu bytes", (size_t)LDS_PER_CU);
         return UHSDR_DEVICE_ERROR;
     }
     // persistent grid: as many workgroups as the CUs hold at once (LDS-limited), each wave

@@ -636,6 +636,17 @@ struct BackArgs
     int beep_n0, beep_n1;
     uint32_t beep_acc;
     int tone_phase;      // FM subaudible tone detector: fm_data.gcount at launch start (mod 400)
+    // channel group of workgroup b is b - grp0 (rx_stream: the back-end workgroups follow the
+    // front's in the grid); 0 for the back-end kernels of their own
+    int grp0;
+    // rx_stream: adec arrives while the kernel runs.  Front wave w of group g stores
+    // sflags[g * swpg + w] = sepoch * 256 + s + 1 once its decimated output of 32-frame call s is
+    // in adec (write-through stores); the back end polls them before it reads a call.  stmo: set
+    // when a poll gave up (a bounded spin).  null sflags: adec is complete at launch.
+    const unsigned* sflags;
+    unsigned sepoch;
+    int swpg;
+    unsigned* stmo;
 };
 
 // softdds_addSingleToneToTwobuffers (softdds.c:142-152): the tone of launch frame n
@@ -728,7 +739,7 @@ struct BackLane
 {
     int lane, c, cl, C, calls;
     bool live;
-    __device__ __forceinline__ explicit BackLane(const BackArgs& a) : BackLane(a, blockIdx.x) {}
+    __device__ __forceinline__ explicit BackLane(const BackArgs& a) : BackLane(a, (int)blockIdx.x - a.grp0) {}
     // channel group grp (channels 64 grp ..): rx_chain's waves name their group themselves
     __device__ __forceinline__ BackLane(const BackArgs& a, int grp)
     {
@@ -750,15 +761,54 @@ struct BackLane
 // LDS_IN (rx_chain): the decimated samples come from the wave's own LDS hand-off `lds`,
 // [sample][lane] with row pitch CHAIN_ADP, instead of adec in HBM
 constexpr int CHAIN_ADP = BACK_CH + 4;
-template <int L, bool LDS_IN = false>
+
+// rx_stream's hand-off of one 32-frame call: every front wave of the lane's group has published
+// it (a relaxed agent-scope poll of swpg words, one per lane, with s_sleep between polls; bounded:
+// a poll that gives up sets stmo and the kernel completes with what adec holds).  The words and the
+// payload are stored write-through by the front (sc1) and read here with sc1 loads, so no acquire
+// fence is needed (MI355X_MICROARCH.md § inter-workgroup visibility, valid forms).
+// (~1 s per poll at the give-up bound; after one give-up the wave polls no more in this launch)
+constexpr unsigned STREAM_SPIN_MAX = 1u << 20;
+__device__ __forceinline__ void stream_wait(const BackArgs& a, int grp, int call, bool& gave_up)
+{
+    const unsigned want = a.sepoch * 256u + (unsigned)call + 1u;
+    const int lane = threadIdx.x & (BACK_CH - 1);
+    const unsigned* f = a.sflags + (size_t)grp * a.swpg + (lane < a.swpg ? lane : 0);
+    for (unsigned spins = 0; !gave_up; ++spins)
+    {
+        const unsigned v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all((int)(v - want) >= 0)) break;
+        if (spins >= STREAM_SPIN_MAX)
+        {
+            if (lane == 0) __hip_atomic_store(a.stmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gave_up = true;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
+}
+
+// STREAM (rx_stream): the decimated samples of a call are read only once the front has published
+// them (stream_wait), by write-through-coherent sc1 loads
+template <int L, bool LDS_IN = false, bool STREAM = false>
 struct InStage
 {
     static constexpr int NDC = BLK / L;
     float xnext[NDC];
     const float* lds;
+    bool gave_up = false;                                // STREAM: a poll of this launch gave up
 
     __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
     {
+        if constexpr (STREAM)
+        {
+            stream_wait(a, (l.c - l.lane) / BACK_CH, call, gave_up);
+            const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m)
+                xnext[m] = __hip_atomic_load(src + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
         if constexpr (LDS_IN)
         {
             // a lane past the last channel reads channel C-1's column (the clamped-load rule: it
@@ -1632,13 +1682,13 @@ __device__ __forceinline__ bool back_agc_prep_in_pre(int dm, const uhsdr_agc_pla
 }
 
 // IIR lattice pre-filter; input: rx_front's decimated I +- Q (SSB) or the demod role's output
-template <int PRE, int L, int W, int DM>
+template <int PRE, int L, int W, int DM, bool STREAM = false>
 __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
-    InStage<L> in;
+    InStage<L, false, STREAM> in;
     LatticeStage<PRE> s;
     s.load(l, P->pre_k, P->pre_v, a.s.pre);
     if (!DM) in.fetch(a, l, 0);
@@ -2086,6 +2136,181 @@ rx_chain(FrontArgs fa, BackArgs ba, int front_floats)
         if (ba.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM_NONE, true, true, false>(ba, smem, grp, adl); return; }
     }
     back_fused_agc<PRE, AA, L, PH, W, DM_NONE, false, true, false>(ba, smem, grp, adl);
+}
+
+// ------------------------------------------------------------------------------------
+// rx_stream: one launch per call for small batches (the SSB / CW / DIGI Hilbert-first paths).
+// The grid holds the call's front and back end side by side on disjoint CUs (one workgroup per
+// CU, forced by the LDS allocation; the host checks that the whole grid is co-resident):
+//   workgroups [0, nfront)        front: F workgroups per channel group of 64; each front wave
+//                                 owns SCPW channels and walks the call's 32-frame calls in time
+//                                 order, publishing each call's decimated output (write-through
+//                                 stores + a per-wave progress word) as soon as it exists
+//   workgroups [nfront, + groups) back end: the rx_back wave pipeline of the group; its pre role
+//                                 polls the progress words before it reads a call (InStage<STREAM>)
+// The back end starts on call 0 while the front still filters calls 1.., with no event, side
+// stream or second launch, and no SIMD shared between the two (a front wave beside a pipeline
+// role on one SIMD slowed the role ~2.5x in the two-stream pipelined mode, profiles/
+// r04_c2_overlap_timeline.txt).  Front workgroups come first in the grid, so a back-end
+// workgroup only ever waits on workgroups dispatched before it; every poll is bounded.
+constexpr int SR = 4;                  // FIR outputs per front lane per 32-frame call
+constexpr int SNB = BLK / SR;          // lanes per channel
+constexpr int SCPW = FRONT_WAVE / SNB; // channels per front wave (8)
+constexpr int SWPG = BACK_CH / SCPW;   // front waves per channel group (8)
+constexpr int STREAM_WAVES = 5;        // workgroup size in waves: the DM_NONE back end's 5 roles
+
+struct StreamArgs
+{
+    unsigned* flags;      // [groups][SWPG] progress words (BackArgs::sflags)
+    unsigned epoch;       // this launch's epoch (>= 1; BackArgs::sepoch)
+    int nfront;           // front workgroups
+    int fpg;              // front workgroups per channel group
+    int wpw;              // front waves per front workgroup (the rest exit)
+    int groups;           // channel groups of 64
+    int lwp, lwd;         // front LDS pitches: pair window, audio-decimator window (floats)
+    int wave_floats;      // LDS floats per front wave (its SCPW pairs of windows)
+};
+
+// front wave w of channel group g: channels 64 g + SCPW w .. + SCPW - 1, all N frames of the call
+template <int T1, int T2, int M, bool F>
+__device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const StreamArgs& sa, int g, int w, float* sm)
+{
+    static_assert(T2 > 0 && M >= 2, "Hilbert-first families with an audio decimator");
+    constexpr int RD = SR / M;
+    constexpr int HQ1 = hist_qp(T1), HQ2 = hist_q(T2);
+    const uhsdr_rx_plan* __restrict__ P = a.plan;
+    const int lane = threadIdx.x & (FRONT_WAVE - 1);
+    const int gl = lane / SNB, bl = lane % SNB;           // channel of the wave, block within a call
+    const int C = a.C, N = a.N, S = N / BLK;
+    const int c0 = g * BACK_CH + w * SCPW;
+    unsigned* const flag = sa.flags + (size_t)g * SWPG + w;
+    if (c0 >= C)
+    {
+        // past the last channel (wave-uniform): nothing to filter, every call published at once
+        if (lane == 0)
+            __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    const int nlive = C - c0 < SCPW ? C - c0 : SCPW;
+    const int c = c0 + gl;
+    const bool live = c < C;
+    const int cl = live ? c : C - 1;
+    float* const smP = sm;                                // pair windows, pitch lwp
+    float* const smD = sm + SCPW * sa.lwp;                // audio-decimator windows, pitch lwd
+    float* const WP = smP + gl * sa.lwp;
+    float* const WD = smD + gl * sa.lwd;
+
+    InputStage in;
+    in.gi = P->iq_gain_i; in.gq = P->iq_gain_q; in.ph = P->iq_phase_balance;
+    in.iq_auto = 0;
+    in.shift = P->freq_shift_hz != 0 ? P->shift_kind : 0;   // 0 or 1 (Fs/4): the host admits no oscillator
+    in.shift_up = P->shift_up;
+    ctaps2_t* tA = as_taps2(a.taps2a);
+    const int comb = a.comb;
+
+    // frames of call 0 and the history rows first, call 1 right behind
+    const int4* src = (const int4*)(a.iq + (size_t)cl * a.ld + bl * SR);
+    int4 raw[SR / 2], rnx[SR / 2];
+#pragma unroll
+    for (int j = 0; j < SR / 2; ++j) raw[j] = src[j];
+    vf4 hA[HQ1], hC[HQ2];
+    group_load_prow<T1>(a.hist1, c0, nlive, lane, hA);
+    group_load_rows<T2>(a.hist2, c0, nlive, lane, hC);
+    if (S > 1)
+    {
+#pragma unroll
+        for (int j = 0; j < SR / 2; ++j) rnx[j] = src[BLK / 2 + j];
+    }
+    group_fill_prow<T1>(smP, sa.lwp, a.hist1, c0, SCPW, nlive, lane, hA);
+    group_fill_rows<T2>(smD, sa.lwd, a.hist2, c0, SCPW, nlive, lane, hC);
+    wave_sync();                                          // the rows' pad floats before the new samples
+    unsigned clip = 0;
+    for (int s = 0; s < S; ++s)
+    {
+        const int blk = s * SNB + bl;                     // the lane's block of SR frames in the call
+        if (a.clip) clip |= clip_flags<SR>(raw);
+        {
+            float xi[SR], xq[SR];
+            convert_block<SR>(raw, in, blk * SR, nullptr, nullptr, nullptr, xi, xq);
+            v2f x2[SR];
+#pragma unroll
+            for (int j = 0; j < SR; ++j) x2[j] = v2f{ xi[j], xq[j] };
+            window_new2(WP, T1, true, blk, x2, SR);
+        }
+#pragma unroll
+        for (int j = 0; j < SR / 2; ++j) raw[j] = rnx[j];
+        if (s + 2 < S)
+        {
+#pragma unroll
+            for (int j = 0; j < SR / 2; ++j) rnx[j] = src[(s + 2) * (BLK / 2) + j];
+        }
+        wave_sync();
+        // Hilbert pair -> I +- Q into the decimator window, then the decimator
+        {
+            v2f h2[SR];
+            float hs[SR];
+            fir_block2<T1, SR, 1, F>(WP + 2 * blk * SR, tA, h2);
+            front_comb_block<SR>(comb, h2, hs);
+            window_new(WD, T2, true, blk, hs, SR);
+        }
+        wave_sync();
+        float o[RD];
+        fir_block<T2, RD, M, 4, F>(WD + blk * SR, as_taps(P->dec), o);
+        if (live)
+        {
+            float* dst = a.adec + (size_t)c * a.ldd + blk * RD;
+#pragma unroll
+            for (int r = 0; r < RD; ++r) __hip_atomic_store(dst + r, o[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // publish call s: this wave's write-through stores complete, then its progress word
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+            __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)s + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (clip && live) atomicOr(a.clip + c, clip);
+    wave_sync();
+    // the next call's history rows
+    group_store_prow<T1>(smP, sa.lwp, a.hist1, c0, nlive, lane, N);
+    group_store_rows<T2>(smD, sa.lwd, a.hist2, c0, nlive, lane, N);
+}
+
+template <int T1, int T2, int M, bool F, int PRE, int AA, int L, int PH, int W>
+__global__ void __launch_bounds__(STREAM_WAVES * FRONT_WAVE) rx_stream(FrontArgs fa, BackArgs ba, StreamArgs sa)
+{
+    static_assert(M == L, "decimation and interpolation rates agree");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / FRONT_WAVE);
+    const int b = blockIdx.x;
+    if (b >= sa.nfront)
+    {
+        // back end of group b - nfront (ba.grp0 = nfront)
+        const BackLds lds = back_lds_carve<BLK / L>(smem);
+        if (wave == 0) rx_back_pre<PRE, L, W, DM_NONE, true>(ba, lds);
+        else if (wave == 1) rx_back_agc<L, W, DM_NONE>(ba, lds);
+        else if (wave == 2) rx_back_audio<L, PH, W, DM_NONE>(ba, lds);
+        else if (wave == 3) rx_back_aa<AA, DM_NONE>(ba, lds);
+        else rx_back_output<DM_NONE>(ba, lds);
+        return;
+    }
+    // front workgroup b -> (channel group, its index f among the group's F): the F workgroups of a
+    // group and the group's back end share b mod 8 when the counts allow (one XCD's L2 under the
+    // observed round-robin placement; placement is never needed for correctness)
+    int g, f;
+    if ((sa.groups & 7) == 0 && (sa.nfront & 7) == 0)
+    {
+        const int x = b & 7, q = b >> 3, gx = sa.groups >> 3;
+        g = x + 8 * (q % gx);
+        f = q / gx;
+    }
+    else
+    {
+        g = b / sa.fpg;
+        f = b % sa.fpg;
+    }
+    if (wave >= sa.wpw) return;
+    const int w = f * sa.wpw + wave;
+    if (w >= SWPG) return;
+    stream_front_wave<T1, T2, M, F>(fa, sa, g, w, smem + wave * sa.wave_floats);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2557,8 +2782,14 @@ struct ChainVariant { int t1, t2, m, decim_first, R, pre, aa, L, ph, w; chain_fn
 #define FRONT_V(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false>, R, rx_front<t1, t2, m, df, R, true>, 0 }
 #define FRONT_ST(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false, true>, R, rx_front<t1, t2, m, df, R, true, true>, 1 }
 struct NotchVariant { int L, dm; back_fn fn; };
+// rx_stream instances: a Hilbert-first front family (t1, t2, m) with a DM_NONE back end
+typedef void (*stream_fn)(FrontArgs, BackArgs, StreamArgs);
+struct StreamVariant { int t1, t2, m, pre, aa, L, ph, w; stream_fn fn, fn_fma; };
+#define STREAM_V(t1, t2, m, pre, aa, ph, w) { t1, t2, m, pre, aa, m, ph, w, \
+    rx_stream<t1, t2, m, false, pre, aa, m, ph, w>, rx_stream<t1, t2, m, true, pre, aa, m, ph, w> }
 #include <uhsdr_rx_variants.inc>
 #undef CHAIN_V
+#undef STREAM_V
 
 static int plan_dm(const uhsdr_rx_plan& p)
 {
@@ -2599,6 +2830,17 @@ static const ChainVariant* find_chain(const uhsdr_rx_plan& p, const BackVariant*
     for (const ChainVariant& v : kChain)
         if (v.t1 == t1 && v.t2 == t2 && v.m == p.decimation_rate && v.decim_first == p.use_decimated_iq &&
             v.pre == bv->pre && v.aa == bv->aa && v.L == bv->L && v.ph == bv->ph && v.w == bv->w)
+            return &v;
+    return nullptr;
+}
+
+static const StreamVariant* find_stream(const uhsdr_rx_plan& p, const BackVariant* bv)
+{
+    if (!bv || bv->dm != DM_NONE || p.stereo || p.notch_enabled || p.dmod_mode == UHSDR_DEMOD_FM || p.use_decimated_iq)
+        return nullptr;
+    for (const StreamVariant& v : kStream)
+        if (v.t1 == p.hilbert_taps && v.t2 == p.dec_taps && v.m == p.decimation_rate && v.pre == bv->pre &&
+            v.aa == bv->aa && v.L == bv->L && v.ph == bv->ph && v.w == bv->w)
             return &v;
     return nullptr;
 }
@@ -2656,6 +2898,7 @@ struct uhsdr_rx_s
     const BackVariant* bv;
     const NotchVariant* nv;  // LMS auto notch kernel (null: notch off)
     const ChainVariant* cv;  // rx_chain instance of the path (null: none)
+    const StreamVariant* sv; // rx_stream instance of the path (null: none)
     int C, N, Nd, Nf;        // Nf: frames per front launch (N split into N / Nf launches)
     int lw;                  // front LDS window pitch (floats)
     int schedule;            // resolved UHSDR_SCHEDULE_SPLIT_PIPE / _SPLIT_FUSED / _CHAIN
@@ -2701,13 +2944,20 @@ struct uhsdr_rx_s
     int nev_cap;
     hipEvent_t* ev;          // [cap][NKERN kernels][start, stop]
     uint8_t* evmask;         // [cap] kernels recorded in each timed call
-    float total_ms[3];
-    int launches[3];
+    float total_ms[4];
+    int launches[4];
+    // rx_stream (UHSDR_SCHEDULE_STREAM): progress words, give-up word, launch geometry
+    unsigned* sflags;        // [groups][SWPG], then the give-up word
+    unsigned* stmo;
+    unsigned stream_epoch;   // rx_stream launches since reset
+    StreamArgs sgeo;         // geometry (flags and epoch are set per launch)
+    size_t s_lds;            // dynamic LDS per workgroup (forces one workgroup per CU)
+    int s_ok;                // the path has an instance, the geometry fits, the grid is co-resident
 };
 
 // kernel slots of the timing API: a call runs rx_front + rx_back (any back-end kernel) or rx_chain
-enum { K_FRONT = 0, K_BACK = 1, K_CHAIN = 2, NKERN = 3 };
-static const char* kKernelNames[NKERN] = { "rx_front", "rx_back", "rx_chain" };
+enum { K_FRONT = 0, K_BACK = 1, K_CHAIN = 2, K_STREAM = 3, NKERN = 4 };
+static const char* kKernelNames[NKERN] = { "rx_front", "rx_back", "rx_chain", "rx_stream" };
 
 static bool side_mode(const uhsdr_rx_s* h) { return h->pipelined; }
 static hipStream_t back_stream(const uhsdr_rx_s* h) { return side_mode(h) ? h->side : h->stream; }
@@ -2912,8 +3162,74 @@ static bool chain_ok(const uhsdr_rx_s* h)
     return h->cv && h->fv->R == h->cv->R && h->Nf == h->N && chain_lds(h) <= 64 * 1024 && !h->plan.agc.remove_dc;
 }
 
-// AUTO: large batches run one kernel (rx_chain) where the path has one, else the fused back end;
-// small ones the back-end wave pipeline (measured crossover BACK_FUSED_MIN_CHANNELS).
+// rx_stream's geometry for the handle's shape.  F front workgroups per channel group of 64 (as many
+// as the CUs left by the back end allow, up to one per front wave), ceil(SWPG / F) front waves in
+// each; one workgroup per CU (the LDS allocation takes more than half a CU's), and the whole grid
+// must be co-resident (occupancy x CUs >= grid): the back end polls the front of its own launch.
+// Pitches: the fewest modeled ds_read_b128 cycles of the two FIR windows (lane = channel l / 8,
+// block l % 8).  Not for the oscillator shift or auto I/Q (their per-launch pre-passes are
+// rx_front's), which keep the split kernels.
+static size_t back_lds(const uhsdr_rx_s* h);
+static int stream_pitch(int need, int stride)
+{
+    int best = need, best_c = 1 << 30;
+    for (int lw = need; lw < need + 64; lw += 4)
+    {
+        int addr[64];
+        for (int l = 0; l < 64; ++l) addr[l] = (l / SNB) * lw + (l % SNB) * stride;
+        const int c = lds_op_cycles(LDS_R128, addr);
+        if (c < best_c) { best_c = c; best = lw; }
+    }
+    return best;
+}
+
+static void stream_geometry(uhsdr_rx_s* h)
+{
+    h->s_ok = 0;
+    const uhsdr_rx_plan& p = h->plan;
+    if (!h->sv || p.iq_auto_correction || (p.freq_shift_hz != 0 && p.shift_kind == 2)) return;
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return;
+    const int cus = prop.multiProcessorCount;
+    const int groups = (h->C + BACK_CH - 1) / BACK_CH;
+    int F = (cus - groups) / groups;
+    if (F > SWPG) F = SWPG;
+    if (F < 1) return;
+    const int wpw = (SWPG + F - 1) / F;
+    if (wpw > STREAM_WAVES) return;
+    const int N = h->N, T1 = h->sv->t1, T2 = h->sv->t2;
+    const int needp = (2 * (T1 - 1 + N) + 3) & ~3;
+    const int nd = T2 - 1 + N > hist_stride(T2) ? T2 - 1 + N : hist_stride(T2);
+    const int lwp = stream_pitch(needp, 2 * SR), lwd = stream_pitch((nd + 3) & ~3, SR);
+    const int wave_floats = (SCPW * (lwp + lwd) + FRONT_SLACK + 3) & ~3;
+    const size_t front = sizeof(float) * (size_t)wpw * wave_floats, back = back_lds(h);
+    size_t lds = front > back ? front : back;
+    if (lds < LDS_PER_CU / 2 + 1024) lds = LDS_PER_CU / 2 + 1024;          // one workgroup per CU
+    if (lds > LDS_PER_CU) return;
+    const int grid = F * groups + groups;
+    for (const void* fn : { (const void*)h->sv->fn, (const void*)h->sv->fn_fma })
+    {
+        int nb = 0;
+        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_PER_CU) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, STREAM_WAVES * FRONT_WAVE, lds) != hipSuccess ||
+            nb < 1 || (long long)nb * cus < grid)
+        {
+            (void)hipGetLastError();
+            return;
+        }
+    }
+    StreamArgs& g = h->sgeo;
+    g.flags = nullptr; g.epoch = 0;
+    g.nfront = F * groups; g.fpg = F; g.wpw = wpw; g.groups = groups;
+    g.lwp = lwp; g.lwd = lwd; g.wave_floats = wave_floats;
+    h->s_lds = lds;
+    h->s_ok = 1;
+}
+
+// AUTO: batches of BACK_FUSED_MIN_CHANNELS channels and more run rx_front + rx_back_fused
+// (SPLIT_FUSED), smaller ones rx_front + the back-end wave pipeline (SPLIT_PIPE); rx_chain (CHAIN)
+// runs only when asked for (measured slower at 1M x 64).
 // Measured and dropped: the fused back end split in two at the interpolator (decimated-rate stages
 // / 48 ksps stages, half the registers each): 0.225 vs 0.211 ms at 1M x 64, and slower on C3 / C5
 // too -- more waves did not raise the VALU issue rate.
@@ -2925,6 +3241,7 @@ static int resolve_schedule(const uhsdr_rx_s* h, int want)
         return h->bv->fused ? UHSDR_SCHEDULE_SPLIT_FUSED : UHSDR_SCHEDULE_SPLIT_PIPE;
     }
     if (want == UHSDR_SCHEDULE_CHAIN) return chain_ok(h) ? want : -1;
+    if (want == UHSDR_SCHEDULE_STREAM) return h->s_ok ? want : -1;
     if (want == UHSDR_SCHEDULE_SPLIT_FUSED) return h->bv->fused ? want : -1;
     if (want == UHSDR_SCHEDULE_SPLIT_PIPE) return want;
     return -1;
@@ -2975,6 +3292,10 @@ extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
     HIPCHK(hipMemcpyAsync(h->osc, osc0, sizeof osc0, hipMemcpyHostToDevice, h->stream));
     // ts.twinpeaks_tested = TWINPEAKS_WAIT at boot (src/uhsdr_main.c:339); the statics start at 0
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->tp, UHSDR_TWINPEAKS_WAIT, (size_t)h->C, h->stream));
+    // rx_stream's progress words restart with the epoch (and its give-up word)
+    if (h->sflags)
+        HIPCHK(hipMemsetAsync(h->sflags, 0, sizeof(unsigned) * (((size_t)(h->C + BACK_CH - 1) / BACK_CH) * SWPG + 4), h->stream));
+    h->stream_epoch = 0;
     if (h->bs.cw)
     {
         // old_siglevel starts at 0.001 (function static, cw_decoder.c:189)
@@ -3024,6 +3345,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->bv = find_back(p);
     h->nv = find_notch(p);
     h->cv = find_chain(p, h->bv);
+    h->sv = find_stream(p, h->bv);
     if (!uhsdr_rx_mode_supported(&p) || !h->fv || !h->bv || (p.notch_enabled && !h->nv))
     {
         free(h);
@@ -3069,12 +3391,14 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         hipMalloc((void**)&h->adec, sizeof(float) * (size_t)C * h->Nd) != hipSuccess ||
         hipMalloc((void**)&h->d_plan, sizeof(uhsdr_rx_plan)) != hipSuccess ||
         hipMalloc((void**)&h->d_taps2, sizeof(float) * 4 * TAPS2_MAX) != hipSuccess ||
-        hipMalloc((void**)&h->d_lanemap, sizeof(uint16_t) * 4 * 64) != hipSuccess)
+        hipMalloc((void**)&h->d_lanemap, sizeof(uint16_t) * 4 * 64) != hipSuccess ||
+        hipMalloc((void**)&h->sflags, sizeof(unsigned) * (((size_t)(C + BACK_CH - 1) / BACK_CH) * SWPG + 4)) != hipSuccess)
     {
         uhsdr_set_error("hipMalloc failed (%zu bytes state)", h->arena_bytes);
         (void)uhsdr_rx_destroy(h);
         return UHSDR_DEVICE_ERROR;
     }
+    h->stmo = h->sflags + ((size_t)(C + BACK_CH - 1) / BACK_CH) * SWPG;
     float* A = (float*)h->arena;
     h->hist1 = A + o_h1; h->hist2 = A + o_h2;
     h->teta = A + o_teta; h->osc = A + o_osc; h->tp = (int*)(A + o_tp);
@@ -3138,6 +3462,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         (void)uhsdr_rx_destroy(h);
         return UHSDR_DEVICE_ERROR;
     }
+    stream_geometry(h);
     const uhsdr_status rs = uhsdr_rx_reset(h);
     if (rs != UHSDR_OK) { (void)uhsdr_rx_destroy(h); return rs; }
     *out = h;
@@ -3275,6 +3600,11 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
         ba.notch_first = h->calls_done == 0;
     }
     ba.tone_phase = (int)(h->calls_done % 400);
+    ba.grp0 = 0;
+    ba.sflags = nullptr;
+    ba.sepoch = 0;
+    ba.swpg = 0;
+    ba.stmo = nullptr;
     {
         // key beep: frames [0, beep_n1) of this launch while calls are left (uhsdr_rx_key_beep)
         const int calls = h->N / BLK;
@@ -3328,7 +3658,36 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
     h->tsample = h->timing && (h->tcalls++ % h->timing) == 0;
     if (h->tsample) h->evmask[h->nev] = 0;
     const bool fma = h->precision == UHSDR_PRECISION_FMA;
-    if (h->schedule == UHSDR_SCHEDULE_CHAIN)
+    if (h->schedule == UHSDR_SCHEDULE_STREAM)
+    {
+        // one kernel: front and back end on disjoint CUs, the hand-off published per 32-frame call;
+        // after every back end still running on the pipelined mode's side stream (state it writes)
+        if (side_mode(h))
+        {
+            HIPCHK(hipEventRecord(h->ev_join, h->side));
+            HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+        }
+        FrontArgs fa = front_args(h, iq, 0, h->adec, nullptr);
+        fa.N = h->N;                                       // the whole call in one launch
+        const BackArgs ba = back_args(h, h->adec, nullptr, audio, audio0, dst);
+        BackArgs bk = back_kernel_args(h, ba);
+        StreamArgs sa = h->sgeo;
+        sa.flags = h->sflags;
+        sa.epoch = ++h->stream_epoch;
+        bk.grp0 = sa.nfront;
+        bk.sflags = h->sflags;
+        bk.sepoch = sa.epoch;
+        bk.swpg = SWPG;
+        bk.stmo = h->stmo;
+        time_mark(h, K_STREAM, 0);
+        hipLaunchKernelGGL(fma ? h->sv->fn_fma : h->sv->fn, dim3(sa.nfront + sa.groups), dim3(STREAM_WAVES * FRONT_WAVE),
+                           h->s_lds, h->stream, fa, bk, sa);
+        line_out_mchf(h, ba, audio0, h->stream);
+        HIPCHK(hipGetLastError());
+        time_mark(h, K_STREAM, 1);
+        h->front_launches += 1;
+    }
+    else if (h->schedule == UHSDR_SCHEDULE_CHAIN)
     {
         // one kernel: front passes and back end per 64 channels, the hand-off in LDS
         // after every back end still running on the pipelined mode's side stream (state it writes)
@@ -3472,7 +3831,7 @@ extern "C" int32_t uhsdr_rx_get_precision(uhsdr_rx_handle h) { return h ? h->pre
 extern "C" uhsdr_status uhsdr_rx_set_schedule(uhsdr_rx_handle h, int32_t schedule)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
-    if (schedule < UHSDR_SCHEDULE_AUTO || schedule > UHSDR_SCHEDULE_CHAIN)
+    if (schedule < UHSDR_SCHEDULE_AUTO || schedule > UHSDR_SCHEDULE_STREAM)
     {
         uhsdr_set_error("schedule %d: not a UHSDR_SCHEDULE_*", (int)schedule);
         return UHSDR_ARGUMENT_ERROR;
@@ -3489,6 +3848,14 @@ extern "C" uhsdr_status uhsdr_rx_set_schedule(uhsdr_rx_handle h, int32_t schedul
 }
 
 extern "C" int32_t uhsdr_rx_get_schedule(uhsdr_rx_handle h) { return h ? h->schedule : -1; }
+
+extern "C" int32_t uhsdr_rx_stream_timeouts(uhsdr_rx_handle h)
+{
+    if (!h || !h->stmo) return -1;
+    unsigned v = 0;
+    if (sync_all(h) != hipSuccess || hipMemcpy(&v, h->stmo, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return (int32_t)v;
+}
 
 extern "C" uhsdr_status uhsdr_rx_set_front_block(uhsdr_rx_handle h, int32_t outputs_per_lane)
 {
@@ -3648,6 +4015,7 @@ extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
     if (h->d_plan) (void)hipFree(h->d_plan);
     if (h->d_taps2) (void)hipFree(h->d_taps2);
     if (h->d_lanemap) (void)hipFree(h->d_lanemap);
+    if (h->sflags) (void)hipFree(h->sflags);
     free(h);
     return UHSDR_OK;
 }

@@ -562,6 +562,7 @@ int uhsdr_rx_mode_supported(const uhsdr_rx_plan* p)
 
 const char* uhsdr_version(void) { return "uhsdr_amd 0.1 (gfx950)"; }
 int32_t uhsdr_sizeof_config(void) { return (int32_t)sizeof(uhsdr_rx_config); }
+int32_t uhsdr_abi_version(void) { return UHSDR_ABI_VERSION; }
 int32_t uhsdr_sizeof_plan(void) { return (int32_t)sizeof(uhsdr_rx_plan); }
 
 /* ================================ transmit ================================ */

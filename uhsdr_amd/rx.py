@@ -151,9 +151,13 @@ class RxChain:
         return self.lib.uhsdr_rx_get_precision(self.handle)
 
     def set_schedule(self, schedule: int) -> None:
-        """SCHEDULE_AUTO / _SPLIT_PIPE / _SPLIT_FUSED / _CHAIN (uhsdr_rx_set_schedule): which kernels
+        """SCHEDULE_AUTO / _SPLIT_PIPE / _SPLIT_FUSED / _CHAIN / _STREAM (uhsdr_rx_set_schedule): which kernels
         run a call; outputs are identical under every one."""
         _abi.check(self.lib.uhsdr_rx_set_schedule(self.handle, int(schedule)), "uhsdr_rx_set_schedule")
+
+    def stream_timeouts(self) -> int:
+        """STREAM schedule: 1 if one of its bounded hand-off polls gave up since reset (synchronises)."""
+        return self.lib.uhsdr_rx_stream_timeouts(self.handle)
 
     @property
     def schedule(self) -> int:

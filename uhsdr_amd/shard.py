@@ -46,12 +46,17 @@ class GatherPipeline:
     Rank 0 hands every completed step to ``sink(step, parts)`` (parts: one tensor per rank,
     in rank order) in step order, right before the receive buffers are reused or at drain().
     Backend-agnostic: only ``dist.gather`` and ``Work.wait`` are used.
+
+    With one rank there is nothing to gather and the collective is skipped, unless `always` is
+    set: then the one-rank group still runs every ``dist.gather`` (device buffers, ``async_op``,
+    ``Work.wait``, the backend's own stream), which exercises the RCCL leg on a one-GPU box.
     """
 
-    def __init__(self, dist, world: int, rank: int, make_buffer, depth: int = 2, sink=None):
+    def __init__(self, dist, world: int, rank: int, make_buffer, depth: int = 2, sink=None, always: bool = False):
         if depth < 1:
             raise ValueError("depth >= 1")
         self.dist, self.world, self.rank, self.depth, self.sink = dist, world, rank, depth, sink
+        self.collective = world > 1 or always
         self.bufs = [make_buffer() for _ in range(depth)]
         self.recv = [[make_buffer() for _ in range(world)] if rank == 0 else None for _ in range(depth)]
         self.work = [None] * depth
@@ -73,7 +78,7 @@ class GatherPipeline:
         k = self.issued % self.depth
         self._retire(k)                       # the gather of step issued - depth read buffer k
         compute(self.bufs[k])
-        if self.world == 1:
+        if not self.collective:
             if self.sink is not None:
                 self.sink(self.issued, [self.bufs[k]])
             self.retired += 1

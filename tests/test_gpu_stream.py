@@ -4,7 +4,7 @@ front's waves and the rx_back wave pipeline on disjoint CUs, the decimated hand-
 CPU oracle like every other schedule:
 
   * every wide (Hilbert-first) SSB / CW / DIGI filter path it serves, ragged batches, several calls;
-  * the launch flags (AGC off / hang, equaliser, CW decoder outputs, key beep, clip flags, mcHF);
+  * the launch flags (AGC off / hang, equaliser, key beep, clip flags, mcHF) and a reset;
   * the C2 shape (4096 x 256) with no synchronisation between calls, and the largest batch;
   * switching to and from it (and out of the pipelined mode) between calls;
   * no bounded hand-off poll ever gives up (uhsdr_rx_stream_timeouts).
@@ -136,29 +136,27 @@ def test_stream_key_beep_and_clip(cuda):
     assert (c[np.arange(C) != 3] & U.ADC_CLIP == 0).all()
 
 
-def test_stream_cw_decoder_outputs(cuda):
-    """CW decoder front end outputs under STREAM equal the wave pipeline's (P48 in CW)."""
+def test_stream_reset_restarts_epoch(cuda):
+    """uhsdr_rx_reset zeroes the progress words with the epoch: calls after a reset (the words'
+    values from before it would otherwise satisfy the polls early) match a fresh handle's."""
     import torch
-    cfg = U.default_config(filter_path=48, dmod_mode=U.DEMOD_CW)
-    C, N, calls = 70, 64, 12
-    iq = synth.ssb_iq(np.arange(C), 0, N * calls)
-    outs = {}
-    for s in (U.SCHEDULE_SPLIT_PIPE, U.SCHEDULE_STREAM):
-        chain = U.RxChain(cfg, channels=C, frames=N, schedule=s)
-        sig = torch.zeros((C, N // 32), dtype=torch.uint8, device="cuda")
-        en = torch.zeros((C, max(chain.cw_blocks_max, 1)), dtype=torch.float32, device="cuda")
-        chain.set_cw_outputs(sig, en)
-        audio = torch.empty((C, N), dtype=torch.float32, device="cuda")
-        rs, re = [], []
-        for k in range(calls):
-            chain.process(torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda(), audio, None)
-            torch.cuda.synchronize()
-            rs.append(sig.cpu().numpy().copy())
-            re.append(en[:, :chain.cw_blocks_last].cpu().numpy().copy())
-        chain.close()
-        outs[s] = (np.concatenate(rs, axis=1), np.concatenate(re, axis=1))
-    np.testing.assert_array_equal(outs[U.SCHEDULE_STREAM][0], outs[U.SCHEDULE_SPLIT_PIPE][0])
-    assert_bitexact(outs[U.SCHEDULE_STREAM][1], outs[U.SCHEDULE_SPLIT_PIPE][1], "cw energy stream")
+    cfg = U.default_config()
+    C, N = 150, 256
+    iq = synth.ssb_iq(np.arange(C), 0, 4 * N)
+    chain = U.RxChain(cfg, channels=C, frames=N, schedule=U.SCHEDULE_STREAM)
+    audio = torch.empty((4, C, N), dtype=torch.float32, device="cuda")
+    xs = [torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda() for k in range(4)]
+    for k in range(4):
+        chain.process(xs[k], audio[k], None)        # epochs 1..4
+    chain.reset()
+    for k in range(4):
+        chain.process(xs[k], audio[k], None)        # epochs 1..4 again, after the words were zeroed
+    chain.synchronize()
+    assert chain.stream_timeouts() == 0
+    got = audio.permute(1, 0, 2).reshape(C, 4 * N).cpu().numpy()
+    chain.close()
+    ref, _ = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    assert_bitexact(got, ref, "stream after reset")
 
 
 def test_stream_c2_shape_unsynchronised(cuda):

@@ -767,16 +767,38 @@ constexpr int CHAIN_ADP = BACK_CH + 4;
 // a poll that gives up sets stmo and the kernel completes with what adec holds).  The words and the
 // payload are stored write-through by the front (sc1) and read here with sc1 loads, so no acquire
 // fence is needed (MI355X_MICROARCH.md § inter-workgroup visibility, valid forms).
+#ifdef UHSDR_STREAM_TRACE
+// timing build (tools/trace_stream.py): s_memrealtime (100 MHz, chip-wide) per workgroup, wave and
+// event of the last rx_stream launch: front waves 0 start, 1 + s after publishing call s, 30 end;
+// back-end roles the start of every pipeline step it, 30 end; the pre role 16 + c when the poll
+// of call c returned
+__device__ unsigned long long g_strace[256][8][32];
+#define STRACE(ev) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) \
+    g_strace[blockIdx.x][threadIdx.x >> 6][(ev)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+extern "C" int uhsdr_strace_read(void* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_strace), sizeof(g_strace)) == hipSuccess ? 0 : -1;
+}
+#else
+#define STRACE(ev) do { } while (0)
+#endif
+
 // (~1 s per poll at the give-up bound; after one give-up the wave polls no more in this launch)
 constexpr unsigned STREAM_SPIN_MAX = 1u << 20;
-__device__ __forceinline__ void stream_wait(const BackArgs& a, int grp, int call, bool& gave_up)
+// v: the word this lane loaded earlier (the poll issued one pipeline step ahead, so its latency
+// hides behind the step); it is re-read only while the call is not yet published
+__device__ __forceinline__ const unsigned* stream_word(const BackArgs& a, int grp)
+{
+    const int lane = threadIdx.x & (BACK_CH - 1);
+    return a.sflags + (size_t)grp * a.swpg + (lane < a.swpg ? lane : 0);
+}
+__device__ __forceinline__ void stream_wait(const BackArgs& a, int grp, int call, unsigned v, bool& gave_up)
 {
     const unsigned want = a.sepoch * 256u + (unsigned)call + 1u;
     const int lane = threadIdx.x & (BACK_CH - 1);
-    const unsigned* f = a.sflags + (size_t)grp * a.swpg + (lane < a.swpg ? lane : 0);
+    const unsigned* f = stream_word(a, grp);
     for (unsigned spins = 0; !gave_up; ++spins)
     {
-        const unsigned v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (__all((int)(v - want) >= 0)) break;
         if (spins >= STREAM_SPIN_MAX)
         {
@@ -784,8 +806,10 @@ __device__ __forceinline__ void stream_wait(const BackArgs& a, int grp, int call
             gave_up = true;
         }
         __builtin_amdgcn_s_sleep(2);
+        v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
+    if (call < 14) STRACE(16 + call);
 }
 
 // STREAM (rx_stream): the decimated samples of a call are read only once the front has published
@@ -797,16 +821,26 @@ struct InStage
     float xnext[NDC];
     const float* lds;
     bool gave_up = false;                                // STREAM: a poll of this launch gave up
+    bool polled = false;                                 // STREAM: fv holds the next call's poll
+    unsigned fv = 0;
 
     __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
     {
         if constexpr (STREAM)
         {
-            stream_wait(a, (l.c - l.lane) / BACK_CH, call, gave_up);
+            const int grp = (l.c - l.lane) / BACK_CH;
+            const unsigned* f = stream_word(a, grp);
+            if (!polled) fv = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            stream_wait(a, grp, call, fv, gave_up);
             const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
 #pragma unroll
             for (int m = 0; m < NDC; ++m)
                 xnext[m] = __hip_atomic_load(src + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef UHSDR_STREAM_EAGER
+            // the poll of the call after this one, answered while this step runs
+            polled = call + 1 < l.calls;
+            if (polled) fv = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
             return;
         }
         if constexpr (LDS_IN)
@@ -1642,6 +1676,7 @@ extern "C" int uhsdr_trace_read(void* out)
     {                                                                                          \
         const int call = it - (ST);                                                            \
         TRACE_MARK(0);                                                                         \
+        if (a.sflags && it < 16) STRACE(it);                                                   \
         if (call >= 0 && call < l.calls)                                                       \
         {
 #define BACK_ROLE_END                                                                          \
@@ -2225,6 +2260,7 @@ __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const Stre
     group_fill_rows<T2>(smD, sa.lwd, a.hist2, c0, SCPW, nlive, lane, hC);
     wave_sync();                                          // the rows' pad floats before the new samples
     unsigned clip = 0;
+    STRACE(0);
     for (int s = 0; s < S; ++s)
     {
         const int blk = s * SNB + bl;                     // the lane's block of SR frames in the call
@@ -2256,22 +2292,40 @@ __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const Stre
         wave_sync();
         float o[RD];
         fir_block<T2, RD, M, 4, F>(WD + blk * SR, as_taps(P->dec), o);
+#ifndef UHSDR_STREAM_EAGER
+        // publish call s - 1 now that this call's FIRs gave its write-through stores time to land
+        // (call 0 is published right away: it sets when the back end starts)
+        if (s > 0)
+        {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0)
+                __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (s < 29) STRACE(s);
+        }
+#endif
         if (live)
         {
             float* dst = a.adec + (size_t)c * a.ldd + blk * RD;
 #pragma unroll
             for (int r = 0; r < RD; ++r) __hip_atomic_store(dst + r, o[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        // publish call s: this wave's write-through stores complete, then its progress word
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)s + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef UHSDR_STREAM_EAGER
+        if (s == 0 || s == S - 1)
+#endif
+        {
+            // publish call s: this wave's write-through stores complete, then its progress word
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0)
+                __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)s + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (s < 29) STRACE(1 + s);
+        }
     }
     if (clip && live) atomicOr(a.clip + c, clip);
     wave_sync();
     // the next call's history rows
     group_store_prow<T1>(smP, sa.lwp, a.hist1, c0, nlive, lane, N);
     group_store_rows<T2>(smD, sa.lwd, a.hist2, c0, nlive, lane, N);
+    STRACE(30);
 }
 
 template <int T1, int T2, int M, bool F, int PRE, int AA, int L, int PH, int W>
@@ -2290,6 +2344,7 @@ __global__ void __launch_bounds__(STREAM_WAVES * FRONT_WAVE) rx_stream(FrontArgs
         else if (wave == 2) rx_back_audio<L, PH, W, DM_NONE>(ba, lds);
         else if (wave == 3) rx_back_aa<AA, DM_NONE>(ba, lds);
         else rx_back_output<DM_NONE>(ba, lds);
+        STRACE(30);
         return;
     }
     // front workgroup b -> (channel group, its index f among the group's F): the F workgroups of a
@@ -2936,6 +2991,7 @@ struct uhsdr_rx_s
     uint8_t* mchf_mute;      // mcHF FM: [C][N/32] squelch on / off per 32-frame call
     long long calls_issued;  // process() calls
     long long pipe_calls;    // calls since the pipelined mode was entered (buffer index, group)
+    int side_dirty;          // back-end work on the side stream not yet joined by a one-kernel call
     // per-kernel timing (uhsdr_rx_enable_timing)
     int timing;               // 0 off, else every timing-th call is bracketed
     int tsample;              // the call being enqueued is a timed one
@@ -3662,10 +3718,11 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
     {
         // one kernel: front and back end on disjoint CUs, the hand-off published per 32-frame call;
         // after every back end still running on the pipelined mode's side stream (state it writes)
-        if (side_mode(h))
+        if (side_mode(h) && h->side_dirty)
         {
             HIPCHK(hipEventRecord(h->ev_join, h->side));
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+            h->side_dirty = 0;
         }
         FrontArgs fa = front_args(h, iq, 0, h->adec, nullptr);
         fa.N = h->N;                                       // the whole call in one launch
@@ -3691,10 +3748,11 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
     {
         // one kernel: front passes and back end per 64 channels, the hand-off in LDS
         // after every back end still running on the pipelined mode's side stream (state it writes)
-        if (side_mode(h))
+        if (side_mode(h) && h->side_dirty)
         {
             HIPCHK(hipEventRecord(h->ev_join, h->side));
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+            h->side_dirty = 0;
         }
         const FrontArgs fa = front_args(h, iq, 0, nullptr, nullptr);
         const BackArgs ba = back_args(h, nullptr, nullptr, audio, audio0, dst);
@@ -3769,6 +3827,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         HIPCHK(hipGetLastError());
         time_mark(h, K_BACK, 1);
         if (h->pipelined) h->pipe_calls += 1;
+        if (side) h->side_dirty = 1;
     }
     h->calls_issued += 1;
     if (h->tsample) h->nev++;

@@ -2188,11 +2188,14 @@ rx_chain(FrontArgs fa, BackArgs ba, int front_floats)
 // role on one SIMD slowed the role ~2.5x in the two-stream pipelined mode, profiles/
 // r04_c2_overlap_timeline.txt).  Front workgroups come first in the grid, so a back-end
 // workgroup only ever waits on workgroups dispatched before it; every poll is bounded.
-constexpr int SR = 4;                  // FIR outputs per front lane per 32-frame call
-constexpr int SNB = BLK / SR;          // lanes per channel
-constexpr int SCPW = FRONT_WAVE / SNB; // channels per front wave (8)
-constexpr int SWPG = BACK_CH / SCPW;   // front waves per channel group (8)
-constexpr int STREAM_WAVES = 5;        // workgroup size in waves: the DM_NONE back end's 5 roles
+constexpr int SR = 2;                  // Hilbert outputs per front lane per 32-frame call
+constexpr int SNB = BLK / SR;          // lanes per channel (16)
+constexpr int SCPW = FRONT_WAVE / SNB; // channels per front wave (4)
+constexpr int SWPG = BACK_CH / SCPW;   // front waves per channel group (16)
+constexpr int STREAM_WAVES = 8;        // workgroup size in waves (the back end's 5 roles use the first 5)
+// (R = 4 outputs per lane, 8 channels and 8 waves per group, one wave per SIMD: 2.9-3.4 us per
+// 32-frame call and the back end waited on every call, C2 0.042-0.045 ms per call; a lone wave
+// hides none of its LDS and tap-load latency, tools/trace_stream.py, profiles/r05_stream_trace_r4.txt)
 
 struct StreamArgs
 {
@@ -2206,16 +2209,58 @@ struct StreamArgs
     int wave_floats;      // LDS floats per front wave (its SCPW pairs of windows)
 };
 
-// front wave w of channel group g: channels 64 g + SCPW w .. + SCPW - 1, all N frames of the call
+// SR = 2 frames n0, n0 + 1 of one channel: int32 -> f32 x 2^-16, manual I/Q correction, the Fs/4
+// exchange (freq_shift.c:219-262) -- convert_block's arithmetic, with the exchange's rotation taken
+// from n0 & 3 (0 or 2 here: a lane's first frame is even, not a multiple of 4) by selects.  The
+// oscillator shift and auto I/Q keep the split kernels (stream_geometry).
+__device__ __forceinline__ void stream_convert2(const int4& raw, const InputStage& s, int n0, float (&xi)[2], float (&xq)[2])
+{
+    xi[0] = ((float)raw.x) * IQ_BIT_SCALE_DOWN; xq[0] = ((float)raw.y) * IQ_BIT_SCALE_DOWN;
+    xi[1] = ((float)raw.z) * IQ_BIT_SCALE_DOWN; xq[1] = ((float)raw.w) * IQ_BIT_SCALE_DOWN;
+    if (s.gi != 1.0f || s.gq != 1.0f)
+    {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) { xi[j] = xi[j] * s.gi; xq[j] = xq[j] * s.gq; }
+    }
+    if (s.ph < 0)
+    {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) { const float e3 = xi[j] * s.ph; xq[j] = xq[j] + e3; }
+    }
+    else if (s.ph > 0)
+    {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) { const float e3 = xq[j] * s.ph; xi[j] = xi[j] + e3; }
+    }
+    if (s.shift == 1)
+    {
+        // (ib, qb) = (I, Q) for FREQ_SHIFT_UP, else (Q, I); frame n gets {x0, -j x1, -x2, j x3}[n & 3]
+        const bool hi = (n0 & 2) != 0;
+        float ib0 = s.shift_up ? xi[0] : xq[0], qb0 = s.shift_up ? xq[0] : xi[0];
+        float ib1 = s.shift_up ? xi[1] : xq[1], qb1 = s.shift_up ? xq[1] : xi[1];
+        // n & 3 == 0 / 2 for the first frame, 1 / 3 for the second
+        const float i0 = ul_sel(hi, -ib0, ib0), q0 = ul_sel(hi, -qb0, qb0);
+        const float i1 = ul_sel(hi, -qb1, qb1), q1 = ul_sel(hi, ib1, -ib1);
+        xi[0] = s.shift_up ? i0 : q0; xq[0] = s.shift_up ? q0 : i0;
+        xi[1] = s.shift_up ? i1 : q1; xq[1] = s.shift_up ? q1 : i1;
+    }
+}
+
+// front wave w of channel group g: channels 64 g + SCPW w .. + SCPW - 1, all N frames of the call.
+// Per 32-frame call s: the Hilbert pair (lane = channel l / 16, SR outputs at 32 s + SR (l % 16)),
+// then the audio decimator on 32 / M outputs per channel (lane = channel l / (32 / M), one output).
 template <int T1, int T2, int M, bool F>
 __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const StreamArgs& sa, int g, int w, float* sm)
 {
-    static_assert(T2 > 0 && M >= 2, "Hilbert-first families with an audio decimator");
-    constexpr int RD = SR / M;
+    static_assert(T2 > 0 && M >= 2 && SR == 2, "Hilbert-first families with an audio decimator");
     constexpr int HQ1 = hist_qp(T1), HQ2 = hist_q(T2);
+    constexpr int DPC = BLK / M;                          // decimated outputs per channel per call
+    constexpr int DV = M % 4 == 0 ? 4 : 2;                // decimator window read width (alignment)
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     const int lane = threadIdx.x & (FRONT_WAVE - 1);
-    const int gl = lane / SNB, bl = lane % SNB;           // channel of the wave, block within a call
+    const int gl = lane / SNB, bl = lane % SNB;           // Hilbert lanes: channel of the wave, block
+    const int gd = lane / DPC, jd = lane % DPC;           // decimator lanes: channel, output
+    const bool dact = gd < SCPW;
     const int C = a.C, N = a.N, S = N / BLK;
     const int c0 = g * BACK_CH + w * SCPW;
     unsigned* const flag = sa.flags + (size_t)g * SWPG + w;
@@ -2228,12 +2273,14 @@ __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const Stre
     }
     const int nlive = C - c0 < SCPW ? C - c0 : SCPW;
     const int c = c0 + gl;
-    const bool live = c < C;
-    const int cl = live ? c : C - 1;
+    const int cl = c < C ? c : C - 1;
+    const int cd = c0 + (dact ? gd : 0);
+    const bool dlive = dact && cd < C;
     float* const smP = sm;                                // pair windows, pitch lwp
     float* const smD = sm + SCPW * sa.lwp;                // audio-decimator windows, pitch lwd
     float* const WP = smP + gl * sa.lwp;
     float* const WD = smD + gl * sa.lwd;
+    float* const WDd = smD + (dact ? gd : 0) * sa.lwd;
 
     InputStage in;
     in.gi = P->iq_gain_i; in.gq = P->iq_gain_q; in.ph = P->iq_phase_balance;
@@ -2245,17 +2292,11 @@ __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const Stre
 
     // frames of call 0 and the history rows first, call 1 right behind
     const int4* src = (const int4*)(a.iq + (size_t)cl * a.ld + bl * SR);
-    int4 raw[SR / 2], rnx[SR / 2];
-#pragma unroll
-    for (int j = 0; j < SR / 2; ++j) raw[j] = src[j];
+    int4 raw = src[0], rnx = raw;
     vf4 hA[HQ1], hC[HQ2];
     group_load_prow<T1>(a.hist1, c0, nlive, lane, hA);
     group_load_rows<T2>(a.hist2, c0, nlive, lane, hC);
-    if (S > 1)
-    {
-#pragma unroll
-        for (int j = 0; j < SR / 2; ++j) rnx[j] = src[BLK / 2 + j];
-    }
+    if (S > 1) rnx = src[BLK / 2];
     group_fill_prow<T1>(smP, sa.lwp, a.hist1, c0, SCPW, nlive, lane, hA);
     group_fill_rows<T2>(smD, sa.lwd, a.hist2, c0, SCPW, nlive, lane, hC);
     wave_sync();                                          // the rows' pad floats before the new samples
@@ -2264,22 +2305,19 @@ __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const Stre
     for (int s = 0; s < S; ++s)
     {
         const int blk = s * SNB + bl;                     // the lane's block of SR frames in the call
-        if (a.clip) clip |= clip_flags<SR>(raw);
+        if (a.clip)
+        {
+            const int4 rr[1] = { raw };
+            clip |= clip_flags<SR>(rr);
+        }
         {
             float xi[SR], xq[SR];
-            convert_block<SR>(raw, in, blk * SR, nullptr, nullptr, nullptr, xi, xq);
-            v2f x2[SR];
-#pragma unroll
-            for (int j = 0; j < SR; ++j) x2[j] = v2f{ xi[j], xq[j] };
+            stream_convert2(raw, in, blk * SR, xi, xq);
+            const v2f x2[SR] = { v2f{ xi[0], xq[0] }, v2f{ xi[1], xq[1] } };
             window_new2(WP, T1, true, blk, x2, SR);
         }
-#pragma unroll
-        for (int j = 0; j < SR / 2; ++j) raw[j] = rnx[j];
-        if (s + 2 < S)
-        {
-#pragma unroll
-            for (int j = 0; j < SR / 2; ++j) rnx[j] = src[(s + 2) * (BLK / 2) + j];
-        }
+        raw = rnx;
+        if (s + 2 < S) rnx = src[(s + 2) * (BLK / 2)];
         wave_sync();
         // Hilbert pair -> I +- Q into the decimator window, then the decimator
         {
@@ -2290,8 +2328,8 @@ __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const Stre
             window_new(WD, T2, true, blk, hs, SR);
         }
         wave_sync();
-        float o[RD];
-        fir_block<T2, RD, M, 4, F>(WD + blk * SR, as_taps(P->dec), o);
+        float o[1];
+        fir_block<T2, 1, M, DV, F>(WDd + s * BLK + jd * M, as_taps(P->dec), o);
 #ifndef UHSDR_STREAM_EAGER
         // publish call s - 1 now that this call's FIRs gave its write-through stores time to land
         // (call 0 is published right away: it sets when the back end starts)
@@ -2300,15 +2338,11 @@ __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const Stre
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0)
                 __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (s < 29) STRACE(s);
+            if (s > 1 && s < 29) STRACE(s);
         }
 #endif
-        if (live)
-        {
-            float* dst = a.adec + (size_t)c * a.ldd + blk * RD;
-#pragma unroll
-            for (int r = 0; r < RD; ++r) __hip_atomic_store(dst + r, o[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (dlive)
+            __hip_atomic_store(a.adec + (size_t)cd * a.ldd + s * DPC + jd, o[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifndef UHSDR_STREAM_EAGER
         if (s == 0 || s == S - 1)
 #endif
@@ -2320,7 +2354,7 @@ __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const Stre
             if (s < 29) STRACE(1 + s);
         }
     }
-    if (clip && live) atomicOr(a.clip + c, clip);
+    if (clip && c < C) atomicOr(a.clip + c, clip);
     wave_sync();
     // the next call's history rows
     group_store_prow<T1>(smP, sa.lwp, a.hist1, c0, nlive, lane, N);
@@ -2337,7 +2371,9 @@ __global__ void __launch_bounds__(STREAM_WAVES * FRONT_WAVE) rx_stream(FrontArgs
     const int b = blockIdx.x;
     if (b >= sa.nfront)
     {
-        // back end of group b - nfront (ba.grp0 = nfront)
+        // back end of group b - nfront (ba.grp0 = nfront): waves 0-4 are the roles, the rest leave
+        // (an ended wave no longer counts at the roles' barriers)
+        if (wave >= back_roles(DM_NONE)) return;
         const BackLds lds = back_lds_carve<BLK / L>(smem);
         if (wave == 0) rx_back_pre<PRE, L, W, DM_NONE, true>(ba, lds);
         else if (wave == 1) rx_back_agc<L, W, DM_NONE>(ba, lds);
@@ -3226,13 +3262,13 @@ static bool chain_ok(const uhsdr_rx_s* h)
 // block l % 8).  Not for the oscillator shift or auto I/Q (their per-launch pre-passes are
 // rx_front's), which keep the split kernels.
 static size_t back_lds(const uhsdr_rx_s* h);
-static int stream_pitch(int need, int stride)
+static int stream_pitch(int need, int per, int stride)
 {
     int best = need, best_c = 1 << 30;
     for (int lw = need; lw < need + 64; lw += 4)
     {
         int addr[64];
-        for (int l = 0; l < 64; ++l) addr[l] = (l / SNB) * lw + (l % SNB) * stride;
+        for (int l = 0; l < 64; ++l) addr[l] = l / per < SCPW ? (l / per) * lw + (l % per) * stride : -1;
         const int c = lds_op_cycles(LDS_R128, addr);
         if (c < best_c) { best_c = c; best = lw; }
     }
@@ -3257,7 +3293,8 @@ static void stream_geometry(uhsdr_rx_s* h)
     const int N = h->N, T1 = h->sv->t1, T2 = h->sv->t2;
     const int needp = (2 * (T1 - 1 + N) + 3) & ~3;
     const int nd = T2 - 1 + N > hist_stride(T2) ? T2 - 1 + N : hist_stride(T2);
-    const int lwp = stream_pitch(needp, 2 * SR), lwd = stream_pitch((nd + 3) & ~3, SR);
+    const int M = h->sv->m;
+    const int lwp = stream_pitch(needp, SNB, 2 * SR), lwd = stream_pitch((nd + 3) & ~3, BLK / M, M);
     const int wave_floats = (SCPW * (lwp + lwd) + FRONT_SLACK + 3) & ~3;
     const size_t front = sizeof(float) * (size_t)wpw * wave_floats, back = back_lds(h);
     size_t lds = front > back ? front : back;

@@ -35,6 +35,7 @@ class RxChain:
         _abi.check(self.lib.uhsdr_rx_create(C.byref(self.config), self.channels, self.frames,
                                             C.c_void_p(stream or 0), C.byref(h)), "uhsdr_rx_create")
         self.handle = h
+        self._process = self.lib.uhsdr_rx_process
         self.plan = _abi.RxPlan()
         _abi.check(self.lib.uhsdr_rx_get_plan(h, C.byref(self.plan)), "uhsdr_rx_get_plan")
         if schedule is not None:
@@ -68,6 +69,24 @@ class RxChain:
             self.handle, C.c_void_p(iq.data_ptr()),
             C.c_void_p(audio.data_ptr() if audio is not None else 0),
             C.c_void_p(dst.data_ptr() if dst is not None else 0)), "uhsdr_rx_process")
+
+    def bind(self, iq, audio=None, dst=None):
+        """Validate one buffer set once (shapes, contiguity: what process() checks every call) and
+        return its raw pointers for process_ptr -- the hot loop's call then costs one ctypes call."""
+        self._shape_ok(iq, (2,))
+        for t, last in ((audio, ()), (dst, (2,))):
+            if t is not None:
+                self._shape_ok(t, last)
+        for t in (iq, audio, dst):
+            if t is not None and not t.is_contiguous():
+                raise ValueError("buffers must be contiguous")
+        return (iq.data_ptr(), audio.data_ptr() if audio is not None else 0, dst.data_ptr() if dst is not None else 0)
+
+    def process_ptr(self, ptrs) -> None:
+        """uhsdr_rx_process on a buffer set bind() validated (the caller keeps the tensors alive)."""
+        st = self._process(self.handle, ptrs[0], ptrs[1], ptrs[2])
+        if st:
+            _abi.check(st, "uhsdr_rx_process")
 
     def process_stereo(self, iq, audio=None, audio0=None, dst=None) -> None:
         """OVI40 two-channel modes: audio = a_buffer[1] (channel 0), audio0 = a_buffer[0] (channel 1)."""

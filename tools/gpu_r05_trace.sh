@@ -16,5 +16,7 @@ for k in 20 1000; do
   timeout -k 10 300 python bench.py --steps $k --warmup 5 --no-cpu --no-northstar --schedule stream > gpurun_out/b_stream_${k}_$tag.json 2> gpurun_out/b_stream_${k}_$tag.err || { tail -20 gpurun_out/b_stream_${k}_$tag.err; exit 1; }
   python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], d['value'], d['config']['schedule'], d['chain']['kernel_ms'])" gpurun_out/b_stream_${k}_$tag.json
 done
-timeout -k 10 200 python tools/host_cost.py > gpurun_out/host_cost_$tag.txt 2>&1 || { tail -20 gpurun_out/host_cost_$tag.txt; exit 1; }
-cat gpurun_out/host_cost_$tag.txt
+if [ -n "$HOSTCOST" ]; then
+  timeout -k 10 200 python tools/host_cost.py > gpurun_out/host_cost_$tag.txt 2>&1 || { tail -20 gpurun_out/host_cost_$tag.txt; exit 1; }
+  cat gpurun_out/host_cost_$tag.txt
+fi

@@ -34,8 +34,9 @@ def main():
     assert lib.uhsdr_strace_read(buf.ctypes.data_as(C.c_void_p)) == 0
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     groups = (Cn + 63) // 64
-    F = min((cus - groups) // groups, 8)
-    wpw = (8 + F - 1) // F
+    SWPG = 16                                                     # front waves per group (uhsdr_rx.hip)
+    F = min((cus - groups) // groups, SWPG)
+    wpw = (SWPG + F - 1) // F
     nfront = F * groups
     S = N // 32
     t = buf.astype(np.int64)
@@ -57,6 +58,17 @@ def main():
             pub[g] = np.maximum(pub[g], [us(t[b, w, 1 + s]) for s in range(S)])
             fend[g] = max(fend[g], us(t[b, w, 30]))
     print(f"C={Cn} N={N}: {nfront} front + {groups} back workgroups ({F} front WGs x {wpw} waves per group)")
+    # front step 3 in detail (events 20-26 of every front wave)
+    fw = []
+    for b in range(nfront):
+        for w in range(wpw):
+            if t[b, w, 20] > 0:
+                fw.append(t[b, w, 20:27] - t[b, w, 20])
+    if fw:
+        fw = np.array(fw) / 100.0
+        lbl = ["convert+prefetch", "wave_sync", "Hilbert FIR", "comb+window+sync", "decimator", "lazy publish", "store+end"]
+        d = np.median(np.diff(fw, axis=1), axis=0)
+        print("front step 3, median us per part: " + ", ".join(f"{lbl[i + 1]} {d[i]:.2f}" for i in range(len(d))))
     print("front publish of call s (group's last wave), median / max over groups:")
     print("  " + " ".join(f"{np.median(pub[:, s]):6.2f}/{pub[:, s].max():6.2f}" for s in range(S)), f" end {np.median(fend):.2f}")
     bk = t[nfront: nfront + groups]

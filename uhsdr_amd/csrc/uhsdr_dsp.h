@@ -62,7 +62,7 @@ __device__ __forceinline__ V fir_mac(V acc, V x, V c)
 }
 
 // V: LDS read width in floats (the lane base is 4V bytes aligned)
-template <int T, int R, int M, int V = 4, bool F = false>
+template <int T, int R, int M, int V = 4, bool F = false, bool TP = false>
 __device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&acc)[R])
 {
     constexpr int WA = (M * (R - 1) + 8 + 7) & ~7;
@@ -75,12 +75,30 @@ __device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&
     for (int r = 0; r < R; ++r) acc[r] = 0.0f;
 #pragma unroll
     for (int j = 0; j < WA; j += V) lds_vec<V>(win + j, w, j);
+    // TP: taps one chunk ahead (fir_block2); here the table is read up to 7 taps past T only in
+    // the tail chunk, which it holds (the plan's decimator taps are UHSDR_MAX_DEC_TAPS = 96 long)
+    float cn[8];
+    if constexpr (TP)
+    {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cn[q] = c[q];
+    }
 #pragma unroll ROT
     for (int ch = 0; ch < NCH; ++ch)
     {
         float cc[8];
+        if constexpr (TP)
+        {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) cc[q] = c[8 * ch + q];
+            for (int q = 0; q < 8; ++q) cc[q] = cn[q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cn[q] = c[8 * (ch + 1) + q];
+        }
+        else
+        {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cc[q] = c[8 * ch + q];
+        }
         float nw[8];
 #pragma unroll
         for (int q = 0; q < 8; q += V) lds_vec<V>(win + 8 * ch + WA + q, nw, q);
@@ -98,7 +116,7 @@ __device__ __forceinline__ void fir_block(const float* win, ctaps_t* c, float (&
 #pragma unroll
     for (int kk = 0; kk < TR; ++kk)
     {
-        const float ck = c[8 * NCH + kk];
+        const float ck = TP ? cn[kk] : c[8 * NCH + kk];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = fir_mac<F>(acc[r], w[r * M + kk], ck);
     }
@@ -129,7 +147,10 @@ __host__ __device__ constexpr int front_pad1(int R, bool decim_first, int M) { r
 
 // PB: the window's pad floats per 8 pairs (pwin_off); win is the lane's first window pair, which
 // starts an 8-pair block when PB > 0
-template <int T, int R, int M, bool F = false, int PB = 0>
+// TP: the next chunk's taps are loaded one chunk ahead (SGPRs carried across the loop), so a wave
+// that runs alone on its SIMD does not wait on the scalar loads at every chunk (SMEM and LDS share
+// lgkmcnt: the wait for a chunk's taps also drained its window prefetch); rx_stream's front
+template <int T, int R, int M, bool F = false, int PB = 0, bool TP = false>
 __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&acc)[R])
 {
     constexpr int WA = (M * (R - 1) + 8 + 7) & ~7;   // window pairs in registers
@@ -144,13 +165,31 @@ __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&
         const vf4 v = *(const vf4*)(win + pwin_off<PB>(j));
         w[j] = v.xy; w[j + 1] = v.zw;
     }
+    v2f cn[8];
+    if constexpr (TP)
+    {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cn[q] = c[q];
+    }
     // unrolled by the rotation period, the window slide is pure register renaming
 #pragma unroll ROT
     for (int ch = 0; ch < NCH; ++ch)
     {
         v2f cc[8];
+        if constexpr (TP)
+        {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) cc[q] = c[8 * ch + q];
+            for (int q = 0; q < 8; ++q) cc[q] = cn[q];
+            // chunk ch + 1's taps (the table is zero-padded to a multiple of 8 taps: the last
+            // chunk's look-ahead reads the tail chunk, or padding)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cn[q] = c[8 * (ch + 1) + q];
+        }
+        else
+        {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cc[q] = c[8 * ch + q];
+        }
         v2f nw[8];
 #pragma unroll
         for (int q = 0; q < 8; q += 2)
@@ -173,7 +212,7 @@ __device__ __forceinline__ void fir_block2(const float* win, ctaps2_t* c, v2f (&
 #pragma unroll
     for (int kk = 0; kk < TR; ++kk)
     {
-        const v2f ck = c[8 * NCH + kk];
+        const v2f ck = TP ? cn[kk] : c[8 * NCH + kk];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = fir_mac<F>(acc[r], w[r * M + kk], ck);
     }

@@ -821,26 +821,37 @@ struct InStage
     float xnext[NDC];
     const float* lds;
     bool gave_up = false;                                // STREAM: a poll of this launch gave up
-    bool polled = false;                                 // STREAM: fv holds the next call's poll
+    bool pending = false;                                // STREAM: xnext not loaded (its call was unpublished)
+    int fcall = -1;                                      // STREAM: the call fv was polled for
     unsigned fv = 0;
+
+    // STREAM: the poll of `call` goes out now and is read at the next step (fv, fcall)
+    __device__ __forceinline__ void stream_poll(const BackArgs& a, const BackLane& l, int call)
+    {
+        if (call >= l.calls) return;
+        fv = __hip_atomic_load(stream_word(a, (l.c - l.lane) / BACK_CH), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fcall = call;
+    }
+    // STREAM: the call's samples once published (fv, polled a step ahead for `call`, answers at
+    // once when the front is ahead), then the poll of the call after it
+    __device__ __forceinline__ void stream_fetch(const BackArgs& a, const BackLane& l, int call)
+    {
+        const int grp = (l.c - l.lane) / BACK_CH;
+        if (fcall != call) fv = __hip_atomic_load(stream_word(a, grp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        stream_wait(a, grp, call, fv, gave_up);
+        const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
+#pragma unroll
+        for (int m = 0; m < NDC; ++m)
+            xnext[m] = __hip_atomic_load(src + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fcall = -1;
+        stream_poll(a, l, call + 1);
+    }
 
     __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
     {
         if constexpr (STREAM)
         {
-            const int grp = (l.c - l.lane) / BACK_CH;
-            const unsigned* f = stream_word(a, grp);
-            if (!polled) fv = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            stream_wait(a, grp, call, fv, gave_up);
-            const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
-#pragma unroll
-            for (int m = 0; m < NDC; ++m)
-                xnext[m] = __hip_atomic_load(src + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifndef UHSDR_STREAM_EAGER
-            // the poll of the call after this one, answered while this step runs
-            polled = call + 1 < l.calls;
-            if (polled) fv = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
+            stream_fetch(a, l, call);
             return;
         }
         if constexpr (LDS_IN)
@@ -865,6 +876,24 @@ struct InStage
 
     __device__ __forceinline__ void begin(const BackArgs& a, const BackLane& l, int call, float (&xin)[NDC])
     {
+        if constexpr (STREAM)
+        {
+            // The step of call k needs call k only: call k + 1 is loaded now if the poll issued
+            // during the last step saw it published, else at the next step (pending); then the poll
+            // for the call after that goes out, answered while this step runs.
+            if (pending) { stream_fetch(a, l, call); pending = false; }
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) xin[m] = xnext[m];
+            if (call + 1 >= l.calls) return;
+            const unsigned want = a.sepoch * 256u + (unsigned)call + 2u;
+            if (fcall == call + 1 && __all((int)(fv - want) >= 0)) stream_fetch(a, l, call + 1);
+            else
+            {
+                pending = true;
+                stream_poll(a, l, call + 1);
+            }
+            return;
+        }
 #pragma unroll
         for (int m = 0; m < NDC; ++m) xin[m] = xnext[m];
         if (call + 1 < l.calls) fetch(a, l, call + 1);
@@ -2318,27 +2347,36 @@ __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const Stre
         }
         raw = rnx;
         if (s + 2 < S) rnx = src[(s + 2) * (BLK / 2)];
+        if (s == 3) STRACE(20);
         wave_sync();
+        if (s == 3) STRACE(21);
         // Hilbert pair -> I +- Q into the decimator window, then the decimator
         {
             v2f h2[SR];
             float hs[SR];
-            fir_block2<T1, SR, 1, F>(WP + 2 * blk * SR, tA, h2);
+            fir_block2<T1, SR, 1, F, 0, true>(WP + 2 * blk * SR, tA, h2);
+            if (s == 3) STRACE(22);
             front_comb_block<SR>(comb, h2, hs);
             window_new(WD, T2, true, blk, hs, SR);
         }
         wave_sync();
+        if (s == 3) STRACE(23);
         float o[1];
-        fir_block<T2, 1, M, DV, F>(WDd + s * BLK + jd * M, as_taps(P->dec), o);
+        fir_block<T2, 1, M, DV, F, true>(WDd + s * BLK + jd * M, as_taps(P->dec), o);
+        if (s == 3) STRACE(24);
 #ifndef UHSDR_STREAM_EAGER
         // publish call s - 1 now that this call's FIRs gave its write-through stores time to land
         // (call 0 is published right away: it sets when the back end starts)
         if (s > 0)
         {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // outstanding: call s - 1's adec store, then (s + 2 < S) this step's frame prefetch;
+            // vector memory operations complete in order, so vmcnt(1) leaves the prefetch in flight
+            if (s + 2 < S) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0)
                 __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (s > 1 && s < 29) STRACE(s);
+            if (s > 1 && s < 20) STRACE(s);
+            if (s == 3) STRACE(25);
         }
 #endif
         if (dlive)
@@ -2351,8 +2389,9 @@ __device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const Stre
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0)
                 __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)s + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (s < 29) STRACE(1 + s);
+            if (s < 19) STRACE(1 + s);
         }
+        if (s == 3) STRACE(26);
     }
     if (clip && c < C) atomicOr(a.clip + c, clip);
     wave_sync();

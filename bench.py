@@ -137,10 +137,10 @@ SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain", 4: "stream"}
 
 
 def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, pool, want_dst, pipelined=False,
-              precision=0, schedule=None, front_block=0, reduce_dev=None):
+              precision=0, schedule=None, front_block=0, reduce_dev=None, board=0):
     """W untimed + K timed steps of one RxChain on this rank; returns (max-rank seconds,
     per-kernel (total ms, launches) from HIP events on the library's stream, plan, finite)."""
-    cfg = U.default_config()
+    cfg = U.default_config(board=board)
     stream = torch.cuda.current_stream(dev)
     chain = U.RxChain(cfg, channels=C, frames=N, stream=stream.cuda_stream, schedule=schedule)
     chain.set_precision(precision)
@@ -273,6 +273,8 @@ def main():
     ap.add_argument("--precision", default="exact", choices=["exact", "fma"],
                     help="FIR MACs: exact (bit-identical to the reference) or fma (1e-5 normwise)")
     ap.add_argument("--pool", type=int, default=8, help="distinct input blocks cycled through")
+    ap.add_argument("--board", default="ovi40", choices=["ovi40", "mchf"],
+                    help="the board's output stage (uhsdr_rx_config.board); the headline is OVI40's")
     ap.add_argument("--schedule", default="auto", choices=sorted(SCHEDULES),
                     help="kernel schedule of a call (uhsdr_rx_set_schedule); auto: the library's choice "
                          "(rx_front + rx_back_fused from 131072 channels on, else rx_front + the back-end wave "
@@ -318,7 +320,8 @@ def main():
     pipelined = args.pipelined or (not args.serial and args.workload != "northstar")
     elapsed, ktimes, plan, ok, sched = timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, args.steps,
                                                  args.warmup, max(1, args.pool), args.dst, pipelined, prec,
-                                                 SCHEDULES[args.schedule], args.front_block, reduce_dev)
+                                                 SCHEDULES[args.schedule], args.front_block, reduce_dev,
+                                                 U.BOARD_MCHF if args.board == "mchf" else U.BOARD_OVI40)
 
     gather = None
     if world > 1 and not args.no_gather:
@@ -383,7 +386,8 @@ def main():
                    "channels_per_gpu": C, "frames_per_call": N, "filter_path": int(plan.filter_path),
                    "parallelism": f"channel-sharded x{world}, no data-path collective",
                    "outputs": "f32 audio" + (" + int32 codec frames" if args.dst else ""),
-                   "pipelined": pipelined, "precision": args.precision, "schedule": sched},
+                   "pipelined": pipelined, "precision": args.precision, "schedule": sched,
+                   **({"board": "mchf"} if args.board == "mchf" else {})},
         "roofline": roofline,
         "chain": {"device_ms_per_step": round(chain_dev_ms, 5),
                   "kernel_ms": {k: round(v, 5) for k, v in kms.items()},

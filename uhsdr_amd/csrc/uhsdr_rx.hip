@@ -617,8 +617,7 @@ struct BackArgs
     const float* adec;   // [C][Nd]  (AM / SAM: decimated I)
     const float* adec_q; // [C][Nd]  AM / SAM: decimated Q
     float* audio;        // [C][N]  or null: adb.a_buffer[1]
-    float* audio0;       // [C][N]  or null: adb.a_buffer[0], stereo only (the second channel)
-    uint8_t* mute;       // [C][N/32] or null: mcHF FM, the squelch's on / off per 32-frame call
+    float* audio0;       // [C][N]  or null: adb.a_buffer[0]: stereo (the second channel) or mcHF (line out)
     int2* dst;           // [C][N]  or null
     BackState s;
     int C, N, Nd;
@@ -636,6 +635,9 @@ struct BackArgs
     int beep_n0, beep_n1;
     uint32_t beep_acc;
     int tone_phase;      // FM subaudible tone detector: fm_data.gcount at launch start (mod 400)
+    int mchf;            // the mcHF board's output stage in line_out4 (plan.single_channel)
+    float* mchf_u;       // mcHF, wave-pipeline back ends: [C][N] scratch for biquad_2's output, which
+                         // rx_line_out_mchf finishes (null: line_out4 runs the whole stage)
     // channel group of workgroup b is b - grp0 (rx_stream: the back-end workgroups follow the
     // front's in the grid); 0 for the back-end kernels of their own
     int grp0;
@@ -1389,22 +1391,66 @@ struct OutputStage
     }
 };
 
-// The OVI40 output stage on four consecutive frames fr0..fr0+3 of a channel (audio_driver.c:
-// 2845-2923; USE_TWO_CHANNEL_AUDIO: a_buffer[1] x LINE_OUT_SCALING_FACTOR in place, a_buffer[0] its
-// copy, the key beep on both, dst {a1, a1}) from u = biquad_2's output x plan.line_out_scale
-// (OutputStage::step); rb + off = the offset of frame fr0 in the [C][N] outputs (the fused back
-// end passes a wave-uniform rb, so its addresses are an SGPR base plus a 32-bit lane offset); call = its 32-frame call (the key
-// beep's test per call is wave-uniform).  on == false:
-// do_mute_output (FM squelch) zeroes both buffers and the codec frames; the key beep is still
-// added to the audio.  mcHF plans run these kernels with line_out_scale 1, no beep and no codec
-// frames into a scratch row, and rx_line_out_mchf finishes their output stage.
+// The board's output stage on four consecutive frames fr0..fr0+3 of a channel, from u = biquad_2's
+// output x plan.line_out_scale (OutputStage::step); rb + off = the offset of frame fr0 in the [C][N]
+// outputs (the fused back end passes a wave-uniform rb, so its addresses are an SGPR base plus a
+// 32-bit lane offset); call = its 32-frame call (the key beep's test per call is wave-uniform).
+//   OVI40 (USE_TWO_CHANNEL_AUDIO, audio_driver.c:2845-2923): a_buffer[1] x LINE_OUT_SCALING_FACTOR
+//     in place (line_out_scale), the key beep added, dst {a1, a1}.
+//   mcHF (audio_driver.c:2870-2897, 2911-2923; a.mchf): line_out_scale is 1, so u is biquad_2's
+//     output; a_buffer[0] = u x LINE_OUT_SCALING_FACTOR (line_out0_scale, audio0), a_buffer[1] =
+//     u x the speaker's software gain (spkr_scale, audio), the beep on a_buffer[1] only, dst {a1, a0}.
+// on == false: do_mute_output (FM squelch) zeroes the buffers before the scaling and the codec frames;
+// the key beep is still added to the audio.  (Round 4 ran the mcHF stage as a separate pass over a
+// [C][N] scratch row the back ends wrote: +8 B per frame of HBM and one more launch per call.)
 __device__ __forceinline__ void line_out4(const BackArgs& a, size_t rb, unsigned off, int call, int fr0,
                                           const float (&u)[4], bool on = true)
 {
+    const bool beep = a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK;     // key beep in this call
+    if (a.mchf && a.mchf_u)
+    {
+        // the wave pipeline's output role is on the per-call critical path: it hands biquad_2's
+        // output to rx_line_out_mchf, which runs the stage over the whole batch in parallel (the
+        // inline stage's second int32 conversion and gains made C2-shaped mcHF calls 0.045 instead
+        // of 0.033 ms, profiles/r05_mchf_fold.txt)
+        *(float4*)((a.mchf_u + rb) + off) = make_float4(on ? u[0] : 0.0f, on ? u[1] : 0.0f, on ? u[2] : 0.0f, on ? u[3] : 0.0f);
+        return;
+    }
+    if (a.mchf)
+    {
+        const uhsdr_rx_plan* __restrict__ P = a.plan;
+        const float sp = P->spkr_scale, lo0 = P->line_out0_scale;
+        float y1[4], y0[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+        {
+            const float v = on ? u[j] : 0.0f;        // +0 when squelched, before the gains as in the reference
+            y1[j] = v * sp;
+            y0[j] = v * lo0;
+        }
+        if (beep)
+        {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (fr0 + j >= a.beep_n0 && fr0 + j < a.beep_n1) y1[j] += beep_tone(a, fr0 + j);
+        }
+        if (a.audio) *(float4*)((a.audio + rb) + off) = make_float4(y1[0], y1[1], y1[2], y1[3]);
+        if (a.audio0) *(float4*)((a.audio0 + rb) + off) = make_float4(y0[0], y0[1], y0[2], y0[3]);
+        if (a.dst)
+        {
+            int2* dd = (a.dst + rb) + off;
+            int d1[4], d0[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { d1[j] = on ? to_dma(y1[j]) : 0; d0[j] = on ? to_dma(y0[j]) : 0; }
+            *(int4*)(dd) = make_int4(d1[0], d0[0], d1[1], d0[1]);
+            *(int4*)(dd + 2) = make_int4(d1[2], d0[2], d1[3], d0[3]);
+        }
+        return;
+    }
     float y[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) y[j] = on ? u[j] : 0.0f;
-    if (a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK)      // key beep in this call
+    if (beep)
     {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -1421,41 +1467,18 @@ __device__ __forceinline__ void line_out4(const BackArgs& a, size_t rb, unsigned
     }
 }
 
-// mcHF output stage (no USE_TWO_CHANNEL_AUDIO, audio_driver.c:2870-2897, 2911-2923) after any back
-// end: u = biquad_2's output (the back end ran with line_out_scale 1, no beep, no codec frames);
-// a_buffer[0] = u x LINE_OUT_SCALING_FACTOR (line out), a_buffer[1] = u x the speaker's software
-// gain (spkr_scale), the key beep on a_buffer[1] only (softdds_addSingleTone, :2896), dst {a1, a0};
-// FM: a squelched call (mute) gives a1 = the beep alone, a0 = 0, dst 0.  Four frames per lane.
-__global__ void __launch_bounds__(256) rx_line_out_mchf(BackArgs a, const float* __restrict__ u, const uint8_t* __restrict__ mute)
+// mcHF output stage after a wave-pipeline back end (rx_back, rx_stream): u = biquad_2's output in
+// the scratch row (line_out4's a.mchf_u), the rest of line_out4's mcHF stage per four frames
+__global__ void __launch_bounds__(256) rx_line_out_mchf(BackArgs a, const float* __restrict__ u)
 {
-    const uhsdr_rx_plan* __restrict__ P = a.plan;
     const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;       // quad of frames
     const int qpc = a.N / 4;
     if (q >= (size_t)a.C * qpc) return;
     const int fr0 = (int)(q % qpc) * 4;
-    const size_t row = q * 4;
-    const float4 x = *(const float4*)(u + row);
-    const bool on = !mute || mute[row / BLK] != 0;
-    const float sp = P->spkr_scale, lo0 = P->line_out0_scale;
+    const float4 x = *(const float4*)(u + q * 4);
     const float v[4] = { x.x, x.y, x.z, x.w };
-    float y1[4], y0[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-    {
-        y1[j] = v[j] * sp;                   // v == +0 when squelched: the product is +0 as the fill's
-        y0[j] = v[j] * lo0;
-        if (fr0 + j >= a.beep_n0 && fr0 + j < a.beep_n1) y1[j] += beep_tone(a, fr0 + j);
-    }
-    if (a.audio) *(float4*)(a.audio + row) = make_float4(y1[0], y1[1], y1[2], y1[3]);
-    if (a.audio0) *(float4*)(a.audio0 + row) = make_float4(y0[0], y0[1], y0[2], y0[3]);
-    if (a.dst)
-    {
-        int d1[4], d0[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { d1[j] = on ? to_dma(y1[j]) : 0; d0[j] = on ? to_dma(y0[j]) : 0; }
-        *(int4*)(a.dst + row) = make_int4(d1[0], d0[0], d1[1], d0[1]);
-        *(int4*)(a.dst + row + 2) = make_int4(d1[2], d0[2], d1[3], d0[3]);
-    }
+    a.mchf_u = nullptr;
+    line_out4(a, q * 4, 0u, fr0 / BLK, fr0, v);
 }
 
 // four consecutive output frames n0..n0+3 of a call (OutputStage::step's): f32 audio and int32 codec frames
@@ -2864,8 +2887,6 @@ __global__ void __launch_bounds__(2 * BACK_CH) rx_fm(BackArgs a)
                     // muted: both buffers zero, the beep still added (audio_driver.c:2845-2898)
                     if (live) line_out4(a, (size_t)c * a.N + call * BLK + n0, 0u, call, call * BLK + n0, v, on);
                 }
-                // mcHF: the call's do_mute_output for rx_line_out_mchf
-                if (a.mute && live) a.mute[(size_t)c * (a.N / BLK) + call] = on ? 1 : 0;
             }
             lds_barrier();
         }
@@ -3051,6 +3072,7 @@ struct uhsdr_rx_s
     int cw_bmax, cw_blocks_last;
     int beep_left;           // key beep: 32-frame calls still to get the tone (uhsdr_rx_key_beep)
     uint32_t beep_acc;       // its softdds accumulator at the next beep frame
+    float* mchf_u;           // mcHF: [C][N] biquad_2 output of a wave-pipeline back end (rx_line_out_mchf's input)
     uint8_t* cw_signal;      // user outputs (uhsdr_rx_set_cw_outputs)
     float* cw_energy;
     long long calls_done;
@@ -3062,8 +3084,6 @@ struct uhsdr_rx_s
     hipEvent_t ev_front, ev_join, ev_back[2];  // ev_back[g % 2]: end of group g's rx_back
     hipEvent_t ev_switch;    // uhsdr_rx_set_stream: new stream after the old one's work
     float *adecp[PIPE_BUFS - 1], *adec_qp[PIPE_BUFS - 1];  // the pipelined mode's other hand-off buffers
-    float* mchf_u;           // mcHF: [C][N] biquad_2 output of the call (rx_line_out_mchf's input)
-    uint8_t* mchf_mute;      // mcHF FM: [C][N/32] squelch on / off per 32-frame call
     long long calls_issued;  // process() calls
     long long pipe_calls;    // calls since the pipelined mode was entered (buffer index, group)
     int side_dirty;          // back-end work on the side stream not yet joined by a one-kernel call
@@ -3515,9 +3535,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const size_t o_notch = take(h->nv ? (size_t)(2 * NOTCH_TAPS + 2 + NOTCH_DELAY) * C : 0);
     const bool cw = p.cw_enabled && p.decimation_rate == 4;
     const size_t o_cw = take(cw ? (size_t)5 * C : 0);
-    const bool mc = p.single_channel != 0;
-    const size_t o_mu = take(mc ? (size_t)C * N : 0);
-    const size_t o_mute = take(mc && h->bv->dm == DM_FM ? ((size_t)C * (N / BLK) + 3) / 4 : 0);
+    const size_t o_mu = take(p.single_channel ? (size_t)C * N : 0);
     h->arena_bytes = fl * sizeof(float);
     if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess ||
         hipMalloc((void**)&h->adec, sizeof(float) * (size_t)C * h->Nd) != hipSuccess ||
@@ -3538,13 +3556,12 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->bs.interp = A + o_ip; h->bs.ring = A + o_ring; h->bs.agc = A + o_agc; h->bs.agci = (int*)(A + o_agci);
     h->bs.sam = am ? A + o_sam : nullptr;
     h->bs.cw = cw ? A + o_cw : nullptr;
+    h->mchf_u = p.single_channel ? A + o_mu : nullptr;
     h->bs.notch = h->nv ? A + o_notch : nullptr;
     h->bs.ring1 = st ? A + o_ring1 : nullptr;
     h->bs.pre1 = st ? A + o_pre1 : nullptr; h->bs.aa1 = st ? A + o_aa1 : nullptr;
     h->bs.bq1_1 = st ? A + o_bq1_1 : nullptr; h->bs.bq2_1 = st ? A + o_bq2_1 : nullptr;
     h->bs.interp1 = st ? A + o_ip1 : nullptr;
-    h->mchf_u = mc ? A + o_mu : nullptr;
-    h->mchf_mute = mc && h->bv->dm == DM_FM ? (uint8_t*)(A + o_mute) : nullptr;
     {
         // blocks per call: one completes at the end of every ceil(blocksize / NDC)-th call
         const int ndc = BLK / p.decimation_rate, cpb = (p.cw_blocksize + ndc - 1) / ndc;
@@ -3716,8 +3733,9 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     ba.adec = adec;
     ba.adec_q = adec_q;
     ba.audio = audio;
-    ba.audio0 = h->plan.stereo ? audio0 : nullptr;
-    ba.mute = nullptr;
+    ba.audio0 = h->plan.stereo || h->plan.single_channel ? audio0 : nullptr;   // stereo / mcHF: a_buffer[0]
+    ba.mchf = h->plan.single_channel != 0;
+    ba.mchf_u = nullptr;
     ba.dst = (int2*)dst;
     ba.s = h->bs;
     ba.C = h->C; ba.N = h->N; ba.Nd = h->Nd;
@@ -3761,26 +3779,12 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     return ba;
 }
 
-// mcHF: the back kernels' arguments (their OVI40 output stage reduced to biquad_2's output into
-// the scratch row) and the finishing pass over it, ordered after them on their stream
-static BackArgs back_kernel_args(const uhsdr_rx_s* h, const BackArgs& ba)
+// mcHF after a wave-pipeline back end: the rest of the board's output stage over the scratch row
+static void line_out_mchf(const uhsdr_rx_s* h, const BackArgs& ba, hipStream_t s)
 {
-    if (!h->plan.single_channel) return ba;
-    BackArgs bk = ba;
-    bk.audio = h->mchf_u;
-    bk.audio0 = nullptr;
-    bk.dst = nullptr;
-    bk.beep_n0 = bk.beep_n1 = 0;
-    bk.mute = h->mchf_mute;
-    return bk;
-}
-static void line_out_mchf(const uhsdr_rx_s* h, BackArgs ba, float* audio0, hipStream_t s)
-{
-    if (!h->plan.single_channel) return;
-    ba.audio0 = audio0;
+    if (!h->mchf_u) return;
     const size_t quads = (size_t)h->C * h->N / 4;
-    hipLaunchKernelGGL(rx_line_out_mchf, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, ba,
-                       (const float*)h->mchf_u, (const uint8_t*)h->mchf_mute);
+    hipLaunchKernelGGL(rx_line_out_mchf, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, ba, (const float*)h->mchf_u);
 }
 
 static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, float* audio0, int32_t* dst)
@@ -3803,7 +3807,8 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         FrontArgs fa = front_args(h, iq, 0, h->adec, nullptr);
         fa.N = h->N;                                       // the whole call in one launch
         const BackArgs ba = back_args(h, h->adec, nullptr, audio, audio0, dst);
-        BackArgs bk = back_kernel_args(h, ba);
+        BackArgs bk = ba;
+        bk.mchf_u = h->mchf_u;                             // mcHF: finished by rx_line_out_mchf
         StreamArgs sa = h->sgeo;
         sa.flags = h->sflags;
         sa.epoch = ++h->stream_epoch;
@@ -3815,7 +3820,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         time_mark(h, K_STREAM, 0);
         hipLaunchKernelGGL(fma ? h->sv->fn_fma : h->sv->fn, dim3(sa.nfront + sa.groups), dim3(STREAM_WAVES * FRONT_WAVE),
                            h->s_lds, h->stream, fa, bk, sa);
-        line_out_mchf(h, ba, audio0, h->stream);
+        line_out_mchf(h, ba, h->stream);
         HIPCHK(hipGetLastError());
         time_mark(h, K_STREAM, 1);
         h->front_launches += 1;
@@ -3834,8 +3839,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         const BackArgs ba = back_args(h, nullptr, nullptr, audio, audio0, dst);
         time_mark(h, K_CHAIN, 0);
         hipLaunchKernelGGL(fma ? h->cv->fn_fma : h->cv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(FRONT_WAVE),
-                           chain_lds(h), h->stream, fa, back_kernel_args(h, ba), (int)chain_front_floats(h));
-        line_out_mchf(h, ba, audio0, h->stream);
+                           chain_lds(h), h->stream, fa, ba, (int)chain_front_floats(h));
         HIPCHK(hipGetLastError());
         time_mark(h, K_CHAIN, 1);
         h->front_launches += 1;
@@ -3871,7 +3875,12 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         time_mark(h, K_FRONT, 1);
 
         const BackArgs ba = back_args(h, adec, adec_q, audio, audio0, dst);
-        const BackArgs bk = back_kernel_args(h, ba);
+        const bool fused = h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo;
+        // mcHF after the wave pipeline (rx_back): biquad_2's output to the scratch row, then
+        // rx_line_out_mchf; the other back ends run the board's stage inline (line_out4)
+        const bool mc_pass = h->mchf_u && !fused && h->bv->dm != DM_FM;
+        BackArgs bk = ba;
+        if (mc_pass) bk.mchf_u = h->mchf_u;
         const hipStream_t bst = back_stream(h);
         if (side) HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
         time_mark(h, K_BACK, 0);
@@ -3880,26 +3889,23 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             hipLaunchKernelGGL(h->nv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, bk);
             HIPCHK(hipGetLastError());
         }
-        const bool fused = h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo;
         const back_fn bfn = fused ? fused_back_fn(h) : h->bv->fn;
         const dim3 bgrid((h->C + BACK_CH - 1) / BACK_CH), bblock(fused ? BACK_CH : back_roles(h->bv->dm) * BACK_CH);
         const size_t blds = fused ? 0 : back_lds(h);
-        // pipelined: the group's last rx_back (mcHF: its finishing pass) records ev_back[grp] as it completes
-        const bool mc = h->plan.single_channel != 0;
-        if (side && group_end && !mc)
+        // pipelined: the group's last rx_back (mcHF pass: the finishing kernel) records ev_back[grp]
+        // as it completes
+        if (side && group_end && !mc_pass)
             hipExtLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, nullptr, h->ev_back[grp], 0, bk);
         else
             hipLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, bk);
-        if (mc && side && group_end)
+        if (mc_pass && side && group_end)
         {
-            BackArgs bo = ba;
-            bo.audio0 = audio0;
             const size_t quads = (size_t)h->C * h->N / 4;
             hipExtLaunchKernelGGL(rx_line_out_mchf, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, bst, nullptr,
-                                  h->ev_back[grp], 0, bo, (const float*)h->mchf_u, (const uint8_t*)h->mchf_mute);
+                                  h->ev_back[grp], 0, ba, (const float*)h->mchf_u);
         }
-        else
-            line_out_mchf(h, ba, audio0, bst);
+        else if (mc_pass)
+            line_out_mchf(h, ba, bst);
         HIPCHK(hipGetLastError());
         time_mark(h, K_BACK, 1);
         if (h->pipelined) h->pipe_calls += 1;

@@ -75,7 +75,13 @@ def test_fir_matches_oracle_distinct_channels(cuda, mode, T, B):
         assert normwise(got, ref) < TOL
 
 
-WAVE_CASES = [(m, w) for m in (U.fir.EXACT, U.fir.MFMA) for w in (1, 2, 4)] + [(U.fir.MFMA, w) for w in (7, 16)]
+WAVE_CASES = [(m, w) for m in (U.fir.EXACT, U.fir.MFMA) for w in (1, 2, 4)] + [(U.fir.MFMA, w) for w in (7, 8, 16)]
+
+
+def mfma_default_waves(T):
+    """513 taps (K = 528 = 16 x 33): fir_mfma_rb, the taps' B fragments in registers, 8 waves per
+    workgroup at most; every other tap count: fir_mfma, 16 windows"""
+    return 8 if (T + 15 + 15) // 16 == 33 else 16
 
 
 @pytest.mark.parametrize("mode,waves", WAVE_CASES, ids=[f"{'mfma' if m else 'exact'}-{w}" for m, w in WAVE_CASES])
@@ -89,7 +95,12 @@ def test_fir_waves_per_workgroup(cuda, mode, waves, T, B):
     taps = np.load(os.path.join(GOLD, "fir513_kaiser.npy")) if T == 513 else rng.uniform(-0.3, 0.3, T).astype(np.float32)
     x = rng.normal(0, 1000, (C, 2 * B)).astype(np.float32)
     fir = U.FirBatch(taps, C, B, mode)
-    assert fir.waves == (16 if mode == U.fir.MFMA else 2)       # MFMA: 16 windows fit these shapes
+    assert fir.waves == (mfma_default_waves(T) if mode == U.fir.MFMA else 2)
+    if mode == U.fir.MFMA and waves > mfma_default_waves(T):
+        with pytest.raises(RuntimeError):
+            fir.set_waves(waves)
+        fir.close()
+        return
     fir.set_waves(waves)
     assert fir.waves == waves
     got = run(fir, x, B)
@@ -114,6 +125,12 @@ def test_fir_set_waves_rejects(cuda):
         with pytest.raises(RuntimeError):
             fir.set_waves(bad)
         assert fir.waves == 16
+    fir.close()
+    fir = U.FirBatch(np.ones(513, np.float32), 4, 256, U.fir.MFMA)
+    for bad in (0, 9, 16, -1):
+        with pytest.raises(RuntimeError):
+            fir.set_waves(bad)
+        assert fir.waves == 8
     fir.close()
 
 

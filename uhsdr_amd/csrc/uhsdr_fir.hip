@@ -350,6 +350,110 @@ __global__ void __launch_bounds__(1024) fir_mfma(FirArgs a)
     if (last_c0 >= 0) fir_store_tile(a, last_c0, a.B - FIR_TILE, lane, last);
 }
 
+// ---- MFMA, the taps' B fragments in registers (round 5) ----
+// The B operand of chunk q (four consecutive taps per lane, the Toeplitz tile's columns) is the same
+// for every tile of every channel: a wave loads its NQ fragments once and keeps them in registers
+// (4 NQ floats per lane, AGPRs or VGPRs), so a chunk reads only its A fragment from LDS -- one
+// ds_read_b128 per four MFMAs instead of two.  The register budget allows two waves per SIMD (8 per
+// workgroup, one workgroup per CU).  For fir_mfma's 2,332 LDS reads per wave at 80 % of its cycles
+// waiting (PMC r04).  NQ = K / 16 is a template parameter: C5's 513 taps, K = 528.
+constexpr int FIR_RB_NQ = 33;
+constexpr int FIR_RB_WAVES = 8;
+
+template <int NQ>
+__device__ __forceinline__ void fir_tile_rb(const float* Wg, int base, int lane, const f32x4 (&bq)[NQ], f32x4& acc)
+{
+    const int r = lane & 15, kq = lane >> 4;
+    const int ai = base + 16 * r + 4 * kq;
+    const float* pa = Wg + ai;
+    int aoff[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) aoff[k] = fir_swz(ai + 16 * k) - ai;
+    acc = f32x4{ 0.0f, 0.0f, 0.0f, 0.0f };
+    constexpr unsigned LGKM1 = 0xC07F | (1 << 8);    // s_waitcnt lgkmcnt(1) (vmcnt, expcnt: no wait)
+    f32x4 av[4];
+    av[0] = *(const f32x4*)(pa + aoff[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    av[1] = *(const f32x4*)(pa + aoff[1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+    {
+        // chunk q's A fragment has landed (chunk q + 1's is the one load still in flight)
+        __builtin_amdgcn_s_waitcnt(LGKM1);
+        if (q + 2 < NQ) av[(q + 2) & 3] = *(const f32x4*)(pa + aoff[(q + 2) & 7] + 128 * ((q + 2) >> 3));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q & 3][s], bq[q][s], acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int NQ>
+__global__ void __launch_bounds__(64 * FIR_RB_WAVES) fir_mfma_rb(FirArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int H = a.T - 1, n = H + a.B;
+    float* cp = sm;
+    for (int i = threadIdx.x; i < a.cp; i += blockDim.x)
+    {
+        const int x = i % a.cpl - i / a.cpl - 16;
+        cp[i] = (x >= 0 && x < a.T) ? a.taps[x] : 0.0f;
+    }
+    float* const Wb = sm + a.cp + (size_t)w * 2 * FIR_MCPW * a.lw;
+    for (int i = lane; i < 2 * FIR_MCPW * a.lw; i += 64) Wb[i] = 0.0f;
+    __syncthreads();
+    // the wave's B fragments, chunk q at bp + 16 q (fir_tile's layout)
+    f32x4 bq[NQ];
+    {
+        const int r = lane & 15, kq = lane >> 4;
+        const float* bp = cp + (r & 3) * a.cpl + 16 + 4 * kq - 4 * (r >> 2);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) bq[q] = *(const f32x4*)(bp + 16 * q);
+    }
+    const bool v4 = a.v4 != 0;
+    const int ng = a.C;
+    const int nwt = gridDim.x * nw;
+    auto fill = [&](int g, int buf) {
+        const int cl = g < a.C ? g : a.C - 1;
+        float* W = Wb + buf * a.lw;
+        if (v4) fir_fill_glds<16>(W, a.hist + (size_t)cl * H, a.src + (size_t)cl * a.B, H, n, lane);
+        else fir_fill_glds<4>(W, a.hist + (size_t)cl * H, a.src + (size_t)cl * a.B, H, n, lane);
+    };
+    int g = blockIdx.x * nw + w, buf = 0;
+    if (g < ng) fill(g, 0);
+    f32x4 last[FIR_MCPW];
+    int last_c0 = -1;
+    for (; g < ng; g += nwt, buf ^= 1)
+    {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (g + nwt < ng) fill(g + nwt, buf ^ 1);
+        if (last_c0 >= 0) fir_store_tile(a, last_c0, a.B - FIR_TILE, lane, last);
+        const float* Wg = Wb + buf * a.lw;
+        const int c0 = g;
+        {
+            const float* W = Wg + a.B;
+            float* hr = a.hist + (size_t)c0 * H;
+            if (v4)
+                for (int i = 4 * lane; i < H; i += 256) *(f32x4*)(hr + i) = *(const f32x4*)(W + fir_swz(a.B + i) - a.B);
+            else
+                for (int i = lane; i < H; i += 64) hr[i] = W[fir_swz(a.B + i) - a.B];
+        }
+        for (int t = 0; t < a.B / FIR_TILE; ++t)
+        {
+            f32x4 acc[FIR_MCPW];
+            fir_tile_rb<NQ>(Wg, FIR_TILE * t, lane, bq, acc[0]);
+            if (t + 1 < a.B / FIR_TILE) fir_store_tile(a, c0, FIR_TILE * t, lane, acc);
+            else last[0] = acc[0];
+        }
+        last_c0 = c0;
+        wave_sync();
+    }
+    if (last_c0 >= 0) fir_store_tile(a, last_c0, a.B - FIR_TILE, lane, last);
+}
+
 } // namespace
 
 constexpr size_t LDS_PER_CU = 160 * 1024;        // MI355X_MICROARCH.md §LDS
@@ -357,6 +461,7 @@ constexpr size_t LDS_PER_CU = 160 * 1024;        // MI355X_MICROARCH.md §LDS
 struct uhsdr_fir_s
 {
     int C, B, T, K, mode, lw, cp, cpl, waves, grid;
+    int rb;                  // MFMA with the B fragments in registers (fir_mfma_rb; K == 16 FIR_RB_NQ)
     hipStream_t stream;
     float* taps;
     float* hist;
@@ -393,9 +498,10 @@ extern "C" uhsdr_status uhsdr_fir_reset(uhsdr_fir_handle h)
 static uhsdr_status fir_configure(uhsdr_fir_s* h, int waves, bool strict)
 {
     const bool mf = h->mode == UHSDR_FIR_MFMA;
-    if (mf ? (waves < 1 || waves > 16) : (waves != 1 && waves != 2 && waves != 4))
+    const int wmax = h->rb ? FIR_RB_WAVES : 16;
+    if (mf ? (waves < 1 || waves > wmax) : (waves != 1 && waves != 2 && waves != 4))
     {
-        uhsdr_set_error("waves per workgroup %d not %s", waves, mf ? "1 .. 16" : "1, 2 or 4");
+        uhsdr_set_error("waves per workgroup %d not %s", waves, mf ? (h->rb ? "1 .. 8" : "1 .. 16") : "1, 2 or 4");
         return UHSDR_ARGUMENT_ERROR;
     }
     // MFMA: one workgroup may hold the whole CU's LDS (MI355X_MICROARCH.md §LDS)
@@ -409,8 +515,9 @@ static uhsdr_status fir_configure(uhsdr_fir_s* h, int waves, bool strict)
     }
     // the attribute belongs to the kernel, not to this handle: raise it once to the whole CU's LDS,
     // so a later handle of another shape never lowers the cap an earlier handle launches with
+    const void* kfn = h->rb ? (const void*)fir_mfma_rb<FIR_RB_NQ> : (const void*)fir_mfma;
     if (mf && fir_lds(h, waves) > 64 * 1024 &&
-        hipFuncSetAttribute((const void*)fir_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_PER_CU) != hipSuccess)
+        hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_PER_CU) != hipSuccess)
     {
         uhsdr_set_error("cannot raise the MFMA FIR kernel's LDS to %zu bytes", (size_t)LDS_PER_CU);
         return UHSDR_DEVICE_ERROR;
@@ -425,6 +532,14 @@ static uhsdr_status fir_configure(uhsdr_fir_s* h, int waves, bool strict)
     int per_cu = (int)(LDS_PER_CU / lds);
     const int thread_cap = 2048 / (64 * waves);
     if (per_cu > thread_cap) per_cu = thread_cap;
+    if (mf)
+    {
+        // the register file may admit fewer workgroups than the LDS: a persistent grid larger than
+        // what is resident would leave its last workgroups to run after the others
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, 64 * waves, lds) == hipSuccess && occ > 0 && occ < per_cu)
+            per_cu = occ;
+    }
     if (per_cu < 1) per_cu = 1;
     const int cpg = h->mode == UHSDR_FIR_MFMA ? FIR_MCPW : FIR_CPW;
     const int groups = (h->C + cpg - 1) / cpg;
@@ -461,10 +576,13 @@ extern "C" uhsdr_status uhsdr_fir_create(const float* coeffs, int32_t num_taps, 
     h->lw = mf ? (num_taps - 1 + block_size + FIR_MTAIL + 15) & ~15 : (fpad(num_taps - 1 + block_size + FIR_TAIL) + 4) & ~3;
     h->cpl = h->K + FIR_MTAIL;
     h->cp = (mf ? 4 : 1) * h->cpl;
+#ifndef UHSDR_FIR_NO_RB
+    h->rb = mf && h->K == 16 * FIR_RB_NQ;
+#endif
     // waves per workgroup: EXACT 2 (one group per wave, more resident waves per CU: C5 513-tap
     // 1.048 -> 0.927 ms per call); MFMA as many as one workgroup's LDS holds, up to 16 (one
     // persistent workgroup per CU); uhsdr_fir_set_waves picks the count explicitly
-    const uhsdr_status st = fir_configure(h, mode == UHSDR_FIR_MFMA ? 16 : 2, false);
+    const uhsdr_status st = fir_configure(h, mode == UHSDR_FIR_MFMA ? (h->rb ? FIR_RB_WAVES : 16) : 2, false);
     if (st != UHSDR_OK)
     {
         free(h);
@@ -493,7 +611,9 @@ extern "C" uhsdr_status uhsdr_fir_process(uhsdr_fir_handle h, const float* src, 
     // 16-byte window fills: carried rows and the caller's block 16-byte aligned
     a.v4 = (h->T - 1) % 4 == 0 && ((uintptr_t)src & 15) == 0;
     const dim3 grid(h->grid), block(64 * h->waves);
-    if (h->mode == UHSDR_FIR_MFMA)
+    if (h->mode == UHSDR_FIR_MFMA && h->rb)
+        hipLaunchKernelGGL(fir_mfma_rb<FIR_RB_NQ>, grid, block, fir_lds(h, h->waves), h->stream, a);
+    else if (h->mode == UHSDR_FIR_MFMA)
         hipLaunchKernelGGL(fir_mfma, grid, block, fir_lds(h, h->waves), h->stream, a);
     else
         hipLaunchKernelGGL(fir_batch_direct, grid, block, fir_lds(h, h->waves), h->stream, a);

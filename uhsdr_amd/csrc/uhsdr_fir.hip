@@ -358,7 +358,10 @@ __global__ void __launch_bounds__(1024) fir_mfma(FirArgs a)
 // workgroup, one workgroup per CU).  For fir_mfma's 2,332 LDS reads per wave at 80 % of its cycles
 // waiting (PMC r04).  NQ = K / 16 is a template parameter: C5's 513 taps, K = 528.
 constexpr int FIR_RB_NQ = 33;
-constexpr int FIR_RB_WAVES = 8;
+#ifndef UHSDR_FIR_RB_WAVES
+#define UHSDR_FIR_RB_WAVES 8
+#endif
+constexpr int FIR_RB_WAVES = UHSDR_FIR_RB_WAVES;
 
 template <int NQ>
 __device__ __forceinline__ void fir_tile_rb(const float* Wg, int base, int lane, const f32x4 (&bq)[NQ], f32x4& acc)
@@ -370,18 +373,26 @@ __device__ __forceinline__ void fir_tile_rb(const float* Wg, int base, int lane,
 #pragma unroll
     for (int k = 0; k < 8; ++k) aoff[k] = fir_swz(ai + 16 * k) - ai;
     acc = f32x4{ 0.0f, 0.0f, 0.0f, 0.0f };
-    constexpr unsigned LGKM1 = 0xC07F | (1 << 8);    // s_waitcnt lgkmcnt(1) (vmcnt, expcnt: no wait)
+#ifndef UHSDR_FIR_RB_AHEAD
+#define UHSDR_FIR_RB_AHEAD 2
+#endif
+    // A fragments load AH chunks ahead (AH - 1 loads in flight while a chunk's MFMAs run)
+    constexpr int AH = UHSDR_FIR_RB_AHEAD;
+    constexpr unsigned LGKMW = 0xC07F | ((AH - 1) << 8);   // s_waitcnt lgkmcnt(AH - 1) (vmcnt, expcnt: no wait)
     f32x4 av[4];
-    av[0] = *(const f32x4*)(pa + aoff[0]);
-    __builtin_amdgcn_sched_barrier(0);
-    av[1] = *(const f32x4*)(pa + aoff[1]);
-    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < AH; ++q)
+    {
+        av[q] = *(const f32x4*)(pa + aoff[q]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
     {
-        // chunk q's A fragment has landed (chunk q + 1's is the one load still in flight)
-        __builtin_amdgcn_s_waitcnt(LGKM1);
-        if (q + 2 < NQ) av[(q + 2) & 3] = *(const f32x4*)(pa + aoff[(q + 2) & 7] + 128 * ((q + 2) >> 3));
+        // chunk q's A fragment has landed (the next AH - 1 chunks' may still be in flight)
+        if (q + AH <= NQ) __builtin_amdgcn_s_waitcnt(LGKMW);
+        else __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (q + AH < NQ) av[(q + AH) & 3] = *(const f32x4*)(pa + aoff[(q + AH) & 7] + 128 * ((q + AH) >> 3));
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q & 3][s], bq[q][s], acc, 0, 0, 0);

@@ -363,44 +363,80 @@ constexpr int FIR_RB_NQ = 33;
 #endif
 constexpr int FIR_RB_WAVES = UHSDR_FIR_RB_WAVES;
 
-template <int NQ>
-__device__ __forceinline__ void fir_tile_rb(const float* Wg, int base, int lane, const f32x4 (&bq)[NQ], f32x4& acc)
+// CH channels per wave (their windows lw floats apart), one accumulator chain each, interleaved
+// per k-step: the 40-cycle dependent latency of v_mfma_f32_16x16x4_f32 (32-cycle issue,
+// MI355X_MICROARCH.md) is covered by the other chain instead of the other wave.
+#ifndef UHSDR_FIR_RB_CH
+#define UHSDR_FIR_RB_CH 1
+#endif
+constexpr int FIR_RB_CH = UHSDR_FIR_RB_CH;
+
+template <int NQ, int CH>
+__device__ __forceinline__ void fir_tile_rb(const float* Wg, int lw, int base, int lane, const f32x4 (&bq)[NQ], f32x4 (&acc)[CH])
 {
     const int r = lane & 15, kq = lane >> 4;
     const int ai = base + 16 * r + 4 * kq;
-    const float* pa = Wg + ai;
+    const float* pa[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) pa[j] = Wg + j * lw + ai;
     int aoff[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) aoff[k] = fir_swz(ai + 16 * k) - ai;
-    acc = f32x4{ 0.0f, 0.0f, 0.0f, 0.0f };
+#pragma unroll
+    for (int j = 0; j < CH; ++j) acc[j] = f32x4{ 0.0f, 0.0f, 0.0f, 0.0f };
 #ifndef UHSDR_FIR_RB_AHEAD
 #define UHSDR_FIR_RB_AHEAD 2
 #endif
-    // A fragments load AH chunks ahead (AH - 1 loads in flight while a chunk's MFMAs run)
+    // A fragments load AH chunks ahead (CH (AH - 1) loads in flight while a chunk's MFMAs run)
     constexpr int AH = UHSDR_FIR_RB_AHEAD;
-    constexpr unsigned LGKMW = 0xC07F | ((AH - 1) << 8);   // s_waitcnt lgkmcnt(AH - 1) (vmcnt, expcnt: no wait)
-    f32x4 av[4];
+    constexpr unsigned LGKMW = 0xC07F | ((CH * (AH - 1)) << 8);   // s_waitcnt lgkmcnt(CH (AH - 1))
+    f32x4 av[4][CH];
 #pragma unroll
     for (int q = 0; q < AH; ++q)
     {
-        av[q] = *(const f32x4*)(pa + aoff[q]);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) av[q][j] = *(const f32x4*)(pa[j] + aoff[q]);
         __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
     {
-        // chunk q's A fragment has landed (the next AH - 1 chunks' may still be in flight)
+        // chunk q's A fragments have landed (the next AH - 1 chunks' may still be in flight)
         if (q + AH <= NQ) __builtin_amdgcn_s_waitcnt(LGKMW);
         else __builtin_amdgcn_s_waitcnt(0xC07F);
-        if (q + AH < NQ) av[(q + AH) & 3] = *(const f32x4*)(pa + aoff[(q + AH) & 7] + 128 * ((q + AH) >> 3));
+        if (q + AH < NQ)
+        {
+#pragma unroll
+            for (int j = 0; j < CH; ++j)
+                av[(q + AH) & 3][j] = *(const f32x4*)(pa[j] + aoff[(q + AH) & 7] + 128 * ((q + AH) >> 3));
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q & 3][s], bq[q][s], acc, 0, 0, 0);
+        for (int s = 0; s < 4; ++s)
+        {
+#pragma unroll
+            for (int j = 0; j < CH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q & 3][j][s], bq[q][s], acc[j], 0, 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-template <int NQ>
+template <int CH>
+__device__ __forceinline__ void fir_store_tile_rb(const FirArgs& a, int c0, int base, int lane, const f32x4 (&acc)[CH])
+{
+    const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+    {
+        const int c = c0 + j;
+        if (c >= a.C) continue;
+        float* d = a.dst + (size_t)c * a.B + base + 64 * kq + r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d[16 * i] = acc[j][i];
+    }
+}
+
+template <int NQ, int CH>
 __global__ void __launch_bounds__(64 * FIR_RB_WAVES) fir_mfma_rb(FirArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -413,8 +449,8 @@ __global__ void __launch_bounds__(64 * FIR_RB_WAVES) fir_mfma_rb(FirArgs a)
         const int x = i % a.cpl - i / a.cpl - 16;
         cp[i] = (x >= 0 && x < a.T) ? a.taps[x] : 0.0f;
     }
-    float* const Wb = sm + a.cp + (size_t)w * 2 * FIR_MCPW * a.lw;
-    for (int i = lane; i < 2 * FIR_MCPW * a.lw; i += 64) Wb[i] = 0.0f;
+    float* const Wb = sm + a.cp + (size_t)w * 2 * CH * a.lw;     // [buffer][channel][lw]
+    for (int i = lane; i < 2 * CH * a.lw; i += 64) Wb[i] = 0.0f;
     __syncthreads();
     // the wave's B fragments, chunk q at bp + 16 q (fir_tile's layout)
     f32x4 bq[NQ];
@@ -425,28 +461,36 @@ __global__ void __launch_bounds__(64 * FIR_RB_WAVES) fir_mfma_rb(FirArgs a)
         for (int q = 0; q < NQ; ++q) bq[q] = *(const f32x4*)(bp + 16 * q);
     }
     const bool v4 = a.v4 != 0;
-    const int ng = a.C;
+    const int ng = (a.C + CH - 1) / CH;
     const int nwt = gridDim.x * nw;
     auto fill = [&](int g, int buf) {
-        const int cl = g < a.C ? g : a.C - 1;
-        float* W = Wb + buf * a.lw;
-        if (v4) fir_fill_glds<16>(W, a.hist + (size_t)cl * H, a.src + (size_t)cl * a.B, H, n, lane);
-        else fir_fill_glds<4>(W, a.hist + (size_t)cl * H, a.src + (size_t)cl * a.B, H, n, lane);
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+        {
+            const int c = g * CH + j;
+            const int cl = c < a.C ? c : a.C - 1;
+            float* W = Wb + (buf * CH + j) * a.lw;
+            if (v4) fir_fill_glds<16>(W, a.hist + (size_t)cl * H, a.src + (size_t)cl * a.B, H, n, lane);
+            else fir_fill_glds<4>(W, a.hist + (size_t)cl * H, a.src + (size_t)cl * a.B, H, n, lane);
+        }
     };
     int g = blockIdx.x * nw + w, buf = 0;
     if (g < ng) fill(g, 0);
-    f32x4 last[FIR_MCPW];
+    f32x4 last[CH];
     int last_c0 = -1;
     for (; g < ng; g += nwt, buf ^= 1)
     {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (g + nwt < ng) fill(g + nwt, buf ^ 1);
-        if (last_c0 >= 0) fir_store_tile(a, last_c0, a.B - FIR_TILE, lane, last);
-        const float* Wg = Wb + buf * a.lw;
-        const int c0 = g;
+        if (last_c0 >= 0) fir_store_tile_rb<CH>(a, last_c0, a.B - FIR_TILE, lane, last);
+        const float* Wg = Wb + buf * CH * a.lw;
+        const int c0 = g * CH;
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
         {
-            const float* W = Wg + a.B;
-            float* hr = a.hist + (size_t)c0 * H;
+            if (c0 + j >= a.C) continue;
+            const float* W = Wg + j * a.lw + a.B;
+            float* hr = a.hist + (size_t)(c0 + j) * H;
             if (v4)
                 for (int i = 4 * lane; i < H; i += 256) *(f32x4*)(hr + i) = *(const f32x4*)(W + fir_swz(a.B + i) - a.B);
             else
@@ -454,15 +498,19 @@ __global__ void __launch_bounds__(64 * FIR_RB_WAVES) fir_mfma_rb(FirArgs a)
         }
         for (int t = 0; t < a.B / FIR_TILE; ++t)
         {
-            f32x4 acc[FIR_MCPW];
-            fir_tile_rb<NQ>(Wg, FIR_TILE * t, lane, bq, acc[0]);
-            if (t + 1 < a.B / FIR_TILE) fir_store_tile(a, c0, FIR_TILE * t, lane, acc);
-            else last[0] = acc[0];
+            f32x4 acc[CH];
+            fir_tile_rb<NQ, CH>(Wg, a.lw, FIR_TILE * t, lane, bq, acc);
+            if (t + 1 < a.B / FIR_TILE) fir_store_tile_rb<CH>(a, c0, FIR_TILE * t, lane, acc);
+            else
+            {
+#pragma unroll
+                for (int j = 0; j < CH; ++j) last[j] = acc[j];
+            }
         }
         last_c0 = c0;
         wave_sync();
     }
-    if (last_c0 >= 0) fir_store_tile(a, last_c0, a.B - FIR_TILE, lane, last);
+    if (last_c0 >= 0) fir_store_tile_rb<CH>(a, last_c0, a.B - FIR_TILE, lane, last);
 }
 
 } // namespace
@@ -483,7 +531,7 @@ struct uhsdr_fir_s
 // the workgroup's LDS: tap copies + per wave its windows (MFMA: two buffers of FIR_MCPW)
 static size_t fir_lds(const uhsdr_fir_s* h, int waves)
 {
-    const size_t per_wave = h->mode == UHSDR_FIR_MFMA ? 2 * FIR_MCPW : FIR_CPW;
+    const size_t per_wave = h->mode == UHSDR_FIR_MFMA ? 2 * (h->rb ? FIR_RB_CH : FIR_MCPW) : FIR_CPW;
     return sizeof(float) * ((size_t)h->cp + (size_t)waves * per_wave * h->lw);
 }
 
@@ -526,7 +574,7 @@ static uhsdr_status fir_configure(uhsdr_fir_s* h, int waves, bool strict)
     }
     // the attribute belongs to the kernel, not to this handle: raise it once to the whole CU's LDS,
     // so a later handle of another shape never lowers the cap an earlier handle launches with
-    const void* kfn = h->rb ? (const void*)fir_mfma_rb<FIR_RB_NQ> : (const void*)fir_mfma;
+    const void* kfn = h->rb ? (const void*)fir_mfma_rb<FIR_RB_NQ, FIR_RB_CH> : (const void*)fir_mfma;
     if (mf && fir_lds(h, waves) > 64 * 1024 &&
         hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_PER_CU) != hipSuccess)
     {
@@ -623,7 +671,7 @@ extern "C" uhsdr_status uhsdr_fir_process(uhsdr_fir_handle h, const float* src, 
     a.v4 = (h->T - 1) % 4 == 0 && ((uintptr_t)src & 15) == 0;
     const dim3 grid(h->grid), block(64 * h->waves);
     if (h->mode == UHSDR_FIR_MFMA && h->rb)
-        hipLaunchKernelGGL(fir_mfma_rb<FIR_RB_NQ>, grid, block, fir_lds(h, h->waves), h->stream, a);
+        hipLaunchKernelGGL((fir_mfma_rb<FIR_RB_NQ, FIR_RB_CH>), grid, block, fir_lds(h, h->waves), h->stream, a);
     else if (h->mode == UHSDR_FIR_MFMA)
         hipLaunchKernelGGL(fir_mfma, grid, block, fir_lds(h, h->waves), h->stream, a);
     else

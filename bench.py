@@ -133,6 +133,7 @@ def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
 
 
 SCHEDULES = {"auto": None, "pipe": 1, "fused": 2, "chain": 3, "stream": 4}   # uhsdr_rx_set_schedule
+DEVICE_HANDOFF = True    # --handoff: device (uhsdr_rx_set_pipelined(h, 2)) or event (1)
 SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain", 4: "stream"}
 
 
@@ -148,7 +149,9 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
         chain.set_front_block(front_block)
     sched = SCHEDULE_NAMES.get(chain.schedule, str(chain.schedule))
     if pipelined:
-        chain.set_pipelined(True)        # call k+1's rx_front overlaps call k's rx_back
+        # call k+1's rx_front overlaps call k's rx_back; 2: the device hand-off (rx_back polls
+        # rx_front's workgroup count instead of waiting on a cross-stream event)
+        chain.set_pipelined(2 if DEVICE_HANDOFF else True)
     plan = chain.plan
     # inputs resident in HBM before timing: a pool of consecutive blocks, cycled
     c0 = shard.channel_range(C, rank)[0]          # weak scaling: rank r owns channels [r*C, (r+1)*C)
@@ -270,6 +273,10 @@ def main():
                          "kernels fill the chip there)")
     ap.add_argument("--pipelined", action="store_true",
                     help="pipelined mode even on the north-star workload (default on for the others)")
+    ap.add_argument("--handoff", default="device", choices=["event", "device"],
+                    help="pipelined mode's front -> back hand-off: rx_back polling the call sequence "
+                         "number a one-lane kernel publishes after rx_front (uhsdr_rx_set_pipelined 2; "
+                         "the default, no cross-stream wait per call), or a cross-stream event per call")
     ap.add_argument("--precision", default="exact", choices=["exact", "fma"],
                     help="FIR MACs: exact (bit-identical to the reference) or fma (1e-5 normwise)")
     ap.add_argument("--pool", type=int, default=8, help="distinct input blocks cycled through")
@@ -285,6 +292,8 @@ def main():
                     help="process group of an N > 1 run: nccl (= RCCL over xGMI, one GPU per rank) or gloo "
                          "(test hook: ranks may share one GPU, the gather leg moves host copies)")
     args = ap.parse_args()
+    global DEVICE_HANDOFF
+    DEVICE_HANDOFF = args.handoff == "device"
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -386,7 +395,8 @@ def main():
                    "channels_per_gpu": C, "frames_per_call": N, "filter_path": int(plan.filter_path),
                    "parallelism": f"channel-sharded x{world}, no data-path collective",
                    "outputs": "f32 audio" + (" + int32 codec frames" if args.dst else ""),
-                   "pipelined": pipelined, "precision": args.precision, "schedule": sched,
+                   "pipelined": pipelined, "handoff": args.handoff if pipelined else None,
+                   "precision": args.precision, "schedule": sched,
                    **({"board": "mchf"} if args.board == "mchf" else {})},
         "roofline": roofline,
         "chain": {"device_ms_per_step": round(chain_dev_ms, 5),

@@ -279,7 +279,15 @@ uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h);
    stream after uhsdr_rx_join() (which orders the handle stream after every rx_back issued
    so far).  The caller must not overwrite an output buffer still being written: reuse across
    calls is safe (rx_back launches are ordered on the side stream).  Replaces nothing in the
-   reference (the firmware runs one ISR at a time); uhsdr_rx_process_host joins itself. */
+   reference (the firmware runs one ISR at a time); uhsdr_rx_process_host joins itself.
+   enable = 1: each rx_back waits for its rx_front through a cross-stream event.
+   enable = 2 (device hand-off): after a call's rx_front a one-lane kernel publishes the call's
+   sequence number, and rx_back -- the wave-pipeline back end without a demodulator or notch
+   (SSB / CW / DIGI), while its grid is at most half the CUs -- polls it on the device and reads
+   the hand-off with L2-bypassing loads; no cross-stream wait per call, so the side stream's back
+   ends run back to back.  Other calls keep the event.  The poll is bounded (seconds); a give-up
+   is counted in uhsdr_rx_stream_timeouts, so work the caller enqueues on the handle's stream
+   between calls must not hold the next rx_front back that long. */
 uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable);
 
 /* Arithmetic of the FIR dot products in rx_front (Hilbert pair, decimators, AM/FM I/Q filters).
@@ -324,8 +332,9 @@ enum { UHSDR_SCHEDULE_AUTO = 0, UHSDR_SCHEDULE_SPLIT_PIPE = 1, UHSDR_SCHEDULE_SP
        UHSDR_SCHEDULE_CHAIN = 3, UHSDR_SCHEDULE_STREAM = 4 };
 uhsdr_status uhsdr_rx_set_schedule(uhsdr_rx_handle h, int32_t schedule);
 int32_t      uhsdr_rx_get_schedule(uhsdr_rx_handle h);    /* -1 for a null handle */
-/* STREAM's bounded polls: 1 if one gave up (its launch then completed on whatever the hand-off
-   buffer held), 0 if none did since the last uhsdr_rx_reset, -1 on error.  Synchronises. */
+/* The bounded polls of STREAM and of the pipelined device hand-off (uhsdr_rx_set_pipelined 2):
+   1 if one gave up (its launch then completed on whatever the hand-off buffer held), 0 if none
+   did since the last uhsdr_rx_reset, -1 on error.  Synchronises. */
 int32_t      uhsdr_rx_stream_timeouts(uhsdr_rx_handle h);
 /* FIR outputs per lane of the front passes: 8 (default: more waves per batch) or 16 (fewer LDS
    window reads per MAC); UHSDR_UNSUPPORTED when the call size does not admit it.  Bit-identical. */

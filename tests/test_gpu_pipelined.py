@@ -15,12 +15,12 @@ from uhsdr_amd import synth
 pytestmark = pytest.mark.gpu
 
 
-def run_pipelined(cfg, iq, N, toggle_at=None, join_each=False, switch=None):
+def run_pipelined(cfg, iq, N, toggle_at=None, join_each=False, switch=None, mode=1, modes=None, timeouts=None):
     import torch
     C, n, _ = iq.shape
     calls = n // N
     chain = U.RxChain(cfg, channels=C, frames=N)
-    chain.set_pipelined(True)
+    chain.set_pipelined(mode)
     xs = [torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda() for k in range(calls)]
     audio = torch.empty((calls, C, N), dtype=torch.float32, device="cuda")
     dst = torch.empty((calls, C, N, 2), dtype=torch.int32, device="cuda")
@@ -32,10 +32,14 @@ def run_pipelined(cfg, iq, N, toggle_at=None, join_each=False, switch=None):
             chain.set_pipelined(True)
         if switch is not None and k in switch:
             chain.set_schedule(switch[k])     # change kernel schedule between calls, still pipelined
+        if modes is not None and k in modes:
+            chain.set_pipelined(modes[k])     # hand-off kind (0 serial, 1 event, 2 device) between calls
         chain.process(xs[k], audio[k], dst[k])
         if join_each:
             chain.join()
     chain.synchronize()
+    if timeouts is not None:
+        timeouts.append(chain.stream_timeouts())
     a = audio.permute(1, 0, 2).reshape(C, n).cpu().numpy()
     d = dst.permute(1, 0, 2, 3).reshape(C, n, 2).cpu().numpy()
     chain.close()
@@ -82,15 +86,20 @@ def test_pipelined_toggle_and_join(cuda):
     np.testing.assert_array_equal(dst, ref_dst)
 
 
+@pytest.mark.parametrize("mode", [1, 2], ids=["event", "device"])
 @pytest.mark.parametrize("first,second", [(1, 2), (2, 1)], ids=["pipe_then_fused", "fused_then_pipe"])
-def test_pipelined_schedule_switch_mid_group(cuda, first, second):
+def test_pipelined_schedule_switch_mid_group(cuda, first, second, mode):
     """Pipelined across 17 calls while the schedule switches to CHAIN inside group 1 and back
-    inside group 2: the hand-off buffers and their events must stay ordered."""
+    inside group 2: the hand-off buffers and their events must stay ordered; with the
+    device hand-off too (STREAM joins in for two calls)."""
     cfg = U.default_config()
     C, N = 96, 128
     iq = synth.ssb_iq(np.arange(C), 0, 17 * N)
     ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
-    a1, dst = run_pipelined(cfg, iq, N, switch={0: first, 5: 3, 9: second, 14: first})
+    sw = {0: first, 5: 3, 9: second, 14: first}
+    if mode == 2:
+        sw.update({11: 4, 13: second})
+    a1, dst = run_pipelined(cfg, iq, N, switch=sw, mode=mode)
     assert_bitexact(a1, ref_a1, f"pipelined, schedule {first} -> chain -> {second} -> {first}")
     np.testing.assert_array_equal(dst, ref_dst)
 
@@ -173,3 +182,68 @@ def test_pipelined_mchf_matches_oracle(cuda, name, kw, gen, C, N, calls):
     assert_bitexact(got[1], ref[1], f"pipelined mcHF {name} a_buffer[0]")
     np.testing.assert_array_equal(got[2], ref[2])
     assert np.abs(ref[0]).max() > 0
+
+
+# The device hand-off (uhsdr_rx_set_pipelined 2): rx_back polls the count of rx_front workgroups
+# (write-through adec stores, then one count per workgroup) instead of waiting on a cross-stream
+# event per call.  Used for the wave-pipeline back end without a demodulator or notch (SSB / CW /
+# DIGI) up to half the CUs' worth of back-end workgroups; every other case keeps the event, so the
+# AM and large-batch cases check that fallback.  No poll may give up (uhsdr_rx_stream_timeouts).
+HANDOFF_CASES = [
+    ("p48_usb", dict(filter_path=48, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 300, 256),
+    ("p35_lsb", dict(filter_path=35, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 130, 128),
+    ("p4_cw", dict(filter_path=4, dmod_mode=U.DEMOD_CW), synth.cw_iq, 65, 64),
+    ("p48_mchf", dict(filter_path=48, board=U.BOARD_MCHF, spkr_gain=24), synth.ssb_iq, 97, 256),
+    ("p48_agc_hang_eq", dict(agc_mode=1, agc_hang_enable=1, bass_gain=-8, treble_gain=6), synth.ssb_iq, 200, 128),
+    ("p70_am_event", dict(filter_path=70, dmod_mode=U.DEMOD_AM), synth.am_iq, 129, 256),
+]
+
+
+@pytest.mark.parametrize("name,kw,gen,C,N", HANDOFF_CASES, ids=[c[0] for c in HANDOFF_CASES])
+def test_device_handoff_matches_oracle(cuda, name, kw, gen, C, N):
+    cfg = U.default_config(**kw)
+    iq = gen(np.arange(C), 0, CALLS * N)
+    tmo = []
+    a1, dst = run_pipelined(cfg, iq, N, mode=2, timeouts=tmo)
+    ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    assert_bitexact(a1, ref_a1, f"device hand-off {name}")
+    np.testing.assert_array_equal(dst, ref_dst)
+    assert tmo == [0]
+
+
+def test_device_handoff_mode_switches(cuda):
+    """Event and device hand-offs and the serial mode alternating between calls, inside groups."""
+    cfg = U.default_config()
+    C, N = 96, 128
+    iq = synth.ssb_iq(np.arange(C), 0, 17 * N)
+    ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    tmo = []
+    a1, dst = run_pipelined(cfg, iq, N, mode=2, modes={3: 1, 5: 2, 9: 0, 10: 2, 14: 1, 15: 2}, timeouts=tmo)
+    assert_bitexact(a1, ref_a1, "device hand-off, modes switched")
+    np.testing.assert_array_equal(dst, ref_dst)
+    assert tmo == [0]
+
+
+@pytest.mark.parametrize("C", [4096, 20000], ids=["c2", "above_grid_limit"])
+def test_device_handoff_large_unsynchronised(cuda, C):
+    """The C2 shape (64 back-end workgroups: the device hand-off) and a batch past half the CUs'
+    worth of back-end workgroups (the event fallback), 12 calls back to back; sampled channels
+    against the oracle."""
+    import torch
+    cfg = U.default_config()
+    N, calls = 256, 12
+    chain = U.RxChain(cfg, channels=C, frames=N)
+    chain.set_pipelined(2)
+    xs = [synth.ssb_iq_torch(0, C, k * N, N, cuda) for k in range(calls)]
+    audio = torch.empty((calls, C, N), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    for k in range(calls):
+        chain.process(xs[k], audio[k], None)
+    chain.synchronize()
+    assert chain.stream_timeouts() == 0
+    chain.close()
+    pick = np.arange(0, C, 61)
+    iq = np.concatenate([x.cpu().numpy()[pick] for x in xs], axis=1)
+    ref, _ = oracle.OracleRx(U.build_plan(cfg), len(pick)).process(np.ascontiguousarray(iq), threads=8)
+    got = audio.permute(1, 0, 2).reshape(C, calls * N).cpu().numpy()[pick]
+    assert_bitexact(got, ref, f"device hand-off C={C}")

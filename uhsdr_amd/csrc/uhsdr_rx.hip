@@ -578,6 +578,14 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
         });
 }
 
+// pipelined device hand-off: launched on the handle's stream after a call's last rx_front, so it
+// runs once that front has completed (its stores written back at the kernel's end); publishes the
+// call's sequence number to the word rx_back polls
+__global__ void __launch_bounds__(64) rx_handoff_signal(unsigned* word, unsigned seq)
+{
+    if (threadIdx.x == 0) __hip_atomic_store(word, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------------------------------
 // rx_back: per-channel recursions.  State arrays are [field][C] (lane-coalesced).
 
@@ -647,6 +655,12 @@ struct BackArgs
     // when a poll gave up (a bounded spin).  null sflags: adec is complete at launch.
     const unsigned* sflags;
     unsigned sepoch;
+    // pipelined device hand-off (uhsdr_rx_set_pipelined 2): the launch reads adec once *dwait has
+    // reached dtarget (the call's sequence number, published by rx_handoff_signal after its
+    // rx_front; wrap-safe compare), by sc1 loads; null: adec is complete at launch (a stream event
+    // ordered it)
+    const unsigned* dwait;
+    unsigned dtarget;
     int swpg;
     unsigned* stmo;
 };
@@ -787,6 +801,9 @@ extern "C" int uhsdr_strace_read(void* out)
 
 // (~1 s per poll at the give-up bound; after one give-up the wave polls no more in this launch)
 constexpr unsigned STREAM_SPIN_MAX = 1u << 20;
+// the device hand-off's bound: ~2^24 polls of >= 128 cycles each, seconds -- past any rx_front
+// the caller's stream can hold up behind its own work between calls (a give-up is an error)
+constexpr unsigned DFLAG_SPIN_MAX = 1u << 24;
 // v: the word this lane loaded earlier (the poll issued one pipeline step ahead, so its latency
 // hides behind the step); it is re-read only while the call is not yet published
 __device__ __forceinline__ const unsigned* stream_word(const BackArgs& a, int grp)
@@ -812,6 +829,24 @@ __device__ __forceinline__ void stream_wait(const BackArgs& a, int grp, int call
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
     if (call < 14) STRACE(16 + call);
+}
+
+// pipelined device hand-off: the published sequence number reaches dtarget (bounded; a give-up is
+// recorded in stmo like rx_stream's)
+__device__ __forceinline__ void dflag_wait(const BackArgs& a, bool& gave_up)
+{
+    unsigned v = __hip_atomic_load(a.dwait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned spins = 0; (int)(v - a.dtarget) < 0 && !gave_up; ++spins)
+    {
+        if (spins >= DFLAG_SPIN_MAX)
+        {
+            if ((threadIdx.x & (BACK_CH - 1)) == 0) __hip_atomic_store(a.stmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gave_up = true;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        v = __hip_atomic_load(a.dwait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
 }
 
 // STREAM (rx_stream): the decimated samples of a call are read only once the front has published
@@ -863,6 +898,17 @@ struct InStage
             const int col = l.cl - (l.c - l.lane);
 #pragma unroll
             for (int m = 0; m < NDC; ++m) xnext[m] = lds[(call * NDC + m) * CHAIN_ADP + col];
+            return;
+        }
+        if (a.dwait)
+        {
+            // device hand-off: once per launch, wait until the call's rx_front has completed
+            // (rx_handoff_signal); then sc1 loads (this XCD's L2 may hold the buffer's previous
+            // contents: the launch may have started before the front finished)
+            if (call == 0) dflag_wait(a, gave_up);
+            const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
+#pragma unroll
+            for (int m = 0; m < NDC; ++m) xnext[m] = __hip_atomic_load(src + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
         // uniform row base (SGPRs) + the lane's 32-bit offset: no 64-bit per-lane address to keep
@@ -3104,6 +3150,17 @@ struct uhsdr_rx_s
     StreamArgs sgeo;         // geometry (flags and epoch are set per launch)
     size_t s_lds;            // dynamic LDS per workgroup (forces one workgroup per CU)
     int s_ok;                // the path has an instance, the geometry fits, the grid is co-resident
+    // pipelined device hand-off (uhsdr_rx_set_pipelined 2): rx_back polls the call sequence number
+    // rx_handoff_signal publishes after each rx_front (the word after stmo) instead of waiting on
+    // a cross-stream event
+    int dflag;
+    int dflag_grid;          // largest rx_back grid it is used for (half the CUs: the polling
+                             // workgroups never crowd out the front they wait for)
+    unsigned dtotal;         // calls published by rx_handoff_signal since reset
+    int main_back;           // back-end state was last written on the handle's stream (a one-kernel
+                             // schedule, a serial call, a reset): the next side-stream rx_back waits
+                             // on ev_front, which orders it after that work; the device hand-off
+                             // orders it after the front only
 };
 
 // kernel slots of the timing API: a call runs rx_front + rx_back (any back-end kernel) or rx_chain
@@ -3448,6 +3505,8 @@ extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
     if (h->sflags)
         HIPCHK(hipMemsetAsync(h->sflags, 0, sizeof(unsigned) * (((size_t)(h->C + BACK_CH - 1) / BACK_CH) * SWPG + 4), h->stream));
     h->stream_epoch = 0;
+    h->dtotal = 0;
+    h->main_back = 1;
     if (h->bs.cw)
     {
         // old_siglevel starts at 0.001 (function static, cw_decoder.c:189)
@@ -3755,6 +3814,8 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     ba.sepoch = 0;
     ba.swpg = 0;
     ba.stmo = nullptr;
+    ba.dwait = nullptr;
+    ba.dtarget = 0;
     {
         // key beep: frames [0, beep_n1) of this launch while calls are left (uhsdr_rx_key_beep)
         const int calls = h->N / BLK;
@@ -3824,6 +3885,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         HIPCHK(hipGetLastError());
         time_mark(h, K_STREAM, 1);
         h->front_launches += 1;
+        h->main_back = 1;
     }
     else if (h->schedule == UHSDR_SCHEDULE_CHAIN)
     {
@@ -3842,6 +3904,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
                            chain_lds(h), h->stream, fa, ba, (int)chain_front_floats(h));
         HIPCHK(hipGetLastError());
         time_mark(h, K_CHAIN, 1);
+        h->main_back = 1;
         h->front_launches += 1;
     }
     else
@@ -3859,30 +3922,47 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         const int cpw = FRONT_WAVE / (h->Nf / h->fv->R);
         const size_t lds = front_lds(h);
         const bool side = side_mode(h);
+        const bool fused = h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo;
+        // device hand-off: rx_back (the wave pipeline, adec its only input from the front) polls
+        // the sequence number rx_handoff_signal publishes after the front instead of waiting on
+        // ev_front: no barrier packet on the side stream, whose back ends then run back to back
+        const bool dfl = side && h->dflag && !h->main_back && !fused && !h->nv && h->bv->dm == DM_NONE &&
+                         !h->fv->st && (h->C + BACK_CH - 1) / BACK_CH <= h->dflag_grid;
         for (int f0 = 0; f0 < h->N; f0 += h->Nf)
         {
             const FrontArgs fa = front_args(h, iq, f0, adec, adec_q);
             const auto fn = fma ? h->fv->fn_fma : h->fv->fn;
             const dim3 grid((h->C + cpw - 1) / cpw), block(FRONT_WAVE);
             // pipelined: the call's last front launch records ev_front as it completes
-            if (side && f0 + h->Nf >= h->N)
+            if (side && !dfl && f0 + h->Nf >= h->N)
                 hipExtLaunchKernelGGL(fn, grid, block, lds, h->stream, nullptr, h->ev_front, 0, fa);
             else
                 hipLaunchKernelGGL(fn, grid, block, lds, h->stream, fa);
             HIPCHK(hipGetLastError());
             h->front_launches += 1;
         }
+        if (dfl)
+        {
+            h->dtotal += 1;
+            hipLaunchKernelGGL(rx_handoff_signal, dim3(1), dim3(64), 0, h->stream, h->stmo + 1, h->dtotal);
+            HIPCHK(hipGetLastError());
+        }
         time_mark(h, K_FRONT, 1);
 
         const BackArgs ba = back_args(h, adec, adec_q, audio, audio0, dst);
-        const bool fused = h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo;
         // mcHF after the wave pipeline (rx_back): biquad_2's output to the scratch row, then
         // rx_line_out_mchf; the other back ends run the board's stage inline (line_out4)
         const bool mc_pass = h->mchf_u && !fused && h->bv->dm != DM_FM;
         BackArgs bk = ba;
         if (mc_pass) bk.mchf_u = h->mchf_u;
+        if (dfl)
+        {
+            bk.dwait = h->stmo + 1;
+            bk.dtarget = h->dtotal;
+            bk.stmo = h->stmo;
+        }
         const hipStream_t bst = back_stream(h);
-        if (side) HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
+        if (side && !dfl) HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
         time_mark(h, K_BACK, 0);
         if (h->nv)
         {
@@ -3910,6 +3990,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         time_mark(h, K_BACK, 1);
         if (h->pipelined) h->pipe_calls += 1;
         if (side) h->side_dirty = 1;
+        h->main_back = !side;
     }
     h->calls_issued += 1;
     if (h->tsample) h->nev++;
@@ -4059,6 +4140,13 @@ extern "C" uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable
         h->pipe_calls = 0;
     }
     h->pipelined = enable != 0;
+    h->dflag = enable == 2;
+    if (h->dflag && !h->dflag_grid)
+    {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            h->dflag_grid = cus / 2;
+    }
     return UHSDR_OK;
 }
 

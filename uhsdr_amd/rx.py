@@ -156,9 +156,10 @@ class RxChain:
         32-frame calls (uhsdr_rx_key_beep)."""
         _abi.check(self.lib.uhsdr_rx_key_beep(self.handle, int(calls)), "uhsdr_rx_key_beep")
 
-    def set_pipelined(self, enable: bool = True) -> None:
+    def set_pipelined(self, enable=True) -> None:
         """Overlap call k+1's rx_front with call k's rx_back (uhsdr_rx_set_pipelined); outputs
-        are complete after synchronize() / a device-wide sync, or join() for the handle's stream."""
+        are complete after synchronize() / a device-wide sync, or join() for the handle's stream.
+        enable: False / 0 off, True / 1 (cross-stream event hand-off), 2 (device hand-off)."""
         _abi.check(self.lib.uhsdr_rx_set_pipelined(self.handle, int(enable)), "uhsdr_rx_set_pipelined")
 
     def set_precision(self, precision: int) -> None:

@@ -851,7 +851,9 @@ __device__ __forceinline__ void dflag_wait(const BackArgs& a, bool& gave_up)
 
 // STREAM (rx_stream): the decimated samples of a call are read only once the front has published
 // them (stream_wait), by write-through-coherent sc1 loads
-template <int L, bool LDS_IN = false, bool STREAM = false>
+// DW: the launch may take the pipelined device hand-off (BackArgs::dwait; rx_back's pre role
+// only -- the fused back ends keep the code out of their register budget)
+template <int L, bool LDS_IN = false, bool STREAM = false, bool DW = false>
 struct InStage
 {
     static constexpr int NDC = BLK / L;
@@ -900,7 +902,7 @@ struct InStage
             for (int m = 0; m < NDC; ++m) xnext[m] = lds[(call * NDC + m) * CHAIN_ADP + col];
             return;
         }
-        if (a.dwait)
+        if (DW && a.dwait)
         {
             // device hand-off: once per launch, wait until the call's rx_front has completed
             // (rx_handoff_signal); then sc1 loads (this XCD's L2 may hold the buffer's previous
@@ -1821,7 +1823,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
-    InStage<L, false, STREAM> in;
+    InStage<L, false, STREAM, !STREAM> in;
     LatticeStage<PRE> s;
     s.load(l, P->pre_k, P->pre_v, a.s.pre);
     if (!DM) in.fetch(a, l, 0);

@@ -2217,7 +2217,10 @@ __device__ __forceinline__ void back_fused_agc(const BackArgs& a, float* ys, int
 // no scratch, 3 waves per SIMD.
 // (the compiler's resource report: the 24 ksps bodies with a pre-filter lattice need 207-220
 // VGPRs at FORM 0 and spill to scratch at 3 waves, so they keep 2)
-__host__ __device__ constexpr int fused1_waves(int pre, int L) { return (L == 2 && pre > 0) ? 2 : 3; }
+#ifndef UHSDR_FUSED1_WAVES
+#define UHSDR_FUSED1_WAVES 3
+#endif
+__host__ __device__ constexpr int fused1_waves(int pre, int L) { return (L == 2 && pre > 0) ? 2 : UHSDR_FUSED1_WAVES; }
 template <int PRE, int AA, int L, int PH, int W, int DM, bool DC = true, int FORM = 0>
 __global__ void __launch_bounds__(BACK_CH)
 __attribute__((amdgpu_waves_per_eu(FORM == 1 ? fused1_waves(PRE, L) : DM == DM_SAM_SB ? 1 : UHSDR_FUSED_WAVES))) rx_back_fused(BackArgs a)
@@ -3973,7 +3976,11 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         }
         const back_fn bfn = fused ? fused_back_fn(h) : h->bv->fn;
         const dim3 bgrid((h->C + BACK_CH - 1) / BACK_CH), bblock(fused ? BACK_CH : back_roles(h->bv->dm) * BACK_CH);
-        const size_t blds = fused ? 0 : back_lds(h);
+#ifndef UHSDR_FUSED_LDS_PAD
+#define UHSDR_FUSED_LDS_PAD 0
+#endif
+        // (UHSDR_FUSED_LDS_PAD: unused dynamic LDS per fused workgroup, an occupancy cap for A/B)
+        const size_t blds = fused ? (size_t)UHSDR_FUSED_LDS_PAD : back_lds(h);
         // pipelined: the group's last rx_back (mcHF pass: the finishing kernel) records ev_back[grp]
         // as it completes
         if (side && group_end && !mc_pass)

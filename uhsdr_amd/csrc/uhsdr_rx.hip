@@ -3162,6 +3162,7 @@ struct uhsdr_rx_s
     int dflag_grid;          // largest rx_back grid it is used for (half the CUs: the polling
                              // workgroups never crowd out the front they wait for)
     unsigned dtotal;         // calls published by rx_handoff_signal since reset
+    int back_attr;           // rx_back's LDS attribute raised for the reserved launch (1), failed (-1)
     int main_back;           // back-end state was last written on the handle's stream (a one-kernel
                              // schedule, a serial call, a reset): the next side-stream rx_back waits
                              // on ev_front, which orders it after that work; the device hand-off
@@ -3979,8 +3980,25 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
 #ifndef UHSDR_FUSED_LDS_PAD
 #define UHSDR_FUSED_LDS_PAD 0
 #endif
+#ifndef UHSDR_BACK_RESERVE
+#define UHSDR_BACK_RESERVE 1
+#endif
         // (UHSDR_FUSED_LDS_PAD: unused dynamic LDS per fused workgroup, an occupancy cap for A/B)
-        const size_t blds = fused ? (size_t)UHSDR_FUSED_LDS_PAD : back_lds(h);
+        size_t blds = fused ? (size_t)UHSDR_FUSED_LDS_PAD : back_lds(h);
+        // device hand-off: rx_back takes nearly all of a CU's LDS, so no rx_front workgroup of the
+        // next calls shares its SIMDs (the role waves are latency-bound; a front wave beside them
+        // stretches every step).  At most half the CUs (dflag_grid); C2 0.0263 -> 0.0257 ms at
+        // 1000 steps, 20 steps unchanged (profiles/r05_c2_back_reserve_ab.txt)
+        if (UHSDR_BACK_RESERVE && dfl)
+        {
+            if (!h->back_attr)
+            {
+                h->back_attr = hipFuncSetAttribute((const void*)h->bv->fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)LDS_PER_CU) == hipSuccess ? 1 : -1;
+                (void)hipGetLastError();
+            }
+            if (h->back_attr > 0) blds = LDS_PER_CU - 4096;
+        }
         // pipelined: the group's last rx_back (mcHF pass: the finishing kernel) records ev_back[grp]
         // as it completes
         if (side && group_end && !mc_pass)

@@ -51,7 +51,7 @@ CASES = [
     ("p35_lsb", dict(filter_path=35, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 130, 128),
     ("p70_am", dict(filter_path=70, dmod_mode=U.DEMOD_AM), synth.am_iq, 200, 256),
     ("p70_sam", dict(filter_path=70, dmod_mode=U.DEMOD_SAM), synth.am_iq, 129, 256),
-    ("p1_fm", dict(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=12), synth.fm_iq, 100, 256),
+    ("p1_fm_event", dict(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=12), synth.fm_iq, 100, 256),
     ("p4_cw", dict(filter_path=4, dmod_mode=U.DEMOD_CW), synth.cw_iq, 65, 64),
 ]
 
@@ -188,7 +188,7 @@ def test_pipelined_mchf_matches_oracle(cuda, name, kw, gen, C, N, calls):
 # (write-through adec stores, then one count per workgroup) instead of waiting on a cross-stream
 # event per call.  Used for the wave-pipeline back end without a demodulator or notch (SSB / CW /
 # DIGI) up to half the CUs' worth of back-end workgroups; every other case keeps the event, so the
-# AM and large-batch cases check that fallback.  No poll may give up (uhsdr_rx_stream_timeouts).
+# AM, FM and large-batch cases check that fallback.  No poll may give up (uhsdr_rx_stream_timeouts).
 HANDOFF_CASES = [
     ("p48_usb", dict(filter_path=48, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 300, 256),
     ("p35_lsb", dict(filter_path=35, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 130, 128),
@@ -196,6 +196,9 @@ HANDOFF_CASES = [
     ("p48_mchf", dict(filter_path=48, board=U.BOARD_MCHF, spkr_gain=24), synth.ssb_iq, 97, 256),
     ("p48_agc_hang_eq", dict(agc_mode=1, agc_hang_enable=1, bass_gain=-8, treble_gain=6), synth.ssb_iq, 200, 128),
     ("p70_am_event", dict(filter_path=70, dmod_mode=U.DEMOD_AM), synth.am_iq, 129, 256),
+    ("p1_fm_event", dict(filter_path=1, dmod_mode=U.DEMOD_FM, fm_sql_threshold=12), synth.fm_iq, 100, 256),
+    ("p2_fm_tone_event", dict(filter_path=2, dmod_mode=U.DEMOD_FM, fm_sql_threshold=0, fm_tone_det=10),
+     synth.fm_iq, 70, 512),
 ]
 
 

@@ -3932,8 +3932,11 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         // device hand-off: rx_back (the wave pipeline, adec its only input from the front) polls
         // the sequence number rx_handoff_signal publishes after the front instead of waiting on
         // ev_front: no barrier packet on the side stream, whose back ends then run back to back
-        const bool dfl = side && h->dflag && !h->main_back && !fused && !h->nv && h->bv->dm == DM_NONE &&
-                         !h->fv->st && (h->C + BACK_CH - 1) / BACK_CH <= h->dflag_grid;
+        const int bgroups = (h->C + BACK_CH - 1) / BACK_CH;
+        // (rx_fm measured slower with it: C4 FM 0.131-0.133 vs 0.115-0.117 ms, its 512 polling
+        // workgroups beside the fronts; profiles/r05_fm_handoff_ab.txt)
+        const bool dfl = side && h->dflag && !h->main_back && !fused && !h->nv && !h->fv->st &&
+                         h->bv->dm == DM_NONE && bgroups <= h->dflag_grid;
         for (int f0 = 0; f0 < h->N; f0 += h->Nf)
         {
             const FrontArgs fa = front_args(h, iq, f0, adec, adec_q);

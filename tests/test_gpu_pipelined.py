@@ -250,3 +250,28 @@ def test_device_handoff_large_unsynchronised(cuda, C):
     ref, _ = oracle.OracleRx(U.build_plan(cfg), len(pick)).process(np.ascontiguousarray(iq), threads=8)
     got = audio.permute(1, 0, 2).reshape(C, calls * N).cpu().numpy()[pick]
     assert_bitexact(got, ref, f"device hand-off C={C}")
+
+
+def test_device_handoff_long_run(cuda):
+    """120 calls back to back at the C2 shape with the device hand-off (every hand-off buffer reused
+    40 times, 30 group transitions): sampled channels against the oracle, no poll giving up.  The
+    inputs cycle through 6 device-generated blocks, so consecutive calls see different data."""
+    import torch
+    cfg = U.default_config()
+    C, N, calls, pool = 4096, 256, 120, 6
+    chain = U.RxChain(cfg, channels=C, frames=N)
+    chain.set_pipelined(2)
+    xs = [synth.ssb_iq_torch(0, C, k * N, N, cuda) for k in range(pool)]
+    pick = np.arange(5, C, 97)
+    full = torch.empty((calls, C, N), dtype=torch.float32, device="cuda")   # 0.5 GB: no join needed
+    torch.cuda.synchronize()
+    for k in range(calls):
+        chain.process(xs[k % pool], full[k], None)     # no synchronisation: fronts run ahead
+    chain.synchronize()
+    audio = full[:, torch.from_numpy(pick).cuda(), :]
+    assert chain.stream_timeouts() == 0
+    chain.close()
+    iq = np.concatenate([xs[k % pool].cpu().numpy()[pick] for k in range(calls)], axis=1)
+    ref, _ = oracle.OracleRx(U.build_plan(cfg), len(pick)).process(np.ascontiguousarray(iq), threads=8)
+    got = audio.permute(1, 0, 2).reshape(len(pick), calls * N).cpu().numpy()
+    assert_bitexact(got, ref, "device hand-off, 120 calls")

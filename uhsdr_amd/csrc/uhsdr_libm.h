@@ -27,6 +27,9 @@
 #include <string.h>
 #include <math.h>
 
+#ifndef UHSDR_ATAN_SHORTDIV
+#define UHSDR_ATAN_SHORTDIV 1
+#endif
 #ifdef __HIPCC__
 #define UHSDR_LIBM_FN __host__ __device__ static inline
 #else
@@ -174,7 +177,18 @@ UHSDR_LIBM_FN float ul_atanf_pos(float a)
     const float den = kb * a + ka;
     const float hi = ul_sel(lo2, ul_sel(i0, atanhi[0], atanhi[1]), ul_sel(i2, atanhi[2], atanhi[3]));
     const float lo = ul_sel(lo2, ul_sel(i0, atanlo[0], atanlo[1]), ul_sel(i2, atanlo[2], atanlo[3]));
-    const float xr = ul_sel(small, a, num / den);
+#if defined(__HIP_DEVICE_COMPILE__) && UHSDR_ATAN_SHORTDIV
+    /* num / den by a reciprocal and one residual correction: equal to the IEEE quotient for every
+       binary32 a that reaches it, checked exhaustively on the device (tools/micro/atan_div_check.hip,
+       profiles/r05_atan_div_check.txt); 4 dependent operations instead of the scaled
+       division's ~10 on the PLL's critical path */
+    const float rr = __builtin_amdgcn_rcpf(den);
+    const float q0 = num * rr;
+    const float quo = fmaf(fmaf(-den, q0, num), rr, q0);
+#else
+    const float quo = num / den;
+#endif
+    const float xr = ul_sel(small, a, quo);
     const float z = xr * xr;
     const float w = z * z;
     const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));

@@ -68,8 +68,7 @@ def algorithmic_bytes(plan, C: int, N: int, write_dst: bool):
     chain = C * ((8 + out_b) * N + 2 * 4 * (fir_hist + back_state) + ring)
     s_live = 4 * (fir_hist + back_state + (AGC_Q * (BLK // M) if plan.agc.mode != 5 else 0))
     # rx_chain (one kernel per call, the hand-off in LDS) moves exactly the chain's bytes
-    # rx_stream (one launch: the hand-off crosses L2 between its front and back-end workgroups)
-    return {"rx_front": front, "rx_back": back, "rx_chain": chain, "rx_stream": chain, "chain": chain,
+    return {"rx_front": front, "rx_back": back, "rx_chain": chain, "chain": chain,
             "s_live_bytes": s_live}
 
 
@@ -132,15 +131,16 @@ def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
                       f"(affinity mask has {cpus} CPUs), channels split evenly; host CPU: {model}"}
 
 
-SCHEDULES = {"auto": None, "pipe": 1, "fused": 2, "chain": 3, "stream": 4}   # uhsdr_rx_set_schedule
+SCHEDULES = {"auto": None, "pipe": 1, "fused": 2, "chain": 3}   # uhsdr_rx_set_schedule
 DEVICE_HANDOFF = True    # --handoff: device (uhsdr_rx_set_pipelined(h, 2)) or event (1)
-SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain", 4: "stream"}
+SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain"}
 
 
 def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, pool, want_dst, pipelined=False,
               precision=0, schedule=None, front_block=0, reduce_dev=None, board=0):
     """W untimed + K timed steps of one RxChain on this rank; returns (max-rank seconds,
-    per-kernel (total ms, launches) from HIP events on the library's stream, plan, finite)."""
+    per-kernel (total ms, launches) from HIP events on the library's stream, plan, finite, schedule,
+    device hand-off give-ups after the timed loop (uhsdr_rx_handoff_timeouts; 0 required))."""
     cfg = U.default_config(board=board)
     stream = torch.cuda.current_stream(dev)
     chain = U.RxChain(cfg, channels=C, frames=N, stream=stream.cuda_stream, schedule=schedule)
@@ -149,8 +149,9 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
         chain.set_front_block(front_block)
     sched = SCHEDULE_NAMES.get(chain.schedule, str(chain.schedule))
     if pipelined:
-        # call k+1's rx_front overlaps call k's rx_back; 2: the device hand-off (rx_back polls
-        # rx_front's workgroup count instead of waiting on a cross-stream event)
+        # call k+1's rx_front overlaps call k's rx_back; 2: the device hand-off (rx_back polls the
+        # call sequence number rx_handoff_signal publishes after the front, then reads the hand-off
+        # with sc1 loads, instead of waiting on a cross-stream event)
         chain.set_pipelined(2 if DEVICE_HANDOFF else True)
     plan = chain.plan
     # inputs resident in HBM before timing: a pool of consecutive blocks, cycled
@@ -166,6 +167,9 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     elapsed = shard.timed_loop(lambda s: chain.process_ptr(ptrs[s % pool]),
                                lambda: torch.cuda.synchronize(dev), steps, warmup, dist, world,
                                dev if reduce_dev is None else reduce_dev)
+    # the device hand-off's failure contract (include/uhsdr.h): a poll that gave up poisons its call
+    # and sets the handle's failure word; the timed calls count only if none did
+    timeouts = chain.handoff_timeouts()
     # per-kernel breakdown in a separate pass: HIP events on the library's own stream bracket
     # every kernel of every call (the records cost host time, so they never share a clock with
     # the throughput loop above)
@@ -183,7 +187,7 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     ok = bool(torch.isfinite(audio).all().item())
     chain.close()
     del inputs
-    return elapsed, ktimes, plan, ok, sched
+    return elapsed, ktimes, plan, ok, sched, timeouts
 
 
 def gather_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, backend="nccl", pool=4, sink=None,
@@ -327,7 +331,7 @@ def main():
     C = args.channels or wl["channels"]
     N = args.frames or wl["frames"]
     pipelined = args.pipelined or (not args.serial and args.workload != "northstar")
-    elapsed, ktimes, plan, ok, sched = timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, args.steps,
+    elapsed, ktimes, plan, ok, sched, timeouts = timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, args.steps,
                                                  args.warmup, max(1, args.pool), args.dst, pipelined, prec,
                                                  SCHEDULES[args.schedule], args.front_block, reduce_dev,
                                                  U.BOARD_MCHF if args.board == "mchf" else U.BOARD_OVI40)
@@ -346,7 +350,7 @@ def main():
 
     def north_star_leg(precision):
         nw = WORKLOADS["northstar"]
-        n_el, n_kt, n_plan, n_ok, n_sched = timed_run(U, synth, shard, torch, dist, dev, 1, 0, nw["channels"],
+        n_el, n_kt, n_plan, n_ok, n_sched, n_tmo = timed_run(U, synth, shard, torch, dist, dev, 1, 0, nw["channels"],
                                                       nw["frames"], NS_STEPS, 10, 3, False, False, precision)
         n_ab = algorithmic_bytes(n_plan, nw["channels"], nw["frames"], False)
         n_roof, n_kms = roofline_of(n_ab, n_kt, pmc_traffic("northstar" if precision == U.PRECISION_EXACT
@@ -360,7 +364,7 @@ def main():
                 "chain_hbm_frac": round(n_ab["chain"] / n_el * NS_STEPS / 1e9 / HBM_PEAK_GBS, 4),
                 "chain_hbm_frac_kernel_events": round(n_ab["chain"] / (n_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "alg_bytes_per_sample": round(n_ab["chain"] / (nw["channels"] * nw["frames"]), 2),
-                "schedule": n_sched, "outputs_finite": n_ok}
+                "schedule": n_sched, "outputs_finite": n_ok, "handoff_timeouts": n_tmo}
 
     ns = None
     if world == 1 and not args.no_northstar and args.workload != "northstar" and not (args.channels or args.frames):
@@ -410,6 +414,7 @@ def main():
                           + ("; pipelined: rx_front of the next call overlaps rx_back in the timed loop; the "
                              "kernel event times come from a separate serial pass" if pipelined else "")},
         "outputs_finite": ok,
+        "handoff_timeouts": timeouts,
     }
     if ns:
         out["north_star"] = ns
@@ -421,6 +426,10 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if timeouts or (ns and (ns["handoff_timeouts"] or ns.get("fma", {}).get("handoff_timeouts"))):
+        print("bench.py: a device hand-off poll gave up during the timed loop (handoff_timeouts != 0): "
+              "the measurement is invalid", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

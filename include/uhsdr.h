@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define UHSDR_ABI_VERSION 4
+#define UHSDR_ABI_VERSION 5
 
 typedef enum
 {
@@ -46,7 +46,10 @@ typedef enum
     UHSDR_ARGUMENT_ERROR = -1,    /* ARM_MATH_ARGUMENT_ERROR */
     UHSDR_LENGTH_ERROR = -2,      /* ARM_MATH_LENGTH_ERROR: N % 32 != 0, bad sizes */
     UHSDR_UNSUPPORTED = -10,      /* mode / filter path not implemented on the device yet */
-    UHSDR_DEVICE_ERROR = -11      /* HIP runtime error */
+    UHSDR_DEVICE_ERROR = -11,     /* HIP runtime error */
+    UHSDR_TIMEOUT = -12           /* a bounded device-side poll gave up (the pipelined device hand-off,
+                                     uhsdr_rx_set_pipelined 2): outputs and handle state are invalid
+                                     until uhsdr_rx_reset */
 } uhsdr_status;
 
 /* sam_sideband_t, drivers/audio/audio_driver.h:181-190 (STEREO: USE_TWO_CHANNEL_AUDIO, OVI40) */
@@ -284,11 +287,26 @@ uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h);
    enable = 2 (device hand-off): after a call's rx_front a one-lane kernel publishes the call's
    sequence number, and rx_back -- the wave-pipeline back end without a demodulator or notch
    (SSB / CW / DIGI), while its grid is at most half the CUs -- polls it on the device and reads
-   the hand-off with L2-bypassing loads; no cross-stream wait per call, so the side stream's back
-   ends run back to back.  Other calls keep the event.  The poll is bounded (seconds); a give-up
-   is counted in uhsdr_rx_stream_timeouts, so work the caller enqueues on the handle's stream
-   between calls must not hold the next rx_front back that long. */
+   the hand-off with L1-bypassing sc1 loads; no cross-stream wait per call, so the side stream's
+   back ends run back to back.  Other calls keep the event.  Any other enable value returns
+   UHSDR_ARGUMENT_ERROR.
+   Failure contract of the device hand-off.  The poll is bounded (uhsdr_rx_set_handoff_bound,
+   default 2^24 polls: seconds).  If rx_back gives up -- the handle's stream held the call's
+   rx_front back that long behind other work, or a profiler serialised the two streams' dispatches
+   -- then (1) that launch is poisoned: every frame of the call's audio is NaN (its codec frames
+   carry what the reference's float -> int32 conversion makes of NaN, 0), so it cannot pass for
+   output; (2) the handle's host-mapped failure word is set, and from
+   then on uhsdr_rx_process, uhsdr_rx_join and uhsdr_rx_synchronize return UHSDR_TIMEOUT (join
+   reports it once the give-up has happened, synchronize always after the calls before it); (3)
+   uhsdr_rx_handoff_timeouts returns 1; (4) uhsdr_rx_reset clears the word and the poisoned state.
+   Under a profiler that serialises dispatches (rocprofv3 --pmc) use enable = 1. */
 uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable);
+/* Poll bound of the device hand-off (polls of >= 128 shader cycles each); for tests of the
+   failure contract.  0 is UHSDR_ARGUMENT_ERROR. */
+uhsdr_status uhsdr_rx_set_handoff_bound(uhsdr_rx_handle h, uint32_t polls);
+/* 1 if a device hand-off poll gave up since the last uhsdr_rx_reset, else 0; -1 on error.
+   Synchronises. */
+int32_t      uhsdr_rx_handoff_timeouts(uhsdr_rx_handle h);
 
 /* Arithmetic of the FIR dot products in rx_front (Hilbert pair, decimators, AM/FM I/Q filters).
    EXACT (default): a rounded multiply then a rounded add per tap, in tap order -- the binary32
@@ -317,25 +335,13 @@ uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h);
  *               their back end, the decimated hand-off kept in LDS (large batches).  SSB / CW /
  *               DIGI mono paths (no notch, no stereo, not AM / SAM / FM) with one front pass per
  *               call; elsewhere UHSDR_UNSUPPORTED.
- *   STREAM      rx_stream: one kernel per call for small batches.  Front and back end run side
- *               by side on disjoint CUs (one workgroup per CU): front waves filter the call's
- *               32-frame blocks in time order and publish each block's decimated output, and the
- *               rx_back wave pipeline of each 64-channel group starts on block 0 while the front
- *               still filters the rest.  No side stream, no event: outputs are complete in the
- *               handle's stream order, whatever uhsdr_rx_set_pipelined says.  Wide SSB / CW / DIGI
- *               mono paths (Hilbert-first, no notch), without the oscillator shift or automatic
- *               I/Q correction, with at most (CUs / 3) * 64 channels; elsewhere UHSDR_UNSUPPORTED.
  * Stereo, AM / SAM / FM and the LMS notch have their own back-end kernels and ignore SPLIT_*.
  * Returns UHSDR_UNSUPPORTED (handle unchanged) for a schedule the handle's path cannot run.
  * Takes effect from the next uhsdr_rx_process; get returns the resolved schedule. */
 enum { UHSDR_SCHEDULE_AUTO = 0, UHSDR_SCHEDULE_SPLIT_PIPE = 1, UHSDR_SCHEDULE_SPLIT_FUSED = 2,
-       UHSDR_SCHEDULE_CHAIN = 3, UHSDR_SCHEDULE_STREAM = 4 };
+       UHSDR_SCHEDULE_CHAIN = 3 };
 uhsdr_status uhsdr_rx_set_schedule(uhsdr_rx_handle h, int32_t schedule);
 int32_t      uhsdr_rx_get_schedule(uhsdr_rx_handle h);    /* -1 for a null handle */
-/* The bounded polls of STREAM and of the pipelined device hand-off (uhsdr_rx_set_pipelined 2):
-   1 if one gave up (its launch then completed on whatever the hand-off buffer held), 0 if none
-   did since the last uhsdr_rx_reset, -1 on error.  Synchronises. */
-int32_t      uhsdr_rx_stream_timeouts(uhsdr_rx_handle h);
 /* FIR outputs per lane of the front passes: 8 (default: more waves per batch) or 16 (fewer LDS
    window reads per MAC); UHSDR_UNSUPPORTED when the call size does not admit it.  Bit-identical. */
 uhsdr_status uhsdr_rx_set_front_block(uhsdr_rx_handle h, int32_t outputs_per_lane);

@@ -29,17 +29,15 @@ def cuda():
     return torch.device("cuda:0")
 
 
-SCHEDULES = {"pipe": 1, "fused": 2, "chain": 3, "stream": 4}   # uhsdr_rx_set_schedule values
+SCHEDULES = {"pipe": 1, "fused": 2, "chain": 3}   # uhsdr_rx_set_schedule values
 
 
-@pytest.fixture(params=["pipe", "fused", "chain", "stream"])
+@pytest.fixture(params=["pipe", "fused", "chain"])
 def back(request, monkeypatch):
     """Every kernel schedule of a call: the back-end wave pipeline (rx_back, small batches), the
     fused one-wave-per-64-channels back end (rx_back_fused), and the one-kernel rx_chain (front
     passes + fused back end per wave, large batches), forced on every RxChain the test makes.
-    rx_chain covers the SSB / CW / DIGI mono paths, rx_stream (one launch, front and back end on disjoint
-    CUs) their wide Hilbert-first ones up to (CUs / 3) * 64 channels; elsewhere the handles keep the
-    AUTO choice."""
+    rx_chain covers the SSB / CW / DIGI mono paths; elsewhere the handles keep the AUTO choice."""
     from uhsdr_amd import rx
     monkeypatch.setattr(rx, "DEFAULT_SCHEDULE", SCHEDULES[request.param])
     return request.param

@@ -39,7 +39,7 @@ def run_pipelined(cfg, iq, N, toggle_at=None, join_each=False, switch=None, mode
             chain.join()
     chain.synchronize()
     if timeouts is not None:
-        timeouts.append(chain.stream_timeouts())
+        timeouts.append(chain.handoff_timeouts())
     a = audio.permute(1, 0, 2).reshape(C, n).cpu().numpy()
     d = dst.permute(1, 0, 2, 3).reshape(C, n, 2).cpu().numpy()
     chain.close()
@@ -91,14 +91,14 @@ def test_pipelined_toggle_and_join(cuda):
 def test_pipelined_schedule_switch_mid_group(cuda, first, second, mode):
     """Pipelined across 17 calls while the schedule switches to CHAIN inside group 1 and back
     inside group 2: the hand-off buffers and their events must stay ordered; with the
-    device hand-off too (STREAM joins in for two calls)."""
+    device hand-off too (CHAIN again for two calls inside group 2)."""
     cfg = U.default_config()
     C, N = 96, 128
     iq = synth.ssb_iq(np.arange(C), 0, 17 * N)
     ref_a1, ref_dst = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
     sw = {0: first, 5: 3, 9: second, 14: first}
     if mode == 2:
-        sw.update({11: 4, 13: second})
+        sw.update({11: 3, 13: second})
     a1, dst = run_pipelined(cfg, iq, N, switch=sw, mode=mode)
     assert_bitexact(a1, ref_a1, f"pipelined, schedule {first} -> chain -> {second} -> {first}")
     np.testing.assert_array_equal(dst, ref_dst)
@@ -184,11 +184,12 @@ def test_pipelined_mchf_matches_oracle(cuda, name, kw, gen, C, N, calls):
     assert np.abs(ref[0]).max() > 0
 
 
-# The device hand-off (uhsdr_rx_set_pipelined 2): rx_back polls the count of rx_front workgroups
-# (write-through adec stores, then one count per workgroup) instead of waiting on a cross-stream
-# event per call.  Used for the wave-pipeline back end without a demodulator or notch (SSB / CW /
-# DIGI) up to half the CUs' worth of back-end workgroups; every other case keeps the event, so the
-# AM, FM and large-batch cases check that fallback.  No poll may give up (uhsdr_rx_stream_timeouts).
+# The device hand-off (uhsdr_rx_set_pipelined 2): after each call's rx_front a one-lane kernel
+# (rx_handoff_signal) publishes the call's sequence number, and rx_back polls it on the device and
+# then reads adec with sc1 loads, instead of waiting on a cross-stream event per call.  Used for the
+# wave-pipeline back end without a demodulator or notch (SSB / CW / DIGI) up to half the CUs' worth
+# of back-end workgroups; every other case keeps the event, so the AM, FM and large-batch cases check
+# that fallback.  No poll may give up (uhsdr_rx_handoff_timeouts).
 HANDOFF_CASES = [
     ("p48_usb", dict(filter_path=48, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 300, 256),
     ("p35_lsb", dict(filter_path=35, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 130, 128),
@@ -243,7 +244,7 @@ def test_device_handoff_large_unsynchronised(cuda, C):
     for k in range(calls):
         chain.process(xs[k], audio[k], None)
     chain.synchronize()
-    assert chain.stream_timeouts() == 0
+    assert chain.handoff_timeouts() == 0
     chain.close()
     pick = np.arange(0, C, 61)
     iq = np.concatenate([x.cpu().numpy()[pick] for x in xs], axis=1)
@@ -269,9 +270,84 @@ def test_device_handoff_long_run(cuda):
         chain.process(xs[k % pool], full[k], None)     # no synchronisation: fronts run ahead
     chain.synchronize()
     audio = full[:, torch.from_numpy(pick).cuda(), :]
-    assert chain.stream_timeouts() == 0
+    assert chain.handoff_timeouts() == 0
     chain.close()
     iq = np.concatenate([xs[k % pool].cpu().numpy()[pick] for k in range(calls)], axis=1)
     ref, _ = oracle.OracleRx(U.build_plan(cfg), len(pick)).process(np.ascontiguousarray(iq), threads=8)
     got = audio.permute(1, 0, 2).reshape(len(pick), calls * N).cpu().numpy()
     assert_bitexact(got, ref, "device hand-off, 120 calls")
+
+
+def test_device_handoff_front_delayed(cuda):
+    """every call's rx_front is held back on the handle's stream (a spin kernel of
+    ~100 us ahead of it, torch.cuda._sleep), so each rx_back -- already running on the side stream
+    -- really polls the sequence word while its front runs, and then reads adec written from another
+    XCD through sc1 loads.  Bit-exact against the oracle, no poll giving up."""
+    import torch
+    cfg = U.default_config()
+    C, N, calls = 4096, 256, 10
+    chain = U.RxChain(cfg, channels=C, frames=N, stream=torch.cuda.current_stream().cuda_stream)
+    chain.set_pipelined(2)
+    xs = [synth.ssb_iq_torch(0, C, k * N, N, cuda) for k in range(calls)]
+    audio = torch.empty((calls, C, N), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    for k in range(calls):
+        torch.cuda._sleep(200_000)                   # on the handle's stream, ahead of rx_front
+        chain.process(xs[k], audio[k], None)
+    chain.synchronize()
+    assert chain.handoff_timeouts() == 0
+    chain.close()
+    pick = np.arange(3, C, 67)
+    iq = np.concatenate([x.cpu().numpy()[pick] for x in xs], axis=1)
+    ref, _ = oracle.OracleRx(U.build_plan(cfg), len(pick)).process(np.ascontiguousarray(iq), threads=8)
+    got = audio.permute(1, 0, 2).reshape(C, calls * N).cpu().numpy()[pick]
+    assert_bitexact(got, ref, "device hand-off, fronts delayed")
+
+
+def test_device_handoff_give_up_fails_loudly(cuda):
+    """the failure contract of the device hand-off.  The poll bound is cut to 64
+    polls and call 3's rx_front is held back ~25 ms on the handle's stream, so its rx_back gives up.
+    Then: the call's audio is NaN (poisoned), synchronize() and every later process() raise
+    UHSDR_TIMEOUT, handoff_timeouts() == 1; after reset() the handle runs bit-exact again."""
+    import torch
+    cfg = U.default_config()
+    C, N = 256, 256
+    iq = synth.ssb_iq(np.arange(C), 0, 6 * N)
+    xs = [torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda() for k in range(6)]
+    chain = U.RxChain(cfg, channels=C, frames=N, stream=torch.cuda.current_stream().cuda_stream)
+    chain.set_pipelined(2)
+    audio = torch.zeros((6, C, N), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    for k in range(3):
+        chain.process(xs[k], audio[k], None)
+    chain.synchronize()
+    assert chain.handoff_timeouts() == 0
+    chain.set_handoff_bound(64)
+    torch.cuda._sleep(50_000_000)                    # ~25 ms ahead of call 3's rx_front
+    chain.process(xs[3], audio[3], None)
+    with pytest.raises(U.UhsdrError) as e:
+        chain.synchronize()
+    assert e.value.status == U.UHSDR_TIMEOUT
+    assert chain.handoff_timeouts() == 1
+    with pytest.raises(U.UhsdrError) as e:
+        chain.process(xs[4], audio[4], None)
+    assert e.value.status == U.UHSDR_TIMEOUT
+    with pytest.raises(U.UhsdrError) as e:
+        chain.join()
+    assert e.value.status == U.UHSDR_TIMEOUT
+    got = audio.cpu().numpy()
+    assert np.isnan(got[3]).all(), "the give-up's output must be poisoned"
+    ref, _ = oracle.OracleRx(U.build_plan(cfg), C).process(np.ascontiguousarray(iq[:, :3 * N]), threads=8)
+    assert_bitexact(got[:3].transpose(1, 0, 2).reshape(C, 3 * N), ref, "calls before the give-up")
+    # reset clears the failure word and the poisoned state; the default bound again
+    chain.reset()
+    chain.set_handoff_bound(1 << 24)
+    assert chain.handoff_timeouts() == 0
+    for k in range(3):
+        chain.process(xs[k], audio[k], None)
+    chain.synchronize()
+    assert chain.handoff_timeouts() == 0
+    assert_bitexact(audio[:3].cpu().numpy().transpose(1, 0, 2).reshape(C, 3 * N), ref, "after reset")
+    with pytest.raises(U.UhsdrError):
+        chain.set_pipelined(3)                       # ADVICE r05: modes are 0, 1, 2
+    chain.close()

@@ -84,8 +84,11 @@ def rx_line(name, cfg, C, N, iq, steps, warmup, cw=False, pipelined=False):
            "msamples_per_s": round(C * N / ms / 1e3, 1),
            "kernel_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kt.items()},
            "alg_bytes_per_frame": round(per, 2), "hbm_frac": round(C * N * per / ms / 1e6 / HBM_PEAK_GBS, 4),
-           "finite": bool(torch.isfinite(audio).all().item())}
+           "finite": bool(torch.isfinite(audio).all().item()),
+           "handoff_timeouts": chain.handoff_timeouts()}      # 0 required (include/uhsdr.h failure contract)
     chain.close()
+    if out["handoff_timeouts"]:
+        raise RuntimeError(f"{name}: a device hand-off poll gave up: the line is invalid")
     return out
 
 

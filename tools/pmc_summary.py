@@ -48,4 +48,18 @@ for k, cs in vals.items():
         # MFMA busy cycles summed over the chip's 1024 SIMDs; GRBM_GUI_ACTIVE summed over its 8 XCDs
         d["mfma_busy_frac"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / max(m["GRBM_GUI_ACTIVE"] / 8 * 1024, 1), 3)
     out[k] = d
+# the bench line of every pass (p<i>.log): which mode the counters come from, and that no pass ran
+# a stalled or failed chain (the device hand-off's give-up is an error since round 6, but an event-mode
+# run is the one that cannot stall under the profiler's serialised dispatch)
+runs = []
+for f in sorted(glob.glob(os.path.join(base, "p*.log"))):
+    for line in open(f):
+        if line.startswith("{") and '"metric"' in line:
+            b = json.loads(line)
+            cfg = b.get("config", {})
+            runs.append({"pass": os.path.basename(f)[:-4], "ms_per_step": b.get("ms_per_step"),
+                         "pipelined": cfg.get("pipelined"), "handoff": cfg.get("handoff"),
+                         "schedule": cfg.get("schedule"), "handoff_timeouts": b.get("handoff_timeouts")})
+if runs:
+    out["_runs"] = runs
 print(json.dumps(out, indent=1))

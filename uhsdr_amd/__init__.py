@@ -7,9 +7,9 @@ from ._abi import (RxConfig, RxPlan, build_plan, plan_supported, plan_fma_ok, co
                    DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI,
                    DEMOD_SSBSTEREO, DEMOD_IQ, SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB,
                    SAM_SIDEBAND_STEREO, DSP_NOTCH_ENABLE, BOARD_OVI40, BOARD_MCHF,
-                   UHSDR_OK, UHSDR_ARGUMENT_ERROR, UHSDR_UNSUPPORTED,
+                   UHSDR_OK, UHSDR_ARGUMENT_ERROR, UHSDR_UNSUPPORTED, UHSDR_TIMEOUT, UhsdrError,
                    PRECISION_EXACT, PRECISION_FMA,
-                   SCHEDULE_AUTO, SCHEDULE_SPLIT_PIPE, SCHEDULE_SPLIT_FUSED, SCHEDULE_CHAIN, SCHEDULE_STREAM, ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP,
+                   SCHEDULE_AUTO, SCHEDULE_SPLIT_PIPE, SCHEDULE_SPLIT_FUSED, SCHEDULE_CHAIN, ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP,
                    TWINPEAKS_SAMPLING, TWINPEAKS_DONE, TWINPEAKS_WAIT, TWINPEAKS_UNCORRECTABLE,
                    TWINPEAKS_CODEC_RESTART,
                    TUNE_OFF, TUNE_SINGLE, TUNE_TWO,

@@ -18,19 +18,20 @@ MAX_INTERP = 16
 IQ_BLOCK_SIZE = 32
 FILTER_PATH_NUM = 87
 
-ABI_VERSION = 4   # include/uhsdr.h UHSDR_ABI_VERSION: checked against the library at load()
+ABI_VERSION = 5   # include/uhsdr.h UHSDR_ABI_VERSION: checked against the library at load()
 UHSDR_OK = 0
 UHSDR_ARGUMENT_ERROR = -1
 UHSDR_LENGTH_ERROR = -2
 UHSDR_UNSUPPORTED = -10
 UHSDR_DEVICE_ERROR = -11
+UHSDR_TIMEOUT = -12          # a bounded device-side hand-off poll gave up (uhsdr_rx_set_pipelined 2)
 
 DEMOD_USB, DEMOD_LSB, DEMOD_CW, DEMOD_AM, DEMOD_SAM, DEMOD_FM, DEMOD_DIGI, DEMOD_SSBSTEREO, DEMOD_IQ = range(9)
 SAM_SIDEBAND_BOTH, SAM_SIDEBAND_LSB, SAM_SIDEBAND_USB, SAM_SIDEBAND_STEREO = range(4)
 BOARD_OVI40, BOARD_MCHF = 0, 1                 # uhsdr_rx_config.board: the UI board's output stage
 DSP_NOTCH_ENABLE, DSP_MNOTCH_ENABLE, DSP_MPEAK_ENABLE = 0x04, 0x10, 0x20
 PRECISION_EXACT, PRECISION_FMA = 0, 1          # uhsdr_rx_set_precision
-SCHEDULE_AUTO, SCHEDULE_SPLIT_PIPE, SCHEDULE_SPLIT_FUSED, SCHEDULE_CHAIN, SCHEDULE_STREAM = range(5)   # uhsdr_rx_set_schedule
+SCHEDULE_AUTO, SCHEDULE_SPLIT_PIPE, SCHEDULE_SPLIT_FUSED, SCHEDULE_CHAIN = range(4)   # uhsdr_rx_set_schedule
 ADC_CLIP, ADC_HALF_CLIP, ADC_QUARTER_CLIP = 1, 2, 4   # uhsdr_rx_set_clip_output bits
 TWINPEAKS_SAMPLING, TWINPEAKS_DONE, TWINPEAKS_WAIT, TWINPEAKS_UNCORRECTABLE, TWINPEAKS_CODEC_RESTART = range(5)
 
@@ -191,7 +192,8 @@ SIGNATURES = {
     "uhsdr_rx_get_precision": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_set_schedule": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_rx_get_schedule": (C.c_int32, [C.c_void_p]),
-    "uhsdr_rx_stream_timeouts": (C.c_int32, [C.c_void_p]),
+    "uhsdr_rx_handoff_timeouts": (C.c_int32, [C.c_void_p]),
+    "uhsdr_rx_set_handoff_bound": (C.c_int, [C.c_void_p, C.c_uint32]),
     "uhsdr_rx_set_front_block": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_rx_set_cw_outputs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "uhsdr_rx_cw_blocks_max": (C.c_int32, [C.c_void_p]),
@@ -294,10 +296,19 @@ def load(path: str | None = None) -> C.CDLL:
     return lib
 
 
+class UhsdrError(RuntimeError):
+    """A uhsdr_status other than UHSDR_OK; .status holds it (UHSDR_TIMEOUT: the device hand-off's
+    failure contract, include/uhsdr.h uhsdr_rx_set_pipelined)."""
+
+    def __init__(self, msg: str, status: int):
+        super().__init__(msg)
+        self.status = status
+
+
 def check(status: int, what: str = "") -> None:
     if status != UHSDR_OK:
         err = load().uhsdr_last_error().decode()
-        raise RuntimeError(f"{what} failed with status {status}: {err}")
+        raise UhsdrError(f"{what} failed with status {status}: {err}", status)
 
 
 def default_config(**overrides) -> RxConfig:

@@ -646,23 +646,16 @@ struct BackArgs
     int mchf;            // the mcHF board's output stage in line_out4 (plan.single_channel)
     float* mchf_u;       // mcHF, wave-pipeline back ends: [C][N] scratch for biquad_2's output, which
                          // rx_line_out_mchf finishes (null: line_out4 runs the whole stage)
-    // channel group of workgroup b is b - grp0 (rx_stream: the back-end workgroups follow the
-    // front's in the grid); 0 for the back-end kernels of their own
-    int grp0;
-    // rx_stream: adec arrives while the kernel runs.  Front wave w of group g stores
-    // sflags[g * swpg + w] = sepoch * 256 + s + 1 once its decimated output of 32-frame call s is
-    // in adec (write-through stores); the back end polls them before it reads a call.  stmo: set
-    // when a poll gave up (a bounded spin).  null sflags: adec is complete at launch.
-    const unsigned* sflags;
-    unsigned sepoch;
     // pipelined device hand-off (uhsdr_rx_set_pipelined 2): the launch reads adec once *dwait has
     // reached dtarget (the call's sequence number, published by rx_handoff_signal after its
     // rx_front; wrap-safe compare), by sc1 loads; null: adec is complete at launch (a stream event
-    // ordered it)
+    // ordered it).  The poll is bounded by spin_max polls; a give-up stores 1 to *fail (the handle's
+    // host-mapped failure word: the host reports UHSDR_TIMEOUT from it) and poisons the launch
+    // (NaN inputs for every call, so its audio is NaN and its codec frames INT32_MIN)
     const unsigned* dwait;
     unsigned dtarget;
-    int swpg;
-    unsigned* stmo;
+    unsigned spin_max;
+    unsigned* fail;
 };
 
 // softdds_addSingleToneToTwobuffers (softdds.c:142-152): the tone of launch frame n
@@ -732,10 +725,11 @@ struct BackLds
     float* mid;   // [2][BLK][64]  audio -> aa
     float* aa;    // [2][BLK][64]  aa -> output
     float* prep;  // [3][2][NDC][64]  pre -> agc: window maximum, fast / hang averages
+    unsigned* poison;  // [1]  pre -> output: the launch's device hand-off gave up (DM_NONE only)
 };
 
 // floats of the hand-off buffers (host: back_lds)
-__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (6 * ndc + 2 * BLK); }
+__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (6 * ndc + 2 * BLK) + 4; }
 
 template <int NDC>
 __device__ __forceinline__ BackLds back_lds_carve(float* smem)
@@ -747,6 +741,7 @@ __device__ __forceinline__ BackLds back_lds_carve(float* smem)
     l.pre = l.agc + 2 * NDC * BACK_CH;
     l.dem = l.pre + 2 * NDC * BACK_CH;
     l.prep = l.dem + 2 * NDC * BACK_CH;
+    l.poison = (unsigned*)(l.prep + 3 * 2 * NDC * BACK_CH);
     return l;
 }
 
@@ -755,7 +750,7 @@ struct BackLane
 {
     int lane, c, cl, C, calls;
     bool live;
-    __device__ __forceinline__ explicit BackLane(const BackArgs& a) : BackLane(a, (int)blockIdx.x - a.grp0) {}
+    __device__ __forceinline__ explicit BackLane(const BackArgs& a) : BackLane(a, (int)blockIdx.x) {}
     // channel group grp (channels 64 grp ..): rx_chain's waves name their group themselves
     __device__ __forceinline__ BackLane(const BackArgs& a, int grp)
     {
@@ -778,69 +773,22 @@ struct BackLane
 // [sample][lane] with row pitch CHAIN_ADP, instead of adec in HBM
 constexpr int CHAIN_ADP = BACK_CH + 4;
 
-// rx_stream's hand-off of one 32-frame call: every front wave of the lane's group has published
-// it (a relaxed agent-scope poll of swpg words, one per lane, with s_sleep between polls; bounded:
-// a poll that gives up sets stmo and the kernel completes with what adec holds).  The words and the
-// payload are stored write-through by the front (sc1) and read here with sc1 loads, so no acquire
-// fence is needed (MI355X_MICROARCH.md § inter-workgroup visibility, valid forms).
-#ifdef UHSDR_STREAM_TRACE
-// timing build (tools/trace_stream.py): s_memrealtime (100 MHz, chip-wide) per workgroup, wave and
-// event of the last rx_stream launch: front waves 0 start, 1 + s after publishing call s, 30 end;
-// back-end roles the start of every pipeline step it, 30 end; the pre role 16 + c when the poll
-// of call c returned
-__device__ unsigned long long g_strace[256][8][32];
-#define STRACE(ev) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) \
-    g_strace[blockIdx.x][threadIdx.x >> 6][(ev)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-extern "C" int uhsdr_strace_read(void* out)
-{
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_strace), sizeof(g_strace)) == hipSuccess ? 0 : -1;
-}
-#else
-#define STRACE(ev) do { } while (0)
-#endif
-
-// (~1 s per poll at the give-up bound; after one give-up the wave polls no more in this launch)
-constexpr unsigned STREAM_SPIN_MAX = 1u << 20;
-// the device hand-off's bound: ~2^24 polls of >= 128 cycles each, seconds -- past any rx_front
-// the caller's stream can hold up behind its own work between calls (a give-up is an error)
+// default bound of the device hand-off's poll (uhsdr_rx_set_handoff_bound): 2^24 polls
 constexpr unsigned DFLAG_SPIN_MAX = 1u << 24;
-// v: the word this lane loaded earlier (the poll issued one pipeline step ahead, so its latency
-// hides behind the step); it is re-read only while the call is not yet published
-__device__ __forceinline__ const unsigned* stream_word(const BackArgs& a, int grp)
-{
-    const int lane = threadIdx.x & (BACK_CH - 1);
-    return a.sflags + (size_t)grp * a.swpg + (lane < a.swpg ? lane : 0);
-}
-__device__ __forceinline__ void stream_wait(const BackArgs& a, int grp, int call, unsigned v, bool& gave_up)
-{
-    const unsigned want = a.sepoch * 256u + (unsigned)call + 1u;
-    const int lane = threadIdx.x & (BACK_CH - 1);
-    const unsigned* f = stream_word(a, grp);
-    for (unsigned spins = 0; !gave_up; ++spins)
-    {
-        if (__all((int)(v - want) >= 0)) break;
-        if (spins >= STREAM_SPIN_MAX)
-        {
-            if (lane == 0) __hip_atomic_store(a.stmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            gave_up = true;
-        }
-        __builtin_amdgcn_s_sleep(2);
-        v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
-    if (call < 14) STRACE(16 + call);
-}
-
-// pipelined device hand-off: the published sequence number reaches dtarget (bounded; a give-up is
-// recorded in stmo like rx_stream's)
+// pipelined device hand-off: the published sequence number reaches dtarget.  Bounded: after
+// a.spin_max polls (>= 128 cycles each; the default 2^24 is seconds, past any rx_front the caller's
+// stream can hold back behind its own work between calls) the wave gives up, stores 1 to the
+// handle's host-mapped failure word (system scope: the host reads it without a synchronisation)
+// and its launch is poisoned (NaN inputs in InStage::fetch, NaN audio from the output role for every
+// frame), so the give-up can never pass for output
 __device__ __forceinline__ void dflag_wait(const BackArgs& a, bool& gave_up)
 {
     unsigned v = __hip_atomic_load(a.dwait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (unsigned spins = 0; (int)(v - a.dtarget) < 0 && !gave_up; ++spins)
     {
-        if (spins >= DFLAG_SPIN_MAX)
+        if (spins >= a.spin_max)
         {
-            if ((threadIdx.x & (BACK_CH - 1)) == 0) __hip_atomic_store(a.stmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((threadIdx.x & (BACK_CH - 1)) == 0) __hip_atomic_store(a.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             gave_up = true;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -849,50 +797,18 @@ __device__ __forceinline__ void dflag_wait(const BackArgs& a, bool& gave_up)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
 }
 
-// STREAM (rx_stream): the decimated samples of a call are read only once the front has published
-// them (stream_wait), by write-through-coherent sc1 loads
 // DW: the launch may take the pipelined device hand-off (BackArgs::dwait; rx_back's pre role
 // only -- the fused back ends keep the code out of their register budget)
-template <int L, bool LDS_IN = false, bool STREAM = false, bool DW = false>
+template <int L, bool LDS_IN = false, bool DW = false>
 struct InStage
 {
     static constexpr int NDC = BLK / L;
     float xnext[NDC];
     const float* lds;
-    bool gave_up = false;                                // STREAM: a poll of this launch gave up
-    bool pending = false;                                // STREAM: xnext not loaded (its call was unpublished)
-    int fcall = -1;                                      // STREAM: the call fv was polled for
-    unsigned fv = 0;
-
-    // STREAM: the poll of `call` goes out now and is read at the next step (fv, fcall)
-    __device__ __forceinline__ void stream_poll(const BackArgs& a, const BackLane& l, int call)
-    {
-        if (call >= l.calls) return;
-        fv = __hip_atomic_load(stream_word(a, (l.c - l.lane) / BACK_CH), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        fcall = call;
-    }
-    // STREAM: the call's samples once published (fv, polled a step ahead for `call`, answers at
-    // once when the front is ahead), then the poll of the call after it
-    __device__ __forceinline__ void stream_fetch(const BackArgs& a, const BackLane& l, int call)
-    {
-        const int grp = (l.c - l.lane) / BACK_CH;
-        if (fcall != call) fv = __hip_atomic_load(stream_word(a, grp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        stream_wait(a, grp, call, fv, gave_up);
-        const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
-#pragma unroll
-        for (int m = 0; m < NDC; ++m)
-            xnext[m] = __hip_atomic_load(src + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        fcall = -1;
-        stream_poll(a, l, call + 1);
-    }
+    bool gave_up = false;                                // DW: this launch's poll gave up
 
     __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
     {
-        if constexpr (STREAM)
-        {
-            stream_fetch(a, l, call);
-            return;
-        }
         if constexpr (LDS_IN)
         {
             // a lane past the last channel reads channel C-1's column (the clamped-load rule: it
@@ -906,11 +822,16 @@ struct InStage
         {
             // device hand-off: once per launch, wait until the call's rx_front has completed
             // (rx_handoff_signal); then sc1 loads (this XCD's L2 may hold the buffer's previous
-            // contents: the launch may have started before the front finished)
+            // contents: the launch may have started before the front finished).  After a give-up
+            // every input of the launch is NaN (the failure contract of uhsdr_rx_set_pipelined)
             if (call == 0) dflag_wait(a, gave_up);
             const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
 #pragma unroll
-            for (int m = 0; m < NDC; ++m) xnext[m] = __hip_atomic_load(src + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int m = 0; m < NDC; ++m)
+            {
+                const float v = __hip_atomic_load(src + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                xnext[m] = gave_up ? __builtin_nanf("") : v;
+            }
             return;
         }
         // uniform row base (SGPRs) + the lane's 32-bit offset: no 64-bit per-lane address to keep
@@ -926,24 +847,6 @@ struct InStage
 
     __device__ __forceinline__ void begin(const BackArgs& a, const BackLane& l, int call, float (&xin)[NDC])
     {
-        if constexpr (STREAM)
-        {
-            // The step of call k needs call k only: call k + 1 is loaded now if the poll issued
-            // during the last step saw it published, else at the next step (pending); then the poll
-            // for the call after that goes out, answered while this step runs.
-            if (pending) { stream_fetch(a, l, call); pending = false; }
-#pragma unroll
-            for (int m = 0; m < NDC; ++m) xin[m] = xnext[m];
-            if (call + 1 >= l.calls) return;
-            const unsigned want = a.sepoch * 256u + (unsigned)call + 2u;
-            if (fcall == call + 1 && __all((int)(fv - want) >= 0)) stream_fetch(a, l, call + 1);
-            else
-            {
-                pending = true;
-                stream_poll(a, l, call + 1);
-            }
-            return;
-        }
 #pragma unroll
         for (int m = 0; m < NDC; ++m) xin[m] = xnext[m];
         if (call + 1 < l.calls) fetch(a, l, call + 1);
@@ -1776,7 +1679,6 @@ extern "C" int uhsdr_trace_read(void* out)
     {                                                                                          \
         const int call = it - (ST);                                                            \
         TRACE_MARK(0);                                                                         \
-        if (a.sflags && it < 16) STRACE(it);                                                   \
         if (call >= 0 && call < l.calls)                                                       \
         {
 #define BACK_ROLE_END                                                                          \
@@ -1817,16 +1719,23 @@ __device__ __forceinline__ bool back_agc_prep_in_pre(int dm, const uhsdr_agc_pla
 }
 
 // IIR lattice pre-filter; input: rx_front's decimated I +- Q (SSB) or the demod role's output
-template <int PRE, int L, int W, int DM, bool STREAM = false>
+template <int PRE, int L, int W, int DM>
 __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
-    InStage<L, false, STREAM, !STREAM> in;
+    InStage<L, false, true> in;
     LatticeStage<PRE> s;
     s.load(l, P->pre_k, P->pre_v, a.s.pre);
-    if (!DM) in.fetch(a, l, 0);
+    if (!DM)
+    {
+        in.fetch(a, l, 0);
+        // the failure contract: a give-up (InStage's poll, call 0) poisons the whole launch's output,
+        // including the frames the AGC's look-ahead delay still takes from the previous launch's
+        // samples -- the output role reads this after the step-0 barrier
+        if (l.lane == 0) *lds.poison = in.gave_up ? 1u : 0u;
+    }
     const uhsdr_agc_plan A = P->agc;
     const bool prep = back_agc_prep_in_pre(DM, A);
     AgcStage<L, W> ag;
@@ -2043,6 +1952,15 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
         for (int n = 0; n < BLK; ++n) y[n] = mi[n * BACK_CH];      // one batch of LDS reads
 #pragma unroll
         for (int n = 0; n < BLK; ++n) y[n] = s.step(y[n]);
+        if constexpr (DM == DM_NONE)
+        {
+            // the pre role's device hand-off gave up (its step-0 word): NaN audio for every frame
+            if (a.dwait && __builtin_amdgcn_readfirstlane(*lds.poison))
+            {
+#pragma unroll
+                for (int n = 0; n < BLK; ++n) y[n] = __builtin_nanf("");
+            }
+        }
 #pragma unroll
         for (int n0 = 0; n0 < BLK; n0 += 4)
         {
@@ -2274,247 +2192,6 @@ rx_chain(FrontArgs fa, BackArgs ba, int front_floats)
         if (ba.plan->cw_enabled) { back_fused_agc<PRE, AA, L, PH, W, DM_NONE, true, true, false>(ba, smem, grp, adl); return; }
     }
     back_fused_agc<PRE, AA, L, PH, W, DM_NONE, false, true, false>(ba, smem, grp, adl);
-}
-
-// ------------------------------------------------------------------------------------
-// rx_stream: one launch per call for small batches (the SSB / CW / DIGI Hilbert-first paths).
-// The grid holds the call's front and back end side by side on disjoint CUs (one workgroup per
-// CU, forced by the LDS allocation; the host checks that the whole grid is co-resident):
-//   workgroups [0, nfront)        front: F workgroups per channel group of 64; each front wave
-//                                 owns SCPW channels and walks the call's 32-frame calls in time
-//                                 order, publishing each call's decimated output (write-through
-//                                 stores + a per-wave progress word) as soon as it exists
-//   workgroups [nfront, + groups) back end: the rx_back wave pipeline of the group; its pre role
-//                                 polls the progress words before it reads a call (InStage<STREAM>)
-// The back end starts on call 0 while the front still filters calls 1.., with no event, side
-// stream or second launch, and no SIMD shared between the two (a front wave beside a pipeline
-// role on one SIMD slowed the role ~2.5x in the two-stream pipelined mode, profiles/
-// r04_c2_overlap_timeline.txt).  Front workgroups come first in the grid, so a back-end
-// workgroup only ever waits on workgroups dispatched before it; every poll is bounded.
-constexpr int SR = 2;                  // Hilbert outputs per front lane per 32-frame call
-constexpr int SNB = BLK / SR;          // lanes per channel (16)
-constexpr int SCPW = FRONT_WAVE / SNB; // channels per front wave (4)
-constexpr int SWPG = BACK_CH / SCPW;   // front waves per channel group (16)
-constexpr int STREAM_WAVES = 8;        // workgroup size in waves (the back end's 5 roles use the first 5)
-// (R = 4 outputs per lane, 8 channels and 8 waves per group, one wave per SIMD: 2.9-3.4 us per
-// 32-frame call and the back end waited on every call, C2 0.042-0.045 ms per call; a lone wave
-// hides none of its LDS and tap-load latency, tools/trace_stream.py, profiles/r05_stream_trace_r4.txt)
-
-struct StreamArgs
-{
-    unsigned* flags;      // [groups][SWPG] progress words (BackArgs::sflags)
-    unsigned epoch;       // this launch's epoch (>= 1; BackArgs::sepoch)
-    int nfront;           // front workgroups
-    int fpg;              // front workgroups per channel group
-    int wpw;              // front waves per front workgroup (the rest exit)
-    int groups;           // channel groups of 64
-    int lwp, lwd;         // front LDS pitches: pair window, audio-decimator window (floats)
-    int wave_floats;      // LDS floats per front wave (its SCPW pairs of windows)
-};
-
-// SR = 2 frames n0, n0 + 1 of one channel: int32 -> f32 x 2^-16, manual I/Q correction, the Fs/4
-// exchange (freq_shift.c:219-262) -- convert_block's arithmetic, with the exchange's rotation taken
-// from n0 & 3 (0 or 2 here: a lane's first frame is even, not a multiple of 4) by selects.  The
-// oscillator shift and auto I/Q keep the split kernels (stream_geometry).
-__device__ __forceinline__ void stream_convert2(const int4& raw, const InputStage& s, int n0, float (&xi)[2], float (&xq)[2])
-{
-    xi[0] = ((float)raw.x) * IQ_BIT_SCALE_DOWN; xq[0] = ((float)raw.y) * IQ_BIT_SCALE_DOWN;
-    xi[1] = ((float)raw.z) * IQ_BIT_SCALE_DOWN; xq[1] = ((float)raw.w) * IQ_BIT_SCALE_DOWN;
-    if (s.gi != 1.0f || s.gq != 1.0f)
-    {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) { xi[j] = xi[j] * s.gi; xq[j] = xq[j] * s.gq; }
-    }
-    if (s.ph < 0)
-    {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) { const float e3 = xi[j] * s.ph; xq[j] = xq[j] + e3; }
-    }
-    else if (s.ph > 0)
-    {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) { const float e3 = xq[j] * s.ph; xi[j] = xi[j] + e3; }
-    }
-    if (s.shift == 1)
-    {
-        // (ib, qb) = (I, Q) for FREQ_SHIFT_UP, else (Q, I); frame n gets {x0, -j x1, -x2, j x3}[n & 3]
-        const bool hi = (n0 & 2) != 0;
-        float ib0 = s.shift_up ? xi[0] : xq[0], qb0 = s.shift_up ? xq[0] : xi[0];
-        float ib1 = s.shift_up ? xi[1] : xq[1], qb1 = s.shift_up ? xq[1] : xi[1];
-        // n & 3 == 0 / 2 for the first frame, 1 / 3 for the second
-        const float i0 = ul_sel(hi, -ib0, ib0), q0 = ul_sel(hi, -qb0, qb0);
-        const float i1 = ul_sel(hi, -qb1, qb1), q1 = ul_sel(hi, ib1, -ib1);
-        xi[0] = s.shift_up ? i0 : q0; xq[0] = s.shift_up ? q0 : i0;
-        xi[1] = s.shift_up ? i1 : q1; xq[1] = s.shift_up ? q1 : i1;
-    }
-}
-
-// front wave w of channel group g: channels 64 g + SCPW w .. + SCPW - 1, all N frames of the call.
-// Per 32-frame call s: the Hilbert pair (lane = channel l / 16, SR outputs at 32 s + SR (l % 16)),
-// then the audio decimator on 32 / M outputs per channel (lane = channel l / (32 / M), one output).
-template <int T1, int T2, int M, bool F>
-__device__ __forceinline__ void stream_front_wave(const FrontArgs& a, const StreamArgs& sa, int g, int w, float* sm)
-{
-    static_assert(T2 > 0 && M >= 2 && SR == 2, "Hilbert-first families with an audio decimator");
-    constexpr int HQ1 = hist_qp(T1), HQ2 = hist_q(T2);
-    constexpr int DPC = BLK / M;                          // decimated outputs per channel per call
-    constexpr int DV = M % 4 == 0 ? 4 : 2;                // decimator window read width (alignment)
-    const uhsdr_rx_plan* __restrict__ P = a.plan;
-    const int lane = threadIdx.x & (FRONT_WAVE - 1);
-    const int gl = lane / SNB, bl = lane % SNB;           // Hilbert lanes: channel of the wave, block
-    const int gd = lane / DPC, jd = lane % DPC;           // decimator lanes: channel, output
-    const bool dact = gd < SCPW;
-    const int C = a.C, N = a.N, S = N / BLK;
-    const int c0 = g * BACK_CH + w * SCPW;
-    unsigned* const flag = sa.flags + (size_t)g * SWPG + w;
-    if (c0 >= C)
-    {
-        // past the last channel (wave-uniform): nothing to filter, every call published at once
-        if (lane == 0)
-            __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    const int nlive = C - c0 < SCPW ? C - c0 : SCPW;
-    const int c = c0 + gl;
-    const int cl = c < C ? c : C - 1;
-    const int cd = c0 + (dact ? gd : 0);
-    const bool dlive = dact && cd < C;
-    float* const smP = sm;                                // pair windows, pitch lwp
-    float* const smD = sm + SCPW * sa.lwp;                // audio-decimator windows, pitch lwd
-    float* const WP = smP + gl * sa.lwp;
-    float* const WD = smD + gl * sa.lwd;
-    float* const WDd = smD + (dact ? gd : 0) * sa.lwd;
-
-    InputStage in;
-    in.gi = P->iq_gain_i; in.gq = P->iq_gain_q; in.ph = P->iq_phase_balance;
-    in.iq_auto = 0;
-    in.shift = P->freq_shift_hz != 0 ? P->shift_kind : 0;   // 0 or 1 (Fs/4): the host admits no oscillator
-    in.shift_up = P->shift_up;
-    ctaps2_t* tA = as_taps2(a.taps2a);
-    const int comb = a.comb;
-
-    // frames of call 0 and the history rows first, call 1 right behind
-    const int4* src = (const int4*)(a.iq + (size_t)cl * a.ld + bl * SR);
-    int4 raw = src[0], rnx = raw;
-    vf4 hA[HQ1], hC[HQ2];
-    group_load_prow<T1>(a.hist1, c0, nlive, lane, hA);
-    group_load_rows<T2>(a.hist2, c0, nlive, lane, hC);
-    if (S > 1) rnx = src[BLK / 2];
-    group_fill_prow<T1>(smP, sa.lwp, a.hist1, c0, SCPW, nlive, lane, hA);
-    group_fill_rows<T2>(smD, sa.lwd, a.hist2, c0, SCPW, nlive, lane, hC);
-    wave_sync();                                          // the rows' pad floats before the new samples
-    unsigned clip = 0;
-    STRACE(0);
-    for (int s = 0; s < S; ++s)
-    {
-        const int blk = s * SNB + bl;                     // the lane's block of SR frames in the call
-        if (a.clip)
-        {
-            const int4 rr[1] = { raw };
-            clip |= clip_flags<SR>(rr);
-        }
-        {
-            float xi[SR], xq[SR];
-            stream_convert2(raw, in, blk * SR, xi, xq);
-            const v2f x2[SR] = { v2f{ xi[0], xq[0] }, v2f{ xi[1], xq[1] } };
-            window_new2(WP, T1, true, blk, x2, SR);
-        }
-        raw = rnx;
-        if (s + 2 < S) rnx = src[(s + 2) * (BLK / 2)];
-        if (s == 3) STRACE(20);
-        wave_sync();
-        if (s == 3) STRACE(21);
-        // Hilbert pair -> I +- Q into the decimator window, then the decimator
-        {
-            v2f h2[SR];
-            float hs[SR];
-            fir_block2<T1, SR, 1, F, 0, true>(WP + 2 * blk * SR, tA, h2);
-            if (s == 3) STRACE(22);
-            front_comb_block<SR>(comb, h2, hs);
-            window_new(WD, T2, true, blk, hs, SR);
-        }
-        wave_sync();
-        if (s == 3) STRACE(23);
-        float o[1];
-        fir_block<T2, 1, M, DV, F, true>(WDd + s * BLK + jd * M, as_taps(P->dec), o);
-        if (s == 3) STRACE(24);
-#ifndef UHSDR_STREAM_EAGER
-        // publish call s - 1 now that this call's FIRs gave its write-through stores time to land
-        // (call 0 is published right away: it sets when the back end starts)
-        if (s > 0)
-        {
-            // outstanding: call s - 1's adec store, then (s + 2 < S) this step's frame prefetch;
-            // vector memory operations complete in order, so vmcnt(1) leaves the prefetch in flight
-            if (s + 2 < S) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0)
-                __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (s > 1 && s < 20) STRACE(s);
-            if (s == 3) STRACE(25);
-        }
-#endif
-        if (dlive)
-            __hip_atomic_store(a.adec + (size_t)cd * a.ldd + s * DPC + jd, o[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifndef UHSDR_STREAM_EAGER
-        if (s == 0 || s == S - 1)
-#endif
-        {
-            // publish call s: this wave's write-through stores complete, then its progress word
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0)
-                __hip_atomic_store(flag, sa.epoch * 256u + (unsigned)s + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (s < 19) STRACE(1 + s);
-        }
-        if (s == 3) STRACE(26);
-    }
-    if (clip && c < C) atomicOr(a.clip + c, clip);
-    wave_sync();
-    // the next call's history rows
-    group_store_prow<T1>(smP, sa.lwp, a.hist1, c0, nlive, lane, N);
-    group_store_rows<T2>(smD, sa.lwd, a.hist2, c0, nlive, lane, N);
-    STRACE(30);
-}
-
-template <int T1, int T2, int M, bool F, int PRE, int AA, int L, int PH, int W>
-__global__ void __launch_bounds__(STREAM_WAVES * FRONT_WAVE) rx_stream(FrontArgs fa, BackArgs ba, StreamArgs sa)
-{
-    static_assert(M == L, "decimation and interpolation rates agree");
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / FRONT_WAVE);
-    const int b = blockIdx.x;
-    if (b >= sa.nfront)
-    {
-        // back end of group b - nfront (ba.grp0 = nfront): waves 0-4 are the roles, the rest leave
-        // (an ended wave no longer counts at the roles' barriers)
-        if (wave >= back_roles(DM_NONE)) return;
-        const BackLds lds = back_lds_carve<BLK / L>(smem);
-        if (wave == 0) rx_back_pre<PRE, L, W, DM_NONE, true>(ba, lds);
-        else if (wave == 1) rx_back_agc<L, W, DM_NONE>(ba, lds);
-        else if (wave == 2) rx_back_audio<L, PH, W, DM_NONE>(ba, lds);
-        else if (wave == 3) rx_back_aa<AA, DM_NONE>(ba, lds);
-        else rx_back_output<DM_NONE>(ba, lds);
-        STRACE(30);
-        return;
-    }
-    // front workgroup b -> (channel group, its index f among the group's F): the F workgroups of a
-    // group and the group's back end share b mod 8 when the counts allow (one XCD's L2 under the
-    // observed round-robin placement; placement is never needed for correctness)
-    int g, f;
-    if ((sa.groups & 7) == 0 && (sa.nfront & 7) == 0)
-    {
-        const int x = b & 7, q = b >> 3, gx = sa.groups >> 3;
-        g = x + 8 * (q % gx);
-        f = q / gx;
-    }
-    else
-    {
-        g = b / sa.fpg;
-        f = b % sa.fpg;
-    }
-    if (wave >= sa.wpw) return;
-    const int w = f * sa.wpw + wave;
-    if (w >= SWPG) return;
-    stream_front_wave<T1, T2, M, F>(fa, sa, g, w, smem + wave * sa.wave_floats);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2984,14 +2661,8 @@ struct ChainVariant { int t1, t2, m, decim_first, R, pre, aa, L, ph, w; chain_fn
 #define FRONT_V(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false>, R, rx_front<t1, t2, m, df, R, true>, 0 }
 #define FRONT_ST(t1, t2, m, df, R) { t1, t2, m, df, rx_front<t1, t2, m, df, R, false, true>, R, rx_front<t1, t2, m, df, R, true, true>, 1 }
 struct NotchVariant { int L, dm; back_fn fn; };
-// rx_stream instances: a Hilbert-first front family (t1, t2, m) with a DM_NONE back end
-typedef void (*stream_fn)(FrontArgs, BackArgs, StreamArgs);
-struct StreamVariant { int t1, t2, m, pre, aa, L, ph, w; stream_fn fn, fn_fma; };
-#define STREAM_V(t1, t2, m, pre, aa, ph, w) { t1, t2, m, pre, aa, m, ph, w, \
-    rx_stream<t1, t2, m, false, pre, aa, m, ph, w>, rx_stream<t1, t2, m, true, pre, aa, m, ph, w> }
 #include <uhsdr_rx_variants.inc>
 #undef CHAIN_V
-#undef STREAM_V
 
 static int plan_dm(const uhsdr_rx_plan& p)
 {
@@ -3032,17 +2703,6 @@ static const ChainVariant* find_chain(const uhsdr_rx_plan& p, const BackVariant*
     for (const ChainVariant& v : kChain)
         if (v.t1 == t1 && v.t2 == t2 && v.m == p.decimation_rate && v.decim_first == p.use_decimated_iq &&
             v.pre == bv->pre && v.aa == bv->aa && v.L == bv->L && v.ph == bv->ph && v.w == bv->w)
-            return &v;
-    return nullptr;
-}
-
-static const StreamVariant* find_stream(const uhsdr_rx_plan& p, const BackVariant* bv)
-{
-    if (!bv || bv->dm != DM_NONE || p.stereo || p.notch_enabled || p.dmod_mode == UHSDR_DEMOD_FM || p.use_decimated_iq)
-        return nullptr;
-    for (const StreamVariant& v : kStream)
-        if (v.t1 == p.hilbert_taps && v.t2 == p.dec_taps && v.m == p.decimation_rate && v.pre == bv->pre &&
-            v.aa == bv->aa && v.L == bv->L && v.ph == bv->ph && v.w == bv->w)
             return &v;
     return nullptr;
 }
@@ -3100,7 +2760,6 @@ struct uhsdr_rx_s
     const BackVariant* bv;
     const NotchVariant* nv;  // LMS auto notch kernel (null: notch off)
     const ChainVariant* cv;  // rx_chain instance of the path (null: none)
-    const StreamVariant* sv; // rx_stream instance of the path (null: none)
     int C, N, Nd, Nf;        // Nf: frames per front launch (N split into N / Nf launches)
     int lw;                  // front LDS window pitch (floats)
     int schedule;            // resolved UHSDR_SCHEDULE_SPLIT_PIPE / _SPLIT_FUSED / _CHAIN
@@ -3148,17 +2807,17 @@ struct uhsdr_rx_s
     uint8_t* evmask;         // [cap] kernels recorded in each timed call
     float total_ms[4];
     int launches[4];
-    // rx_stream (UHSDR_SCHEDULE_STREAM): progress words, give-up word, launch geometry
-    unsigned* sflags;        // [groups][SWPG], then the give-up word
-    unsigned* stmo;
-    unsigned stream_epoch;   // rx_stream launches since reset
-    StreamArgs sgeo;         // geometry (flags and epoch are set per launch)
-    size_t s_lds;            // dynamic LDS per workgroup (forces one workgroup per CU)
-    int s_ok;                // the path has an instance, the geometry fits, the grid is co-resident
+    // failure contract of the bounded device-side polls: fail_host is host-mapped coherent memory
+    // (fail_dev its device address) that a poll giving up sets to 1; process / join / synchronize
+    // return UHSDR_TIMEOUT while it is set, uhsdr_rx_reset clears it
+    volatile unsigned* fail_host;
+    unsigned* fail_dev;
+    unsigned spin_max;       // polls before a give-up (uhsdr_rx_set_handoff_bound; default 2^24)
     // pipelined device hand-off (uhsdr_rx_set_pipelined 2): rx_back polls the call sequence number
-    // rx_handoff_signal publishes after each rx_front (the word after stmo) instead of waiting on
+    // rx_handoff_signal publishes after each rx_front (dword, device memory) instead of waiting on
     // a cross-stream event
     int dflag;
+    unsigned* dword;         // the published call sequence number
     int dflag_grid;          // largest rx_back grid it is used for (half the CUs: the polling
                              // workgroups never crowd out the front they wait for)
     unsigned dtotal;         // calls published by rx_handoff_signal since reset
@@ -3170,8 +2829,8 @@ struct uhsdr_rx_s
 };
 
 // kernel slots of the timing API: a call runs rx_front + rx_back (any back-end kernel) or rx_chain
-enum { K_FRONT = 0, K_BACK = 1, K_CHAIN = 2, K_STREAM = 3, NKERN = 4 };
-static const char* kKernelNames[NKERN] = { "rx_front", "rx_back", "rx_chain", "rx_stream" };
+enum { K_FRONT = 0, K_BACK = 1, K_CHAIN = 2, NKERN = 3 };
+static const char* kKernelNames[NKERN] = { "rx_front", "rx_back", "rx_chain" };
 
 static bool side_mode(const uhsdr_rx_s* h) { return h->pipelined; }
 static hipStream_t back_stream(const uhsdr_rx_s* h) { return side_mode(h) ? h->side : h->stream; }
@@ -3376,71 +3035,7 @@ static bool chain_ok(const uhsdr_rx_s* h)
     return h->cv && h->fv->R == h->cv->R && h->Nf == h->N && chain_lds(h) <= 64 * 1024 && !h->plan.agc.remove_dc;
 }
 
-// rx_stream's geometry for the handle's shape.  F front workgroups per channel group of 64 (as many
-// as the CUs left by the back end allow, up to one per front wave), ceil(SWPG / F) front waves in
-// each; one workgroup per CU (the LDS allocation takes more than half a CU's), and the whole grid
-// must be co-resident (occupancy x CUs >= grid): the back end polls the front of its own launch.
-// Pitches: the fewest modeled ds_read_b128 cycles of the two FIR windows (lane = channel l / 8,
-// block l % 8).  Not for the oscillator shift or auto I/Q (their per-launch pre-passes are
-// rx_front's), which keep the split kernels.
 static size_t back_lds(const uhsdr_rx_s* h);
-static int stream_pitch(int need, int per, int stride)
-{
-    int best = need, best_c = 1 << 30;
-    for (int lw = need; lw < need + 64; lw += 4)
-    {
-        int addr[64];
-        for (int l = 0; l < 64; ++l) addr[l] = l / per < SCPW ? (l / per) * lw + (l % per) * stride : -1;
-        const int c = lds_op_cycles(LDS_R128, addr);
-        if (c < best_c) { best_c = c; best = lw; }
-    }
-    return best;
-}
-
-static void stream_geometry(uhsdr_rx_s* h)
-{
-    h->s_ok = 0;
-    const uhsdr_rx_plan& p = h->plan;
-    if (!h->sv || p.iq_auto_correction || (p.freq_shift_hz != 0 && p.shift_kind == 2)) return;
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return;
-    const int cus = prop.multiProcessorCount;
-    const int groups = (h->C + BACK_CH - 1) / BACK_CH;
-    int F = (cus - groups) / groups;
-    if (F > SWPG) F = SWPG;
-    if (F < 1) return;
-    const int wpw = (SWPG + F - 1) / F;
-    if (wpw > STREAM_WAVES) return;
-    const int N = h->N, T1 = h->sv->t1, T2 = h->sv->t2;
-    const int needp = (2 * (T1 - 1 + N) + 3) & ~3;
-    const int nd = T2 - 1 + N > hist_stride(T2) ? T2 - 1 + N : hist_stride(T2);
-    const int M = h->sv->m;
-    const int lwp = stream_pitch(needp, SNB, 2 * SR), lwd = stream_pitch((nd + 3) & ~3, BLK / M, M);
-    const int wave_floats = (SCPW * (lwp + lwd) + FRONT_SLACK + 3) & ~3;
-    const size_t front = sizeof(float) * (size_t)wpw * wave_floats, back = back_lds(h);
-    size_t lds = front > back ? front : back;
-    if (lds < LDS_PER_CU / 2 + 1024) lds = LDS_PER_CU / 2 + 1024;          // one workgroup per CU
-    if (lds > LDS_PER_CU) return;
-    const int grid = F * groups + groups;
-    for (const void* fn : { (const void*)h->sv->fn, (const void*)h->sv->fn_fma })
-    {
-        int nb = 0;
-        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_PER_CU) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, STREAM_WAVES * FRONT_WAVE, lds) != hipSuccess ||
-            nb < 1 || (long long)nb * cus < grid)
-        {
-            (void)hipGetLastError();
-            return;
-        }
-    }
-    StreamArgs& g = h->sgeo;
-    g.flags = nullptr; g.epoch = 0;
-    g.nfront = F * groups; g.fpg = F; g.wpw = wpw; g.groups = groups;
-    g.lwp = lwp; g.lwd = lwd; g.wave_floats = wave_floats;
-    h->s_lds = lds;
-    h->s_ok = 1;
-}
 
 // AUTO: batches of BACK_FUSED_MIN_CHANNELS channels and more run rx_front + rx_back_fused
 // (SPLIT_FUSED), smaller ones rx_front + the back-end wave pipeline (SPLIT_PIPE); rx_chain (CHAIN)
@@ -3456,7 +3051,6 @@ static int resolve_schedule(const uhsdr_rx_s* h, int want)
         return h->bv->fused ? UHSDR_SCHEDULE_SPLIT_FUSED : UHSDR_SCHEDULE_SPLIT_PIPE;
     }
     if (want == UHSDR_SCHEDULE_CHAIN) return chain_ok(h) ? want : -1;
-    if (want == UHSDR_SCHEDULE_STREAM) return h->s_ok ? want : -1;
     if (want == UHSDR_SCHEDULE_SPLIT_FUSED) return h->bv->fused ? want : -1;
     if (want == UHSDR_SCHEDULE_SPLIT_PIPE) return want;
     return -1;
@@ -3507,10 +3101,10 @@ extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
     HIPCHK(hipMemcpyAsync(h->osc, osc0, sizeof osc0, hipMemcpyHostToDevice, h->stream));
     // ts.twinpeaks_tested = TWINPEAKS_WAIT at boot (src/uhsdr_main.c:339); the statics start at 0
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->tp, UHSDR_TWINPEAKS_WAIT, (size_t)h->C, h->stream));
-    // rx_stream's progress words restart with the epoch (and its give-up word)
-    if (h->sflags)
-        HIPCHK(hipMemsetAsync(h->sflags, 0, sizeof(unsigned) * (((size_t)(h->C + BACK_CH - 1) / BACK_CH) * SWPG + 4), h->stream));
-    h->stream_epoch = 0;
+    // the device hand-off's sequence word restarts with dtotal; a poll's give-up is cleared (the
+    // state it poisoned was zeroed above)
+    HIPCHK(hipMemsetAsync(h->dword, 0, sizeof(unsigned), h->stream));
+    *h->fail_host = 0;
     h->dtotal = 0;
     h->main_back = 1;
     if (h->bs.cw)
@@ -3562,7 +3156,6 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->bv = find_back(p);
     h->nv = find_notch(p);
     h->cv = find_chain(p, h->bv);
-    h->sv = find_stream(p, h->bv);
     if (!uhsdr_rx_mode_supported(&p) || !h->fv || !h->bv || (p.notch_enabled && !h->nv))
     {
         free(h);
@@ -3607,13 +3200,16 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         hipMalloc((void**)&h->d_plan, sizeof(uhsdr_rx_plan)) != hipSuccess ||
         hipMalloc((void**)&h->d_taps2, sizeof(float) * 4 * TAPS2_MAX) != hipSuccess ||
         hipMalloc((void**)&h->d_lanemap, sizeof(uint16_t) * 4 * 64) != hipSuccess ||
-        hipMalloc((void**)&h->sflags, sizeof(unsigned) * (((size_t)(C + BACK_CH - 1) / BACK_CH) * SWPG + 4)) != hipSuccess)
+        hipMalloc((void**)&h->dword, 64) != hipSuccess ||
+        hipHostMalloc((void**)&h->fail_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&h->fail_dev, (void*)h->fail_host, 0) != hipSuccess)
     {
         uhsdr_set_error("hipMalloc failed (%zu bytes state)", h->arena_bytes);
         (void)uhsdr_rx_destroy(h);
         return UHSDR_DEVICE_ERROR;
     }
-    h->stmo = h->sflags + ((size_t)(C + BACK_CH - 1) / BACK_CH) * SWPG;
+    *h->fail_host = 0;
+    h->spin_max = DFLAG_SPIN_MAX;
     float* A = (float*)h->arena;
     h->hist1 = A + o_h1; h->hist2 = A + o_h2;
     h->teta = A + o_teta; h->osc = A + o_osc; h->tp = (int*)(A + o_tp);
@@ -3676,7 +3272,6 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         (void)uhsdr_rx_destroy(h);
         return UHSDR_DEVICE_ERROR;
     }
-    stream_geometry(h);
     const uhsdr_status rs = uhsdr_rx_reset(h);
     if (rs != UHSDR_OK) { (void)uhsdr_rx_destroy(h); return rs; }
     *out = h;
@@ -3815,13 +3410,10 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
         ba.notch_first = h->calls_done == 0;
     }
     ba.tone_phase = (int)(h->calls_done % 400);
-    ba.grp0 = 0;
-    ba.sflags = nullptr;
-    ba.sepoch = 0;
-    ba.swpg = 0;
-    ba.stmo = nullptr;
     ba.dwait = nullptr;
     ba.dtarget = 0;
+    ba.spin_max = h->spin_max;
+    ba.fail = h->fail_dev;
     {
         // key beep: frames [0, beep_n1) of this launch while calls are left (uhsdr_rx_key_beep)
         const int calls = h->N / BLK;
@@ -3854,46 +3446,28 @@ static void line_out_mchf(const uhsdr_rx_s* h, const BackArgs& ba, hipStream_t s
     hipLaunchKernelGGL(rx_line_out_mchf, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, ba, (const float*)h->mchf_u);
 }
 
+// the failure word a bounded device-side poll sets when it gives up (BackArgs::fail)
+static uhsdr_status check_fail(const uhsdr_rx_s* h)
+{
+    if (!*h->fail_host) return UHSDR_OK;
+    uhsdr_set_error("the pipelined device hand-off gave up waiting for rx_front (a poll bound of %u polls): the "
+                    "outputs of that call are poisoned (NaN audio) and the handle's state is invalid until "
+                    "uhsdr_rx_reset", h->spin_max);
+    return UHSDR_TIMEOUT;
+}
+
 static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audio, float* audio0, int32_t* dst)
 {
     if (!h || !iq) { uhsdr_set_error("null argument"); return UHSDR_ARGUMENT_ERROR; }
+    {
+        const uhsdr_status fs = check_fail(h);
+        if (fs != UHSDR_OK) return fs;
+    }
     if (h->timing && h->nev >= h->nev_cap) time_harvest(h);
     h->tsample = h->timing && (h->tcalls++ % h->timing) == 0;
     if (h->tsample) h->evmask[h->nev] = 0;
     const bool fma = h->precision == UHSDR_PRECISION_FMA;
-    if (h->schedule == UHSDR_SCHEDULE_STREAM)
-    {
-        // one kernel: front and back end on disjoint CUs, the hand-off published per 32-frame call;
-        // after every back end still running on the pipelined mode's side stream (state it writes)
-        if (side_mode(h) && h->side_dirty)
-        {
-            HIPCHK(hipEventRecord(h->ev_join, h->side));
-            HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-            h->side_dirty = 0;
-        }
-        FrontArgs fa = front_args(h, iq, 0, h->adec, nullptr);
-        fa.N = h->N;                                       // the whole call in one launch
-        const BackArgs ba = back_args(h, h->adec, nullptr, audio, audio0, dst);
-        BackArgs bk = ba;
-        bk.mchf_u = h->mchf_u;                             // mcHF: finished by rx_line_out_mchf
-        StreamArgs sa = h->sgeo;
-        sa.flags = h->sflags;
-        sa.epoch = ++h->stream_epoch;
-        bk.grp0 = sa.nfront;
-        bk.sflags = h->sflags;
-        bk.sepoch = sa.epoch;
-        bk.swpg = SWPG;
-        bk.stmo = h->stmo;
-        time_mark(h, K_STREAM, 0);
-        hipLaunchKernelGGL(fma ? h->sv->fn_fma : h->sv->fn, dim3(sa.nfront + sa.groups), dim3(STREAM_WAVES * FRONT_WAVE),
-                           h->s_lds, h->stream, fa, bk, sa);
-        line_out_mchf(h, ba, h->stream);
-        HIPCHK(hipGetLastError());
-        time_mark(h, K_STREAM, 1);
-        h->front_launches += 1;
-        h->main_back = 1;
-    }
-    else if (h->schedule == UHSDR_SCHEDULE_CHAIN)
+    if (h->schedule == UHSDR_SCHEDULE_CHAIN)
     {
         // one kernel: front passes and back end per 64 channels, the hand-off in LDS
         // after every back end still running on the pipelined mode's side stream (state it writes)
@@ -3953,7 +3527,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         if (dfl)
         {
             h->dtotal += 1;
-            hipLaunchKernelGGL(rx_handoff_signal, dim3(1), dim3(64), 0, h->stream, h->stmo + 1, h->dtotal);
+            hipLaunchKernelGGL(rx_handoff_signal, dim3(1), dim3(64), 0, h->stream, h->dword, h->dtotal);
             HIPCHK(hipGetLastError());
         }
         time_mark(h, K_FRONT, 1);
@@ -3966,9 +3540,8 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         if (mc_pass) bk.mchf_u = h->mchf_u;
         if (dfl)
         {
-            bk.dwait = h->stmo + 1;
+            bk.dwait = h->dword;
             bk.dtarget = h->dtotal;
-            bk.stmo = h->stmo;
         }
         const hipStream_t bst = back_stream(h);
         if (side && !dfl) HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
@@ -4057,7 +3630,7 @@ extern "C" uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
     HIPCHK(sync_all(h));
-    return UHSDR_OK;
+    return check_fail(h);
 }
 
 extern "C" uhsdr_status uhsdr_rx_set_precision(uhsdr_rx_handle h, int32_t precision)
@@ -4083,7 +3656,7 @@ extern "C" int32_t uhsdr_rx_get_precision(uhsdr_rx_handle h) { return h ? h->pre
 extern "C" uhsdr_status uhsdr_rx_set_schedule(uhsdr_rx_handle h, int32_t schedule)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
-    if (schedule < UHSDR_SCHEDULE_AUTO || schedule > UHSDR_SCHEDULE_STREAM)
+    if (schedule < UHSDR_SCHEDULE_AUTO || schedule > UHSDR_SCHEDULE_CHAIN)
     {
         uhsdr_set_error("schedule %d: not a UHSDR_SCHEDULE_*", (int)schedule);
         return UHSDR_ARGUMENT_ERROR;
@@ -4101,12 +3674,18 @@ extern "C" uhsdr_status uhsdr_rx_set_schedule(uhsdr_rx_handle h, int32_t schedul
 
 extern "C" int32_t uhsdr_rx_get_schedule(uhsdr_rx_handle h) { return h ? h->schedule : -1; }
 
-extern "C" int32_t uhsdr_rx_stream_timeouts(uhsdr_rx_handle h)
+extern "C" int32_t uhsdr_rx_handoff_timeouts(uhsdr_rx_handle h)
 {
-    if (!h || !h->stmo) return -1;
-    unsigned v = 0;
-    if (sync_all(h) != hipSuccess || hipMemcpy(&v, h->stmo, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    return (int32_t)v;
+    if (!h || sync_all(h) != hipSuccess) return -1;
+    return (int32_t)*h->fail_host;
+}
+
+extern "C" uhsdr_status uhsdr_rx_set_handoff_bound(uhsdr_rx_handle h, uint32_t polls)
+{
+    if (!h) return UHSDR_ARGUMENT_ERROR;
+    if (polls == 0) { uhsdr_set_error("handoff bound: at least one poll"); return UHSDR_ARGUMENT_ERROR; }
+    h->spin_max = polls;
+    return UHSDR_OK;
 }
 
 extern "C" uhsdr_status uhsdr_rx_set_front_block(uhsdr_rx_handle h, int32_t outputs_per_lane)
@@ -4133,12 +3712,17 @@ extern "C" uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h)
         HIPCHK(hipEventRecord(h->ev_join, h->side));
         HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
     }
-    return UHSDR_OK;
+    return check_fail(h);
 }
 
 extern "C" uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
+    if (enable < 0 || enable > 2)
+    {
+        uhsdr_set_error("pipelined mode %d: 0 (off), 1 (event hand-off) or 2 (device hand-off)", (int)enable);
+        return UHSDR_ARGUMENT_ERROR;
+    }
     if (enable && !h->side)
     {
         const size_t nd = (size_t)h->C * h->Nd;
@@ -4274,7 +3858,8 @@ extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
     if (h->d_plan) (void)hipFree(h->d_plan);
     if (h->d_taps2) (void)hipFree(h->d_taps2);
     if (h->d_lanemap) (void)hipFree(h->d_lanemap);
-    if (h->sflags) (void)hipFree(h->sflags);
+    if (h->dword) (void)hipFree(h->dword);
+    if (h->fail_host) (void)hipHostFree((void*)h->fail_host);
     free(h);
     return UHSDR_OK;
 }

@@ -159,7 +159,9 @@ class RxChain:
     def set_pipelined(self, enable=True) -> None:
         """Overlap call k+1's rx_front with call k's rx_back (uhsdr_rx_set_pipelined); outputs
         are complete after synchronize() / a device-wide sync, or join() for the handle's stream.
-        enable: False / 0 off, True / 1 (cross-stream event hand-off), 2 (device hand-off)."""
+        enable: False / 0 off, True / 1 (cross-stream event hand-off), 2 (device hand-off: a poll
+        that gives up poisons that call's audio with NaN, and process / join / synchronize then
+        raise UhsdrError with status UHSDR_TIMEOUT until reset())."""
         _abi.check(self.lib.uhsdr_rx_set_pipelined(self.handle, int(enable)), "uhsdr_rx_set_pipelined")
 
     def set_precision(self, precision: int) -> None:
@@ -171,13 +173,19 @@ class RxChain:
         return self.lib.uhsdr_rx_get_precision(self.handle)
 
     def set_schedule(self, schedule: int) -> None:
-        """SCHEDULE_AUTO / _SPLIT_PIPE / _SPLIT_FUSED / _CHAIN / _STREAM (uhsdr_rx_set_schedule): which kernels
+        """SCHEDULE_AUTO / _SPLIT_PIPE / _SPLIT_FUSED / _CHAIN (uhsdr_rx_set_schedule): which kernels
         run a call; outputs are identical under every one."""
         _abi.check(self.lib.uhsdr_rx_set_schedule(self.handle, int(schedule)), "uhsdr_rx_set_schedule")
 
-    def stream_timeouts(self) -> int:
-        """STREAM schedule: 1 if one of its bounded hand-off polls gave up since reset (synchronises)."""
-        return self.lib.uhsdr_rx_stream_timeouts(self.handle)
+    def handoff_timeouts(self) -> int:
+        """1 if a bounded device hand-off poll gave up since reset, else 0 (synchronises;
+        uhsdr_rx_handoff_timeouts)."""
+        return self.lib.uhsdr_rx_handoff_timeouts(self.handle)
+
+    def set_handoff_bound(self, polls: int) -> None:
+        """Polls before the device hand-off gives up (uhsdr_rx_set_handoff_bound; tests of the
+        failure contract)."""
+        _abi.check(self.lib.uhsdr_rx_set_handoff_bound(self.handle, int(polls)), "uhsdr_rx_set_handoff_bound")
 
     @property
     def schedule(self) -> int:

@@ -150,8 +150,8 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
     sched = SCHEDULE_NAMES.get(chain.schedule, str(chain.schedule))
     if pipelined:
         # call k+1's rx_front overlaps call k's rx_back; 2: the device hand-off (rx_back polls the
-        # call sequence number rx_handoff_signal publishes after the front, then reads the hand-off
-        # with sc1 loads, instead of waiting on a cross-stream event)
+        # arrival counters the front waves of its channel group bump, then reads the hand-off with
+        # sc1 loads, instead of waiting on a cross-stream event)
         chain.set_pipelined(2 if DEVICE_HANDOFF else True)
     plan = chain.plan
     # inputs resident in HBM before timing: a pool of consecutive blocks, cycled

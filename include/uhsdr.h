@@ -284,12 +284,15 @@ uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h);
    calls is safe (rx_back launches are ordered on the side stream).  Replaces nothing in the
    reference (the firmware runs one ISR at a time); uhsdr_rx_process_host joins itself.
    enable = 1: each rx_back waits for its rx_front through a cross-stream event.
-   enable = 2 (device hand-off): after a call's rx_front a one-lane kernel publishes the call's
-   sequence number, and rx_back -- the wave-pipeline back end without a demodulator or notch
-   (SSB / CW / DIGI), while its grid is at most half the CUs -- polls it on the device and reads
-   the hand-off with L1-bypassing sc1 loads; no cross-stream wait per call, so the side stream's
-   back ends run back to back.  Other calls keep the event.  Any other enable value returns
-   UHSDR_ARGUMENT_ERROR.
+   enable = 2 (device hand-off): rx_front stores the decimated hand-off write-through and each of
+   its waves, once its stores have completed, bumps an arrival counter of its 64-channel group;
+   rx_back -- the wave-pipeline back end without a demodulator or notch (SSB / CW / DIGI), while
+   its grid is at most half the CUs -- polls its group's counter on the device and reads the
+   hand-off with L1-bypassing sc1 loads: no cross-stream wait and no extra kernel per call, so the
+   side stream's back ends run back to back.  When the next call's front has already arrived, a
+   back-end launch also runs its first pipeline roles ahead into that call instead of draining
+   (bit-identical; the next launch then starts without a pipeline fill).  Other calls keep the
+   event.  Any other enable value returns UHSDR_ARGUMENT_ERROR.
    Failure contract of the device hand-off.  The poll is bounded (uhsdr_rx_set_handoff_bound,
    default 2^24 polls: seconds).  If rx_back gives up -- the handle's stream held the call's
    rx_front back that long behind other work, or a profiler serialised the two streams' dispatches

@@ -184,9 +184,10 @@ def test_pipelined_mchf_matches_oracle(cuda, name, kw, gen, C, N, calls):
     assert np.abs(ref[0]).max() > 0
 
 
-# The device hand-off (uhsdr_rx_set_pipelined 2): after each call's rx_front a one-lane kernel
-# (rx_handoff_signal) publishes the call's sequence number, and rx_back polls it on the device and
-# then reads adec with sc1 loads, instead of waiting on a cross-stream event per call.  Used for the
+# The device hand-off (uhsdr_rx_set_pipelined 2): rx_front's waves store adec write-through and bump
+# their 64-channel group's arrival counter, and rx_back polls it on the device and then reads adec
+# with sc1 loads, instead of waiting on a cross-stream event per call (and runs ahead into the next
+# call when it has arrived: BackSched).  Used for the
 # wave-pipeline back end without a demodulator or notch (SSB / CW / DIGI) up to half the CUs' worth
 # of back-end workgroups; every other case keeps the event, so the AM, FM and large-batch cases check
 # that fallback.  No poll may give up (uhsdr_rx_handoff_timeouts).
@@ -351,3 +352,31 @@ def test_device_handoff_give_up_fails_loudly(cuda):
     with pytest.raises(U.UhsdrError):
         chain.set_pipelined(3)                       # modes are 0, 1, 2
     chain.close()
+
+
+@pytest.mark.parametrize("N", [128, 256], ids=["n4", "n8"])
+def test_device_handoff_skew_transitions(cuda, N):
+    """BackSched (the skewed wave pipeline): a launch runs ahead into the next
+    call only when that call's front has already published; fronts delayed on every third call (and
+    two in a row) make launches alternate between running ahead, draining, filling and starting
+    skewed, in every combination, with N / 32 == BACK_SKEW (n4: the pre role has none of its own call
+    left in a skewed launch) and 8.  Bit-exact against the oracle, no poll giving up."""
+    import torch
+    cfg = U.default_config()
+    C, calls = 640, 19
+    chain = U.RxChain(cfg, channels=C, frames=N, stream=torch.cuda.current_stream().cuda_stream)
+    chain.set_pipelined(2)
+    iq = synth.ssb_iq(np.arange(C), 0, calls * N)
+    xs = [torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda() for k in range(calls)]
+    audio = torch.empty((calls, C, N), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    for k in range(calls):
+        if k % 3 == 2 or k in (10, 11):
+            torch.cuda._sleep(150_000)
+        chain.process(xs[k], audio[k], None)
+    chain.synchronize()
+    assert chain.handoff_timeouts() == 0
+    chain.close()
+    ref, _ = oracle.OracleRx(U.build_plan(cfg), C).process(iq, threads=8)
+    got = audio.permute(1, 0, 2).reshape(C, calls * N).cpu().numpy()
+    assert_bitexact(got, ref, f"skew transitions N={N}")

@@ -37,6 +37,9 @@
 #include "uhsdr_libm.h"
 #include "uhsdr_dsp.h"
 
+// channels per back-end workgroup (lane == channel): the unit of the device hand-off's arrival counters
+#define BACK_CH 64
+
 struct FrontArgs
 {
     const uhsdr_rx_plan* plan;
@@ -62,6 +65,12 @@ struct FrontArgs
                              // for conflict-free ds_read_b128, front_window_pitch)
     int comb;                // demodulator of the Hilbert pair (audio_driver.c:2755-2790, FRONT_COMB_*)
     float* fm_prev;          // FM: [2][C] the last {I, Q} of the previous launch (rx_fm's i_prev, q_prev)
+    // pipelined device hand-off: the arrival counters of this launch's hand-off buffer, one per
+    // 64-channel back-end group ([groups]).  Non-null: adec is stored write-through (sc1), and each
+    // wave, once its stores have completed (vmcnt(0)), adds 1 to the counter of every group its
+    // channels belong to -- rx_back polls them with sc1 loads (MI355X_MICROARCH.md, inter-workgroup
+    // visibility: sc1 payload, drained, one agent-scope add per storing workgroup, sc1 poll and loads)
+    unsigned* gcnt;
 };
 
 // what rx_front makes of the Hilbert pair (I', Q'): a_buffer[0] (and a_buffer[1] in stereo)
@@ -565,7 +574,13 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
         {
             if (!live) return;
             float* dst = a.adec + (size_t)c * a.ldd + b * RD;
-            if (RD % 4 == 0)
+            if (a.gcnt)
+            {
+                // device hand-off: write-through stores (the back end may be reading from another XCD)
+#pragma unroll
+                for (int r = 0; r < RD; ++r) __hip_atomic_store(dst + r, o[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            else if (RD % 4 == 0)
             {
 #pragma unroll
                 for (int r = 0; r < RD; r += 4) *(float4*)(dst + r) = make_float4(o[r], o[r + 1], o[r + 2], o[r + 3]);
@@ -576,14 +591,20 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
                 for (int r = 0; r < RD; ++r) dst[r] = o[r];
             }
         });
-}
-
-// pipelined device hand-off: launched on the handle's stream after a call's last rx_front, so it
-// runs once that front has completed (its stores written back at the kernel's end); publishes the
-// call's sequence number to the word rx_back polls
-__global__ void __launch_bounds__(64) rx_handoff_signal(unsigned* word, unsigned seq)
-{
-    if (threadIdx.x == 0) __hip_atomic_store(word, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.gcnt)
+    {
+        // arrival: every store of this wave (the workgroup) has completed, then one add per back-end
+        // group its channels belong to (at most two: cpw need not divide 64)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if ((threadIdx.x & (FRONT_WAVE - 1)) == 0)
+        {
+            const int c0 = blockIdx.x * a.cpw;
+            const int c1 = (c0 + a.cpw < a.C ? c0 + a.cpw : a.C) - 1;
+            __hip_atomic_fetch_add(a.gcnt + c0 / BACK_CH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c1 / BACK_CH != c0 / BACK_CH)
+                __hip_atomic_fetch_add(a.gcnt + c1 / BACK_CH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -646,16 +667,29 @@ struct BackArgs
     int mchf;            // the mcHF board's output stage in line_out4 (plan.single_channel)
     float* mchf_u;       // mcHF, wave-pipeline back ends: [C][N] scratch for biquad_2's output, which
                          // rx_line_out_mchf finishes (null: line_out4 runs the whole stage)
-    // pipelined device hand-off (uhsdr_rx_set_pipelined 2): the launch reads adec once *dwait has
-    // reached dtarget (the call's sequence number, published by rx_handoff_signal after its
-    // rx_front; wrap-safe compare), by sc1 loads; null: adec is complete at launch (a stream event
-    // ordered it).  The poll is bounded by spin_max polls; a give-up stores 1 to *fail (the handle's
-    // host-mapped failure word: the host reports UHSDR_TIMEOUT from it) and poisons the launch
-    // (NaN inputs for every call, so its audio is NaN and its codec frames INT32_MIN)
+    // pipelined device hand-off (uhsdr_rx_set_pipelined 2): the launch reads adec once the arrival
+    // counter of its group, dwait[group] (FrontArgs::gcnt of the call's buffer), has reached
+    // dtarget x the front waves of the group (dtarget = front launches into that buffer since reset;
+    // wrap-safe compare), by sc1 loads; null: adec is complete at launch (a stream event ordered it).
+    // The poll is bounded by spin_max polls; a give-up stores 1 to *fail (the handle's host-mapped
+    // failure word: the host reports UHSDR_TIMEOUT from it) and poisons the launch (NaN inputs and
+    // NaN audio for every frame).  fcpw: the front's channels per wave.
     const unsigned* dwait;
     unsigned dtarget;
+    int fcpw;
     unsigned spin_max;
     unsigned* fail;
+    // skewed pipeline (BackSched, rx_back with the device hand-off): adec_next = the next call's
+    // hand-off buffer, read once its counters dwait_next[group] have reached dnext x the group's
+    // front waves (a peek, never a wait; null: no running ahead); skew[group] = the group's pipeline
+    // ends skewed; bnd = each role's pending input sub-call ([6 NDC + 2 BLK][C]: AGC role pre / rmax
+    // / fb / hb, audio role agc / volts, aa mid, output aa)
+    const float* adec_next;
+    const unsigned* dwait_next;
+    unsigned dnext;
+    int* skew;
+    float* bnd;
+    int bnd_mid;         // bnd's field of the aa role's pending input (6 NDC); the output role's follows it
 };
 
 // softdds_addSingleToneToTwobuffers (softdds.c:142-152): the tone of launch frame n
@@ -690,7 +724,6 @@ __device__ __forceinline__ int to_dma(float f)
     return (int)((unsigned)v << 16);
 }
 
-#define BACK_CH 64
 // rx_back_fused: waves per SIMD the register allocation targets (2: 256 VGPRs, no scratch; 3
 // spills to scratch and measured 0.265 vs 0.217 ms at 1M x 64)
 #ifndef UHSDR_FUSED_WAVES
@@ -726,6 +759,7 @@ struct BackLds
     float* aa;    // [2][BLK][64]  aa -> output
     float* prep;  // [3][2][NDC][64]  pre -> agc: window maximum, fast / hang averages
     unsigned* poison;  // [1]  pre -> output: the launch's device hand-off gave up (DM_NONE only)
+    unsigned* ext;     // [1]  pre -> every role: the launch runs ahead into the next call (BackSched)
 };
 
 // floats of the hand-off buffers (host: back_lds)
@@ -742,6 +776,7 @@ __device__ __forceinline__ BackLds back_lds_carve(float* smem)
     l.dem = l.pre + 2 * NDC * BACK_CH;
     l.prep = l.dem + 2 * NDC * BACK_CH;
     l.poison = (unsigned*)(l.prep + 3 * 2 * NDC * BACK_CH);
+    l.ext = l.poison + 1;
     return l;
 }
 
@@ -781,10 +816,18 @@ constexpr unsigned DFLAG_SPIN_MAX = 1u << 24;
 // handle's host-mapped failure word (system scope: the host reads it without a synchronisation)
 // and its launch is poisoned (NaN inputs in InStage::fetch, NaN audio from the output role for every
 // frame), so the give-up can never pass for output
+// front waves of group g (FrontArgs::gcnt's arrivals per front launch): cpw need not divide 64
+__device__ __forceinline__ unsigned front_waves_of(const BackArgs& a, int g)
+{
+    const int c0 = g * BACK_CH, c1 = (c0 + BACK_CH < a.C ? c0 + BACK_CH : a.C) - 1;
+    return (unsigned)(c1 / a.fcpw - c0 / a.fcpw + 1);
+}
 __device__ __forceinline__ void dflag_wait(const BackArgs& a, bool& gave_up)
 {
-    unsigned v = __hip_atomic_load(a.dwait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (unsigned spins = 0; (int)(v - a.dtarget) < 0 && !gave_up; ++spins)
+    const int g = blockIdx.x;
+    const unsigned want = a.dtarget * front_waves_of(a, g);
+    unsigned v = __hip_atomic_load(a.dwait + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned spins = 0; (int)(v - want) < 0 && !gave_up; ++spins)
     {
         if (spins >= a.spin_max)
         {
@@ -792,7 +835,7 @@ __device__ __forceinline__ void dflag_wait(const BackArgs& a, bool& gave_up)
             gave_up = true;
         }
         __builtin_amdgcn_s_sleep(2);
-        v = __hip_atomic_load(a.dwait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = __hip_atomic_load(a.dwait + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
 }
@@ -806,6 +849,7 @@ struct InStage
     float xnext[NDC];
     const float* lds;
     bool gave_up = false;                                // DW: this launch's poll gave up
+    int lim = -1;                                        // prefetch bound (sub-calls); -1: the launch's calls
 
     __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
     {
@@ -820,12 +864,15 @@ struct InStage
         }
         if (DW && a.dwait)
         {
-            // device hand-off: once per launch, wait until the call's rx_front has completed
-            // (rx_handoff_signal); then sc1 loads (this XCD's L2 may hold the buffer's previous
-            // contents: the launch may have started before the front finished).  After a give-up
+            // device hand-off: once per launch, wait until every front wave of the group has arrived
+            // (FrontArgs::gcnt); then sc1 loads (the front's write-through stores may come from
+            // another XCD while this launch runs).  After a give-up
             // every input of the launch is NaN (the failure contract of uhsdr_rx_set_pipelined)
+            // (sub-calls past the launch's own: the next call's buffer, BackSched's running ahead,
+            // read only after the pre role's peek found it published)
             if (call == 0) dflag_wait(a, gave_up);
-            const float* src = a.adec + (size_t)l.cl * a.Nd + call * NDC;
+            const float* src = call < l.calls ? a.adec + (size_t)l.cl * a.Nd + call * NDC
+                                              : a.adec_next + (size_t)l.cl * a.Nd + (call - l.calls) * NDC;
 #pragma unroll
             for (int m = 0; m < NDC; ++m)
             {
@@ -849,7 +896,7 @@ struct InStage
     {
 #pragma unroll
         for (int m = 0; m < NDC; ++m) xin[m] = xnext[m];
-        if (call + 1 < l.calls) fetch(a, l, call + 1);
+        if (call + 1 < (lim < 0 ? l.calls : lim)) fetch(a, l, call + 1);
     }
 };
 
@@ -913,6 +960,7 @@ struct AgcStage
     float rnext[NCH][NDC];                               // ring slot of the next call
     float old[NCH][NDC], sfx[NDC], wmax, pmax;           // this call's ring slot, suffix maxima
     float* ring_out[NCH];
+    int lim = -1;                                        // ring prefetch bound (sub-calls); -1: the launch's calls
 
     __device__ __forceinline__ static float* ring_of(const BackArgs& a, int ch) { return ch ? a.s.ring1 : a.s.ring; }
 
@@ -974,7 +1022,7 @@ struct AgcStage
         for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
             for (int m = 0; m < NDC; ++m) old[ch][m] = rnext[ch][m];
-        if (call + 1 < l.calls) fetch(a, l, call + 1);
+        if (call + 1 < (lim < 0 ? l.calls : lim)) fetch(a, l, call + 1);
         sfx[NDC - 1] = absn([&](int ch) { return old[ch][NDC - 1]; });
 #pragma unroll
         for (int m = NDC - 2; m >= 0; --m) sfx[m] = fmaxf(sfx[m + 1], absn([&](int ch) { return old[ch][m]; }));
@@ -1674,12 +1722,52 @@ extern "C" int uhsdr_trace_read(void* out)
 #else
 #define TRACE_MARK(k) do { } while (0)
 #endif
+// Skewed pipeline (the device hand-off's back end, DM_NONE).  A launch of n
+// 32-frame calls used to take n + 4 lockstep steps: 4 of them pipeline fill (the later roles idle)
+// and drain (the earlier roles idle).  Sub-calls are numbered g relative to the launch's first; role
+// r at step `it` works on g = it - r + gofs.  When the next call's rx_front has already published
+// (the pre role peeks the sequence word; it never waits for it), roles 0 .. 3 run ahead into the
+// next call's first 4 - r sub-calls instead of idling (`ext`: role r's range ends at n + 4 - r
+// instead of n), every role stores its state as usual, and each role r >= 1 writes the one sub-call
+// of input it has not consumed (its LDS hand-off slot) to `bnd` in HBM.  The group's skew word
+// records it, and the next launch starts skewed (`pin`: gofs = 4, n steps, no fill): role r loads
+// its pending input from `bnd` and continues at g = 4 - r.  Each role still runs its recursion over
+// the same samples in the same order, so outputs stay bit-identical; the output role (r = 4) always
+// covers exactly the launch's own n sub-calls.  A launch that finds the next call unpublished drains
+// as before and the next one fills.
+constexpr int BACK_SKEW = 4;            // back_roles(DM_NONE) - 1
+struct BackSched
+{
+    int steps, gofs;
+    bool pin;       // this launch starts skewed (the previous one ran ahead into its call)
+    bool may_ext;   // it may run ahead into the next call (device hand-off, a.adec_next)
+    template <int DM>
+    __device__ __forceinline__ static BackSched make(const BackArgs& a, const BackLane& l)
+    {
+        BackSched s;
+        s.pin = false;
+        s.may_ext = false;
+        if constexpr (DM == DM_NONE)
+        {
+            s.pin = a.skew && __builtin_amdgcn_readfirstlane(a.skew[blockIdx.x]) != 0;
+            s.may_ext = a.adec_next != nullptr;
+        }
+        s.gofs = s.pin ? BACK_SKEW : 0;
+        s.steps = l.calls + (s.pin ? 0 : back_roles(DM) - 1);
+        return s;
+    }
+};
+// role ST's range of sub-calls is [.., glim): l.calls, or with `ext` l.calls + BACK_SKEW - ST -- roles
+// ST >= 1 learn `ext` from the pre role's LDS word (written in the step that made the decision, at
+// g = n - 1 of role 0, a step barrier before any other role reaches g = n)
 #define BACK_ROLE_LOOP(ST)                                                                     \
-    for (int it = 0; it < l.calls + back_roles(DM) - 1; ++it)                                  \
+    for (int it = 0; it < sch.steps; ++it)                                                     \
     {                                                                                          \
-        const int call = it - (ST);                                                            \
+        const int call = it - (ST) + sch.gofs;                                                 \
+        if ((ST) > 0 && sch.may_ext && call == l.calls)                                        \
+            glim = __builtin_amdgcn_readfirstlane(*lds.ext) ? l.calls + BACK_SKEW - (ST) : l.calls; \
         TRACE_MARK(0);                                                                         \
-        if (call >= 0 && call < l.calls)                                                       \
+        if (call >= 0 && call < glim)                                                          \
         {
 #define BACK_ROLE_END                                                                          \
         }                                                                                      \
@@ -1694,6 +1782,8 @@ __device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     constexpr bool LEV = DM != DM_SAM;                   // DM_SAM: the leveler runs in the pre role
+    const BackSched sch = BackSched::make<DM>(a, l);
+    int glim = l.calls;
     DemodStage<L, DM, LEV> s;
     s.load(a, l);
     s.fetch(a, l, 0);
@@ -1711,6 +1801,27 @@ __device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
     s.store(a, l);
 }
 
+// BackSched's pending input sub-call of a role: `rows` rows of its LDS hand-off slot ([m][64]) to and
+// from bnd's fields f0 .. f0 + rows - 1 ([field][C], lane-coalesced)
+template <int ROWS>
+__device__ __forceinline__ void bnd_load(const BackArgs& a, const BackLane& l, int f0, float* slot)
+{
+#pragma unroll
+    for (int m = 0; m < ROWS; ++m) slot[m * BACK_CH + l.lane] = a.bnd[(size_t)(f0 + m) * l.C + l.cl];
+}
+template <int ROWS>
+__device__ __forceinline__ void bnd_store(const BackArgs& a, const BackLane& l, int f0, const float* slot)
+{
+    if (!l.live) return;
+#pragma unroll
+    for (int m = 0; m < ROWS; ++m) a.bnd[(size_t)(f0 + m) * l.C + l.c] = slot[m * BACK_CH + l.lane];
+}
+// the launch ran ahead (the pre role's word; BackSched): read after the loop's last barrier
+__device__ __forceinline__ bool back_ext(const BackSched& sch, const BackLds& lds)
+{
+    return sch.may_ext && __builtin_amdgcn_readfirstlane(*lds.ext) != 0;
+}
+
 // the AGC's ring side (AgcStage::prep) runs in the pre role, its recursion in the AGC role and
 // its gain in the audio role: SSB / CW / DIGI with the AGC on and no DC removal
 __device__ __forceinline__ bool back_agc_prep_in_pre(int dm, const uhsdr_agc_plan& A)
@@ -1725,28 +1836,58 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
+    const BackSched sch = BackSched::make<DM>(a, l);
+    int glim = l.calls;
     InStage<L, false, true> in;
     LatticeStage<PRE> s;
     s.load(l, P->pre_k, P->pre_v, a.s.pre);
+    const uhsdr_agc_plan A = P->agc;
+    const bool prep = back_agc_prep_in_pre(DM, A);
+    AgcStage<L, W> ag;
+    // BackSched: the first sub-call of this role, and whether it runs ahead into the next call -- a
+    // peek of the sequence word (never a wait), refreshed at g = n - 2, decided at g = n - 1 (or at
+    // once when nothing of the launch's own call is left to this role)
+    const int g0 = sch.gofs;
+    unsigned seen = 0;
+    bool ext = false;
+    auto peek = [&]() {
+        seen = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(a.dwait_next + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    };
+    auto decide = [&]() {
+        ext = (int)(seen - a.dnext * front_waves_of(a, blockIdx.x)) >= 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // the next call's loads stay below
+        glim = ext ? l.calls + BACK_SKEW : l.calls;
+        in.lim = glim;
+        if (l.lane == 0) *lds.ext = ext ? 1u : 0u;
+    };
+    if (sch.may_ext)
+    {
+        ag.lim = l.calls + BACK_SKEW;                // the ring slots do not depend on the front
+        peek();
+        if (g0 >= l.calls) decide();
+    }
     if (!DM)
     {
-        in.fetch(a, l, 0);
+        if (g0 < glim) in.fetch(a, l, g0);
         // the failure contract: a give-up (InStage's poll, call 0) poisons the whole launch's output,
         // including the frames the AGC's look-ahead delay still takes from the previous launch's
         // samples -- the output role reads this after the step-0 barrier
         if (l.lane == 0) *lds.poison = in.gave_up ? 1u : 0u;
     }
-    const uhsdr_agc_plan A = P->agc;
-    const bool prep = back_agc_prep_in_pre(DM, A);
-    AgcStage<L, W> ag;
     if (prep)
     {
         ag.load(a, l, A);
-        ag.fetch(a, l, 0);
+        ag.fetch(a, l, g0);
     }
     FadeStage fl;
     if (DM == DM_SAM) fl.load(a, l);
     BACK_ROLE_LOOP(DM ? 1 : 0)
+        if (sch.may_ext)
+        {
+            if (call == l.calls - 2) peek();
+            if (call == l.calls - 1) decide();
+        }
         float xin[NDC];
         if (DM)
         {
@@ -1796,6 +1937,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
     s.store(l, a.s.pre);
     if (DM == DM_SAM) fl.store(a, l);
     if (prep) ag.store(a, l, { true, false });
+    if (DM == DM_NONE && a.skew && l.lane == 0) a.skew[blockIdx.x] = ext ? 1 : 0;   // the next launch's `pin`
 }
 
 template <int L, int W, int DM>
@@ -1805,10 +1947,23 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
     constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     const uhsdr_agc_plan A = P->agc;
+    const BackSched sch = BackSched::make<DM>(a, l);
+    int glim = l.calls;
     AgcStage<L, W> s;
     s.load(a, l, A);
     const bool prep = back_agc_prep_in_pre(DM, A);
-    if (!prep) s.fetch(a, l, 0);
+    const int g0 = sch.gofs - 1;                      // BackSched: this role's first sub-call (if >= 0)
+    if (sch.may_ext) s.lim = l.calls + BACK_SKEW - 1;
+    if (!prep) s.fetch(a, l, g0 > 0 ? g0 : 0);
+    if (sch.pin)
+    {
+        // the pre role's output for g0, left by the previous launch
+        const int o = (g0 & 1) * NDC * BACK_CH;
+        bnd_load<NDC>(a, l, 0, lds.pre + o);
+        bnd_load<NDC>(a, l, NDC, lds.prep + o);
+        bnd_load<NDC>(a, l, 2 * NDC, lds.prep + 2 * NDC * BACK_CH + o);
+        bnd_load<NDC>(a, l, 3 * NDC, lds.prep + 4 * NDC * BACK_CH + o);
+    }
     BACK_ROLE_LOOP(DM ? 2 : 1)
         const float* pi = lds.pre + (call & 1) * NDC * BACK_CH + l.lane;
         float* ao = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
@@ -1860,6 +2015,14 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
         }
     BACK_ROLE_END
     s.store(a, l, { !prep, true }, !DM);
+    if (back_ext(sch, lds))
+    {
+        const int o = ((l.calls + BACK_SKEW - 1) & 1) * NDC * BACK_CH;
+        bnd_store<NDC>(a, l, 0, lds.pre + o);
+        bnd_store<NDC>(a, l, NDC, lds.prep + o);
+        bnd_store<NDC>(a, l, 2 * NDC, lds.prep + 2 * NDC * BACK_CH + o);
+        bnd_store<NDC>(a, l, 3 * NDC, lds.prep + 4 * NDC * BACK_CH + o);
+    }
 }
 
 template <int L, int PH, int W, int DM>
@@ -1867,6 +2030,8 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
     constexpr int NDC = BLK / L;
+    const BackSched sch = BackSched::make<DM>(a, l);
+    int glim = l.calls;
     AudioStage<L, PH, DM> s;
     s.load(a, l);
     const uhsdr_agc_plan A = a.plan->agc;
@@ -1874,6 +2039,13 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
     // DM: the AGC's DC removal (audio_agc.c:575-593) runs here after the gain, with its state
     float wold = DM ? a.s.agc[5 * l.C + l.cl] : 0.0f;
     const bool dc = DM && agc_on && A.remove_dc;
+    if (sch.pin)
+    {
+        // the AGC role's output (delayed samples, volts) for this role's first sub-call
+        const int o = ((sch.gofs - 2) & 1) * NDC * BACK_CH;
+        bnd_load<NDC>(a, l, 4 * NDC, lds.agc + o);
+        bnd_load<NDC>(a, l, 5 * NDC, lds.dem + o);
+    }
     BACK_ROLE_LOOP(DM ? 3 : 2)
         const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
         float* mo = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
@@ -1912,6 +2084,12 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
     BACK_ROLE_END
     s.store(a, l);
     if (DM && l.live) a.s.agc[5 * l.C + l.c] = wold;
+    if (back_ext(sch, lds))
+    {
+        const int o = ((l.calls + BACK_SKEW - 2) & 1) * NDC * BACK_CH;
+        bnd_store<NDC>(a, l, 4 * NDC, lds.agc + o);
+        bnd_store<NDC>(a, l, 5 * NDC, lds.dem + o);
+    }
 }
 
 // anti-alias lattice at 48 ksps
@@ -1922,8 +2100,11 @@ __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     // (Measured and dropped: the scalar lattice with VGPR coefficients, full-rate VOP2 instead of
     // packed f32 with SGPR pairs, here and in the pre role: C2 0.0327 -> 0.0366 ms per step.)
+    const BackSched sch = BackSched::make<DM>(a, l);
+    int glim = l.calls;
     LatticeStage<AA> s;
     s.load(l, P->aa_k, P->aa_v, a.s.aa);
+    if (sch.pin) bnd_load<BLK>(a, l, a.bnd_mid, lds.mid + ((sch.gofs - 3) & 1) * BLK * BACK_CH);
     BACK_ROLE_LOOP(DM ? 4 : 3)
         const float* mi = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
         float* mo = lds.aa + (call & 1) * BLK * BACK_CH + l.lane;
@@ -1937,14 +2118,18 @@ __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
         for (int n = 0; n < BLK; ++n) mo[n * BACK_CH] = s.step(x[n], n);
     BACK_ROLE_END
     s.store(l, a.s.aa);
+    if (back_ext(sch, lds)) bnd_store<BLK>(a, l, a.bnd_mid, lds.mid + ((l.calls + BACK_SKEW - 3) & 1) * BLK * BACK_CH);
 }
 
 template <int DM>
 __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
+    const BackSched sch = BackSched::make<DM>(a, l);
+    int glim = l.calls;
     OutputStage s;
     s.load(a, l);
+    if (sch.pin) bnd_load<BLK>(a, l, a.bnd_mid + BLK, lds.aa + ((sch.gofs - 4) & 1) * BLK * BACK_CH);
     BACK_ROLE_LOOP(DM ? 5 : 4)
         const float* mi = lds.aa + (call & 1) * BLK * BACK_CH + l.lane;
         float y[BLK];
@@ -1954,8 +2139,10 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
         for (int n = 0; n < BLK; ++n) y[n] = s.step(y[n]);
         if constexpr (DM == DM_NONE)
         {
-            // the pre role's device hand-off gave up (its step-0 word): NaN audio for every frame
-            if (a.dwait && __builtin_amdgcn_readfirstlane(*lds.poison))
+            // the pre role's device hand-off gave up (its step-0 word): NaN audio for every frame.
+            // Only a launch that starts unskewed waits (BackSched); a skewed one has this role at
+            // work in step 0, before the word is written, so it must not read it
+            if (!sch.pin && a.dwait && __builtin_amdgcn_readfirstlane(*lds.poison))
             {
 #pragma unroll
                 for (int n = 0; n < BLK; ++n) y[n] = __builtin_nanf("");
@@ -1969,6 +2156,7 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
         }
     BACK_ROLE_END
     s.store(a, l);
+    if (back_ext(sch, lds)) bnd_store<BLK>(a, l, a.bnd_mid + BLK, lds.aa + ((l.calls + BACK_SKEW - 4) & 1) * BLK * BACK_CH);
 }
 #undef BACK_ROLE_LOOP
 #undef BACK_ROLE_END
@@ -2749,7 +2937,10 @@ constexpr int BACK_FUSED_MIN_CHANNELS = 131072;   // measured crossover (64-fram
 // launches (hipExtLaunchKernelGGL) a call costs the host 2 launches + 1 stream wait (+1 per
 // group) instead of 2 launches + 2 records + 2 waits: C2's host submission, 22-25 us per call,
 // was as long as the GPU's, and the GPU idled between calls (rocprofv3 kernel trace, r03).
-constexpr int PIPE_GROUP = 4;
+#ifndef UHSDR_PIPE_GROUP
+#define UHSDR_PIPE_GROUP 4
+#endif
+constexpr int PIPE_GROUP = UHSDR_PIPE_GROUP;
 constexpr int PIPE_BUFS = 2 * PIPE_GROUP;
 
 struct uhsdr_rx_s
@@ -2813,14 +3004,15 @@ struct uhsdr_rx_s
     volatile unsigned* fail_host;
     unsigned* fail_dev;
     unsigned spin_max;       // polls before a give-up (uhsdr_rx_set_handoff_bound; default 2^24)
-    // pipelined device hand-off (uhsdr_rx_set_pipelined 2): rx_back polls the call sequence number
-    // rx_handoff_signal publishes after each rx_front (dword, device memory) instead of waiting on
-    // a cross-stream event
+    // pipelined device hand-off (uhsdr_rx_set_pipelined 2): rx_back polls the arrival counters the
+    // front waves of its group bump (FrontArgs::gcnt) instead of waiting on a cross-stream event
     int dflag;
-    unsigned* dword;         // the published call sequence number
+    unsigned* gcnt;          // [PIPE_BUFS][groups] arrival counters, one row per hand-off buffer
+    unsigned fills[PIPE_BUFS];   // counted front launches into each buffer since reset
+    int* skew;               // BackSched: per group, the wave pipeline ended a launch skewed (arena)
+    float* bnd;              // BackSched: the roles' pending input sub-calls (arena)
     int dflag_grid;          // largest rx_back grid it is used for (half the CUs: the polling
                              // workgroups never crowd out the front they wait for)
-    unsigned dtotal;         // calls published by rx_handoff_signal since reset
     int back_attr;           // rx_back's LDS attribute raised for the reserved launch (1), failed (-1)
     int main_back;           // back-end state was last written on the handle's stream (a one-kernel
                              // schedule, a serial call, a reset): the next side-stream rx_back waits
@@ -3101,11 +3293,11 @@ extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
     HIPCHK(hipMemcpyAsync(h->osc, osc0, sizeof osc0, hipMemcpyHostToDevice, h->stream));
     // ts.twinpeaks_tested = TWINPEAKS_WAIT at boot (src/uhsdr_main.c:339); the statics start at 0
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->tp, UHSDR_TWINPEAKS_WAIT, (size_t)h->C, h->stream));
-    // the device hand-off's sequence word restarts with dtotal; a poll's give-up is cleared (the
+    // the device hand-off's arrival counters restart with fills; a poll's give-up is cleared (the
     // state it poisoned was zeroed above)
-    HIPCHK(hipMemsetAsync(h->dword, 0, sizeof(unsigned), h->stream));
+    HIPCHK(hipMemsetAsync(h->gcnt, 0, sizeof(unsigned) * PIPE_BUFS * (((size_t)h->C + BACK_CH - 1) / BACK_CH), h->stream));
     *h->fail_host = 0;
-    h->dtotal = 0;
+    memset(h->fills, 0, sizeof h->fills);
     h->main_back = 1;
     if (h->bs.cw)
     {
@@ -3194,13 +3386,19 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const bool cw = p.cw_enabled && p.decimation_rate == 4;
     const size_t o_cw = take(cw ? (size_t)5 * C : 0);
     const size_t o_mu = take(p.single_channel ? (size_t)C * N : 0);
+    // the wave pipeline's running ahead (BackSched): per group its skew word, per channel the roles'
+    // pending input sub-calls
+    const bool skewable = h->bv->dm == DM_NONE && !st && p.interp_L > 0;
+    const size_t bnd_rows = skewable ? (size_t)6 * (BLK / p.interp_L) + 2 * BLK : 0;
+    const size_t o_skew = take(skewable ? (size_t)(C + BACK_CH - 1) / BACK_CH : 0);
+    const size_t o_bnd = take(skewable ? bnd_rows * C : 0);
     h->arena_bytes = fl * sizeof(float);
     if (hipMalloc(&h->arena, h->arena_bytes) != hipSuccess ||
         hipMalloc((void**)&h->adec, sizeof(float) * (size_t)C * h->Nd) != hipSuccess ||
         hipMalloc((void**)&h->d_plan, sizeof(uhsdr_rx_plan)) != hipSuccess ||
         hipMalloc((void**)&h->d_taps2, sizeof(float) * 4 * TAPS2_MAX) != hipSuccess ||
         hipMalloc((void**)&h->d_lanemap, sizeof(uint16_t) * 4 * 64) != hipSuccess ||
-        hipMalloc((void**)&h->dword, 64) != hipSuccess ||
+        hipMalloc((void**)&h->gcnt, sizeof(unsigned) * PIPE_BUFS * (((size_t)C + BACK_CH - 1) / BACK_CH)) != hipSuccess ||
         hipHostMalloc((void**)&h->fail_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&h->fail_dev, (void*)h->fail_host, 0) != hipSuccess)
     {
@@ -3218,6 +3416,8 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->bs.sam = am ? A + o_sam : nullptr;
     h->bs.cw = cw ? A + o_cw : nullptr;
     h->mchf_u = p.single_channel ? A + o_mu : nullptr;
+    h->skew = skewable ? (int*)(A + o_skew) : nullptr;
+    h->bnd = skewable ? A + o_bnd : nullptr;
     h->bs.notch = h->nv ? A + o_notch : nullptr;
     h->bs.ring1 = st ? A + o_ring1 : nullptr;
     h->bs.pre1 = st ? A + o_pre1 : nullptr; h->bs.aa1 = st ? A + o_aa1 : nullptr;
@@ -3380,6 +3580,7 @@ static FrontArgs front_args(const uhsdr_rx_s* h, const int32_t* iq, int f0, floa
     fa.taps2a = h->d_taps2;
     fa.taps2b = h->d_taps2 + 2 * TAPS2_MAX;
     fa.comb = front_comb_of(h->plan);
+    fa.gcnt = nullptr;
     fa.fm_prev = h->bs.sam;                          // FM: fields 0, 1 of rx_fm's state
     return fa;
 }
@@ -3414,6 +3615,13 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     ba.dtarget = 0;
     ba.spin_max = h->spin_max;
     ba.fail = h->fail_dev;
+    ba.adec_next = nullptr;
+    ba.dwait_next = nullptr;
+    ba.dnext = 0;
+    ba.fcpw = 1;
+    ba.skew = h->skew;
+    ba.bnd = h->bnd;
+    ba.bnd_mid = h->bnd ? 6 * (BLK / h->plan.interp_L) : 0;   // (FM has no interpolator: interp_L 0)
     {
         // key beep: frames [0, beep_n1) of this launch while calls are left (uhsdr_rx_key_beep)
         const int calls = h->N / BLK;
@@ -3504,16 +3712,24 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         const bool side = side_mode(h);
         const bool fused = h->schedule == UHSDR_SCHEDULE_SPLIT_FUSED || h->plan.stereo;
         // device hand-off: rx_back (the wave pipeline, adec its only input from the front) polls
-        // the sequence number rx_handoff_signal publishes after the front instead of waiting on
-        // ev_front: no barrier packet on the side stream, whose back ends then run back to back
+        // the arrival counters its group's front waves bump (FrontArgs::gcnt) instead of waiting on
+        // ev_front: no barrier packet on the side stream, whose back ends then run back to back,
+        // and no signal kernel between the fronts (round 5's rx_handoff_signal: ~4.7 us of the
+        // handle stream per call)
         const int bgroups = (h->C + BACK_CH - 1) / BACK_CH;
         // (rx_fm measured slower with it: C4 FM 0.131-0.133 vs 0.115-0.117 ms, its 512 polling
         // workgroups beside the fronts; profiles/r05_fm_handoff_ab.txt)
         const bool dfl = side && h->dflag && !h->main_back && !fused && !h->nv && !h->fv->st &&
                          h->bv->dm == DM_NONE && bgroups <= h->dflag_grid;
+        unsigned* const gc = h->gcnt + (size_t)par * bgroups;
         for (int f0 = 0; f0 < h->N; f0 += h->Nf)
         {
-            const FrontArgs fa = front_args(h, iq, f0, adec, adec_q);
+            FrontArgs fa = front_args(h, iq, f0, adec, adec_q);
+            if (dfl)
+            {
+                fa.gcnt = gc;
+                h->fills[par] += 1;
+            }
             const auto fn = fma ? h->fv->fn_fma : h->fv->fn;
             const dim3 grid((h->C + cpw - 1) / cpw), block(FRONT_WAVE);
             // pipelined: the call's last front launch records ev_front as it completes
@@ -3523,12 +3739,6 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
                 hipLaunchKernelGGL(fn, grid, block, lds, h->stream, fa);
             HIPCHK(hipGetLastError());
             h->front_launches += 1;
-        }
-        if (dfl)
-        {
-            h->dtotal += 1;
-            hipLaunchKernelGGL(rx_handoff_signal, dim3(1), dim3(64), 0, h->stream, h->dword, h->dtotal);
-            HIPCHK(hipGetLastError());
         }
         time_mark(h, K_FRONT, 1);
 
@@ -3540,8 +3750,26 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         if (mc_pass) bk.mchf_u = h->mchf_u;
         if (dfl)
         {
-            bk.dwait = h->dword;
-            bk.dtarget = h->dtotal;
+            bk.dwait = gc;
+            bk.dtarget = h->fills[par];
+            bk.fcpw = cpw;
+#ifndef UHSDR_BACK_SKEW
+#define UHSDR_BACK_SKEW 1
+#endif
+            // BackSched: run ahead into the next call if it has arrived by then.  The next buffer
+            // of the rotation is filled next by the next call only (its later reuse waits for this
+            // launch: ev_back), and its counters move only with a device hand-off front -- whose
+            // call's back end is then this same kernel on this stream (a mode change in between
+            // joins the side stream first, so no later front starts before this launch ends).  Not
+            // with the CW decoder (its per-call outputs belong to the launch's own call) or calls of
+            // fewer than BACK_SKEW 32-frame blocks.
+            if (UHSDR_BACK_SKEW && h->skew && h->N / BLK >= BACK_SKEW && !h->bs.cw)
+            {
+                const int parn = (int)((pk + 1) % PIPE_BUFS);
+                bk.adec_next = parn ? h->adecp[parn - 1] : h->adec;
+                bk.dwait_next = h->gcnt + (size_t)parn * bgroups;
+                bk.dnext = h->fills[parn] + (unsigned)((h->N + h->Nf - 1) / h->Nf);
+            }
         }
         const hipStream_t bst = back_stream(h);
         if (side && !dfl) HIPCHK(hipStreamWaitEvent(bst, h->ev_front, 0));
@@ -3858,7 +4086,7 @@ extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
     if (h->d_plan) (void)hipFree(h->d_plan);
     if (h->d_taps2) (void)hipFree(h->d_taps2);
     if (h->d_lanemap) (void)hipFree(h->d_lanemap);
-    if (h->dword) (void)hipFree(h->dword);
+    if (h->gcnt) (void)hipFree(h->gcnt);
     if (h->fail_host) (void)hipHostFree((void*)h->fail_host);
     free(h);
     return UHSDR_OK;

@@ -22,14 +22,17 @@ def main():
     sam = len(sys.argv) > 3 and sys.argv[3] == "sam"          # C3's SAM P70 chain (demod role first)
     cfg = U.default_config(filter_path=70, dmod_mode=U.DEMOD_SAM) if sam else U.default_config()
     chain = U.RxChain(cfg, channels=Cn, frames=N, schedule=U.SCHEDULE_SPLIT_PIPE)
+    pipe = len(sys.argv) > 3 and sys.argv[3] == "device"      # the device hand-off: the last launch
+    if pipe:                                                   # starts skewed (BackSched) and drains
+        chain.set_pipelined(2)
     if sam:
         x = torch.from_numpy(synth.am_iq(np.arange(Cn), 0, N)).cuda()
     else:
         x = synth.ssb_iq_torch(0, Cn, 0, N, "cuda")
     audio = torch.empty((Cn, N), dtype=torch.float32, device="cuda")
-    for _ in range(5):
+    for _ in range(30 if pipe else 5):
         chain.process(x, audio)
-    torch.cuda.synchronize()
+    chain.synchronize()
     lib = U.load()
     buf = np.zeros((64, 8, 40, 3), np.uint64)
     lib.uhsdr_trace_read.argtypes = [C.c_void_p]
@@ -37,6 +40,9 @@ def main():
     calls = N // 32
     roles = 6 if sam else 5
     its = calls + roles - 1
+    if pipe:
+        its = calls                                            # a skewed launch: n steps, no fill
+    ent = buf[:, :roles, 39, :2].astype(np.int64)
     t = buf[:, :roles, :its, :].astype(np.int64)
     t0 = t[:, :, 0, 0].min(axis=1)[:, None, None]
     work = (t[:, :, :, 1] - t[:, :, :, 0])
@@ -48,6 +54,12 @@ def main():
         print(f"step {it:2d}: {row}")
     total = int(np.median(t[:, 0, its - 1, 2] - t[:, 0, 0, 0]))
     print(f"total cycles (median WG): {total}")
+    e0 = ent[:, :, 0].min(axis=1)
+    print("entry -> first step start, per role (median cycles):",
+          [int(np.median(t[:, r, 0, 0] - e0)) for r in range(roles)])
+    print("last barrier -> exit, per role (median cycles):",
+          [int(np.median(ent[:, r, 1] - t[:, r, its - 1, 2])) for r in range(roles)])
+    print("entry -> last exit (median WG):", int(np.median(ent[:, :, 1].max(axis=1) - e0)))
 
 
 if __name__ == "__main__":

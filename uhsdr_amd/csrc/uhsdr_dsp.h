@@ -672,6 +672,62 @@ __device__ __forceinline__ float lattice_step_pk(float x, float (&g)[S > 0 ? S :
     }
 }
 
+// Two consecutive samples x0 (even position) and x1 of lattice_step_pk, with the output (ladder)
+// sums of both on packed f32: each sample's recursion runs as in lattice_step_pk, its ladder
+// products q_0 .. q_S = {gn_i v_i}, f v_S are kept, and acc = ((0 + q_0) + q_1) + ... runs for both
+// samples at once (v_pk_add_f32), element-wise the reference's order.  The ladder does not feed
+// the recursion, so pairing two samples' sums only removes S + 1 adds per pair from the issue of a
+// latency-bound single wave (the anti-alias role of the C2 back end, round 6).
+template <int S>
+__device__ __forceinline__ void lattice_step2_pk(float x0, float x1, float (&g)[S > 0 ? S : 1], const float* k,
+                                                 const float* v, float& y0, float& y1)
+{
+    static_assert(S >= 3, "packed form");
+    float q[2][S + 1];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+    {
+        float gn[S];
+        float f = h ? x1 : x0;
+        int i = 0;
+        if (h)
+        {
+            f = f - (k[0] * g[0]);
+            gn[0] = (f * k[0]) + g[0];
+            q[h][0] = gn[0] * v[0];
+            i = 1;
+        }
+#pragma unroll
+        for (; i + 1 < S; i += 2)
+        {
+            const v2f gp = v2f{ g[i], g[i + 1] }, kp = v2f{ k[i], k[i + 1] };
+            const v2f kg = kp * gp;
+            const float f0 = f - kg.x;
+            const float f1 = f0 - kg.y;
+            const v2f gnp = (v2f{ f0, f1 } * kp) + gp;
+            const v2f qp = gnp * v2f{ v[i], v[i + 1] };
+            gn[i] = gnp.x; gn[i + 1] = gnp.y;
+            q[h][i] = qp.x; q[h][i + 1] = qp.y;
+            f = f1;
+        }
+        if (i < S)
+        {
+            f = f - (k[i] * g[i]);
+            gn[i] = (f * k[i]) + g[i];
+            q[h][i] = gn[i] * v[i];
+        }
+        q[h][S] = f * v[S];
+#pragma unroll
+        for (int j = 0; j + 1 < S; ++j) g[j] = gn[j + 1];
+        g[S - 1] = f;
+    }
+    v2f acc = v2f{ 0.0f, 0.0f };
+#pragma unroll
+    for (int j = 0; j <= S; ++j) acc = acc + v2f{ q[0][j], q[1][j] };
+    y0 = acc.x;
+    y1 = acc.y;
+}
+
 // arm_biquad_cascade_df1_f32 (.../arm_biquad_cascade_df1_f32.c:349-418), one stage
 __device__ __forceinline__ float biquad_step(float x, float& x1, float& x2, float& y1, float& y2, const float* c)
 {

@@ -39,6 +39,10 @@
 
 // channels per back-end workgroup (lane == channel): the unit of the device hand-off's arrival counters
 #define BACK_CH 64
+// arrival counters one 128-byte line apart: the front's 32 adds per group then queue on their own
+// line (the atomics of a line serialise at ~12 ns each, MI355X_MICROARCH.md fanin; 64 counters
+// packed in two lines made every C2 front wait for ~2048 of them)
+constexpr int CNT_PITCH = 32;
 
 struct FrontArgs
 {
@@ -600,9 +604,9 @@ __global__ void __launch_bounds__(FRONT_WAVE) rx_front(FrontArgs a)
         {
             const int c0 = blockIdx.x * a.cpw;
             const int c1 = (c0 + a.cpw < a.C ? c0 + a.cpw : a.C) - 1;
-            __hip_atomic_fetch_add(a.gcnt + c0 / BACK_CH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(a.gcnt + (c0 / BACK_CH) * CNT_PITCH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (c1 / BACK_CH != c0 / BACK_CH)
-                __hip_atomic_fetch_add(a.gcnt + c1 / BACK_CH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(a.gcnt + (c1 / BACK_CH) * CNT_PITCH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -668,7 +672,7 @@ struct BackArgs
     float* mchf_u;       // mcHF, wave-pipeline back ends: [C][N] scratch for biquad_2's output, which
                          // rx_line_out_mchf finishes (null: line_out4 runs the whole stage)
     // pipelined device hand-off (uhsdr_rx_set_pipelined 2): the launch reads adec once the arrival
-    // counter of its group, dwait[group] (FrontArgs::gcnt of the call's buffer), has reached
+    // counter of its group, dwait[group * CNT_PITCH] (FrontArgs::gcnt of the call's buffer), has reached
     // dtarget x the front waves of the group (dtarget = front launches into that buffer since reset;
     // wrap-safe compare), by sc1 loads; null: adec is complete at launch (a stream event ordered it).
     // The poll is bounded by spin_max polls; a give-up stores 1 to *fail (the handle's host-mapped
@@ -826,7 +830,7 @@ __device__ __forceinline__ void dflag_wait(const BackArgs& a, bool& gave_up)
 {
     const int g = blockIdx.x;
     const unsigned want = a.dtarget * front_waves_of(a, g);
-    unsigned v = __hip_atomic_load(a.dwait + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned v = __hip_atomic_load(a.dwait + g * CNT_PITCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (unsigned spins = 0; (int)(v - want) < 0 && !gave_up; ++spins)
     {
         if (spins >= a.spin_max)
@@ -835,7 +839,7 @@ __device__ __forceinline__ void dflag_wait(const BackArgs& a, bool& gave_up)
             gave_up = true;
         }
         __builtin_amdgcn_s_sleep(2);
-        v = __hip_atomic_load(a.dwait + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = __hip_atomic_load(a.dwait + g * CNT_PITCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
 }
@@ -930,6 +934,17 @@ struct LatticeStage
         if constexpr (S > 0 && PK) return (par & 1) ? lattice_step_pk<S, 1>(x, g, k, v) : lattice_step_pk<S, 0>(x, g, k, v);
         if constexpr (S > 0 && !PK) return lattice_step<S>(x, g, k, v);
         return x;
+    }
+
+    // two consecutive samples from an even position: the ladder sums paired (lattice_step2_pk)
+    __device__ __forceinline__ void step2(float x0, float x1, float& y0, float& y1)
+    {
+        if constexpr (S >= 3 && PK) lattice_step2_pk<S>(x0, x1, g, k, v, y0, y1);
+        else
+        {
+            y0 = step(x0, 0);
+            y1 = step(x1, 1);
+        }
     }
 
     __device__ __forceinline__ void store(const BackLane& l, float* st)
@@ -1741,20 +1756,54 @@ struct BackSched
     int steps, gofs;
     bool pin;       // this launch starts skewed (the previous one ran ahead into its call)
     bool may_ext;   // it may run ahead into the next call (device hand-off, a.adec_next)
+    // the group's skew word is loaded first (word) and consumed after the role's state loads and
+    // its speculative `bnd` loads (make), so one memory latency covers all of them at launch start
+    // (consumed at once it cost a second round trip: ~1.5 k cycles of entry, UHSDR_TRACE r06)
     template <int DM>
-    __device__ __forceinline__ static BackSched make(const BackArgs& a, const BackLane& l)
+    __device__ __forceinline__ static int word(const BackArgs& a)
+    {
+        if constexpr (DM == DM_NONE) return a.skew ? a.skew[blockIdx.x] : 0;
+        else return 0;
+    }
+    template <int DM>
+    __device__ __forceinline__ static BackSched make(const BackArgs& a, const BackLane& l, int w)
     {
         BackSched s;
         s.pin = false;
         s.may_ext = false;
         if constexpr (DM == DM_NONE)
         {
-            s.pin = a.skew && __builtin_amdgcn_readfirstlane(a.skew[blockIdx.x]) != 0;
+            s.pin = __builtin_amdgcn_readfirstlane(w) != 0;
             s.may_ext = a.adec_next != nullptr;
         }
         s.gofs = s.pin ? BACK_SKEW : 0;
         s.steps = l.calls + (s.pin ? 0 : back_roles(DM) - 1);
         return s;
+    }
+};
+// BackSched's pending input sub-call of a role, loaded from `bnd` before the role knows whether the
+// launch starts skewed (unused otherwise); put() moves rows [R0, R0 + n) into an LDS hand-off slot
+template <int ROWS>
+struct BndRegs
+{
+    float v[ROWS];
+    template <int DM>
+    __device__ __forceinline__ void load(const BackArgs& a, const BackLane& l, int f0)
+    {
+        if constexpr (DM == DM_NONE)
+        {
+            if (a.bnd)
+            {
+#pragma unroll
+                for (int m = 0; m < ROWS; ++m) v[m] = a.bnd[(size_t)(f0 + m) * l.C + l.cl];
+            }
+        }
+    }
+    template <int R0, int NR>
+    __device__ __forceinline__ void put(const BackLane& l, float* slot) const
+    {
+#pragma unroll
+        for (int m = 0; m < NR; ++m) slot[m * BACK_CH + l.lane] = v[R0 + m];
     }
 };
 // role ST's range of sub-calls is [.., glim): l.calls, or with `ext` l.calls + BACK_SKEW - ST -- roles
@@ -1782,7 +1831,7 @@ __device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     constexpr bool LEV = DM != DM_SAM;                   // DM_SAM: the leveler runs in the pre role
-    const BackSched sch = BackSched::make<DM>(a, l);
+    const BackSched sch = BackSched::make<DM>(a, l, 0);
     int glim = l.calls;
     DemodStage<L, DM, LEV> s;
     s.load(a, l);
@@ -1801,14 +1850,8 @@ __device__ __forceinline__ void rx_back_demod(const BackArgs& a, BackLds lds)
     s.store(a, l);
 }
 
-// BackSched's pending input sub-call of a role: `rows` rows of its LDS hand-off slot ([m][64]) to and
-// from bnd's fields f0 .. f0 + rows - 1 ([field][C], lane-coalesced)
-template <int ROWS>
-__device__ __forceinline__ void bnd_load(const BackArgs& a, const BackLane& l, int f0, float* slot)
-{
-#pragma unroll
-    for (int m = 0; m < ROWS; ++m) slot[m * BACK_CH + l.lane] = a.bnd[(size_t)(f0 + m) * l.C + l.cl];
-}
+// BackSched's pending input sub-call of a role: ROWS rows of its LDS hand-off slot ([m][64]) to bnd's
+// fields f0 .. f0 + ROWS - 1 ([field][C], lane-coalesced; BndRegs loads them back)
 template <int ROWS>
 __device__ __forceinline__ void bnd_store(const BackArgs& a, const BackLane& l, int f0, const float* slot)
 {
@@ -1836,26 +1879,28 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
-    const BackSched sch = BackSched::make<DM>(a, l);
-    int glim = l.calls;
+    const int skw = BackSched::word<DM>(a);
     InStage<L, false, true> in;
     LatticeStage<PRE> s;
     s.load(l, P->pre_k, P->pre_v, a.s.pre);
     const uhsdr_agc_plan A = P->agc;
     const bool prep = back_agc_prep_in_pre(DM, A);
     AgcStage<L, W> ag;
+    if (prep) ag.load(a, l, A);
+    const BackSched sch = BackSched::make<DM>(a, l, skw);
+    int glim = l.calls;
     // BackSched: the first sub-call of this role, and whether it runs ahead into the next call -- a
-    // peek of the sequence word (never a wait), refreshed at g = n - 2, decided at g = n - 1 (or at
-    // once when nothing of the launch's own call is left to this role)
+    // peek of the next buffer's arrival counter (never a wait) issued at g = n - 3 and consumed two
+    // steps later, at g = n - 1, so its latency stays off the step (a load consumed at once cost
+    // ~1-2 us in the pipeline's lockstep); at once when the launch's range starts past those points
     const int g0 = sch.gofs;
-    unsigned seen = 0;
+    unsigned seen = 0;                                 // per lane until decide() (no wait at the peek)
     bool ext = false;
     auto peek = [&]() {
-        seen = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(a.dwait_next + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        seen = __hip_atomic_load(a.dwait_next + blockIdx.x * CNT_PITCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto decide = [&]() {
-        ext = (int)(seen - a.dnext * front_waves_of(a, blockIdx.x)) >= 0;
+        ext = (int)(__builtin_amdgcn_readfirstlane(seen) - a.dnext * front_waves_of(a, blockIdx.x)) >= 0;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // the next call's loads stay below
         glim = ext ? l.calls + BACK_SKEW : l.calls;
         in.lim = glim;
@@ -1864,7 +1909,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
     if (sch.may_ext)
     {
         ag.lim = l.calls + BACK_SKEW;                // the ring slots do not depend on the front
-        peek();
+        if (g0 > l.calls - 3) peek();
         if (g0 >= l.calls) decide();
     }
     if (!DM)
@@ -1875,17 +1920,13 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
         // samples -- the output role reads this after the step-0 barrier
         if (l.lane == 0) *lds.poison = in.gave_up ? 1u : 0u;
     }
-    if (prep)
-    {
-        ag.load(a, l, A);
-        ag.fetch(a, l, g0);
-    }
+    if (prep) ag.fetch(a, l, g0);
     FadeStage fl;
     if (DM == DM_SAM) fl.load(a, l);
     BACK_ROLE_LOOP(DM ? 1 : 0)
         if (sch.may_ext)
         {
-            if (call == l.calls - 2) peek();
+            if (call == l.calls - 3) peek();
             if (call == l.calls - 1) decide();
         }
         float xin[NDC];
@@ -1947,10 +1988,13 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
     constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     const uhsdr_agc_plan A = P->agc;
-    const BackSched sch = BackSched::make<DM>(a, l);
-    int glim = l.calls;
+    const int skw = BackSched::word<DM>(a);
     AgcStage<L, W> s;
     s.load(a, l, A);
+    BndRegs<4 * NDC> br;
+    br.template load<DM>(a, l, 0);
+    const BackSched sch = BackSched::make<DM>(a, l, skw);
+    int glim = l.calls;
     const bool prep = back_agc_prep_in_pre(DM, A);
     const int g0 = sch.gofs - 1;                      // BackSched: this role's first sub-call (if >= 0)
     if (sch.may_ext) s.lim = l.calls + BACK_SKEW - 1;
@@ -1959,10 +2003,10 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
     {
         // the pre role's output for g0, left by the previous launch
         const int o = (g0 & 1) * NDC * BACK_CH;
-        bnd_load<NDC>(a, l, 0, lds.pre + o);
-        bnd_load<NDC>(a, l, NDC, lds.prep + o);
-        bnd_load<NDC>(a, l, 2 * NDC, lds.prep + 2 * NDC * BACK_CH + o);
-        bnd_load<NDC>(a, l, 3 * NDC, lds.prep + 4 * NDC * BACK_CH + o);
+        br.template put<0, NDC>(l, lds.pre + o);
+        br.template put<NDC, NDC>(l, lds.prep + o);
+        br.template put<2 * NDC, NDC>(l, lds.prep + 2 * NDC * BACK_CH + o);
+        br.template put<3 * NDC, NDC>(l, lds.prep + 4 * NDC * BACK_CH + o);
     }
     BACK_ROLE_LOOP(DM ? 2 : 1)
         const float* pi = lds.pre + (call & 1) * NDC * BACK_CH + l.lane;
@@ -2030,8 +2074,7 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
     constexpr int NDC = BLK / L;
-    const BackSched sch = BackSched::make<DM>(a, l);
-    int glim = l.calls;
+    const int skw = BackSched::word<DM>(a);
     AudioStage<L, PH, DM> s;
     s.load(a, l);
     const uhsdr_agc_plan A = a.plan->agc;
@@ -2039,12 +2082,16 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
     // DM: the AGC's DC removal (audio_agc.c:575-593) runs here after the gain, with its state
     float wold = DM ? a.s.agc[5 * l.C + l.cl] : 0.0f;
     const bool dc = DM && agc_on && A.remove_dc;
+    BndRegs<2 * NDC> br;
+    br.template load<DM>(a, l, 4 * NDC);
+    const BackSched sch = BackSched::make<DM>(a, l, skw);
+    int glim = l.calls;
     if (sch.pin)
     {
         // the AGC role's output (delayed samples, volts) for this role's first sub-call
         const int o = ((sch.gofs - 2) & 1) * NDC * BACK_CH;
-        bnd_load<NDC>(a, l, 4 * NDC, lds.agc + o);
-        bnd_load<NDC>(a, l, 5 * NDC, lds.dem + o);
+        br.template put<0, NDC>(l, lds.agc + o);
+        br.template put<NDC, NDC>(l, lds.dem + o);
     }
     BACK_ROLE_LOOP(DM ? 3 : 2)
         const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
@@ -2100,11 +2147,14 @@ __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     // (Measured and dropped: the scalar lattice with VGPR coefficients, full-rate VOP2 instead of
     // packed f32 with SGPR pairs, here and in the pre role: C2 0.0327 -> 0.0366 ms per step.)
-    const BackSched sch = BackSched::make<DM>(a, l);
-    int glim = l.calls;
+    const int skw = BackSched::word<DM>(a);
     LatticeStage<AA> s;
     s.load(l, P->aa_k, P->aa_v, a.s.aa);
-    if (sch.pin) bnd_load<BLK>(a, l, a.bnd_mid, lds.mid + ((sch.gofs - 3) & 1) * BLK * BACK_CH);
+    BndRegs<BLK> br;
+    br.template load<DM>(a, l, a.bnd_mid);
+    const BackSched sch = BackSched::make<DM>(a, l, skw);
+    int glim = l.calls;
+    if (sch.pin) br.template put<0, BLK>(l, lds.mid + ((sch.gofs - 3) & 1) * BLK * BACK_CH);
     BACK_ROLE_LOOP(DM ? 4 : 3)
         const float* mi = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
         float* mo = lds.aa + (call & 1) * BLK * BACK_CH + l.lane;
@@ -2114,8 +2164,16 @@ __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
         float x[BLK];
 #pragma unroll
         for (int n = 0; n < BLK; ++n) x[n] = mi[n * BACK_CH];
+        // samples in pairs: the two ladder sums on packed f32 (4440 -> ~3900 cycles per step, the
+        // pipeline's critical role; UHSDR_TRACE r06)
 #pragma unroll
-        for (int n = 0; n < BLK; ++n) mo[n * BACK_CH] = s.step(x[n], n);
+        for (int n = 0; n < BLK; n += 2)
+        {
+            float y0, y1;
+            s.step2(x[n], x[n + 1], y0, y1);
+            mo[n * BACK_CH] = y0;
+            mo[(n + 1) * BACK_CH] = y1;
+        }
     BACK_ROLE_END
     s.store(l, a.s.aa);
     if (back_ext(sch, lds)) bnd_store<BLK>(a, l, a.bnd_mid, lds.mid + ((l.calls + BACK_SKEW - 3) & 1) * BLK * BACK_CH);
@@ -2125,11 +2183,14 @@ template <int DM>
 __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
-    const BackSched sch = BackSched::make<DM>(a, l);
-    int glim = l.calls;
+    const int skw = BackSched::word<DM>(a);
     OutputStage s;
     s.load(a, l);
-    if (sch.pin) bnd_load<BLK>(a, l, a.bnd_mid + BLK, lds.aa + ((sch.gofs - 4) & 1) * BLK * BACK_CH);
+    BndRegs<BLK> br;
+    br.template load<DM>(a, l, a.bnd_mid + BLK);
+    const BackSched sch = BackSched::make<DM>(a, l, skw);
+    int glim = l.calls;
+    if (sch.pin) br.template put<0, BLK>(l, lds.aa + ((sch.gofs - 4) & 1) * BLK * BACK_CH);
     BACK_ROLE_LOOP(DM ? 5 : 4)
         const float* mi = lds.aa + (call & 1) * BLK * BACK_CH + l.lane;
         float y[BLK];
@@ -2180,6 +2241,11 @@ __global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
     // AM / SAM: the demod role (the per-sample PLL recursion) is the pipeline's longest; the other
     // roles, sharing its SIMD, issue after it (still above a concurrent rx_front)
     if (UHSDR_ROLE_PRIO && DM && role >= 0) __builtin_amdgcn_s_setprio(2);
+#ifdef UHSDR_TRACE
+    // (tools/trace_back.py) the wave's entry and exit in slot 39
+    if ((threadIdx.x & (BACK_CH - 1)) == 0 && blockIdx.x < 64)
+        g_trace[blockIdx.x][threadIdx.x / BACK_CH][39][0] = __builtin_readcyclecounter();
+#endif
     if (role < 0)
         rx_back_demod<L, DM>(a, lds);
     else if (role == 0)
@@ -2192,6 +2258,10 @@ __global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
         rx_back_aa<AA, DM>(a, lds);
     else
         rx_back_output<DM>(a, lds);
+#ifdef UHSDR_TRACE
+    if ((threadIdx.x & (BACK_CH - 1)) == 0 && blockIdx.x < 64)
+        g_trace[blockIdx.x][threadIdx.x / BACK_CH][39][1] = __builtin_readcyclecounter();
+#endif
 }
 
 // Fused back end for large batches: one wave per 64 channels runs every stage per sample with
@@ -3007,7 +3077,7 @@ struct uhsdr_rx_s
     // pipelined device hand-off (uhsdr_rx_set_pipelined 2): rx_back polls the arrival counters the
     // front waves of its group bump (FrontArgs::gcnt) instead of waiting on a cross-stream event
     int dflag;
-    unsigned* gcnt;          // [PIPE_BUFS][groups] arrival counters, one row per hand-off buffer
+    unsigned* gcnt;          // [PIPE_BUFS][groups][CNT_PITCH] arrival counters, one row per hand-off buffer
     unsigned fills[PIPE_BUFS];   // counted front launches into each buffer since reset
     int* skew;               // BackSched: per group, the wave pipeline ended a launch skewed (arena)
     float* bnd;              // BackSched: the roles' pending input sub-calls (arena)
@@ -3295,7 +3365,7 @@ extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->tp, UHSDR_TWINPEAKS_WAIT, (size_t)h->C, h->stream));
     // the device hand-off's arrival counters restart with fills; a poll's give-up is cleared (the
     // state it poisoned was zeroed above)
-    HIPCHK(hipMemsetAsync(h->gcnt, 0, sizeof(unsigned) * PIPE_BUFS * (((size_t)h->C + BACK_CH - 1) / BACK_CH), h->stream));
+    HIPCHK(hipMemsetAsync(h->gcnt, 0, sizeof(unsigned) * CNT_PITCH * PIPE_BUFS * (((size_t)h->C + BACK_CH - 1) / BACK_CH), h->stream));
     *h->fail_host = 0;
     memset(h->fills, 0, sizeof h->fills);
     h->main_back = 1;
@@ -3398,7 +3468,7 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
         hipMalloc((void**)&h->d_plan, sizeof(uhsdr_rx_plan)) != hipSuccess ||
         hipMalloc((void**)&h->d_taps2, sizeof(float) * 4 * TAPS2_MAX) != hipSuccess ||
         hipMalloc((void**)&h->d_lanemap, sizeof(uint16_t) * 4 * 64) != hipSuccess ||
-        hipMalloc((void**)&h->gcnt, sizeof(unsigned) * PIPE_BUFS * (((size_t)C + BACK_CH - 1) / BACK_CH)) != hipSuccess ||
+        hipMalloc((void**)&h->gcnt, sizeof(unsigned) * CNT_PITCH * PIPE_BUFS * (((size_t)C + BACK_CH - 1) / BACK_CH)) != hipSuccess ||
         hipHostMalloc((void**)&h->fail_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&h->fail_dev, (void*)h->fail_host, 0) != hipSuccess)
     {
@@ -3721,7 +3791,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         // workgroups beside the fronts; profiles/r05_fm_handoff_ab.txt)
         const bool dfl = side && h->dflag && !h->main_back && !fused && !h->nv && !h->fv->st &&
                          h->bv->dm == DM_NONE && bgroups <= h->dflag_grid;
-        unsigned* const gc = h->gcnt + (size_t)par * bgroups;
+        unsigned* const gc = h->gcnt + (size_t)par * bgroups * CNT_PITCH;
         for (int f0 = 0; f0 < h->N; f0 += h->Nf)
         {
             FrontArgs fa = front_args(h, iq, f0, adec, adec_q);
@@ -3745,7 +3815,10 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         const BackArgs ba = back_args(h, adec, adec_q, audio, audio0, dst);
         // mcHF after the wave pipeline (rx_back): biquad_2's output to the scratch row, then
         // rx_line_out_mchf; the other back ends run the board's stage inline (line_out4)
-        const bool mc_pass = h->mchf_u && !fused && h->bv->dm != DM_FM;
+#ifndef UHSDR_MCHF_PASS
+#define UHSDR_MCHF_PASS 1
+#endif
+        const bool mc_pass = UHSDR_MCHF_PASS && h->mchf_u && !fused && h->bv->dm != DM_FM;
         BackArgs bk = ba;
         if (mc_pass) bk.mchf_u = h->mchf_u;
         if (dfl)
@@ -3767,7 +3840,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             {
                 const int parn = (int)((pk + 1) % PIPE_BUFS);
                 bk.adec_next = parn ? h->adecp[parn - 1] : h->adec;
-                bk.dwait_next = h->gcnt + (size_t)parn * bgroups;
+                bk.dwait_next = h->gcnt + (size_t)parn * bgroups * CNT_PITCH;
                 bk.dnext = h->fills[parn] + (unsigned)((h->N + h->Nf - 1) / h->Nf);
             }
         }

@@ -3775,6 +3775,9 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         const bool group_end = h->pipelined && pk % PIPE_GROUP == PIPE_GROUP - 1;
         float* adec = par ? h->adecp[par - 1] : h->adec;
         float* adec_q = par ? h->adec_qp[par - 1] : h->adec_q;
+        // (Measured and dropped in round 6, profiles/r06_c2_ab_group.txt: skipping this wait when a
+        // host query finds the event complete, and groups of 8 or 16 calls: no gain at 20 steps,
+        // 0.0229-0.0235 vs 0.0221 ms at 1000 steps for the larger rotations)
         if (side_mode(h) && pk % PIPE_GROUP == 0) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[grp], 0));
         time_mark(h, K_FRONT, 0);
         const int cpw = FRONT_WAVE / (h->Nf / h->fv->R);

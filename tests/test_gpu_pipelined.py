@@ -138,11 +138,10 @@ def test_pipelined_host_entry(cuda):
     assert_bitexact(np.concatenate([o[0] for o in outs], axis=1), ref_a1, "pipelined host entry")
 
 
-# mcHF in the pipelined mode: the group's last finishing pass
-# (rx_line_out_mchf) records the group event instead of the back end, and every call's back end
-# writes the single [C][N] scratch row and FM mute array that the finishing pass reads on the
-# side stream.  No synchronisation between calls; a key beep starts in the last call of group 0
-# and runs into group 1.
+# mcHF in the pipelined mode: the board's
+# output stage runs inline in every back end -- in the wave pipeline on its tail waves, one step
+# behind the output role -- with no finishing pass or scratch row since round 6.  No
+# synchronisation between calls; a key beep starts in the last call of group 0 and runs into group 1.
 MCHF_PIPE_CASES = [
     ("p48_usb", dict(filter_path=48, spkr_gain=24), synth.ssb_iq, 130, 256, 15),
     ("p70_sam", dict(filter_path=70, dmod_mode=U.DEMOD_SAM, spkr_gain=30), synth.am_iq, 97, 256, 17),

@@ -19,10 +19,14 @@ def main():
     from uhsdr_amd import synth
     Cn = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-    sam = len(sys.argv) > 3 and sys.argv[3] == "sam"          # C3's SAM P70 chain (demod role first)
-    cfg = U.default_config(filter_path=70, dmod_mode=U.DEMOD_SAM) if sam else U.default_config()
+    opts = sys.argv[3:]
+    sam = "sam" in opts                                        # C3's SAM P70 chain (demod role first)
+    mchf = "mchf" in opts                                      # the mcHF board's output stage
+    want_dst = "dst" in opts                                   # int32 codec frames too
+    cfg = (U.default_config(filter_path=70, dmod_mode=U.DEMOD_SAM) if sam else
+           U.default_config(board=U.BOARD_MCHF) if mchf else U.default_config())
     chain = U.RxChain(cfg, channels=Cn, frames=N, schedule=U.SCHEDULE_SPLIT_PIPE)
-    pipe = len(sys.argv) > 3 and sys.argv[3] == "device"      # the device hand-off: the last launch
+    pipe = "device" in opts                                   # the device hand-off: the last launch
     if pipe:                                                   # starts skewed (BackSched) and drains
         chain.set_pipelined(2)
     if sam:
@@ -30,16 +34,21 @@ def main():
     else:
         x = synth.ssb_iq_torch(0, Cn, 0, N, "cuda")
     audio = torch.empty((Cn, N), dtype=torch.float32, device="cuda")
+    audio0 = torch.empty((Cn, N), dtype=torch.float32, device="cuda")
+    dst = torch.empty((Cn, N, 2), dtype=torch.int32, device="cuda") if want_dst else None
     for _ in range(30 if pipe else 5):
-        chain.process(x, audio)
+        if mchf:
+            chain.process_stereo(x, audio, audio0, dst)
+        else:
+            chain.process(x, audio, dst)
     chain.synchronize()
     lib = U.load()
-    buf = np.zeros((64, 8, 40, 3), np.uint64)
+    buf = np.zeros((64, 10, 40, 3), np.uint64)
     lib.uhsdr_trace_read.argtypes = [C.c_void_p]
     assert lib.uhsdr_trace_read(buf.ctypes.data_as(C.c_void_p)) == 0
     calls = N // 32
-    roles = 6 if sam else 5
-    its = calls + roles - 1
+    roles = (6 if sam else 5) + 4                              # + the four tail waves
+    its = calls + roles - 5
     if pipe:
         its = calls                                            # a skewed launch: n steps, no fill
     ent = buf[:, :roles, 39, :2].astype(np.int64)
@@ -47,7 +56,7 @@ def main():
     t0 = t[:, :, 0, 0].min(axis=1)[:, None, None]
     work = (t[:, :, :, 1] - t[:, :, :, 0])
     wait = (t[:, :, :, 2] - t[:, :, :, 1])
-    names = (["demod"] if sam else []) + ["pre", "agc", "audio", "aa", "output"]
+    names = (["demod"] if sam else []) + ["pre", "agc", "audio", "aa", "output", "tail0", "tail1", "tail2", "tail3"]
     print(f"C={Cn} N={N}: per-step cycles (median over workgroups), work / barrier wait")
     for it in range(its):
         row = " ".join(f"{names[r]:>6} {int(np.median(work[:, r, it])):6d}/{int(np.median(wait[:, r, it])):6d}" for r in range(roles))

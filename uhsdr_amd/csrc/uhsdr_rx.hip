@@ -669,8 +669,6 @@ struct BackArgs
     uint32_t beep_acc;
     int tone_phase;      // FM subaudible tone detector: fm_data.gcount at launch start (mod 400)
     int mchf;            // the mcHF board's output stage in line_out4 (plan.single_channel)
-    float* mchf_u;       // mcHF, wave-pipeline back ends: [C][N] scratch for biquad_2's output, which
-                         // rx_line_out_mchf finishes (null: line_out4 runs the whole stage)
     // pipelined device hand-off (uhsdr_rx_set_pipelined 2): the launch reads adec once the arrival
     // counter of its group, dwait[group * CNT_PITCH] (FrontArgs::gcnt of the call's buffer), has reached
     // dtarget x the front waves of the group (dtarget = front launches into that buffer since reset;
@@ -764,10 +762,11 @@ struct BackLds
     float* prep;  // [3][2][NDC][64]  pre -> agc: window maximum, fast / hang averages
     unsigned* poison;  // [1]  pre -> output: the launch's device hand-off gave up (DM_NONE only)
     unsigned* ext;     // [1]  pre -> every role: the launch runs ahead into the next call (BackSched)
+    float* ys;         // [2][64][BLK + 1]  output -> tail: the output role's call, one row per channel
 };
 
 // floats of the hand-off buffers (host: back_lds)
-__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (6 * ndc + 2 * BLK) + 4; }
+__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (6 * ndc + 2 * BLK) + 4 + 2 * BACK_CH * (BLK + 1); }
 
 template <int NDC>
 __device__ __forceinline__ BackLds back_lds_carve(float* smem)
@@ -781,6 +780,7 @@ __device__ __forceinline__ BackLds back_lds_carve(float* smem)
     l.prep = l.dem + 2 * NDC * BACK_CH;
     l.poison = (unsigned*)(l.prep + 3 * 2 * NDC * BACK_CH);
     l.ext = l.poison + 1;
+    l.ys = (float*)(l.poison + 4);
     return l;
 }
 
@@ -1421,15 +1421,6 @@ __device__ __forceinline__ void line_out4(const BackArgs& a, size_t rb, unsigned
                                           const float (&u)[4], bool on = true)
 {
     const bool beep = a.beep_n1 > call * BLK && a.beep_n0 < (call + 1) * BLK;     // key beep in this call
-    if (a.mchf && a.mchf_u)
-    {
-        // the wave pipeline's output role is on the per-call critical path: it hands biquad_2's
-        // output to rx_line_out_mchf, which runs the stage over the whole batch in parallel (the
-        // inline stage's second int32 conversion and gains made C2-shaped mcHF calls 0.045 instead
-        // of 0.033 ms, profiles/r05_mchf_fold.txt)
-        *(float4*)((a.mchf_u + rb) + off) = make_float4(on ? u[0] : 0.0f, on ? u[1] : 0.0f, on ? u[2] : 0.0f, on ? u[3] : 0.0f);
-        return;
-    }
     if (a.mchf)
     {
         const uhsdr_rx_plan* __restrict__ P = a.plan;
@@ -1481,26 +1472,33 @@ __device__ __forceinline__ void line_out4(const BackArgs& a, size_t rb, unsigned
     }
 }
 
-// mcHF output stage after a wave-pipeline back end (rx_back, rx_stream): u = biquad_2's output in
-// the scratch row (line_out4's a.mchf_u), the rest of line_out4's mcHF stage per four frames
-__global__ void __launch_bounds__(256) rx_line_out_mchf(BackArgs a, const float* __restrict__ u)
+
+// pitch of a channel's row in the LDS output staging of the fused back end and the wave pipeline's output role (odd: conflict-free)
+constexpr int FUSED_YPITCH = BLK + 1;
+
+// a call's 32 output frames of the wave's 64 channels from LDS to HBM: lane (g, j) = (lane / 8,
+// lane % 8) takes frames 4j..4j+3 of channels 8k + g, so one store instruction covers 8 rows
+__device__ __forceinline__ void fused_store_call(const BackArgs& a, const BackLane& l, int call, const float* ys)
 {
-    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;       // quad of frames
-    const int qpc = a.N / 4;
-    if (q >= (size_t)a.C * qpc) return;
-    const int fr0 = (int)(q % qpc) * 4;
-    const float4 x = *(const float4*)(u + q * 4);
-    const float v[4] = { x.x, x.y, x.z, x.w };
-    a.mchf_u = nullptr;
-    line_out4(a, q * 4, 0u, fr0 / BLK, fr0, v);
+    wave_sync();                                         // the wave's rows are complete
+    const int g = l.lane >> 3, j = l.lane & 7;
+    const int c0 = l.c - l.lane;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+    {
+        const int cc = 8 * k + g;
+        const float* r = ys + cc * FUSED_YPITCH + 4 * j;
+        const float v[4] = { r[0], r[1], r[2], r[3] };
+        const int c = c0 + cc;
+        if (c >= a.C) continue;
+        // uniform base of rows c0 + 8k.. (SGPRs) + the lane's 32-bit offset
+        const size_t rb = (size_t)(c0 + 8 * k) * a.N + call * BLK;
+        const unsigned off = (unsigned)g * (unsigned)a.N + 4 * j;
+        line_out4(a, rb, off, call, call * BLK + 4 * j, v);
+    }
+    wave_sync();                                         // rows read before the next call writes
 }
 
-// four consecutive output frames n0..n0+3 of a call (OutputStage::step's): f32 audio and int32 codec frames
-__device__ __forceinline__ void back_store4(const BackArgs& a, const BackLane& l, int call, int n0, const float (&u)[4])
-{
-    if (!l.live) return;
-    line_out4(a, (size_t)l.c * a.N + call * BLK + n0, 0u, call, call * BLK + n0, u);
-}
 
 // ---- demod stage: AudioDriver_DemodSAM (audio_driver.c:1990-2166): AM envelope
 //      (:2008-2020) or the SAM PLL (:2021-2147), fade leveler (:1911-1923) ----
@@ -1727,7 +1725,7 @@ struct FadeStage
 #ifdef UHSDR_TRACE
 // timing build (tools/trace_back.py): per workgroup, role and iteration the shader clock when the
 // role starts its call, ends it, and leaves the barrier
-__device__ unsigned long long g_trace[64][8][40][3];
+__device__ unsigned long long g_trace[64][10][40][3];
 #define TRACE_MARK(k) do { if (l.lane == 0 && blockIdx.x < 64 && it < 40) \
     g_trace[blockIdx.x][threadIdx.x / BACK_CH][it][k] = __builtin_readcyclecounter(); } while (0)
 extern "C" int uhsdr_trace_read(void* out)
@@ -2209,23 +2207,65 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
                 for (int n = 0; n < BLK; ++n) y[n] = __builtin_nanf("");
             }
         }
+        // to the tail waves (rx_back_tail), one row per channel: the board's output stage and the
+        // stores are elementwise, and as this role's own per-sample tail they made it the
+        // pipeline's critical role (int32 codec frames 4400-5700, mcHF 8800-9800 cycles per step
+        // against the anti-alias role's 4300; UHSDR_TRACE r06)
+        float* yl = lds.ys + (call & 1) * BACK_CH * FUSED_YPITCH + l.lane * FUSED_YPITCH;
 #pragma unroll
-        for (int n0 = 0; n0 < BLK; n0 += 4)
-        {
-            const float y4[4] = { y[n0], y[n0 + 1], y[n0 + 2], y[n0 + 3] };
-            back_store4(a, l, call, n0, y4);
-        }
+        for (int n = 0; n < BLK; ++n) yl[n] = y[n];
     BACK_ROLE_END
     s.store(a, l);
     if (back_ext(sch, lds)) bnd_store<BLK>(a, l, a.bnd_mid + BLK, lds.aa + ((l.calls + BACK_SKEW - 4) & 1) * BLK * BACK_CH);
 }
 #undef BACK_ROLE_LOOP
+
+// Tail waves of the wave pipeline: the output role's call of the previous step (its transposed
+// rows in ys) through the board's output stage (line_out4: key beep, mcHF gains, codec frames) to
+// coalesced row stores, each tail wave 64 / BACK_TAILS of the 64 channels' rows; the launch's last call after the
+// final barrier.  Elementwise, so it needs no state and no place in BackSched's skew.
+// (2 tail waves took 4500-5500 cycles per step with mcHF codec frames, above the anti-alias role)
+constexpr int BACK_TAILS = 4;
+template <int DM>
+__device__ __forceinline__ void rx_back_tail(const BackArgs& a, BackLds lds, int half)
+{
+    const BackLane l(a);
+    const BackSched sch = BackSched::make<DM>(a, l, BackSched::word<DM>(a));
+    constexpr int ST = back_roles(DM);                  // one step behind the output role
+    const int g8 = l.lane >> 3, j = l.lane & 7;
+    const int c0 = l.c - l.lane;
+    auto store_call = [&](int call) {
+        const float* ys = lds.ys + (call & 1) * BACK_CH * FUSED_YPITCH;
+#pragma unroll
+        for (int kk = 0; kk < 8 / BACK_TAILS; ++kk)
+        {
+            const int k = half * (8 / BACK_TAILS) + kk;
+            const int cc = 8 * k + g8;
+            const float* r = ys + cc * FUSED_YPITCH + 4 * j;
+            const float v[4] = { r[0], r[1], r[2], r[3] };
+            if (c0 + cc >= a.C) continue;
+            const size_t rb = (size_t)(c0 + 8 * k) * a.N + call * BLK;
+            const unsigned off = (unsigned)g8 * (unsigned)a.N + 4 * j;
+            line_out4(a, rb, off, call, call * BLK + 4 * j, v);
+        }
+    };
+    for (int it = 0; it < sch.steps; ++it)
+    {
+        const int call = it - ST + sch.gofs;
+        TRACE_MARK(0);
+        if (call >= 0 && call < l.calls) store_call(call);
+        TRACE_MARK(1);
+        lds_barrier();
+        TRACE_MARK(2);
+    }
+    store_call(l.calls - 1);
+}
 #undef BACK_ROLE_END
 
 // PRE / AA lattice stages, L interpolation factor, PH polyphase length, W AGC window,
 // DM demodulator (DM_NONE: SSB/CW/DIGI)
 template <int PRE, int AA, int L, int PH, int W, int DM>
-__global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
+__global__ void __launch_bounds__((6 + BACK_TAILS) * BACK_CH) rx_back(BackArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const BackLds lds = back_lds_carve<BLK / L>(smem);
@@ -2256,8 +2296,15 @@ __global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
         rx_back_audio<L, PH, W, DM>(a, lds);
     else if (role == 3)
         rx_back_aa<AA, DM>(a, lds);
-    else
+    else if (role == 4)
         rx_back_output<DM>(a, lds);
+    else
+    {
+        // below every role: a tail wave shares a SIMD with a role wave (9-10 waves on 4 SIMDs), and
+        // the roles are the per-step critical path
+        __builtin_amdgcn_s_setprio(1);
+        rx_back_tail<DM>(a, lds, role - back_roles(DM) + (DM ? 1 : 0));
+    }
 #ifdef UHSDR_TRACE
     if ((threadIdx.x & (BACK_CH - 1)) == 0 && blockIdx.x < 64)
         g_trace[blockIdx.x][threadIdx.x / BACK_CH][39][1] = __builtin_readcyclecounter();
@@ -2268,32 +2315,6 @@ __global__ void __launch_bounds__(6 * BACK_CH) rx_back(BackArgs a)
 // all state in registers -- no LDS, no barriers, no pipeline fill / drain.  With enough
 // channels to keep every SIMD busy this beats the wave pipeline, whose only purpose is to
 // shorten the per-call critical path when channels are few.
-// pitch of a channel's row in the fused back end's LDS output staging (odd: conflict-free)
-constexpr int FUSED_YPITCH = BLK + 1;
-
-// a call's 32 output frames of the wave's 64 channels from LDS to HBM: lane (g, j) = (lane / 8,
-// lane % 8) takes frames 4j..4j+3 of channels 8k + g, so one store instruction covers 8 rows
-__device__ __forceinline__ void fused_store_call(const BackArgs& a, const BackLane& l, int call, const float* ys)
-{
-    wave_sync();                                         // the wave's rows are complete
-    const int g = l.lane >> 3, j = l.lane & 7;
-    const int c0 = l.c - l.lane;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-    {
-        const int cc = 8 * k + g;
-        const float* r = ys + cc * FUSED_YPITCH + 4 * j;
-        const float v[4] = { r[0], r[1], r[2], r[3] };
-        const int c = c0 + cc;
-        if (c >= a.C) continue;
-        // uniform base of rows c0 + 8k.. (SGPRs) + the lane's 32-bit offset
-        const size_t rb = (size_t)(c0 + 8 * k) * a.N + call * BLK;
-        const unsigned off = (unsigned)g * (unsigned)a.N + 4 * j;
-        line_out4(a, rb, off, call, call * BLK + 4 * j, v);
-    }
-    wave_sync();                                         // rows read before the next call writes
-}
-
 // AGC_ON (mode != 5) and CW (decoder front end) are launch constants, made compile-time so the
 // per-sample code carries no uniform branches; the AGC's DC removal is on for AM / SAM (compile-
 // time for the demodulating bodies, a select behind rx_notch)
@@ -3043,7 +3064,6 @@ struct uhsdr_rx_s
     int cw_bmax, cw_blocks_last;
     int beep_left;           // key beep: 32-frame calls still to get the tone (uhsdr_rx_key_beep)
     uint32_t beep_acc;       // its softdds accumulator at the next beep frame
-    float* mchf_u;           // mcHF: [C][N] biquad_2 output of a wave-pipeline back end (rx_line_out_mchf's input)
     uint8_t* cw_signal;      // user outputs (uhsdr_rx_set_cw_outputs)
     float* cw_energy;
     long long calls_done;
@@ -3455,7 +3475,6 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     const size_t o_notch = take(h->nv ? (size_t)(2 * NOTCH_TAPS + 2 + NOTCH_DELAY) * C : 0);
     const bool cw = p.cw_enabled && p.decimation_rate == 4;
     const size_t o_cw = take(cw ? (size_t)5 * C : 0);
-    const size_t o_mu = take(p.single_channel ? (size_t)C * N : 0);
     // the wave pipeline's running ahead (BackSched): per group its skew word, per channel the roles'
     // pending input sub-calls
     const bool skewable = h->bv->dm == DM_NONE && !st && p.interp_L > 0;
@@ -3485,7 +3504,6 @@ extern "C" uhsdr_status uhsdr_rx_create(const uhsdr_rx_config* cfg, int32_t C, i
     h->bs.interp = A + o_ip; h->bs.ring = A + o_ring; h->bs.agc = A + o_agc; h->bs.agci = (int*)(A + o_agci);
     h->bs.sam = am ? A + o_sam : nullptr;
     h->bs.cw = cw ? A + o_cw : nullptr;
-    h->mchf_u = p.single_channel ? A + o_mu : nullptr;
     h->skew = skewable ? (int*)(A + o_skew) : nullptr;
     h->bnd = skewable ? A + o_bnd : nullptr;
     h->bs.notch = h->nv ? A + o_notch : nullptr;
@@ -3666,7 +3684,6 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     ba.audio = audio;
     ba.audio0 = h->plan.stereo || h->plan.single_channel ? audio0 : nullptr;   // stereo / mcHF: a_buffer[0]
     ba.mchf = h->plan.single_channel != 0;
-    ba.mchf_u = nullptr;
     ba.dst = (int2*)dst;
     ba.s = h->bs;
     ba.C = h->C; ba.N = h->N; ba.Nd = h->Nd;
@@ -3716,13 +3733,6 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     return ba;
 }
 
-// mcHF after a wave-pipeline back end: the rest of the board's output stage over the scratch row
-static void line_out_mchf(const uhsdr_rx_s* h, const BackArgs& ba, hipStream_t s)
-{
-    if (!h->mchf_u) return;
-    const size_t quads = (size_t)h->C * h->N / 4;
-    hipLaunchKernelGGL(rx_line_out_mchf, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, ba, (const float*)h->mchf_u);
-}
 
 // the failure word a bounded device-side poll sets when it gives up (BackArgs::fail)
 static uhsdr_status check_fail(const uhsdr_rx_s* h)
@@ -3815,15 +3825,9 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         }
         time_mark(h, K_FRONT, 1);
 
-        const BackArgs ba = back_args(h, adec, adec_q, audio, audio0, dst);
-        // mcHF after the wave pipeline (rx_back): biquad_2's output to the scratch row, then
-        // rx_line_out_mchf; the other back ends run the board's stage inline (line_out4)
-#ifndef UHSDR_MCHF_PASS
-#define UHSDR_MCHF_PASS 1
-#endif
-        const bool mc_pass = UHSDR_MCHF_PASS && h->mchf_u && !fused && h->bv->dm != DM_FM;
-        BackArgs bk = ba;
-        if (mc_pass) bk.mchf_u = h->mchf_u;
+        // (the mcHF output stage runs inline in every back end: the wave pipeline's tail waves,
+        // line_out4; round 5's finishing pass rx_line_out_mchf and its [C][N] scratch are gone)
+        BackArgs bk = back_args(h, adec, adec_q, audio, audio0, dst);
         if (dfl)
         {
             bk.dwait = gc;
@@ -3856,7 +3860,9 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             HIPCHK(hipGetLastError());
         }
         const back_fn bfn = fused ? fused_back_fn(h) : h->bv->fn;
-        const dim3 bgrid((h->C + BACK_CH - 1) / BACK_CH), bblock(fused ? BACK_CH : back_roles(h->bv->dm) * BACK_CH);
+        // (the wave pipeline: its role waves and BACK_TAILS tail waves; rx_fm: its two; the fused kernels: one)
+        const int bwaves = fused ? 1 : h->bv->dm == DM_FM ? back_roles(DM_FM) : back_roles(h->bv->dm) + BACK_TAILS;
+        const dim3 bgrid((h->C + BACK_CH - 1) / BACK_CH), bblock(bwaves * BACK_CH);
 #ifndef UHSDR_FUSED_LDS_PAD
 #define UHSDR_FUSED_LDS_PAD 0
 #endif
@@ -3879,20 +3885,11 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             }
             if (h->back_attr > 0) blds = LDS_PER_CU - 4096;
         }
-        // pipelined: the group's last rx_back (mcHF pass: the finishing kernel) records ev_back[grp]
-        // as it completes
-        if (side && group_end && !mc_pass)
+        // pipelined: the group's last rx_back records ev_back[grp] as it completes
+        if (side && group_end)
             hipExtLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, nullptr, h->ev_back[grp], 0, bk);
         else
             hipLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, bk);
-        if (mc_pass && side && group_end)
-        {
-            const size_t quads = (size_t)h->C * h->N / 4;
-            hipExtLaunchKernelGGL(rx_line_out_mchf, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, bst, nullptr,
-                                  h->ev_back[grp], 0, ba, (const float*)h->mchf_u);
-        }
-        else if (mc_pass)
-            line_out_mchf(h, ba, bst);
         HIPCHK(hipGetLastError());
         time_mark(h, K_BACK, 1);
         if (h->pipelined) h->pipe_calls += 1;

@@ -15,5 +15,5 @@ cat gpurun_out/bench20_$tag.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_$tag -o kt -- python bench.py --steps 20 --warmup 5 --no-cpu --no-northstar > gpurun_out/kt_$tag.log 2>&1 || { tail -20 gpurun_out/kt_$tag.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ss_$tag -o ss -- python bench.py --steps 300 --warmup 5 --no-cpu --no-northstar > gpurun_out/ss_$tag.log 2>&1 || { tail -20 gpurun_out/ss_$tag.log; exit 1; }
 python tools/c2_steady.py gpurun_out/ss_$tag 305 | tee gpurun_out/ss_$tag.txt
-timeout -k 10 600 python tools/bench_configs.py --only c3,c4fm,c5 > gpurun_out/cfg_$tag.jsonl 2> gpurun_out/cfg_$tag.err || { tail -20 gpurun_out/cfg_$tag.err; exit 1; }
+timeout -k 10 600 python tools/bench_configs.py --only c3,c3spec,c4fm,c4tx,c4txfma,c5,c5fir > gpurun_out/cfg_$tag.jsonl 2> gpurun_out/cfg_$tag.err || { tail -20 gpurun_out/cfg_$tag.err; exit 1; }
 cat gpurun_out/cfg_$tag.jsonl

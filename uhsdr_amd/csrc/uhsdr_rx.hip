@@ -2177,6 +2177,16 @@ __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
     if (back_ext(sch, lds)) bnd_store<BLK>(a, l, a.bnd_mid, lds.mid + ((l.calls + BACK_SKEW - 3) & 1) * BLK * BACK_CH);
 }
 
+// (2 tail waves took 4500-5500 cycles per step with mcHF codec frames, above the anti-alias role)
+constexpr int BACK_TAILS = 4;
+// tail waves of a back end: BACK_TAILS for the demodulator-free pipeline; UHSDR_DM_TAILS for the AM /
+// SAM ones, 0 (the output role stores its call itself): their grids are large (C3: 512 workgroups)
+// and 4 more waves per workgroup took C3's SAM back end from 0.118 to 0.193 ms
+// (profiles/r06_configs_tails.jsonl)
+#ifndef UHSDR_DM_TAILS
+#define UHSDR_DM_TAILS 0
+#endif
+__host__ __device__ constexpr int back_tails(int dm) { return dm == DM_NONE ? BACK_TAILS : UHSDR_DM_TAILS; }
 template <int DM>
 __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
 {
@@ -2214,6 +2224,7 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
         float* yl = lds.ys + (call & 1) * BACK_CH * FUSED_YPITCH + l.lane * FUSED_YPITCH;
 #pragma unroll
         for (int n = 0; n < BLK; ++n) yl[n] = y[n];
+        if constexpr (back_tails(DM) == 0) fused_store_call(a, l, call, lds.ys + (call & 1) * BACK_CH * FUSED_YPITCH);
     BACK_ROLE_END
     s.store(a, l);
     if (back_ext(sch, lds)) bnd_store<BLK>(a, l, a.bnd_mid + BLK, lds.aa + ((l.calls + BACK_SKEW - 4) & 1) * BLK * BACK_CH);
@@ -2224,8 +2235,6 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
 // rows in ys) through the board's output stage (line_out4: key beep, mcHF gains, codec frames) to
 // coalesced row stores, each tail wave 64 / BACK_TAILS of the 64 channels' rows; the launch's last call after the
 // final barrier.  Elementwise, so it needs no state and no place in BackSched's skew.
-// (2 tail waves took 4500-5500 cycles per step with mcHF codec frames, above the anti-alias role)
-constexpr int BACK_TAILS = 4;
 template <int DM>
 __device__ __forceinline__ void rx_back_tail(const BackArgs& a, BackLds lds, int half)
 {
@@ -2236,10 +2245,11 @@ __device__ __forceinline__ void rx_back_tail(const BackArgs& a, BackLds lds, int
     const int c0 = l.c - l.lane;
     auto store_call = [&](int call) {
         const float* ys = lds.ys + (call & 1) * BACK_CH * FUSED_YPITCH;
+        constexpr int KT = 8 / (back_tails(DM) ? back_tails(DM) : 1);   // row groups of 8 channels per tail wave
 #pragma unroll
-        for (int kk = 0; kk < 8 / BACK_TAILS; ++kk)
+        for (int kk = 0; kk < KT; ++kk)
         {
-            const int k = half * (8 / BACK_TAILS) + kk;
+            const int k = half * KT + kk;
             const int cc = 8 * k + g8;
             const float* r = ys + cc * FUSED_YPITCH + 4 * j;
             const float v[4] = { r[0], r[1], r[2], r[3] };
@@ -2265,7 +2275,7 @@ __device__ __forceinline__ void rx_back_tail(const BackArgs& a, BackLds lds, int
 // PRE / AA lattice stages, L interpolation factor, PH polyphase length, W AGC window,
 // DM demodulator (DM_NONE: SSB/CW/DIGI)
 template <int PRE, int AA, int L, int PH, int W, int DM>
-__global__ void __launch_bounds__((6 + BACK_TAILS) * BACK_CH) rx_back(BackArgs a)
+__global__ void __launch_bounds__((back_roles(DM) + back_tails(DM)) * BACK_CH) rx_back(BackArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const BackLds lds = back_lds_carve<BLK / L>(smem);
@@ -2298,7 +2308,7 @@ __global__ void __launch_bounds__((6 + BACK_TAILS) * BACK_CH) rx_back(BackArgs a
         rx_back_aa<AA, DM>(a, lds);
     else if (role == 4)
         rx_back_output<DM>(a, lds);
-    else
+    else if constexpr (back_tails(DM) > 0)
     {
         // below every role: a tail wave shares a SIMD with a role wave (9-10 waves on 4 SIMDs), and
         // the roles are the per-step critical path
@@ -3861,7 +3871,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         }
         const back_fn bfn = fused ? fused_back_fn(h) : h->bv->fn;
         // (the wave pipeline: its role waves and BACK_TAILS tail waves; rx_fm: its two; the fused kernels: one)
-        const int bwaves = fused ? 1 : h->bv->dm == DM_FM ? back_roles(DM_FM) : back_roles(h->bv->dm) + BACK_TAILS;
+        const int bwaves = fused ? 1 : h->bv->dm == DM_FM ? back_roles(DM_FM) : back_roles(h->bv->dm) + back_tails(h->bv->dm);
         const dim3 bgrid((h->C + BACK_CH - 1) / BACK_CH), bblock(bwaves * BACK_CH);
 #ifndef UHSDR_FUSED_LDS_PAD
 #define UHSDR_FUSED_LDS_PAD 0

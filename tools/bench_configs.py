@@ -203,7 +203,10 @@ def main():
             fir = U.FirBatch(taps, C, N, mode, stream=s.cuda_stream)
             if a.fir_waves:
                 fir.set_waves(a.fir_waves)
-            ms = time_calls(lambda: fir.process(x, y), a.steps, a.warmup)
+            # at least 200 warm-up calls: in a process that runs only this line, the chip's clock dips
+            # during the first ~50 MFMA launches (2.26 -> 1.91 -> 2.31 GHz, profiles/r05_fir_clock.txt)
+            # and a 5-call warm-up timed the dip (0.314 vs 0.285 ms, profiles/r06_c5fir_alone.txt)
+            ms = time_calls(lambda: fir.process(x, y), a.steps, max(a.warmup, 200))
             waves = fir.waves
             fir.close()
             per = 8 + 2 * 4 * (T - 1) / N                 # 4 B in + 4 B out, carried samples in + out

@@ -132,7 +132,7 @@ def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
 
 
 SCHEDULES = {"auto": None, "pipe": 1, "fused": 2, "chain": 3}   # uhsdr_rx_set_schedule
-DEVICE_HANDOFF = True    # --handoff: device (uhsdr_rx_set_pipelined(h, 2)) or event (1)
+DEVICE_HANDOFF = 2       # --handoff: uhsdr_rx_set_pipelined's mode (event 1, device 2, persistent 3)
 SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain"}
 
 
@@ -152,7 +152,7 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
         # call k+1's rx_front overlaps call k's rx_back; 2: the device hand-off (rx_back polls the
         # arrival counters the front waves of its channel group bump, then reads the hand-off with
         # sc1 loads, instead of waiting on a cross-stream event)
-        chain.set_pipelined(2 if DEVICE_HANDOFF else True)
+        chain.set_pipelined(DEVICE_HANDOFF)
     plan = chain.plan
     # inputs resident in HBM before timing: a pool of consecutive blocks, cycled
     c0 = shard.channel_range(C, rank)[0]          # weak scaling: rank r owns channels [r*C, (r+1)*C)
@@ -277,10 +277,11 @@ def main():
                          "kernels fill the chip there)")
     ap.add_argument("--pipelined", action="store_true",
                     help="pipelined mode even on the north-star workload (default on for the others)")
-    ap.add_argument("--handoff", default="device", choices=["event", "device"],
-                    help="pipelined mode's front -> back hand-off: rx_back polling the call sequence "
-                         "number a one-lane kernel publishes after rx_front (uhsdr_rx_set_pipelined 2; "
-                         "the default, no cross-stream wait per call), or a cross-stream event per call")
+    ap.add_argument("--handoff", default="device", choices=["event", "device", "persistent"],
+                    help="pipelined mode's front -> back hand-off: rx_back polling the arrival counters "
+                         "its channel group's front waves bump (uhsdr_rx_set_pipelined 2, the default: no "
+                         "cross-stream wait per call), a cross-stream event per call (1), or the "
+                         "persistent back end (3: one rx_back launch runs call after call)")
     ap.add_argument("--precision", default="exact", choices=["exact", "fma"],
                     help="FIR MACs: exact (bit-identical to the reference) or fma (1e-5 normwise)")
     ap.add_argument("--pool", type=int, default=8, help="distinct input blocks cycled through")
@@ -297,7 +298,7 @@ def main():
                          "(test hook: ranks may share one GPU, the gather leg moves host copies)")
     args = ap.parse_args()
     global DEVICE_HANDOFF
-    DEVICE_HANDOFF = args.handoff == "device"
+    DEVICE_HANDOFF = {"event": 1, "device": 2, "persistent": 3}[args.handoff]
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))

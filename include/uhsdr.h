@@ -292,7 +292,19 @@ uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h);
    side stream's back ends run back to back.  When the next call's front has already arrived, a
    back-end launch also runs its first pipeline roles ahead into that call instead of draining
    (bit-identical; the next launch then starts without a pipeline fill).  Other calls keep the
-   event.  Any other enable value returns UHSDR_ARGUMENT_ERROR.
+   event.
+   enable = 3 (persistent back end): the device hand-off, and one rx_back launch runs call after
+   call -- wave-pipeline back ends without the CW decoder and with calls of 256+ frames; others as
+   enable = 2.  Each uhsdr_rx_process writes the call's descriptor (its hand-off buffer, outputs and
+   key beep) into host-mapped memory and grants the call to the running launch, which takes it with
+   its state in registers; a launch that finds no grant when it needs the next call ends (the host
+   then starts a new one with the next call).  uhsdr_rx_join, uhsdr_rx_synchronize, uhsdr_rx_reset
+   and every mode or schedule change end the running launch after the calls granted so far, so a
+   device-wide synchronisation (or join) completes without further calls.  The host waits in
+   uhsdr_rx_process before refilling a hand-off buffer the back end has not read yet (8 calls
+   back).  Same failure contract as enable = 2 (a give-up inside a launch poisons the call it
+   waited for, and may poison the end of the call before it).  Any other enable value returns
+   UHSDR_ARGUMENT_ERROR.
    Failure contract of the device hand-off.  The poll is bounded (uhsdr_rx_set_handoff_bound,
    default 2^24 polls: seconds).  If rx_back gives up -- the handle's stream held the call's
    rx_front back that long behind other work, or a profiler serialised the two streams' dispatches
@@ -305,8 +317,13 @@ uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h);
    Under a profiler that serialises dispatches (rocprofv3 --pmc) use enable = 1. */
 uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable);
 /* Poll bound of the device hand-off (polls of >= 128 shader cycles each); for tests of the
-   failure contract.  0 is UHSDR_ARGUMENT_ERROR. */
+   failure contract.  0 is UHSDR_ARGUMENT_ERROR.  A running persistent launch keeps the bound it
+   started with. */
 uhsdr_status uhsdr_rx_set_handoff_bound(uhsdr_rx_handle h, uint32_t polls);
+/* Test hook of the persistent back end (enable = 3): out[0..7] = its grant, close, exit and decision
+   words, group 0's consumed word, whether a launch may take the next grant, the last call granted,
+   and the launches started.  UHSDR_UNSUPPORTED before the mode was first entered. */
+uhsdr_status uhsdr_rx_debug_persist(uhsdr_rx_handle h, uint32_t* out);
 /* 1 if a device hand-off poll gave up since the last uhsdr_rx_reset, else 0; -1 on error.
    Synchronises. */
 int32_t      uhsdr_rx_handoff_timeouts(uhsdr_rx_handle h);

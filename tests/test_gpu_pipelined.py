@@ -192,6 +192,7 @@ def test_pipelined_mchf_matches_oracle(cuda, name, kw, gen, C, N, calls):
 # that fallback.  No poll may give up (uhsdr_rx_handoff_timeouts).
 HANDOFF_CASES = [
     ("p48_usb", dict(filter_path=48, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 300, 256),
+    ("p48_usb_n16", dict(filter_path=48, dmod_mode=U.DEMOD_USB), synth.ssb_iq, 130, 512),
     ("p35_lsb", dict(filter_path=35, dmod_mode=U.DEMOD_LSB), synth.ssb_iq, 130, 128),
     ("p4_cw", dict(filter_path=4, dmod_mode=U.DEMOD_CW), synth.cw_iq, 65, 64),
     ("p48_mchf", dict(filter_path=48, board=U.BOARD_MCHF, spkr_gain=24), synth.ssb_iq, 97, 256),
@@ -349,7 +350,7 @@ def test_device_handoff_give_up_fails_loudly(cuda):
     assert chain.handoff_timeouts() == 0
     assert_bitexact(audio[:3].cpu().numpy().transpose(1, 0, 2).reshape(C, 3 * N), ref, "after reset")
     with pytest.raises(U.UhsdrError):
-        chain.set_pipelined(3)                       # modes are 0, 1, 2
+        chain.set_pipelined(4)                       # modes are 0 .. 3 (3: persistent)
     chain.close()
 
 

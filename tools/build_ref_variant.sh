@@ -5,7 +5,8 @@ set -e
 rev=$1; tag=$2; shift 2
 cd "$(dirname "$0")/.."
 tmp=$(mktemp -d)
-git archive "$rev" uhsdr_amd/csrc include | tar -x -C "$tmp"
+if [ "$rev" = . ]; then mkdir -p "$tmp/uhsdr_amd" && cp -r uhsdr_amd/csrc "$tmp/uhsdr_amd/" && cp -r include "$tmp/"
+else git archive "$rev" uhsdr_amd/csrc include | tar -x -C "$tmp"; fi
 mkdir -p uhsdr_amd/lib/variants "$tmp/obj"
 for f in "$tmp"/uhsdr_amd/csrc/*.hip; do
   [ "$(basename $f)" = uhsdr_cmsis.hip ] && continue

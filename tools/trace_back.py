@@ -66,9 +66,20 @@ def main():
     e0 = ent[:, :, 0].min(axis=1)
     print("entry -> first step start, per role (median cycles):",
           [int(np.median(t[:, r, 0, 0] - e0)) for r in range(roles)])
+    print("wave start after the workgroup's first, per role (median cycles):",
+          [int(np.median(ent[:, r, 0] - e0)) for r in range(roles)])
+    sk = buf[:, :roles, 39, 2].astype(np.int64)
+    print("own entry -> skew word consumed, per role (median cycles):",
+          [int(np.median(sk[:, r] - ent[:, r, 0])) for r in range(roles)])
     print("last barrier -> exit, per role (median cycles):",
           [int(np.median(ent[:, r, 1] - t[:, r, its - 1, 2])) for r in range(roles)])
     print("entry -> last exit (median WG):", int(np.median(ent[:, :, 1].max(axis=1) - e0)))
+    rt = buf[:, :roles, 38, :2].astype(np.int64)               # s_memrealtime (100 MHz) at entry / exit
+    if rt.any():
+        cyc = ent[:, :, 1] - ent[:, :, 0]
+        ns = (rt[:, :, 1] - rt[:, :, 0]) * 10.0
+        print(f"shader clock (median over waves): {np.median(cyc / np.maximum(ns, 1)):.3f} GHz; "
+              f"wave life median {np.median(ns) / 1e3:.2f} us")
 
 
 if __name__ == "__main__":

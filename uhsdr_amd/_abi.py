@@ -194,6 +194,7 @@ SIGNATURES = {
     "uhsdr_rx_get_schedule": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_handoff_timeouts": (C.c_int32, [C.c_void_p]),
     "uhsdr_rx_set_handoff_bound": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "uhsdr_rx_debug_persist": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "uhsdr_rx_set_front_block": (C.c_int, [C.c_void_p, C.c_int32]),
     "uhsdr_rx_set_cw_outputs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "uhsdr_rx_cw_blocks_max": (C.c_int32, [C.c_void_p]),

@@ -33,6 +33,7 @@
 #include <string.h>
 #include <stdlib.h>
 #include <math.h>
+#include <chrono>
 #include "uhsdr_internal.h"
 #include "uhsdr_libm.h"
 #include "uhsdr_dsp.h"
@@ -692,7 +693,54 @@ struct BackArgs
     int* skew;
     float* bnd;
     int bnd_mid;         // bnd's field of the aa role's pending input (6 NDC); the output role's follows it
+    // persistent back end (uhsdr_rx_set_pipelined 3, PersistCtl): pctl = the handle's host-mapped
+    // control words, pdesc = its host-mapped ring of call descriptors, seq0 = this launch's first call;
+    // null pctl: one call per launch
+    unsigned* pctl;
+    const struct BackDesc* pdesc;
+    unsigned* pdec;
+    unsigned seq0;
 };
+
+// Persistent back end (uhsdr_rx_set_pipelined 3).  One rx_back launch runs call after call with its
+// roles' state in registers and their LDS hand-offs in place, instead of one launch per call: each
+// launch's dispatch, state loads and stores (~5 us of a ~21 us C2 call: 3.2 us outside the waves,
+// ~1.6 us entry, ~0.4 us exit; UHSDR_TRACE r06) are paid once per run of calls.  The host writes call
+// k's descriptor into a ring in host-mapped memory, then grants k (PC_GRANT); the pre role, four
+// sub-calls before the end of call k - 1, reads the grant and the descriptor and runs on into call k
+// (BackSched's running ahead, every call), the other roles following at the step barriers.  With no
+// grant it closes: it stores k - 1 to PC_EXIT, re-reads the grant after a sequentially consistent
+// fence and stores its decision to PC_DECIDED; the host, after granting k, reads PC_EXIT and, when it
+// finds k - 1 there, waits for that decision and relaunches if the kernel closed (Dekker: one of the
+// two sees the other's store).  PC_CLOSE ends a launch at a given call (uhsdr_rx_join and every
+// synchronisation point), PC_CONSUMED orders the hand-off buffers' reuse (the host waits before
+// overwriting the buffer of call k - PIPE_BUFS until every channel group has read it).  The decision is
+// the launch's, not each workgroup's: group 0's pre role makes it (the host protocol above) and
+// publishes it per call in device memory (BackArgs::pdec); the other groups read it there, so all of
+// them run the same calls.
+constexpr int DESC_RING = 16;
+struct BackDesc
+{
+    const float* adec;       // the call's hand-off buffer
+    const unsigned* cnt;     // its arrival counters (FrontArgs::gcnt row)
+    float* audio;
+    float* audio0;
+    int2* dst;
+    unsigned target;         // BackArgs::dtarget of the call
+    unsigned seq;            // written last: the descriptor is complete
+    int beep_n0, beep_n1;
+    uint32_t beep_acc;
+    unsigned pad;
+};
+static_assert(sizeof(BackDesc) == 64, "one descriptor per 64 B");
+// control words (unsigned, 64 B apart)
+enum { PC_GRANT = 0, PC_CLOSE = 16, PC_EXIT = 32, PC_DECIDED = 48, PC_WORDS = 64 };
+// then the descriptors, then one PC_CONSUMED word per channel group (PC_MAX_GROUPS)
+constexpr int PC_CONSUMED = PC_WORDS + DESC_RING * 16, PC_MAX_GROUPS = 256;
+constexpr int PC_BYTES = 4 * (PC_CONSUMED + PC_MAX_GROUPS);
+// the launch's decision per call, made by group 0 and read by the others (device memory, BackArgs::pdec,
+// DESC_RING words 32 apart): (call << 1) | closed
+constexpr int PDEC_PITCH = 32;
 
 // softdds_addSingleToneToTwobuffers (softdds.c:142-152): the tone of launch frame n
 __device__ __forceinline__ float beep_tone(const BackArgs& a, int n)
@@ -762,11 +810,12 @@ struct BackLds
     float* prep;  // [3][2][NDC][64]  pre -> agc: window maximum, fast / hang averages
     unsigned* poison;  // [1]  pre -> output: the launch's device hand-off gave up (DM_NONE only)
     unsigned* ext;     // [1]  pre -> every role: the launch runs ahead into the next call (BackSched)
+    unsigned* desc;    // [2][16]  pre -> tail: the persistent back end's call outputs (BackDesc words)
     float* ys;         // [2][64][BLK + 1]  output -> tail: the output role's call, one row per channel
 };
 
 // floats of the hand-off buffers (host: back_lds)
-__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (6 * ndc + 2 * BLK) + 4 + 2 * BACK_CH * (BLK + 1); }
+__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (6 * ndc + 2 * BLK) + 4 + 32 + 2 * BACK_CH * (BLK + 1); }
 
 template <int NDC>
 __device__ __forceinline__ BackLds back_lds_carve(float* smem)
@@ -780,7 +829,8 @@ __device__ __forceinline__ BackLds back_lds_carve(float* smem)
     l.prep = l.dem + 2 * NDC * BACK_CH;
     l.poison = (unsigned*)(l.prep + 3 * 2 * NDC * BACK_CH);
     l.ext = l.poison + 1;
-    l.ys = (float*)(l.poison + 4);
+    l.desc = l.poison + 4;
+    l.ys = (float*)(l.poison + 4 + 32);
     return l;
 }
 
@@ -826,11 +876,11 @@ __device__ __forceinline__ unsigned front_waves_of(const BackArgs& a, int g)
     const int c0 = g * BACK_CH, c1 = (c0 + BACK_CH < a.C ? c0 + BACK_CH : a.C) - 1;
     return (unsigned)(c1 / a.fcpw - c0 / a.fcpw + 1);
 }
-__device__ __forceinline__ void dflag_wait(const BackArgs& a, bool& gave_up)
+__device__ __forceinline__ void dflag_wait(const BackArgs& a, const unsigned* cnt, unsigned target, bool& gave_up)
 {
     const int g = blockIdx.x;
-    const unsigned want = a.dtarget * front_waves_of(a, g);
-    unsigned v = __hip_atomic_load(a.dwait + g * CNT_PITCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned want = target * front_waves_of(a, g);
+    unsigned v = __hip_atomic_load(cnt + g * CNT_PITCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (unsigned spins = 0; (int)(v - want) < 0 && !gave_up; ++spins)
     {
         if (spins >= a.spin_max)
@@ -839,7 +889,7 @@ __device__ __forceinline__ void dflag_wait(const BackArgs& a, bool& gave_up)
             gave_up = true;
         }
         __builtin_amdgcn_s_sleep(2);
-        v = __hip_atomic_load(a.dwait + g * CNT_PITCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = __hip_atomic_load(cnt + g * CNT_PITCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no load moves above the poll
 }
@@ -853,6 +903,9 @@ struct InStage
     float xnext[NDC];
     const float* lds;
     bool gave_up = false;                                // DW: this launch's poll gave up
+#ifdef UHSDR_PDEBUG
+    unsigned arrived = 0;
+#endif
     int lim = -1;                                        // prefetch bound (sub-calls); -1: the launch's calls
 
     __device__ __forceinline__ void fetch(const BackArgs& a, const BackLane& l, int call)
@@ -874,7 +927,15 @@ struct InStage
             // every input of the launch is NaN (the failure contract of uhsdr_rx_set_pipelined)
             // (sub-calls past the launch's own: the next call's buffer, BackSched's running ahead,
             // read only after the pre role's peek found it published)
-            if (call == 0) dflag_wait(a, gave_up);
+            if (call == 0) dflag_wait(a, a.dwait, a.dtarget, gave_up);
+            // the persistent back end runs on into a granted call before its front has arrived
+            if (a.pctl && call == l.calls)
+            {
+                dflag_wait(a, a.dwait_next, a.dnext, gave_up);
+#ifdef UHSDR_PDEBUG
+                arrived = __hip_atomic_load(a.dwait_next + blockIdx.x * CNT_PITCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+            }
             const float* src = call < l.calls ? a.adec + (size_t)l.cl * a.Nd + call * NDC
                                               : a.adec_next + (size_t)l.cl * a.Nd + (call - l.calls) * NDC;
 #pragma unroll
@@ -1749,6 +1810,14 @@ extern "C" int uhsdr_trace_read(void* out)
 // covers exactly the launch's own n sub-calls.  A launch that finds the next call unpublished drains
 // as before and the next one fills.
 constexpr int BACK_SKEW = 4;            // back_roles(DM_NONE) - 1
+// BackSched's second chance at running ahead (rx_back_pre): 0 decides on the early peek alone
+#ifndef UHSDR_LATE_EXT
+#define UHSDR_LATE_EXT 1
+#endif
+// and its pre role's speculative first input of a skewed launch: 0 loads it after the skew word
+#ifndef UHSDR_SPEC_IN
+#define UHSDR_SPEC_IN 1
+#endif
 struct BackSched
 {
     int steps, gofs;
@@ -1772,13 +1841,75 @@ struct BackSched
         if constexpr (DM == DM_NONE)
         {
             s.pin = __builtin_amdgcn_readfirstlane(w) != 0;
-            s.may_ext = a.adec_next != nullptr;
+            s.may_ext = a.adec_next != nullptr || a.pctl != nullptr;
         }
         s.gofs = s.pin ? BACK_SKEW : 0;
         s.steps = l.calls + (s.pin ? 0 : back_roles(DM) - 1);
+#ifdef UHSDR_TRACE
+        // (tools/trace_back.py) the skew word consumed: the role's launch-start loads have arrived
+        if ((threadIdx.x & (BACK_CH - 1)) == 0 && blockIdx.x < 64)
+            g_trace[blockIdx.x][threadIdx.x / BACK_CH][39][2] = __builtin_readcyclecounter();
+#endif
+        return s;
+    }
+    // the persistent back end's next call (PersistCtl): it started skewed, its predecessor ran ahead
+    __device__ __forceinline__ static BackSched next(const BackLane& l)
+    {
+        BackSched s;
+        s.pin = true;
+        s.may_ext = true;
+        s.gofs = BACK_SKEW;
+        s.steps = l.calls;
         return s;
     }
 };
+#ifdef UHSDR_PDEBUG
+// (tools/debug_persist2.py) per call (seq % 64), group 0's pre role: seq, adec_next, cnt, target,
+// arrival count after the wait, dst from the descriptor, fast path, gave up
+__device__ unsigned long long g_pdbg[64][8];
+__device__ unsigned long long g_pdbg2[64][4][2];   // per call and group 0..3: decision word seen, polls
+extern "C" int uhsdr_pdbg_read(void* out)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pdbg), sizeof(g_pdbg)) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol((char*)out + sizeof(g_pdbg), HIP_SYMBOL(g_pdbg2), sizeof(g_pdbg2)) == hipSuccess ? 0 : -1;
+}
+#endif
+// the persistent back end (PersistCtl): its control words and descriptors live in host memory
+__device__ __forceinline__ unsigned sys_load(const unsigned* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// call s may run in the launch that started at call seq0: granted, and no close at or past seq0 before it
+__device__ __forceinline__ bool pers_granted(unsigned seq0, unsigned s, unsigned grant, unsigned close_at)
+{
+    const bool closed = (int)(close_at - seq0) >= 0 && (int)(s - close_at) > 0;
+    return (int)(grant - s) >= 0 && !closed;
+}
+// a descriptor, one 32-bit word per lane 0..15 (one VGPR while its loads are in flight; PersistCtl)
+__device__ __forceinline__ unsigned desc_word_load(const BackDesc* d, int lane)
+{
+    return sys_load((const unsigned*)d + (lane & 15));
+}
+// (the builtins return int: through unsigned, so a low word is never sign-extended into the high one)
+__device__ __forceinline__ unsigned desc_u32(unsigned w, int i) { return (unsigned)__builtin_amdgcn_readlane(w, i); }
+__device__ __forceinline__ unsigned long long desc_u64(unsigned w, int i)
+{
+    return (unsigned long long)desc_u32(w, i + 1) << 32 | desc_u32(w, i);
+}
+// BackDesc's word offsets
+enum { DW_ADEC = 0, DW_CNT = 2, DW_AUDIO = 4, DW_AUDIO0 = 6, DW_DST = 8, DW_TARGET = 10, DW_SEQ = 11,
+       DW_BEEP0 = 12, DW_BEEP1 = 13, DW_BACC = 14 };
+// the tail waves' copy of a call's descriptor (lds.desc [2][16])
+__device__ __forceinline__ void desc_get(BackArgs& a, const unsigned* slot)
+{
+    auto w = [&](int i) { return (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(slot[i]); };
+    a.audio = (float*)(w(DW_AUDIO + 1) << 32 | w(DW_AUDIO));
+    a.audio0 = (float*)(w(DW_AUDIO0 + 1) << 32 | w(DW_AUDIO0));
+    a.dst = (int2*)(w(DW_DST + 1) << 32 | w(DW_DST));
+    a.beep_n0 = (int)w(DW_BEEP0);
+    a.beep_n1 = (int)w(DW_BEEP1);
+    a.beep_acc = (uint32_t)w(DW_BACC);
+}
 // BackSched's pending input sub-call of a role, loaded from `bnd` before the role knows whether the
 // launch starts skewed (unused otherwise); put() moves rows [R0, R0 + n) into an LDS hand-off slot
 template <int ROWS>
@@ -1872,8 +2003,9 @@ __device__ __forceinline__ bool back_agc_prep_in_pre(int dm, const uhsdr_agc_pla
 
 // IIR lattice pre-filter; input: rx_front's decimated I +- Q (SSB) or the demod role's output
 template <int PRE, int L, int W, int DM>
-__device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
+__device__ __forceinline__ void rx_back_pre(const BackArgs& a0, BackLds lds)
 {
+    BackArgs a = a0;                                   // the call's (the persistent back end moves it on)
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
@@ -1885,7 +2017,17 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
     const bool prep = back_agc_prep_in_pre(DM, A);
     AgcStage<L, W> ag;
     if (prep) ag.load(a, l, A);
-    const BackSched sch = BackSched::make<DM>(a, l, skw);
+    // a launch that starts skewed takes sub-call BACK_SKEW first: its input (found arrived by the
+    // previous launch's peek, a kernel boundary ago) and ring slot are loaded before the skew word is
+    // consumed, so the role's entry waits one memory latency, not two (UHSDR_SPEC_IN)
+    const bool spec = UHSDR_SPEC_IN && DM == DM_NONE && a.skew && l.calls > BACK_SKEW;
+    if (spec)
+    {
+        in.fetch(a, l, BACK_SKEW);
+        if (prep) ag.fetch(a, l, BACK_SKEW);
+    }
+    BackSched sch = BackSched::make<DM>(a, l, skw);
+    const bool have = spec && sch.pin;                 // g0's input and ring slot are in flight
     int glim = l.calls;
     // BackSched: the first sub-call of this role, and whether it runs ahead into the next call -- a
     // peek of the next buffer's arrival counter (never a wait) issued at g = n - 3 and consumed two
@@ -1904,28 +2046,143 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
         in.lim = glim;
         if (l.lane == 0) *lds.ext = ext ? 1u : 0u;
     };
+    // the persistent back end (PersistCtl): four sub-calls before the end of a call the grant, the
+    // close word and the next descriptor's seq are read; the descriptor itself once its seq has
+    // arrived (written before it); the decision at the call's last sub-call (pers_decide)
+    const bool pers = DM == DM_NONE && a.pctl != nullptr;
+    unsigned seq = a.seq0;
+    // lane 0 PC_GRANT, lane 1 PC_CLOSE, lane 2 the next descriptor's seq; then the descriptor, word
+    // per lane (one VGPR each while in flight)
+    unsigned pv = 0, dw = 0, dv = 0;
+    bool fast = false;                                 // the next descriptor was found complete
+    bool ldone = false;                                // group 0: the decision is published
+    const bool leader = blockIdx.x == 0;
+    auto pdesc = [&](unsigned k) { return a.pdesc + (k % DESC_RING); };
+    auto pctl_load = [&]() {
+        const unsigned* p = l.lane == 0 ? a.pctl + PC_GRANT : l.lane == 1 ? a.pctl + PC_CLOSE
+                                                                         : (const unsigned*)pdesc(seq + 1) + DW_SEQ;
+        pv = sys_load(p);
+    };
+    auto pdec = [&](unsigned k) { return a.pdec + (k % DESC_RING) * PDEC_PITCH; };
+    auto publish = [&](unsigned k, bool go) {
+        if (l.lane == 0) (void)__hip_atomic_exchange(pdec(k), (k << 1) | (go ? 0u : 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto pers_decide = [&]() {
+        const unsigned s1 = seq + 1;
+        bool go = ldone;
+        if (leader && !ldone)
+        {
+            // closing: announce it, then look again (the host, having granted s1, looks at PC_EXIT)
+            if (l.lane == 0) __hip_atomic_store(a.pctl + PC_EXIT, seq, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+            pctl_load();
+            go = pers_granted(a.seq0, s1, desc_u32(pv, 0), desc_u32(pv, 1));
+            if (go)
+            {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // the descriptor was written before the grant
+                dw = desc_word_load(pdesc(s1), l.lane);
+            }
+            publish(s1, go);
+            if (l.lane == 0)
+                __hip_atomic_store(a.pctl + PC_DECIDED, (seq << 1) | (go ? 0u : 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (!leader)
+        {
+            // group 0's decision (loaded a step ago; polled if not there yet, bounded)
+            const unsigned want = s1 & 0x7FFFFFFFu;
+            unsigned v = __builtin_amdgcn_readfirstlane(dv);
+            for (unsigned spins = 0; (v >> 1) != want && !in.gave_up; ++spins)
+            {
+                if (spins >= a.spin_max)
+                {
+                    if (l.lane == 0) __hip_atomic_store(a.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    in.gave_up = true;                 // this group stops here, its output poisoned
+                }
+                __builtin_amdgcn_s_sleep(2);
+                v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(pdec(s1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            }
+            go = (v >> 1) == want && !(v & 1u);
+#ifdef UHSDR_PDEBUG
+            if (blockIdx.x < 4 && l.lane == 0) { g_pdbg2[s1 % 64][blockIdx.x][0] = v; g_pdbg2[s1 % 64][blockIdx.x][1] = in.gave_up; }
+#endif
+            if (go && !fast)
+            {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // written before the grant group 0 saw
+                dw = desc_word_load(pdesc(s1), l.lane);
+            }
+        }
+        ext = go;
+        if (go)
+        {
+            a.adec_next = (const float*)desc_u64(dw, DW_ADEC);
+            a.dwait_next = (const unsigned*)desc_u64(dw, DW_CNT);
+            a.dnext = desc_u32(dw, DW_TARGET);
+            if (l.lane < 16) lds.desc[(s1 & 1) * 16 + l.lane] = dw;   // the tail waves' copy
+#ifdef UHSDR_PDEBUG
+            if (blockIdx.x == 0 && l.lane == 0)
+            {
+                unsigned long long* r = g_pdbg[s1 % 64];
+                r[0] = s1; r[1] = (unsigned long long)a.adec_next; r[2] = (unsigned long long)a.dwait_next;
+                r[3] = a.dnext; r[5] = desc_u64(dw, DW_DST); r[6] = fast;
+            }
+#endif
+        }
+        glim = go ? l.calls + BACK_SKEW : l.calls;
+        in.lim = go ? l.calls + BACK_SKEW + 1 : l.calls;  // + the next call's first sub-call of this role
+        if (l.lane == 0) *lds.ext = go ? 1u : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     if (sch.may_ext)
     {
-        ag.lim = l.calls + BACK_SKEW;                // the ring slots do not depend on the front
-        if (g0 > l.calls - 3) peek();
-        if (g0 >= l.calls) decide();
+        ag.lim = l.calls + BACK_SKEW + (pers ? 1 : 0);   // the ring slots do not depend on the front
+        if (!pers && g0 > l.calls - 3) peek();
+        if (!pers && g0 >= l.calls) decide();
     }
     if (!DM)
     {
-        if (g0 < glim) in.fetch(a, l, g0);
+        if (g0 < glim && !have) in.fetch(a, l, g0);
         // the failure contract: a give-up (InStage's poll, call 0) poisons the whole launch's output,
         // including the frames the AGC's look-ahead delay still takes from the previous launch's
         // samples -- the output role reads this after the step-0 barrier
         if (l.lane == 0) *lds.poison = in.gave_up ? 1u : 0u;
     }
-    if (prep) ag.fetch(a, l, g0);
+    if (prep && !have) ag.fetch(a, l, g0);
     FadeStage fl;
     if (DM == DM_SAM) fl.load(a, l);
+    for (;;)
+    {
     BACK_ROLE_LOOP(DM ? 1 : 0)
-        if (sch.may_ext)
+        if (pers)
+        {
+            if (call == l.calls - 4) pctl_load();
+            if (call == l.calls - 3)
+            {
+                fast = desc_u32(pv, 2) == seq + 1;
+                if (fast)
+                {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    dw = desc_word_load(pdesc(seq + 1), l.lane);
+                }
+                // group 0: granted already -- published now, two steps before the others need it
+                if (leader && fast && pers_granted(a.seq0, seq + 1, desc_u32(pv, 0), desc_u32(pv, 1)))
+                {
+                    publish(seq + 1, true);
+                    ldone = true;
+                }
+            }
+            if (call == l.calls - 2 && !leader) dv = __hip_atomic_load(pdec(seq + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (call == l.calls - 1) pers_decide();
+        }
+        else if (sch.may_ext)
         {
             if (call == l.calls - 3) peek();
-            if (call == l.calls - 1) decide();
+            if (call == l.calls - 1)
+            {
+                decide();
+                // second chance (UHSDR_LATE_EXT): the next call had not arrived two steps ago -- peek
+                // again now and consume it at this step's end, where the step's work has hidden it
+                if (UHSDR_LATE_EXT && !ext) peek();
+            }
         }
         float xin[NDC];
         if (DM)
@@ -1972,7 +2229,45 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
 #pragma unroll
             for (int m = 0; m < NDC; ++m) po[m * BACK_CH] = s.step(xin[m], m);
         }
+        if (UHSDR_LATE_EXT && !pers && sch.may_ext && call == l.calls - 1 && !ext)
+        {
+            decide();                                  // the LDS word is read after this step's barrier
+            if (ext) in.fetch(a, l, l.calls);          // g = n, consumed by in.begin at the next step
+        }
+#ifdef UHSDR_PDEBUG
+        if (pers && call == l.calls - 1 && ext && blockIdx.x == 0 && l.lane == 0)
+        {
+            g_pdbg[(seq + 1) % 64][4] = __builtin_amdgcn_readfirstlane(in.arrived);
+            g_pdbg[(seq + 1) % 64][7] = in.gave_up;
+        }
+#endif
+        if (pers)
+        {
+            // a give-up poisons the output from here on (the output role reads the word every sub-call)
+            if (l.lane == 0 && in.gave_up) *lds.poison = 1u;
+            // the call's hand-off buffer is read (its last sub-call's samples are in use above): the
+            // host may refill it (no fence: the load of the next call's first sub-call stays in flight)
+            if (call == l.calls - 1 && l.lane == 0)
+            {
+                asm volatile("" ::: "memory");
+                __hip_atomic_store(a.pctl + PC_CONSUMED + blockIdx.x, seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
     BACK_ROLE_END
+        if (!pers || !ext) break;
+        // on into the next call: its buffer and counters become the launch's own
+        a.adec = a.adec_next;
+        a.dwait = a.dwait_next;
+        a.dtarget = a.dnext;
+        a.ring_phase = (a.ring_phase + l.calls) % AGC_Q;
+        seq += 1;
+        sch = BackSched::next(l);
+        glim = l.calls;
+        in.lim = l.calls;
+        ext = false;
+        fast = false;
+        ldone = false;
+    }
     s.store(l, a.s.pre);
     if (DM == DM_SAM) fl.store(a, l);
     if (prep) ag.store(a, l, { true, false });
@@ -1980,8 +2275,9 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a, BackLds lds)
 }
 
 template <int L, int W, int DM>
-__device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
+__device__ __forceinline__ void rx_back_agc(const BackArgs& a0, BackLds lds)
 {
+    BackArgs a = a0;                                   // the call's ring phase moves on (PersistCtl)
     const BackLane l(a);
     constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
@@ -1991,11 +2287,12 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
     s.load(a, l, A);
     BndRegs<4 * NDC> br;
     br.template load<DM>(a, l, 0);
-    const BackSched sch = BackSched::make<DM>(a, l, skw);
+    BackSched sch = BackSched::make<DM>(a, l, skw);
     int glim = l.calls;
     const bool prep = back_agc_prep_in_pre(DM, A);
+    const bool pers = DM == DM_NONE && a.pctl != nullptr;
     const int g0 = sch.gofs - 1;                      // BackSched: this role's first sub-call (if >= 0)
-    if (sch.may_ext) s.lim = l.calls + BACK_SKEW - 1;
+    if (sch.may_ext) s.lim = l.calls + BACK_SKEW - 1 + (pers ? 1 : 0);
     if (!prep) s.fetch(a, l, g0 > 0 ? g0 : 0);
     if (sch.pin)
     {
@@ -2006,6 +2303,8 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
         br.template put<2 * NDC, NDC>(l, lds.prep + 2 * NDC * BACK_CH + o);
         br.template put<3 * NDC, NDC>(l, lds.prep + 4 * NDC * BACK_CH + o);
     }
+    for (;;)
+    {
     BACK_ROLE_LOOP(DM ? 2 : 1)
         const float* pi = lds.pre + (call & 1) * NDC * BACK_CH + l.lane;
         float* ao = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
@@ -2056,6 +2355,11 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a, BackLds lds)
         s.end(l);
         }
     BACK_ROLE_END
+        if (!pers || !back_ext(sch, lds)) break;
+        a.ring_phase = (a.ring_phase + l.calls) % AGC_Q;   // the persistent back end's next call
+        sch = BackSched::next(l);
+        glim = l.calls;
+    }
     s.store(a, l, { !prep, true }, !DM);
     if (back_ext(sch, lds))
     {
@@ -2082,8 +2386,9 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
     const bool dc = DM && agc_on && A.remove_dc;
     BndRegs<2 * NDC> br;
     br.template load<DM>(a, l, 4 * NDC);
-    const BackSched sch = BackSched::make<DM>(a, l, skw);
+    BackSched sch = BackSched::make<DM>(a, l, skw);
     int glim = l.calls;
+    const bool pers = DM == DM_NONE && a.pctl != nullptr;
     if (sch.pin)
     {
         // the AGC role's output (delayed samples, volts) for this role's first sub-call
@@ -2091,6 +2396,8 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
         br.template put<0, NDC>(l, lds.agc + o);
         br.template put<NDC, NDC>(l, lds.dem + o);
     }
+    for (;;)
+    {
     BACK_ROLE_LOOP(DM ? 3 : 2)
         const float* ai = lds.agc + (call & 1) * NDC * BACK_CH + l.lane;
         float* mo = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
@@ -2127,6 +2434,10 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
         }
         s.end(a, l, call);
     BACK_ROLE_END
+        if (!pers || !back_ext(sch, lds)) break;
+        sch = BackSched::next(l);                      // the persistent back end's next call
+        glim = l.calls;
+    }
     s.store(a, l);
     if (DM && l.live) a.s.agc[5 * l.C + l.c] = wold;
     if (back_ext(sch, lds))
@@ -2150,9 +2461,12 @@ __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
     s.load(l, P->aa_k, P->aa_v, a.s.aa);
     BndRegs<BLK> br;
     br.template load<DM>(a, l, a.bnd_mid);
-    const BackSched sch = BackSched::make<DM>(a, l, skw);
+    BackSched sch = BackSched::make<DM>(a, l, skw);
     int glim = l.calls;
+    const bool pers = DM == DM_NONE && a.pctl != nullptr;
     if (sch.pin) br.template put<0, BLK>(l, lds.mid + ((sch.gofs - 3) & 1) * BLK * BACK_CH);
+    for (;;)
+    {
     BACK_ROLE_LOOP(DM ? 4 : 3)
         const float* mi = lds.mid + (call & 1) * BLK * BACK_CH + l.lane;
         float* mo = lds.aa + (call & 1) * BLK * BACK_CH + l.lane;
@@ -2173,12 +2487,19 @@ __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
             mo[(n + 1) * BACK_CH] = y1;
         }
     BACK_ROLE_END
+        if (!pers || !back_ext(sch, lds)) break;
+        sch = BackSched::next(l);                      // the persistent back end's next call
+        glim = l.calls;
+    }
     s.store(l, a.s.aa);
     if (back_ext(sch, lds)) bnd_store<BLK>(a, l, a.bnd_mid, lds.mid + ((l.calls + BACK_SKEW - 3) & 1) * BLK * BACK_CH);
 }
 
 // (2 tail waves took 4500-5500 cycles per step with mcHF codec frames, above the anti-alias role)
-constexpr int BACK_TAILS = 4;
+#ifndef UHSDR_BACK_TAILS
+#define UHSDR_BACK_TAILS 4
+#endif
+constexpr int BACK_TAILS = UHSDR_BACK_TAILS;
 // tail waves of a back end: BACK_TAILS for the demodulator-free pipeline; UHSDR_DM_TAILS for the AM /
 // SAM ones, 0 (the output role stores its call itself): their grids are large (C3: 512 workgroups)
 // and 4 more waves per workgroup took C3's SAM back end from 0.118 to 0.193 ms
@@ -2196,9 +2517,13 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
     s.load(a, l);
     BndRegs<BLK> br;
     br.template load<DM>(a, l, a.bnd_mid + BLK);
-    const BackSched sch = BackSched::make<DM>(a, l, skw);
+    BackSched sch = BackSched::make<DM>(a, l, skw);
     int glim = l.calls;
+    const bool pers = DM == DM_NONE && a.pctl != nullptr;
     if (sch.pin) br.template put<0, BLK>(l, lds.aa + ((sch.gofs - 4) & 1) * BLK * BACK_CH);
+    bool pread = !sch.pin;                             // the poison word is written (see below)
+    for (;;)
+    {
     BACK_ROLE_LOOP(DM ? 5 : 4)
         const float* mi = lds.aa + (call & 1) * BLK * BACK_CH + l.lane;
         float y[BLK];
@@ -2210,8 +2535,10 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
         {
             // the pre role's device hand-off gave up (its step-0 word): NaN audio for every frame.
             // Only a launch that starts unskewed waits (BackSched); a skewed one has this role at
-            // work in step 0, before the word is written, so it must not read it
-            if (!sch.pin && a.dwait && __builtin_amdgcn_readfirstlane(*lds.poison))
+            // work in step 0, before the word is written, so it must not read it.  The persistent
+            // back end waits at every call: its pre role sets the word at a give-up, read every
+            // sub-call after the launch's first call
+            if (pread && a.dwait && __builtin_amdgcn_readfirstlane(*lds.poison))
             {
 #pragma unroll
                 for (int n = 0; n < BLK; ++n) y[n] = __builtin_nanf("");
@@ -2226,6 +2553,11 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
         for (int n = 0; n < BLK; ++n) yl[n] = y[n];
         if constexpr (back_tails(DM) == 0) fused_store_call(a, l, call, lds.ys + (call & 1) * BACK_CH * FUSED_YPITCH);
     BACK_ROLE_END
+        if (!pers || !back_ext(sch, lds)) break;
+        sch = BackSched::next(l);                      // the persistent back end's next call
+        glim = l.calls;
+        pread = true;
+    }
     s.store(a, l);
     if (back_ext(sch, lds)) bnd_store<BLK>(a, l, a.bnd_mid + BLK, lds.aa + ((l.calls + BACK_SKEW - 4) & 1) * BLK * BACK_CH);
 }
@@ -2236,10 +2568,12 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
 // coalesced row stores, each tail wave 64 / BACK_TAILS of the 64 channels' rows; the launch's last call after the
 // final barrier.  Elementwise, so it needs no state and no place in BackSched's skew.
 template <int DM>
-__device__ __forceinline__ void rx_back_tail(const BackArgs& a, BackLds lds, int half)
+__device__ __forceinline__ void rx_back_tail(const BackArgs& a0, BackLds lds, int half)
 {
+    BackArgs a = a0;                                   // the call's outputs (PersistCtl: from lds.desc)
     const BackLane l(a);
-    const BackSched sch = BackSched::make<DM>(a, l, BackSched::word<DM>(a));
+    BackSched sch = BackSched::make<DM>(a, l, BackSched::word<DM>(a));
+    const bool pers = DM == DM_NONE && a.pctl != nullptr;
     constexpr int ST = back_roles(DM);                  // one step behind the output role
     const int g8 = l.lane >> 3, j = l.lane & 7;
     const int c0 = l.c - l.lane;
@@ -2259,16 +2593,22 @@ __device__ __forceinline__ void rx_back_tail(const BackArgs& a, BackLds lds, int
             line_out4(a, rb, off, call, call * BLK + 4 * j, v);
         }
     };
-    for (int it = 0; it < sch.steps; ++it)
+    for (unsigned seq = a.seq0;; ++seq)
     {
-        const int call = it - ST + sch.gofs;
-        TRACE_MARK(0);
-        if (call >= 0 && call < l.calls) store_call(call);
-        TRACE_MARK(1);
-        lds_barrier();
-        TRACE_MARK(2);
+        for (int it = 0; it < sch.steps; ++it)
+        {
+            const int call = it - ST + sch.gofs;
+            TRACE_MARK(0);
+            if (call >= 0 && call < l.calls) store_call(call);
+            TRACE_MARK(1);
+            lds_barrier();
+            TRACE_MARK(2);
+        }
+        store_call(l.calls - 1);
+        if (!pers || !back_ext(sch, lds)) break;
+        desc_get(a, lds.desc + ((seq + 1) & 1) * 16);  // the persistent back end's next call
+        sch = BackSched::next(l);
     }
-    store_call(l.calls - 1);
 }
 #undef BACK_ROLE_END
 
@@ -2294,7 +2634,10 @@ __global__ void __launch_bounds__((back_roles(DM) + back_tails(DM)) * BACK_CH) r
 #ifdef UHSDR_TRACE
     // (tools/trace_back.py) the wave's entry and exit in slot 39
     if ((threadIdx.x & (BACK_CH - 1)) == 0 && blockIdx.x < 64)
+    {
         g_trace[blockIdx.x][threadIdx.x / BACK_CH][39][0] = __builtin_readcyclecounter();
+        g_trace[blockIdx.x][threadIdx.x / BACK_CH][38][0] = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+    }
 #endif
     if (role < 0)
         rx_back_demod<L, DM>(a, lds);
@@ -2317,7 +2660,10 @@ __global__ void __launch_bounds__((back_roles(DM) + back_tails(DM)) * BACK_CH) r
     }
 #ifdef UHSDR_TRACE
     if ((threadIdx.x & (BACK_CH - 1)) == 0 && blockIdx.x < 64)
+    {
         g_trace[blockIdx.x][threadIdx.x / BACK_CH][39][1] = __builtin_readcyclecounter();
+        g_trace[blockIdx.x][threadIdx.x / BACK_CH][38][1] = __builtin_amdgcn_s_memrealtime();
+    }
 #endif
 }
 
@@ -3042,6 +3388,9 @@ constexpr int BACK_FUSED_MIN_CHANNELS = 131072;   // measured crossover (64-fram
 #define UHSDR_PIPE_GROUP 4
 #endif
 constexpr int PIPE_GROUP = UHSDR_PIPE_GROUP;
+#ifndef UHSDR_BACK_SKEW
+#define UHSDR_BACK_SKEW 1
+#endif
 constexpr int PIPE_BUFS = 2 * PIPE_GROUP;
 
 struct uhsdr_rx_s
@@ -3114,6 +3463,17 @@ struct uhsdr_rx_s
     int dflag_grid;          // largest rx_back grid it is used for (half the CUs: the polling
                              // workgroups never crowd out the front they wait for)
     int back_attr;           // rx_back's LDS attribute raised for the reserved launch (1), failed (-1)
+    // persistent back end (uhsdr_rx_set_pipelined 3, PersistCtl): pmem = host-mapped coherent memory,
+    // PC_WORDS control words then DESC_RING call descriptors (pmem_dev: its device address); plive:
+    // a launch may still take the next grant; plast: the last call granted; pprev: the previous call
+    // ran on it (else the next one starts a new run: both streams synchronised, the words reset)
+    int pers;
+    unsigned* pmem;
+    unsigned* pmem_dev;
+    unsigned* pdec;          // device memory: group 0's decision per call (BackArgs::pdec)
+    int plive, pprev;
+    unsigned plast;
+    unsigned plaunches;      // persistent launches since creation (uhsdr_rx_debug_persist)
     int main_back;           // back-end state was last written on the handle's stream (a one-kernel
                              // schedule, a serial call, a reset): the next side-stream rx_back waits
                              // on ev_front, which orders it after that work; the device hand-off
@@ -3134,9 +3494,19 @@ static void time_mark(uhsdr_rx_s* h, int k, int which)
     if (which) h->evmask[h->nev] |= (uint8_t)(1u << k);
 }
 
+// the persistent back end takes no grant past the last one (PersistCtl: PC_CLOSE); its launch ends
+// after that call
+static void pers_close(uhsdr_rx_s* h)
+{
+    if (!h->plive) return;
+    __atomic_store_n(h->pmem + PC_CLOSE, h->plast, __ATOMIC_SEQ_CST);
+    h->plive = 0;
+}
+
 // every call enqueued so far, on both streams, has finished
 static hipError_t sync_all(uhsdr_rx_s* h)
 {
+    pers_close(h);
     hipError_t e = hipStreamSynchronize(h->stream);
     if (e == hipSuccess && h->side) e = hipStreamSynchronize(h->side);
     return e;
@@ -3399,6 +3769,7 @@ extern "C" uhsdr_status uhsdr_rx_reset(uhsdr_rx_handle h)
     *h->fail_host = 0;
     memset(h->fills, 0, sizeof h->fills);
     h->main_back = 1;
+    h->pprev = 0;
     if (h->bs.cw)
     {
         // old_siglevel starts at 0.001 (function static, cw_decoder.c:189)
@@ -3719,6 +4090,10 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     ba.skew = h->skew;
     ba.bnd = h->bnd;
     ba.bnd_mid = h->bnd ? 6 * (BLK / h->plan.interp_L) : 0;   // (FM has no interpolator: interp_L 0)
+    ba.pctl = nullptr;
+    ba.pdesc = nullptr;
+    ba.pdec = nullptr;
+    ba.seq0 = 0;
     {
         // key beep: frames [0, beep_n1) of this launch while calls are left (uhsdr_rx_key_beep)
         const int calls = h->N / BLK;
@@ -3795,11 +4170,6 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         const bool group_end = h->pipelined && pk % PIPE_GROUP == PIPE_GROUP - 1;
         float* adec = par ? h->adecp[par - 1] : h->adec;
         float* adec_q = par ? h->adec_qp[par - 1] : h->adec_q;
-        // (Measured and dropped in round 6, profiles/r06_c2_ab_group.txt: skipping this wait when a
-        // host query finds the event complete, and groups of 8 or 16 calls: no gain at 20 steps,
-        // 0.0229-0.0235 vs 0.0221 ms at 1000 steps for the larger rotations)
-        if (side_mode(h) && pk % PIPE_GROUP == 0) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[grp], 0));
-        time_mark(h, K_FRONT, 0);
         const int cpw = FRONT_WAVE / (h->Nf / h->fv->R);
         const size_t lds = front_lds(h);
         const bool side = side_mode(h);
@@ -3815,6 +4185,54 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         const bool dfl = side && h->dflag && !h->main_back && !fused && !h->nv && !h->fv->st &&
                          h->bv->dm == DM_NONE && bgroups <= h->dflag_grid;
         unsigned* const gc = h->gcnt + (size_t)par * bgroups * CNT_PITCH;
+        // persistent back end (PersistCtl): the wave pipeline's skewed form, calls of 8+ sub-calls
+        const bool pm = dfl && h->pers && h->skew && UHSDR_BACK_SKEW && h->N / BLK >= 2 * BACK_SKEW && !h->bs.cw &&
+                        bgroups <= PC_MAX_GROUPS;
+        const unsigned seq = (unsigned)pk;
+        unsigned* const pw = h->pmem;
+        if (!pm && h->plive) HIPCHK(sync_all(h));     // leaving it: its launch ends, and everything completes
+        if (pm && !h->pprev)
+        {
+            // a new run: the buffers are free once everything enqueued has completed
+            HIPCHK(sync_all(h));
+            // no call's decision yet (ordered before the run's first launch on the side stream)
+            HIPCHK(hipMemsetAsync(h->pdec, 0xFF, sizeof(unsigned) * DESC_RING * PDEC_PITCH, h->side));
+            for (int g = 0; g < bgroups; ++g) __atomic_store_n(pw + PC_CONSUMED + g, seq, __ATOMIC_SEQ_CST);
+            __atomic_store_n(pw + PC_GRANT, seq - 1, __ATOMIC_SEQ_CST);
+            __atomic_store_n(pw + PC_CLOSE, seq - 1, __ATOMIC_SEQ_CST);
+            __atomic_store_n(pw + PC_EXIT, seq - 2, __ATOMIC_SEQ_CST);
+            __atomic_store_n(pw + PC_DECIDED, ((seq - 2) << 1) | 1u, __ATOMIC_SEQ_CST);
+        }
+        h->pprev = pm;
+        if (pm)
+        {
+            // the buffer (and descriptor) of call seq - PIPE_BUFS is refilled once the back end has
+            // read it: the host waits (seconds at most: a give-up still moves the word on)
+            const unsigned need = seq - (PIPE_BUFS - 1);
+            auto behind = [&]() {
+                for (int g = 0; g < bgroups; ++g)
+                    if ((int)(__atomic_load_n(pw + PC_CONSUMED + g, __ATOMIC_ACQUIRE) - need) < 0) return true;
+                return false;
+            };
+            if (behind())
+            {
+                const auto t0 = std::chrono::steady_clock::now();
+                while (behind())
+                {
+                    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
+                    {
+                        uhsdr_set_error("persistent back end: call %u's hand-off buffer not released within 30 s", seq);
+                        return UHSDR_TIMEOUT;
+                    }
+                }
+            }
+        }
+        // (Measured and dropped in round 6, profiles/r06_c2_ab_group.txt: skipping this wait when a
+        // host query finds the event complete, and groups of 8 or 16 calls: no gain at 20 steps,
+        // 0.0229-0.0235 vs 0.0221 ms at 1000 steps for the larger rotations)
+        else if (side_mode(h) && pk % PIPE_GROUP == 0)
+            HIPCHK(hipStreamWaitEvent(h->stream, h->ev_back[grp], 0));
+        time_mark(h, K_FRONT, 0);
         for (int f0 = 0; f0 < h->N; f0 += h->Nf)
         {
             FrontArgs fa = front_args(h, iq, f0, adec, adec_q);
@@ -3843,9 +4261,6 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             bk.dwait = gc;
             bk.dtarget = h->fills[par];
             bk.fcpw = cpw;
-#ifndef UHSDR_BACK_SKEW
-#define UHSDR_BACK_SKEW 1
-#endif
             // BackSched: run ahead into the next call if it has arrived by then.  The next buffer
             // of the rotation is filled next by the next call only (its later reuse waits for this
             // launch: ev_back), and its counters move only with a device hand-off front -- whose
@@ -3859,6 +4274,59 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
                 bk.adec_next = parn ? h->adecp[parn - 1] : h->adec;
                 bk.dwait_next = h->gcnt + (size_t)parn * bgroups * CNT_PITCH;
                 bk.dnext = h->fills[parn] + (unsigned)((h->N + h->Nf - 1) / h->Nf);
+            }
+        }
+        bool plaunch = true;
+        if (pm)
+        {
+            // the call's descriptor, then its grant; a running launch takes it unless it is closing
+            // after the previous call (PC_EXIT): then its decision tells (PersistCtl)
+            BackDesc* d = (BackDesc*)(pw + PC_WORDS) + seq % DESC_RING;
+            d->adec = adec;
+            d->cnt = gc;
+            d->audio = bk.audio;
+            d->audio0 = bk.audio0;
+            d->dst = bk.dst;
+            d->target = h->fills[par];
+            d->beep_n0 = bk.beep_n0;
+            d->beep_n1 = bk.beep_n1;
+            d->beep_acc = bk.beep_acc;
+            __atomic_store_n(&d->seq, seq, __ATOMIC_RELEASE);
+#ifdef UHSDR_PDEBUG
+            fprintf(stderr, "host call %u: adec %p cnt %p target %u dst %p waves(g0)x? live %d\n", seq, (void*)adec,
+                    (void*)gc, h->fills[par], (void*)bk.dst, h->plive);
+#endif
+            __atomic_store_n(pw + PC_GRANT, seq, __ATOMIC_SEQ_CST);
+            if (h->plive)
+            {
+                plaunch = false;
+                if (__atomic_load_n(pw + PC_EXIT, __ATOMIC_SEQ_CST) == seq - 1)
+                {
+                    const unsigned want = (seq - 1) & 0x7FFFFFFFu;
+                    const auto t0 = std::chrono::steady_clock::now();
+                    unsigned dv;
+                    while (((dv = __atomic_load_n(pw + PC_DECIDED, __ATOMIC_ACQUIRE)) >> 1) != want)
+                    {
+                        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
+                        {
+                            uhsdr_set_error("persistent back end: no decision after call %u within 30 s", seq - 1);
+                            return UHSDR_TIMEOUT;
+                        }
+                    }
+                    plaunch = dv & 1u;               // it closed: a new launch takes this call
+                }
+            }
+            h->plast = seq;
+            if (plaunch)
+            {
+                bk.pctl = h->pmem_dev;
+                bk.pdesc = (const BackDesc*)(h->pmem_dev + PC_WORDS);
+                bk.pdec = h->pdec;
+                bk.seq0 = seq;
+                bk.adec_next = nullptr;
+                bk.dwait_next = nullptr;
+                h->plive = 1;
+                h->plaunches += 1;
             }
         }
         const hipStream_t bst = back_stream(h);
@@ -3895,8 +4363,13 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             }
             if (h->back_attr > 0) blds = LDS_PER_CU - 4096;
         }
-        // pipelined: the group's last rx_back records ev_back[grp] as it completes
-        if (side && group_end)
+        // pipelined: the group's last rx_back records ev_back[grp] as it completes (the persistent
+        // back end: a launch only to start a run of calls; the buffers' reuse waits on PC_CONSUMED)
+        if (pm)
+        {
+            if (plaunch) hipLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, bk);
+        }
+        else if (side && group_end)
             hipExtLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, nullptr, h->ev_back[grp], 0, bk);
         else
             hipLaunchKernelGGL(bfn, bgrid, bblock, blds, bst, bk);
@@ -4015,9 +4488,24 @@ extern "C" uhsdr_status uhsdr_rx_set_front_block(uhsdr_rx_handle h, int32_t outp
     return UHSDR_OK;
 }
 
+// test hook: the persistent back end's control words (PC_GRANT, PC_CLOSE, PC_EXIT, PC_DECIDED,
+// PC_CONSUMED) and the host's plive / plast / plaunches
+extern "C" uhsdr_status uhsdr_rx_debug_persist(uhsdr_rx_handle h, uint32_t* out)
+{
+    if (!h || !out) return UHSDR_ARGUMENT_ERROR;
+    if (!h->pmem) return UHSDR_UNSUPPORTED;
+    const int w[5] = { PC_GRANT, PC_CLOSE, PC_EXIT, PC_DECIDED, PC_CONSUMED };
+    for (int i = 0; i < 5; ++i) out[i] = __atomic_load_n(h->pmem + w[i], __ATOMIC_SEQ_CST);   // (group 0's PC_CONSUMED)
+    out[5] = (uint32_t)h->plive;
+    out[6] = h->plast;
+    out[7] = h->plaunches;
+    return UHSDR_OK;
+}
+
 extern "C" uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
+    pers_close(h);                                     // the persistent back end ends after the last call
     if (side_mode(h))
     {
         HIPCHK(hipEventRecord(h->ev_join, h->side));
@@ -4029,11 +4517,21 @@ extern "C" uhsdr_status uhsdr_rx_join(uhsdr_rx_handle h)
 extern "C" uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable)
 {
     if (!h) return UHSDR_ARGUMENT_ERROR;
-    if (enable < 0 || enable > 2)
+    if (enable < 0 || enable > 3)
     {
-        uhsdr_set_error("pipelined mode %d: 0 (off), 1 (event hand-off) or 2 (device hand-off)", (int)enable);
+        uhsdr_set_error("pipelined mode %d: 0 (off), 1 (event hand-off), 2 (device hand-off) or 3 (persistent "
+                        "back end)", (int)enable);
         return UHSDR_ARGUMENT_ERROR;
     }
+    if (enable == 3 && !h->pmem)
+    {
+        HIPCHK(hipHostMalloc((void**)&h->pmem, PC_BYTES, hipHostMallocCoherent | hipHostMallocMapped));
+        memset(h->pmem, 0, PC_BYTES);
+        HIPCHK(hipHostGetDevicePointer((void**)&h->pmem_dev, h->pmem, 0));
+        HIPCHK(hipMalloc((void**)&h->pdec, sizeof(unsigned) * DESC_RING * PDEC_PITCH));
+    }
+    // into or out of the persistent back end: everything enqueued completes first
+    if ((enable == 3) != (h->pers != 0)) HIPCHK(sync_all(h));
     if (enable && !h->side)
     {
         const size_t nd = (size_t)h->C * h->Nd;
@@ -4065,7 +4563,9 @@ extern "C" uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable
         h->pipe_calls = 0;
     }
     h->pipelined = enable != 0;
-    h->dflag = enable == 2;
+    h->dflag = enable >= 2;
+    h->pers = enable == 3;
+    h->pprev = 0;
     if (h->dflag && !h->dflag_grid)
     {
         int dev = 0, cus = 0;
@@ -4171,6 +4671,8 @@ extern "C" uhsdr_status uhsdr_rx_destroy(uhsdr_rx_handle h)
     if (h->d_lanemap) (void)hipFree(h->d_lanemap);
     if (h->gcnt) (void)hipFree(h->gcnt);
     if (h->fail_host) (void)hipHostFree((void*)h->fail_host);
+    if (h->pmem) (void)hipHostFree(h->pmem);
+    if (h->pdec) (void)hipFree(h->pdec);
     free(h);
     return UHSDR_OK;
 }

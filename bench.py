@@ -132,7 +132,7 @@ def cpu_baseline(plan, frames: int, budget_s: float = 10.0):
 
 
 SCHEDULES = {"auto": None, "pipe": 1, "fused": 2, "chain": 3}   # uhsdr_rx_set_schedule
-DEVICE_HANDOFF = 2       # --handoff: uhsdr_rx_set_pipelined's mode (event 1, device 2, persistent 3)
+DEVICE_HANDOFF = 3       # --handoff: uhsdr_rx_set_pipelined's mode (event 1, device 2, persistent 3)
 SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain"}
 
 
@@ -277,11 +277,12 @@ def main():
                          "kernels fill the chip there)")
     ap.add_argument("--pipelined", action="store_true",
                     help="pipelined mode even on the north-star workload (default on for the others)")
-    ap.add_argument("--handoff", default="device", choices=["event", "device", "persistent"],
-                    help="pipelined mode's front -> back hand-off: rx_back polling the arrival counters "
-                         "its channel group's front waves bump (uhsdr_rx_set_pipelined 2, the default: no "
-                         "cross-stream wait per call), a cross-stream event per call (1), or the "
-                         "persistent back end (3: one rx_back launch runs call after call)")
+    ap.add_argument("--handoff", default="persistent", choices=["event", "device", "persistent"],
+                    help="pipelined mode's front -> back hand-off: the persistent back end (uhsdr_rx_set_"
+                         "pipelined 3, the default: one rx_back launch runs call after call, taking each "
+                         "call the host grants), rx_back per call polling the arrival counters its channel "
+                         "group's front waves bump (2: no cross-stream wait per call), or a cross-stream "
+                         "event per call (1; for profilers that serialise dispatches)")
     ap.add_argument("--precision", default="exact", choices=["exact", "fma"],
                     help="FIR MACs: exact (bit-identical to the reference) or fma (1e-5 normwise)")
     ap.add_argument("--pool", type=int, default=8, help="distinct input blocks cycled through")

@@ -320,8 +320,8 @@ uhsdr_status uhsdr_rx_set_pipelined(uhsdr_rx_handle h, int32_t enable);
    failure contract.  0 is UHSDR_ARGUMENT_ERROR.  A running persistent launch keeps the bound it
    started with. */
 uhsdr_status uhsdr_rx_set_handoff_bound(uhsdr_rx_handle h, uint32_t polls);
-/* Test hook of the persistent back end (enable = 3): out[0..7] = its grant, close, exit and decision
-   words, group 0's consumed word, whether a launch may take the next grant, the last call granted,
+/* Test hook of the persistent back end (enable = 3): out[0..7] = its grant word, the launch epoch,
+   its exit and decision words, group 0's consumed word, whether a launch may take the next grant, the last call granted,
    and the launches started.  UHSDR_UNSUPPORTED before the mode was first entered. */
 uhsdr_status uhsdr_rx_debug_persist(uhsdr_rx_handle h, uint32_t* out);
 /* 1 if a device hand-off poll gave up since the last uhsdr_rx_reset, else 0; -1 on error.

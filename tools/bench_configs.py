@@ -54,7 +54,7 @@ def time_calls(fn, steps, warmup, join=None):
 
 
 FRONT_BLOCK = 0     # --front-block: the RX lines' front outputs per lane (0 = the library's choice)
-HANDOFF = "device"  # --handoff: the pipelined RX lines' front -> back hand-off (uhsdr_rx_set_pipelined 2 / 1)
+HANDOFF = "persistent"  # --handoff: the pipelined RX lines' front -> back hand-off (uhsdr_rx_set_pipelined 3 / 2 / 1)
 
 
 def rx_line(name, cfg, C, N, iq, steps, warmup, cw=False, pipelined=False):
@@ -66,7 +66,7 @@ def rx_line(name, cfg, C, N, iq, steps, warmup, cw=False, pipelined=False):
     if FRONT_BLOCK:
         chain.set_front_block(FRONT_BLOCK)
     if pipelined:
-        chain.set_pipelined(2 if HANDOFF == "device" else True)
+        chain.set_pipelined({"event": 1, "device": 2, "persistent": 3}[HANDOFF])
     audio = torch.empty((C, N), dtype=torch.float32, device="cuda")
     if cw:
         sig = torch.empty((C, N // 32), dtype=torch.uint8, device="cuda")
@@ -102,8 +102,9 @@ def main():
                     help="C4 FM-RX / SSB-TX handles in their serial mode (default: pipelined, measured faster there; "
                          "C3 SAM and C5 CW run serial, where the pipelined mode measured slower / the same)")
     ap.add_argument("--front-block", type=int, default=0, choices=[0, 8, 16], help="RX lines: front outputs per lane")
-    ap.add_argument("--handoff", default="device", choices=["event", "device"],
-                    help="pipelined RX lines: the device hand-off (uhsdr_rx_set_pipelined 2) or a cross-stream event")
+    ap.add_argument("--handoff", default="persistent", choices=["event", "device", "persistent"],
+                    help="pipelined RX lines: the persistent back end (uhsdr_rx_set_pipelined 3; other back ends "
+                         "fall back to 2), the device hand-off (2) or a cross-stream event (1)")
     a = ap.parse_args()
     global FRONT_BLOCK, HANDOFF
     FRONT_BLOCK = a.front_block

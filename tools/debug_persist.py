@@ -25,7 +25,7 @@ def main():
     xs = [synth.ssb_iq_torch(0, Cn, k * N, N, torch.device("cuda")) for k in range(calls)]
     audio = torch.empty((calls, Cn, N), dtype=torch.float32, device="cuda")
     w = (C.c_uint32 * 7)()
-    names = ["grant", "close", "exit", "decided", "consumed", "plive", "plast"]
+    names = ["grant", "epoch", "exit", "decided", "consumed", "plive", "plast"]
 
     def show(tag):
         lib.uhsdr_rx_debug_persist(chain.handle, w)

@@ -32,12 +32,22 @@ def main():
         dst = torch.empty((calls, Cn, N, 2), dtype=torch.int32, device="cuda") if "dst" in opts else None
         torch.cuda.synchronize()
         for k in range(calls):
-            chain.process(xs[k], audio[k], dst[k] if dst is not None else None)
-            if "join" in opts:
-                chain.join()
+            try:
+                chain.process(xs[k], audio[k], dst[k] if dst is not None else None)
+                if "join" in opts:
+                    chain.join()
+            except U.UhsdrError as e:
+                print("call", k, "raised", e.status, flush=True)
+            if mode == 3 and "trace" in opts:
+                w = (C.c_uint32 * 8)()
+                lib.uhsdr_rx_debug_persist(chain.handle, w)
+                print("  after call", k, list(w), flush=True)
             if pause:
                 time.sleep(pause)
-        chain.synchronize()
+        try:
+            chain.synchronize()
+        except U.UhsdrError as e:
+            print("synchronize raised", e.status, flush=True)
         if mode == 3:
             w = (C.c_uint32 * 8)()
             lib.uhsdr_rx_debug_persist(chain.handle, w)
@@ -55,7 +65,8 @@ def main():
                     print(f"dev call {int(r[0])}: adec {int(r[1]):#x} cnt {int(r[2]):#x} target {int(r[3])} "
                           f"arrived {int(r[4])} dst {int(r[5]):#x} fast {int(r[6])} gave_up {int(r[7])}", flush=True)
         outs[mode] = audio.cpu().numpy()
-        print("mode", mode, "timeouts", chain.handoff_timeouts(), flush=True)
+        print("mode", mode, "timeouts", chain.handoff_timeouts(), "nan calls",
+              [k for k in range(calls) if not np.isfinite(outs[mode][k]).all()], flush=True)
         chain.close()
     if 2 not in outs:
         return

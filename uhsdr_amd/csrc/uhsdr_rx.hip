@@ -700,6 +700,7 @@ struct BackArgs
     const struct BackDesc* pdesc;
     unsigned* pdec;
     unsigned seq0;
+    unsigned pepoch;     // this launch's epoch: PC_GRANT's top byte while the host grants it calls
 };
 
 // Persistent back end (uhsdr_rx_set_pipelined 3).  One rx_back launch runs call after call with its
@@ -712,9 +713,11 @@ struct BackArgs
 // grant it closes: it stores k - 1 to PC_EXIT, re-reads the grant after a sequentially consistent
 // fence and stores its decision to PC_DECIDED; the host, after granting k, reads PC_EXIT and, when it
 // finds k - 1 there, waits for that decision and relaunches if the kernel closed (Dekker: one of the
-// two sees the other's store).  PC_CLOSE ends a launch at a given call (uhsdr_rx_join and every
-// synchronisation point), PC_CONSUMED orders the hand-off buffers' reuse (the host waits before
-// overwriting the buffer of call k - PIPE_BUFS until every channel group has read it).  The decision is
+// two sees the other's store).  The grant word carries the launch's epoch (BackArgs::pepoch): uhsdr_rx_join
+// and every synchronisation point end a launch after the calls granted so far by moving the host on to
+// the next epoch, so the launch finds no more grants of its own (grant and close in one word: lanes of
+// one load may see two words at different times).  PC_CONSUMED orders the hand-off buffers' reuse (the
+// host waits before overwriting the buffer of call k - PIPE_BUFS until every channel group has read it).  The decision is
 // the launch's, not each workgroup's: group 0's pre role makes it (the host protocol above) and
 // publishes it per call in device memory (BackArgs::pdec); the other groups read it there, so all of
 // them run the same calls.
@@ -734,7 +737,7 @@ struct BackDesc
 };
 static_assert(sizeof(BackDesc) == 64, "one descriptor per 64 B");
 // control words (unsigned, 64 B apart)
-enum { PC_GRANT = 0, PC_CLOSE = 16, PC_EXIT = 32, PC_DECIDED = 48, PC_WORDS = 64 };
+enum { PC_GRANT = 0, PC_EXIT = 32, PC_DECIDED = 48, PC_WORDS = 64 };
 // then the descriptors, then one PC_CONSUMED word per channel group (PC_MAX_GROUPS)
 constexpr int PC_CONSUMED = PC_WORDS + DESC_RING * 16, PC_MAX_GROUPS = 256;
 constexpr int PC_BYTES = 4 * (PC_CONSUMED + PC_MAX_GROUPS);
@@ -896,7 +899,7 @@ __device__ __forceinline__ void dflag_wait(const BackArgs& a, const unsigned* cn
 
 // DW: the launch may take the pipelined device hand-off (BackArgs::dwait; rx_back's pre role
 // only -- the fused back ends keep the code out of their register budget)
-template <int L, bool LDS_IN = false, bool DW = false>
+template <int L, bool LDS_IN = false, bool DW = false, bool PERS = false>
 struct InStage
 {
     static constexpr int NDC = BLK / L;
@@ -929,7 +932,7 @@ struct InStage
             // read only after the pre role's peek found it published)
             if (call == 0) dflag_wait(a, a.dwait, a.dtarget, gave_up);
             // the persistent back end runs on into a granted call before its front has arrived
-            if (a.pctl && call == l.calls)
+            if (PERS && a.pctl && call == l.calls)
             {
                 dflag_wait(a, a.dwait_next, a.dnext, gave_up);
 #ifdef UHSDR_PDEBUG
@@ -1832,7 +1835,7 @@ struct BackSched
         if constexpr (DM == DM_NONE) return a.skew ? a.skew[blockIdx.x] : 0;
         else return 0;
     }
-    template <int DM>
+    template <int DM, bool PERS = false>
     __device__ __forceinline__ static BackSched make(const BackArgs& a, const BackLane& l, int w)
     {
         BackSched s;
@@ -1841,7 +1844,7 @@ struct BackSched
         if constexpr (DM == DM_NONE)
         {
             s.pin = __builtin_amdgcn_readfirstlane(w) != 0;
-            s.may_ext = a.adec_next != nullptr || a.pctl != nullptr;
+            s.may_ext = a.adec_next != nullptr || (PERS && a.pctl != nullptr);
         }
         s.gofs = s.pin ? BACK_SKEW : 0;
         s.steps = l.calls + (s.pin ? 0 : back_roles(DM) - 1);
@@ -1879,11 +1882,12 @@ __device__ __forceinline__ unsigned sys_load(const unsigned* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// call s may run in the launch that started at call seq0: granted, and no close at or past seq0 before it
-__device__ __forceinline__ bool pers_granted(unsigned seq0, unsigned s, unsigned grant, unsigned close_at)
+// PC_GRANT = epoch << 24 | the last call granted (24 bits): one word, so a launch never sees a later
+// launch's grant (a close is the host moving on to the next epoch); call s may run in the launch of
+// epoch `epoch` if the word carries that epoch and a call at or past s
+__device__ __forceinline__ bool pers_granted(unsigned epoch, unsigned s, unsigned grant)
 {
-    const bool closed = (int)(close_at - seq0) >= 0 && (int)(s - close_at) > 0;
-    return (int)(grant - s) >= 0 && !closed;
+    return (grant >> 24) == (epoch & 0xFFu) && (int)(((grant & 0xFFFFFFu) - (s & 0xFFFFFFu)) << 8) >= 0;
 }
 // a descriptor, one 32-bit word per lane 0..15 (one VGPR while its loads are in flight; PersistCtl)
 __device__ __forceinline__ unsigned desc_word_load(const BackDesc* d, int lane)
@@ -2002,7 +2006,7 @@ __device__ __forceinline__ bool back_agc_prep_in_pre(int dm, const uhsdr_agc_pla
 }
 
 // IIR lattice pre-filter; input: rx_front's decimated I +- Q (SSB) or the demod role's output
-template <int PRE, int L, int W, int DM>
+template <int PRE, int L, int W, int DM, bool PERS>
 __device__ __forceinline__ void rx_back_pre(const BackArgs& a0, BackLds lds)
 {
     BackArgs a = a0;                                   // the call's (the persistent back end moves it on)
@@ -2010,7 +2014,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a0, BackLds lds)
     constexpr int NDC = BLK / L;
     const uhsdr_rx_plan* __restrict__ P = a.plan;
     const int skw = BackSched::word<DM>(a);
-    InStage<L, false, true> in;
+    InStage<L, false, true, PERS> in;
     LatticeStage<PRE> s;
     s.load(l, P->pre_k, P->pre_v, a.s.pre);
     const uhsdr_agc_plan A = P->agc;
@@ -2026,7 +2030,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a0, BackLds lds)
         in.fetch(a, l, BACK_SKEW);
         if (prep) ag.fetch(a, l, BACK_SKEW);
     }
-    BackSched sch = BackSched::make<DM>(a, l, skw);
+    BackSched sch = BackSched::make<DM, PERS>(a, l, skw);
     const bool have = spec && sch.pin;                 // g0's input and ring slot are in flight
     int glim = l.calls;
     // BackSched: the first sub-call of this role, and whether it runs ahead into the next call -- a
@@ -2049,18 +2053,18 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a0, BackLds lds)
     // the persistent back end (PersistCtl): four sub-calls before the end of a call the grant, the
     // close word and the next descriptor's seq are read; the descriptor itself once its seq has
     // arrived (written before it); the decision at the call's last sub-call (pers_decide)
-    const bool pers = DM == DM_NONE && a.pctl != nullptr;
+    const bool pers = PERS && DM == DM_NONE && a.pctl != nullptr;
     unsigned seq = a.seq0;
-    // lane 0 PC_GRANT, lane 1 PC_CLOSE, lane 2 the next descriptor's seq; then the descriptor, word
-    // per lane (one VGPR each while in flight)
+    // lane 0 PC_GRANT, lane 2 the next descriptor's seq (one load: the two may be seen at different
+    // times, hence the grant's epoch in the same word as the call); then the descriptor, word per lane
+    // (one VGPR each while in flight)
     unsigned pv = 0, dw = 0, dv = 0;
     bool fast = false;                                 // the next descriptor was found complete
     bool ldone = false;                                // group 0: the decision is published
     const bool leader = blockIdx.x == 0;
     auto pdesc = [&](unsigned k) { return a.pdesc + (k % DESC_RING); };
     auto pctl_load = [&]() {
-        const unsigned* p = l.lane == 0 ? a.pctl + PC_GRANT : l.lane == 1 ? a.pctl + PC_CLOSE
-                                                                         : (const unsigned*)pdesc(seq + 1) + DW_SEQ;
+        const unsigned* p = l.lane == 0 ? a.pctl + PC_GRANT : (const unsigned*)pdesc(seq + 1) + DW_SEQ;
         pv = sys_load(p);
     };
     auto pdec = [&](unsigned k) { return a.pdec + (k % DESC_RING) * PDEC_PITCH; };
@@ -2076,7 +2080,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a0, BackLds lds)
             if (l.lane == 0) __hip_atomic_store(a.pctl + PC_EXIT, seq, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
             pctl_load();
-            go = pers_granted(a.seq0, s1, desc_u32(pv, 0), desc_u32(pv, 1));
+            go = pers_granted(a.pepoch, s1, desc_u32(pv, 0));
             if (go)
             {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // the descriptor was written before the grant
@@ -2164,7 +2168,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a0, BackLds lds)
                     dw = desc_word_load(pdesc(seq + 1), l.lane);
                 }
                 // group 0: granted already -- published now, two steps before the others need it
-                if (leader && fast && pers_granted(a.seq0, seq + 1, desc_u32(pv, 0), desc_u32(pv, 1)))
+                if (leader && fast && pers_granted(a.pepoch, seq + 1, desc_u32(pv, 0)))
                 {
                     publish(seq + 1, true);
                     ldone = true;
@@ -2274,7 +2278,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a0, BackLds lds)
     if (DM == DM_NONE && a.skew && l.lane == 0) a.skew[blockIdx.x] = ext ? 1 : 0;   // the next launch's `pin`
 }
 
-template <int L, int W, int DM>
+template <int L, int W, int DM, bool PERS>
 __device__ __forceinline__ void rx_back_agc(const BackArgs& a0, BackLds lds)
 {
     BackArgs a = a0;                                   // the call's ring phase moves on (PersistCtl)
@@ -2287,10 +2291,10 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a0, BackLds lds)
     s.load(a, l, A);
     BndRegs<4 * NDC> br;
     br.template load<DM>(a, l, 0);
-    BackSched sch = BackSched::make<DM>(a, l, skw);
+    BackSched sch = BackSched::make<DM, PERS>(a, l, skw);
     int glim = l.calls;
     const bool prep = back_agc_prep_in_pre(DM, A);
-    const bool pers = DM == DM_NONE && a.pctl != nullptr;
+    const bool pers = PERS && DM == DM_NONE && a.pctl != nullptr;
     const int g0 = sch.gofs - 1;                      // BackSched: this role's first sub-call (if >= 0)
     if (sch.may_ext) s.lim = l.calls + BACK_SKEW - 1 + (pers ? 1 : 0);
     if (!prep) s.fetch(a, l, g0 > 0 ? g0 : 0);
@@ -2371,7 +2375,7 @@ __device__ __forceinline__ void rx_back_agc(const BackArgs& a0, BackLds lds)
     }
 }
 
-template <int L, int PH, int W, int DM>
+template <int L, int PH, int W, int DM, bool PERS>
 __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
@@ -2386,9 +2390,9 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
     const bool dc = DM && agc_on && A.remove_dc;
     BndRegs<2 * NDC> br;
     br.template load<DM>(a, l, 4 * NDC);
-    BackSched sch = BackSched::make<DM>(a, l, skw);
+    BackSched sch = BackSched::make<DM, PERS>(a, l, skw);
     int glim = l.calls;
-    const bool pers = DM == DM_NONE && a.pctl != nullptr;
+    const bool pers = PERS && DM == DM_NONE && a.pctl != nullptr;
     if (sch.pin)
     {
         // the AGC role's output (delayed samples, volts) for this role's first sub-call
@@ -2449,7 +2453,7 @@ __device__ __forceinline__ void rx_back_audio(const BackArgs& a, BackLds lds)
 }
 
 // anti-alias lattice at 48 ksps
-template <int AA, int DM>
+template <int AA, int DM, bool PERS>
 __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
@@ -2461,9 +2465,9 @@ __device__ __forceinline__ void rx_back_aa(const BackArgs& a, BackLds lds)
     s.load(l, P->aa_k, P->aa_v, a.s.aa);
     BndRegs<BLK> br;
     br.template load<DM>(a, l, a.bnd_mid);
-    BackSched sch = BackSched::make<DM>(a, l, skw);
+    BackSched sch = BackSched::make<DM, PERS>(a, l, skw);
     int glim = l.calls;
-    const bool pers = DM == DM_NONE && a.pctl != nullptr;
+    const bool pers = PERS && DM == DM_NONE && a.pctl != nullptr;
     if (sch.pin) br.template put<0, BLK>(l, lds.mid + ((sch.gofs - 3) & 1) * BLK * BACK_CH);
     for (;;)
     {
@@ -2508,7 +2512,7 @@ constexpr int BACK_TAILS = UHSDR_BACK_TAILS;
 #define UHSDR_DM_TAILS 0
 #endif
 __host__ __device__ constexpr int back_tails(int dm) { return dm == DM_NONE ? BACK_TAILS : UHSDR_DM_TAILS; }
-template <int DM>
+template <int DM, bool PERS>
 __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
 {
     const BackLane l(a);
@@ -2517,9 +2521,9 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
     s.load(a, l);
     BndRegs<BLK> br;
     br.template load<DM>(a, l, a.bnd_mid + BLK);
-    BackSched sch = BackSched::make<DM>(a, l, skw);
+    BackSched sch = BackSched::make<DM, PERS>(a, l, skw);
     int glim = l.calls;
-    const bool pers = DM == DM_NONE && a.pctl != nullptr;
+    const bool pers = PERS && DM == DM_NONE && a.pctl != nullptr;
     if (sch.pin) br.template put<0, BLK>(l, lds.aa + ((sch.gofs - 4) & 1) * BLK * BACK_CH);
     bool pread = !sch.pin;                             // the poison word is written (see below)
     for (;;)
@@ -2567,13 +2571,13 @@ __device__ __forceinline__ void rx_back_output(const BackArgs& a, BackLds lds)
 // rows in ys) through the board's output stage (line_out4: key beep, mcHF gains, codec frames) to
 // coalesced row stores, each tail wave 64 / BACK_TAILS of the 64 channels' rows; the launch's last call after the
 // final barrier.  Elementwise, so it needs no state and no place in BackSched's skew.
-template <int DM>
+template <int DM, bool PERS>
 __device__ __forceinline__ void rx_back_tail(const BackArgs& a0, BackLds lds, int half)
 {
     BackArgs a = a0;                                   // the call's outputs (PersistCtl: from lds.desc)
     const BackLane l(a);
-    BackSched sch = BackSched::make<DM>(a, l, BackSched::word<DM>(a));
-    const bool pers = DM == DM_NONE && a.pctl != nullptr;
+    BackSched sch = BackSched::make<DM, PERS>(a, l, BackSched::word<DM>(a));
+    const bool pers = PERS && DM == DM_NONE && a.pctl != nullptr;
     constexpr int ST = back_roles(DM);                  // one step behind the output role
     const int g8 = l.lane >> 3, j = l.lane & 7;
     const int c0 = l.c - l.lane;
@@ -2614,7 +2618,7 @@ __device__ __forceinline__ void rx_back_tail(const BackArgs& a0, BackLds lds, in
 
 // PRE / AA lattice stages, L interpolation factor, PH polyphase length, W AGC window,
 // DM demodulator (DM_NONE: SSB/CW/DIGI)
-template <int PRE, int AA, int L, int PH, int W, int DM>
+template <int PRE, int AA, int L, int PH, int W, int DM, bool PERS = false>
 __global__ void __launch_bounds__((back_roles(DM) + back_tails(DM)) * BACK_CH) rx_back(BackArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -2642,21 +2646,21 @@ __global__ void __launch_bounds__((back_roles(DM) + back_tails(DM)) * BACK_CH) r
     if (role < 0)
         rx_back_demod<L, DM>(a, lds);
     else if (role == 0)
-        rx_back_pre<PRE, L, W, DM>(a, lds);
+        rx_back_pre<PRE, L, W, DM, PERS>(a, lds);
     else if (role == 1)
-        rx_back_agc<L, W, DM>(a, lds);
+        rx_back_agc<L, W, DM, PERS>(a, lds);
     else if (role == 2)
-        rx_back_audio<L, PH, W, DM>(a, lds);
+        rx_back_audio<L, PH, W, DM, PERS>(a, lds);
     else if (role == 3)
-        rx_back_aa<AA, DM>(a, lds);
+        rx_back_aa<AA, DM, PERS>(a, lds);
     else if (role == 4)
-        rx_back_output<DM>(a, lds);
+        rx_back_output<DM, PERS>(a, lds);
     else if constexpr (back_tails(DM) > 0)
     {
         // below every role: a tail wave shares a SIMD with a role wave (9-10 waves on 4 SIMDs), and
         // the roles are the per-step critical path
         __builtin_amdgcn_s_setprio(1);
-        rx_back_tail<DM>(a, lds, role - back_roles(DM) + (DM ? 1 : 0));
+        rx_back_tail<DM, PERS>(a, lds, role - back_roles(DM) + (DM ? 1 : 0));
     }
 #ifdef UHSDR_TRACE
     if ((threadIdx.x & (BACK_CH - 1)) == 0 && blockIdx.x < 64)
@@ -3272,7 +3276,14 @@ struct FrontVariant { int t1, t2, m, decim_first; front_fn fn; int R; front_fn f
 // fused_nodc: rx_back_fused without the AGC's DC removal (the demodulator-free back end when the
 // AGC does not remove DC: SSB / CW / DIGI); the same kernel as `fused` for the demodulators
 // fused_ssb: fused_nodc for a launch with the AGC on and the CW decoder off (FORM 1), or null
-struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; back_fn fused_nodc; back_fn fused_ssb; };
+// fn_pers: the persistent back end's instance of fn (uhsdr_rx_set_pipelined 3; DM_NONE only)
+struct BackVariant { int pre, aa, L, ph, w, dm; back_fn fn; back_fn fused; back_fn fused_nodc; back_fn fused_ssb; back_fn fn_pers; };
+template <int PRE, int AA, int L, int PH, int W, int DM>
+constexpr back_fn pers_of()
+{
+    if constexpr (DM == DM_NONE) return rx_back<PRE, AA, L, PH, W, DM, true>;
+    else return nullptr;
+}
 template <int PRE, int AA, int L, int PH, int W, int DM>
 constexpr back_fn fused_nodc_of()
 {
@@ -3473,6 +3484,7 @@ struct uhsdr_rx_s
     unsigned* pdec;          // device memory: group 0's decision per call (BackArgs::pdec)
     int plive, pprev;
     unsigned plast;
+    unsigned pepoch;         // the running (or last) launch's epoch (BackArgs::pepoch)
     unsigned plaunches;      // persistent launches since creation (uhsdr_rx_debug_persist)
     int main_back;           // back-end state was last written on the handle's stream (a one-kernel
                              // schedule, a serial call, a reset): the next side-stream rx_back waits
@@ -3494,12 +3506,10 @@ static void time_mark(uhsdr_rx_s* h, int k, int which)
     if (which) h->evmask[h->nev] |= (uint8_t)(1u << k);
 }
 
-// the persistent back end takes no grant past the last one (PersistCtl: PC_CLOSE); its launch ends
-// after that call
+// the persistent back end's running launch gets no more grants (PersistCtl: the next call goes to a
+// new launch of the next epoch); it ends after the calls granted so far
 static void pers_close(uhsdr_rx_s* h)
 {
-    if (!h->plive) return;
-    __atomic_store_n(h->pmem + PC_CLOSE, h->plast, __ATOMIC_SEQ_CST);
     h->plive = 0;
 }
 
@@ -4094,6 +4104,7 @@ static BackArgs back_args(uhsdr_rx_s* h, float* adec, float* adec_q, float* audi
     ba.pdesc = nullptr;
     ba.pdec = nullptr;
     ba.seq0 = 0;
+    ba.pepoch = 0;
     {
         // key beep: frames [0, beep_n1) of this launch while calls are left (uhsdr_rx_key_beep)
         const int calls = h->N / BLK;
@@ -4187,7 +4198,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
         unsigned* const gc = h->gcnt + (size_t)par * bgroups * CNT_PITCH;
         // persistent back end (PersistCtl): the wave pipeline's skewed form, calls of 8+ sub-calls
         const bool pm = dfl && h->pers && h->skew && UHSDR_BACK_SKEW && h->N / BLK >= 2 * BACK_SKEW && !h->bs.cw &&
-                        bgroups <= PC_MAX_GROUPS;
+                        bgroups <= PC_MAX_GROUPS && h->bv->fn_pers;
         const unsigned seq = (unsigned)pk;
         unsigned* const pw = h->pmem;
         if (!pm && h->plive) HIPCHK(sync_all(h));     // leaving it: its launch ends, and everything completes
@@ -4198,8 +4209,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             // no call's decision yet (ordered before the run's first launch on the side stream)
             HIPCHK(hipMemsetAsync(h->pdec, 0xFF, sizeof(unsigned) * DESC_RING * PDEC_PITCH, h->side));
             for (int g = 0; g < bgroups; ++g) __atomic_store_n(pw + PC_CONSUMED + g, seq, __ATOMIC_SEQ_CST);
-            __atomic_store_n(pw + PC_GRANT, seq - 1, __ATOMIC_SEQ_CST);
-            __atomic_store_n(pw + PC_CLOSE, seq - 1, __ATOMIC_SEQ_CST);
+            __atomic_store_n(pw + PC_GRANT, 0u, __ATOMIC_SEQ_CST);
             __atomic_store_n(pw + PC_EXIT, seq - 2, __ATOMIC_SEQ_CST);
             __atomic_store_n(pw + PC_DECIDED, ((seq - 2) << 1) | 1u, __ATOMIC_SEQ_CST);
         }
@@ -4296,9 +4306,10 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             fprintf(stderr, "host call %u: adec %p cnt %p target %u dst %p waves(g0)x? live %d\n", seq, (void*)adec,
                     (void*)gc, h->fills[par], (void*)bk.dst, h->plive);
 #endif
-            __atomic_store_n(pw + PC_GRANT, seq, __ATOMIC_SEQ_CST);
+            auto grant = [&]() { return h->pepoch << 24 | (seq & 0xFFFFFFu); };
             if (h->plive)
             {
+                __atomic_store_n(pw + PC_GRANT, grant(), __ATOMIC_SEQ_CST);
                 plaunch = false;
                 if (__atomic_load_n(pw + PC_EXIT, __ATOMIC_SEQ_CST) == seq - 1)
                 {
@@ -4319,6 +4330,10 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             h->plast = seq;
             if (plaunch)
             {
+                // a new launch, of the next epoch: grants of the old one's epoch no longer reach it
+                h->pepoch = (h->pepoch + 1) & 0xFFu;
+                __atomic_store_n(pw + PC_GRANT, grant(), __ATOMIC_SEQ_CST);
+                bk.pepoch = h->pepoch;
                 bk.pctl = h->pmem_dev;
                 bk.pdesc = (const BackDesc*)(h->pmem_dev + PC_WORDS);
                 bk.pdec = h->pdec;
@@ -4337,7 +4352,7 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             hipLaunchKernelGGL(h->nv->fn, dim3((h->C + BACK_CH - 1) / BACK_CH), dim3(BACK_CH), 0, bst, bk);
             HIPCHK(hipGetLastError());
         }
-        const back_fn bfn = fused ? fused_back_fn(h) : h->bv->fn;
+        const back_fn bfn = fused ? fused_back_fn(h) : pm ? h->bv->fn_pers : h->bv->fn;
         // (the wave pipeline: its role waves and BACK_TAILS tail waves; rx_fm: its two; the fused kernels: one)
         const int bwaves = fused ? 1 : h->bv->dm == DM_FM ? back_roles(DM_FM) : back_roles(h->bv->dm) + back_tails(h->bv->dm);
         const dim3 bgrid((h->C + BACK_CH - 1) / BACK_CH), bblock(bwaves * BACK_CH);
@@ -4359,6 +4374,10 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             {
                 h->back_attr = hipFuncSetAttribute((const void*)h->bv->fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                    (int)LDS_PER_CU) == hipSuccess ? 1 : -1;
+                if (h->back_attr > 0 && h->bv->fn_pers &&
+                    hipFuncSetAttribute((const void*)h->bv->fn_pers, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)LDS_PER_CU) != hipSuccess)
+                    h->back_attr = -1;
                 (void)hipGetLastError();
             }
             if (h->back_attr > 0) blds = LDS_PER_CU - 4096;
@@ -4488,14 +4507,14 @@ extern "C" uhsdr_status uhsdr_rx_set_front_block(uhsdr_rx_handle h, int32_t outp
     return UHSDR_OK;
 }
 
-// test hook: the persistent back end's control words (PC_GRANT, PC_CLOSE, PC_EXIT, PC_DECIDED,
+// test hook: the persistent back end's control words (PC_GRANT, the epoch, PC_EXIT, PC_DECIDED,
 // PC_CONSUMED) and the host's plive / plast / plaunches
 extern "C" uhsdr_status uhsdr_rx_debug_persist(uhsdr_rx_handle h, uint32_t* out)
 {
     if (!h || !out) return UHSDR_ARGUMENT_ERROR;
     if (!h->pmem) return UHSDR_UNSUPPORTED;
-    const int w[5] = { PC_GRANT, PC_CLOSE, PC_EXIT, PC_DECIDED, PC_CONSUMED };
-    for (int i = 0; i < 5; ++i) out[i] = __atomic_load_n(h->pmem + w[i], __ATOMIC_SEQ_CST);   // (group 0's PC_CONSUMED)
+    const int w[5] = { PC_GRANT, -1, PC_EXIT, PC_DECIDED, PC_CONSUMED };
+    for (int i = 0; i < 5; ++i) out[i] = w[i] < 0 ? h->pepoch : __atomic_load_n(h->pmem + w[i], __ATOMIC_SEQ_CST);   // (group 0's PC_CONSUMED)
     out[5] = (uint32_t)h->plive;
     out[6] = h->plast;
     out[7] = h->plaunches;

@@ -15,7 +15,7 @@ from uhsdr_amd import synth  # noqa: E402
 C, N = 4096, 256
 dev = torch.device("cuda:0")
 MODES = [("serial", U.SCHEDULE_SPLIT_PIPE, False), ("pipelined", U.SCHEDULE_SPLIT_PIPE, True),
-         ("device hand-off", U.SCHEDULE_SPLIT_PIPE, 2)]
+         ("device hand-off", U.SCHEDULE_SPLIT_PIPE, 2), ("persistent", U.SCHEDULE_SPLIT_PIPE, 3)]
 for name, sched, pipe in MODES:
     stream = torch.cuda.current_stream(dev)
     ch = U.RxChain(U.default_config(), channels=C, frames=N, stream=stream.cuda_stream, schedule=sched)

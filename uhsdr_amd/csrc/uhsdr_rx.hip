@@ -814,11 +814,13 @@ struct BackLds
     unsigned* poison;  // [1]  pre -> output: the launch's device hand-off gave up (DM_NONE only)
     unsigned* ext;     // [1]  pre -> every role: the launch runs ahead into the next call (BackSched)
     unsigned* desc;    // [2][16]  pre -> tail: the persistent back end's call outputs (BackDesc words)
+    unsigned* ctl;     // [2][32]  control tail wave -> pre role: a call's descriptor (words 0-15) and the
+                       //          grant word (16), read from host memory a call ahead (PersistCtl)
     float* ys;         // [2][64][BLK + 1]  output -> tail: the output role's call, one row per channel
 };
 
 // floats of the hand-off buffers (host: back_lds)
-__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (6 * ndc + 2 * BLK) + 4 + 32 + 2 * BACK_CH * (BLK + 1); }
+__host__ __device__ constexpr int back_lds_floats(int ndc) { return BACK_CH * 2 * (6 * ndc + 2 * BLK) + 4 + 32 + 64 + 2 * BACK_CH * (BLK + 1); }
 
 template <int NDC>
 __device__ __forceinline__ BackLds back_lds_carve(float* smem)
@@ -833,7 +835,8 @@ __device__ __forceinline__ BackLds back_lds_carve(float* smem)
     l.poison = (unsigned*)(l.prep + 3 * 2 * NDC * BACK_CH);
     l.ext = l.poison + 1;
     l.desc = l.poison + 4;
-    l.ys = (float*)(l.poison + 4 + 32);
+    l.ctl = l.desc + 32;
+    l.ys = (float*)(l.poison + 4 + 32 + 64);
     return l;
 }
 
@@ -1871,10 +1874,12 @@ struct BackSched
 // arrival count after the wait, dst from the descriptor, fast path, gave up
 __device__ unsigned long long g_pdbg[64][8];
 __device__ unsigned long long g_pdbg2[64][4][2];   // per call and group 0..3: decision word seen, polls
+__device__ unsigned long long g_ptime[1024][8];    // per call (seq % 1024): group 0 at g = 4 / n-4 / n-1 / after the decision / n-3 after the grant / n-2; group 1 before / after its decision
 extern "C" int uhsdr_pdbg_read(void* out)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pdbg), sizeof(g_pdbg)) != hipSuccess) return -1;
-    return hipMemcpyFromSymbol((char*)out + sizeof(g_pdbg), HIP_SYMBOL(g_pdbg2), sizeof(g_pdbg2)) == hipSuccess ? 0 : -1;
+    if (hipMemcpyFromSymbol((char*)out + sizeof(g_pdbg), HIP_SYMBOL(g_pdbg2), sizeof(g_pdbg2)) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol((char*)out + sizeof(g_pdbg) + sizeof(g_pdbg2), HIP_SYMBOL(g_ptime), sizeof(g_ptime)) == hipSuccess ? 0 : -1;
 }
 #endif
 // the persistent back end (PersistCtl): its control words and descriptors live in host memory
@@ -2158,24 +2163,62 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a0, BackLds lds)
     BACK_ROLE_LOOP(DM ? 1 : 0)
         if (pers)
         {
-            if (call == l.calls - 4) pctl_load();
+#ifdef UHSDR_PDEBUG
+            if (blockIdx.x == 0 && l.lane == 0)
+            {
+                if (call == 4) g_ptime[seq % 1024][0] = __builtin_amdgcn_s_memrealtime();
+                if (call == l.calls - 4) g_ptime[seq % 1024][1] = __builtin_amdgcn_s_memrealtime();
+                if (call == l.calls - 1) g_ptime[seq % 1024][2] = __builtin_amdgcn_s_memrealtime();
+            }
+#endif
+            // after the launch's first call the control tail wave has read this call's grant and
+            // descriptor from host memory during the previous call (rx_back_tail): LDS reads here. A
+            // host-memory load of this wave's own would hold up its next HBM load's wait (one in-order
+            // vmcnt): 5-9 us per call measured (UHSDR_PDEBUG, tools/debug_persist3.py)
+            const bool have_ctl = seq != a.seq0;
+            if (call == l.calls - 4 && !have_ctl) pctl_load();
             if (call == l.calls - 3)
             {
-                fast = desc_u32(pv, 2) == seq + 1;
-                if (fast)
+                unsigned gw;
+                if (have_ctl)
                 {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    dw = desc_word_load(pdesc(seq + 1), l.lane);
+                    const unsigned* c = lds.ctl + ((seq + 1) & 1) * 32;
+                    dw = c[l.lane & 15];
+                    gw = __builtin_amdgcn_readfirstlane(c[16]);
+                    // complete only if the control wave saw the grant before reading it (the host
+                    // writes the descriptor first; lanes of one load may see it half written)
+                    fast = desc_u32(dw, DW_SEQ) == seq + 1 && pers_granted(a.pepoch, seq + 1, gw);
                 }
+                else
+                {
+                    fast = desc_u32(pv, 2) == seq + 1;
+                    gw = desc_u32(pv, 0);
+                    if (fast)
+                    {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        dw = desc_word_load(pdesc(seq + 1), l.lane);
+                    }
+                }
+#ifdef UHSDR_PDEBUG
+                if (blockIdx.x == 0 && l.lane == 0) g_ptime[seq % 1024][4] = __builtin_amdgcn_s_memrealtime();
+#endif
                 // group 0: granted already -- published now, two steps before the others need it
-                if (leader && fast && pers_granted(a.pepoch, seq + 1, desc_u32(pv, 0)))
+                if (leader && fast && pers_granted(a.pepoch, seq + 1, gw))
                 {
                     publish(seq + 1, true);
                     ldone = true;
                 }
             }
             if (call == l.calls - 2 && !leader) dv = __hip_atomic_load(pdec(seq + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef UHSDR_PDEBUG
+            if (call == l.calls - 2 && blockIdx.x == 0 && l.lane == 0) g_ptime[seq % 1024][5] = __builtin_amdgcn_s_memrealtime();
+            if (call == l.calls - 1 && blockIdx.x == 1 && l.lane == 0) g_ptime[seq % 1024][6] = __builtin_amdgcn_s_memrealtime();
+#endif
             if (call == l.calls - 1) pers_decide();
+#ifdef UHSDR_PDEBUG
+            if (call == l.calls - 1 && blockIdx.x == 1 && l.lane == 0) g_ptime[seq % 1024][7] = __builtin_amdgcn_s_memrealtime();
+            if (call == l.calls - 1 && blockIdx.x == 0 && l.lane == 0) g_ptime[seq % 1024][3] = __builtin_amdgcn_s_memrealtime();
+#endif
         }
         else if (sch.may_ext)
         {
@@ -2249,13 +2292,7 @@ __device__ __forceinline__ void rx_back_pre(const BackArgs& a0, BackLds lds)
         {
             // a give-up poisons the output from here on (the output role reads the word every sub-call)
             if (l.lane == 0 && in.gave_up) *lds.poison = 1u;
-            // the call's hand-off buffer is read (its last sub-call's samples are in use above): the
-            // host may refill it (no fence: the load of the next call's first sub-call stays in flight)
-            if (call == l.calls - 1 && l.lane == 0)
-            {
-                asm volatile("" ::: "memory");
-                __hip_atomic_store(a.pctl + PC_CONSUMED + blockIdx.x, seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
+            // (PC_CONSUMED: stored by the control tail wave a step later, off this wave's vmcnt)
         }
     BACK_ROLE_END
         if (!pers || !ext) break;
@@ -2597,6 +2634,12 @@ __device__ __forceinline__ void rx_back_tail(const BackArgs& a0, BackLds lds, in
             line_out4(a, rb, off, call, call * BLK + 4 * j, v);
         }
     };
+    // the persistent back end's control wave (the last tail): the host-memory reads of the call after
+    // next (grant word, then its descriptor once the grant has been seen: the host writes it first)
+    // and the PC_CONSUMED store, so no role wave waits on a PCIe round trip; the results go to
+    // lds.ctl at the call's last step (read by the pre role during the next call)
+    const bool ctlw = pers && half == BACK_TAILS - 1;
+    unsigned cg = 0, cd = 0;
     for (unsigned seq = a.seq0;; ++seq)
     {
         for (int it = 0; it < sch.steps; ++it)
@@ -2604,6 +2647,25 @@ __device__ __forceinline__ void rx_back_tail(const BackArgs& a0, BackLds lds, in
             const int call = it - ST + sch.gofs;
             TRACE_MARK(0);
             if (call >= 0 && call < l.calls) store_call(call);
+            if (ctlw)
+            {
+                const BackDesc* d2 = a.pdesc + (seq + 2) % DESC_RING;
+                if (it == 0) cg = sys_load(a.pctl + PC_GRANT);
+                if (it == 3)
+                {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the grant first
+                    cd = sys_load((const unsigned*)d2 + (l.lane & 15));
+                }
+                // the pre role's last read of this call's buffer was in the step before
+                if (it == l.calls - sch.gofs && l.lane == 0)
+                    __hip_atomic_store(a.pctl + PC_CONSUMED + blockIdx.x, seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (it == sch.steps - 1)
+                {
+                    unsigned* c = lds.ctl + ((seq + 2) & 1) * 32;
+                    if (l.lane < 16) c[l.lane] = cd;
+                    if (l.lane == 0) c[16] = __builtin_amdgcn_readfirstlane(cg);
+                }
+            }
             TRACE_MARK(1);
             lds_barrier();
             TRACE_MARK(2);
@@ -4302,10 +4364,6 @@ static uhsdr_status rx_process(uhsdr_rx_handle h, const int32_t* iq, float* audi
             d->beep_n1 = bk.beep_n1;
             d->beep_acc = bk.beep_acc;
             __atomic_store_n(&d->seq, seq, __ATOMIC_RELEASE);
-#ifdef UHSDR_PDEBUG
-            fprintf(stderr, "host call %u: adec %p cnt %p target %u dst %p waves(g0)x? live %d\n", seq, (void*)adec,
-                    (void*)gc, h->fills[par], (void*)bk.dst, h->plive);
-#endif
             auto grant = [&]() { return h->pepoch << 24 | (seq & 0xFFFFFFu); };
             if (h->plive)
             {

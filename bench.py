@@ -137,7 +137,7 @@ SCHEDULE_NAMES = {1: "split_pipe", 2: "split_fused", 3: "chain"}
 
 
 def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmup, pool, want_dst, pipelined=False,
-              precision=0, schedule=None, front_block=0, reduce_dev=None, board=0):
+              precision=0, schedule=None, front_block=0, reduce_dev=None, board=0, ensure_dist=None):
     """W untimed + K timed steps of one RxChain on this rank; returns (max-rank seconds,
     per-kernel (total ms, launches) from HIP events on the library's stream, plan, finite, schedule,
     device hand-off give-ups after the timed loop (uhsdr_rx_handoff_timeouts; 0 required))."""
@@ -153,6 +153,8 @@ def timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, steps, warmu
         # arrival counters the front waves of its channel group bump, then reads the hand-off with
         # sc1 loads, instead of waiting on a cross-stream event)
         chain.set_pipelined(DEVICE_HANDOFF)
+    if ensure_dist is not None:
+        ensure_dist()                                  # the process group after the side stream
     plan = chain.plan
     # inputs resident in HBM before timing: a pool of consecutive blocks, cycled
     c0 = shard.channel_range(C, rank)[0]          # weak scaling: rank r owns channels [r*C, (r+1)*C)
@@ -321,11 +323,17 @@ def main():
         # gloo test hook: ranks may outnumber the GPUs of the box and share them
         dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+
+    def ensure_dist():
+        # after the C2 handle has made its side stream (timed_run): the persistent back end waits in
+        # its launch for fronts enqueued later on the handle's stream, so the side stream must not share
+        # a hardware queue with it; made before RCCL's streams, it takes a queue of its own
+        if world > 1 and not dist.is_initialized():
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group("gloo")
+
     reduce_dev = dev if args.dist_backend == "nccl" else "cpu"
 
     prec = U.PRECISION_FMA if args.precision == "fma" else U.PRECISION_EXACT
@@ -336,7 +344,9 @@ def main():
     elapsed, ktimes, plan, ok, sched, timeouts = timed_run(U, synth, shard, torch, dist, dev, world, rank, C, N, args.steps,
                                                  args.warmup, max(1, args.pool), args.dst, pipelined, prec,
                                                  SCHEDULES[args.schedule], args.front_block, reduce_dev,
-                                                 U.BOARD_MCHF if args.board == "mchf" else U.BOARD_OVI40)
+                                                 U.BOARD_MCHF if args.board == "mchf" else U.BOARD_OVI40,
+                                                 ensure_dist=ensure_dist)
+    ensure_dist()
 
     gather = None
     if world > 1 and not args.no_gather:

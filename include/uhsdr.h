@@ -303,7 +303,11 @@ uhsdr_status uhsdr_rx_synchronize(uhsdr_rx_handle h);
    device-wide synchronisation (or join) completes without further calls.  The host waits in
    uhsdr_rx_process before refilling a hand-off buffer the back end has not read yet (8 calls
    back).  Same failure contract as enable = 2 (a give-up inside a launch poisons the call it
-   waited for, and may poison the end of the call before it).  Any other enable value returns
+   waited for, and may poison the end of the call before it).  A running launch waits for fronts
+   enqueued after it, so the handle's side stream (made at the first uhsdr_rx_set_pipelined) must not
+   share a hardware queue with the handle's stream: HIP spreads streams over GPU_MAX_HW_QUEUES queues
+   (4 by default), so make the handle before other streams of the process (a shared queue shows as a
+   give-up, UHSDR_TIMEOUT, never as silent output).  Any other enable value returns
    UHSDR_ARGUMENT_ERROR.
    Failure contract of the device hand-off.  The poll is bounded (uhsdr_rx_set_handoff_bound,
    default 2^24 polls: seconds).  If rx_back gives up -- the handle's stream held the call's

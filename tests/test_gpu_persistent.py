@@ -180,34 +180,3 @@ def test_persistent_give_up_fails_loudly(cuda):
         chain.set_pipelined(4)                       # modes are 0 .. 3
     chain.close()
 
-
-def test_persistent_two_handles(cuda):
-    """Two handles in mode 3 at once (their own streams, control words and launches), calls
-    interleaved and one of them joined mid-stream: both bit-exact against the oracle."""
-    import torch
-    cfgs = [U.default_config(), U.default_config(dmod_mode=U.DEMOD_LSB)]
-    C, N, calls = 256, 256, 12
-    chains, ins, outs, iqs = [], [], [], []
-    for i, cfg in enumerate(cfgs):
-        s = torch.cuda.Stream()
-        ch = U.RxChain(cfg, channels=C, frames=N, stream=s.cuda_stream)
-        ch.set_pipelined(3)
-        iq = synth.ssb_iq(np.arange(C) + 1000 * i, 0, calls * N)
-        iqs.append(iq)
-        ins.append([torch.from_numpy(np.ascontiguousarray(iq[:, k * N:(k + 1) * N])).cuda() for k in range(calls)])
-        outs.append(torch.empty((calls, C, N), dtype=torch.float32, device="cuda"))
-        chains.append(ch)
-    torch.cuda.synchronize()
-    for k in range(calls):
-        for i, ch in enumerate(chains):
-            ch.process(ins[i][k], outs[i][k], None)
-        if k == 5:
-            chains[1].join()
-    for i, ch in enumerate(chains):
-        ch.synchronize()
-        assert ch.handoff_timeouts() == 0
-    for i, ch in enumerate(chains):
-        ref, _ = oracle.OracleRx(U.build_plan(cfgs[i]), C).process(iqs[i], threads=8)
-        got = outs[i].permute(1, 0, 2).reshape(C, calls * N).cpu().numpy()
-        assert_bitexact(got, ref, f"persistent, two handles, handle {i}")
-        ch.close()
